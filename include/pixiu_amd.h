@@ -1,0 +1,136 @@
+/* pixiu_amd.h — C ABI of the MI355X-native PiXiu batch compress/query core.
+ *
+ * This is the drop-in boundary.  Every entry point is plain C:
+ * pointers, sizes and status codes; no C++ or torch types cross it.  The
+ * source-compatible C++ facade (include/PiXiuCtrl.h) and the Python binding
+ * (pixiu_amd/__init__.py) are thin layers over these calls.
+ *
+ * Object model: a px_ctx is a sharded store.  Records are assigned, in arrival
+ * order, to shards of `records_per_shard` records; every shard is an independent
+ * PiXiuCtrl-equivalent (own generalized suffix tree, chunks, CritBit index), so
+ * shard s's compressed bytes equal what the reference produces when fed exactly
+ * shard s's records.  records_per_shard == 0 means ONE shard: the exact
+ * single-instance semantics of the reference PiXiuCtrl.
+ *
+ * Reference interfaces replaced (file:line in Thunderchen/PiXiu src/):
+ *   px_open / px_close ........ PiXiuCtrl::init_prop / free_prop   (PiXiuCtrl.cpp:77-86)
+ *   px_set_batch .............. PiXiuCtrl::setitem                  (PiXiuCtrl.cpp:12-47)
+ *   px_get_batch .............. PiXiuCtrl::getitem + PXSGen drain   (PiXiuCtrl.cpp:59-61, PiXiuStr.h:129-198)
+ *   px_contains_batch ......... PiXiuCtrl::contains                 (PiXiuCtrl.cpp:55-57)
+ *   px_del_batch .............. PiXiuCtrl::delitem                  (PiXiuCtrl.cpp:63-69)
+ *   px_parse_batch ............ PiXiuStr::parse(from,to,chunk)      (PiXiuStr.cpp:166-176)
+ *   px_export ................. cbt_chunk->getitem(idx) bytes       (PiXiuStr.cpp:202-206, main.cpp:67)
+ *
+ * All calls are synchronous on the context's HIP stream.  A context is not
+ * thread-safe; distinct contexts are fully independent (no globals).
+ */
+#ifndef PIXIU_AMD_H
+#define PIXIU_AMD_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum px_status {
+    PX_OK = 0,
+    PX_EINVAL = 1,      /* bad argument, empty key, escaped doc > 65,535 B */
+    PX_ECAPACITY = 2,   /* internal arena sizing failure */
+    PX_EREFCRASH = 3,   /* input on which the reference dereferences NULL (its GST bug) */
+    PX_ECORRUPT = 4,    /* malformed compressed bytes */
+    PX_EHANG = 5,       /* input on which the reference decoder never terminates */
+    PX_EDEPTH = 6,      /* decode nesting deeper than opts.decode_depth */
+    PX_ESPACE = 7,      /* output buffer too small */
+    PX_ENOTFOUND = 8,   /* getitem/contains/delitem of a missing key */
+    PX_EHIP = 9,        /* HIP runtime error */
+    PX_ENOMEM = 10      /* device allocation failed */
+} px_status;
+
+typedef enum px_mode {
+    PX_COMPAT = 0, /* byte-exact with the reference PXSGen, bugs included */
+    PX_EXACT = 1   /* correct LZ expansion: equals the original escaped doc */
+} px_mode;
+
+typedef struct px_opts {
+    int device;                 /* HIP device ordinal */
+    uint32_t records_per_shard; /* 0 = single shard (reference semantics) */
+    uint32_t decode_depth;      /* frames per decode stack; 0 = 4096 */
+    uint32_t decode_waves;      /* concurrent decode wavefronts; 0 = auto */
+    uint32_t host_threads;      /* host CritBit worker threads; 0 = auto */
+} px_opts;
+
+typedef struct px_ctx px_ctx;
+
+/* per-record result of px_set_batch */
+typedef struct px_set_result {
+    uint32_t status;   /* px_status */
+    uint32_t replaced; /* 1 = CBT_SET_REPLACE (duplicate key in the same shard) */
+    uint32_t shard;
+    uint32_t chunk;    /* chunk sequence number inside the shard (rotation count) */
+    uint32_t idx;      /* chunk-local slot (the `idx` that references point at) */
+    uint32_t comp_len; /* compressed length */
+    uint32_t doc_len;  /* escaped doc length (esc(k)+[251,0]+esc(v)+[251,2]) */
+    uint32_t pad;
+} px_set_result;
+
+/* a stored record, as addressed by px_parse_batch / px_export */
+typedef struct px_rec {
+    uint32_t shard, chunk, idx;
+    int32_t from, to; /* parse range (escaped coordinates); [0, 65535) = whole record */
+} px_rec;
+
+typedef struct px_stats {
+    uint64_t records, shards, chunks;
+    uint64_t raw_bytes, doc_bytes, comp_bytes;
+    uint64_t ub_reads;        /* reads the reference makes out of bounds (UB there) */
+    uint64_t device_bytes;    /* device memory held */
+    double last_set_kernel_ms;    /* k_gst_encode time of the last px_set_batch */
+    double last_decode_kernel_ms; /* k_decode time of the last get/parse batch */
+} px_stats;
+
+px_ctx *px_open(const px_opts *opts);
+void px_close(px_ctx *ctx);
+const char *px_strerror(int status);
+
+/* Batch setitem.  Record i: key = keys[koff[i] .. koff[i+1]), value =
+ * vals[voff[i] .. voff[i+1]) (empty value = key-only record).  If on_device, the
+ * four pointers are device pointers (inputs already resident in HBM); otherwise
+ * host pointers.  res (host, n entries) may be NULL.  Returns PX_OK if every
+ * record was stored, else the first failing status (others may have succeeded). */
+int px_set_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff,
+                 const uint8_t *vals, const uint64_t *voff, int on_device, px_set_result *res);
+
+/* Batch getitem: keys are host CSR.  The expanded doc of key i lands in
+ * out[out_off[i] .. out_off[i] + out_len[i]) (out is a device pointer when
+ * out_on_device, else host).  status[i] = PX_OK or PX_ENOTFOUND/...  If out_cap
+ * is too small the call returns PX_ESPACE and *needed (if non-NULL) holds the
+ * required capacity.  out_off/out_len/status are host arrays of n entries. */
+int px_get_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff, int mode,
+                 uint8_t *out, uint64_t out_cap, int out_on_device, uint64_t *out_off,
+                 uint32_t *out_len, uint32_t *status, uint64_t *needed);
+
+/* Batch PiXiuStr::parse(from, to) of stored records (the kernel-level boundary). */
+int px_parse_batch(px_ctx *ctx, uint32_t n, const px_rec *recs, int mode, uint8_t *out,
+                   uint64_t out_cap, int out_on_device, uint64_t *out_off, uint32_t *out_len,
+                   uint32_t *status, uint64_t *needed);
+
+/* contains / delitem by key (host keys).  result[i] = 1/0 (contains) or
+ * 0 deleted / 1 CBT_DEL_NOT_FOUND (delitem), as the reference returns. */
+int px_contains_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff,
+                      uint32_t *result);
+int px_del_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff,
+                 uint32_t *result);
+
+/* Compressed bytes of stored records, copied to host CSR (out_off has n+1 entries). */
+int px_export(px_ctx *ctx, uint32_t n, const px_rec *recs, uint8_t *out, uint64_t out_cap,
+              uint64_t *out_off);
+
+int px_stats_get(px_ctx *ctx, px_stats *st);
+
+/* HIP stream the context runs on (a hipStream_t), for callers that order their
+ * own work against it. */
+void *px_stream(px_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,107 @@
+// px_common.h — layouts shared by the HIP kernels (px_kernels.hip) and the host
+// runtime (px_runtime.cpp).  Everything here is plain data: sizes and field order
+// are part of the device ABI between the two translation units.
+#pragma once
+#include <stdint.h>
+
+namespace px {
+
+// ---- PiXiu encoding constants (PiXiuStr.h:11-21) ----
+constexpr uint8_t kEsc = 251;      // PXS_UNIQUE
+constexpr uint8_t kKeyEnd = 0;     // PXS_KEY
+constexpr uint8_t kValEnd = 2;     // PXS_KEY_SEC
+constexpr uint8_t kBigSign = 1;    // PXS_COMPRESS
+constexpr int kMaxDoc = 65535;     // PXSG_MAX_TO
+constexpr int kChunkSlots = 65535; // PXC_STR_NUM
+
+// ---- MemPool emulation (MemPool.h:6-7, MemPool.cpp:7-37; PiXiuCtrl.cpp:13) ----
+constexpr int kPoolBlocks = 65535;
+constexpr int kNodeBlocks = 5;   // sizeof(STNode) = 40 B
+constexpr int kEdgeBlocks = 3;   // sizeof(SGTNode<STNode>) = 24 B
+constexpr int kRotatePools = 2048;
+
+// ---- GST arena ----
+// Node (16 B):  x = suffix link, y = label start relative to the chunk's text base,
+//               z = doc | from << 16,  w = to | flags << 16
+constexpr uint32_t kRoot = 0;
+constexpr uint32_t kNone = 0xffffffffu;
+constexpr uint32_t kFlagKids = 1;  // node has >= 1 child (STNode::is_inner for non-root)
+// child-map hash entry (u64): epoch:4 | parent:26 | byte:8 | child:26; epoch 0 == empty
+constexpr int kNodeBits = 26;
+constexpr uint32_t kMaxNodes = (1u << kNodeBits) - 1;
+constexpr int kMaxEpoch = 15;
+constexpr int kProbe = 16;  // lanes per hash probe window
+
+// persistent per-shard GST state (device resident between batches)
+struct ShardState {
+    uint32_t n_nodes;      // nodes allocated in the live chunk (root included)
+    int32_t pools;         // MemPool::nth
+    int32_t used_blocks;   // MemPool::used_num
+    int32_t pool_open;     // MemPool::curr_pool != NULL
+    uint32_t n_docs;       // docs in the live chunk (SuffixTree::local_chunk.used_num)
+    uint32_t chunk_seq;    // how many rotations this shard has seen
+    uint32_t epoch;        // current hash epoch (1..15)
+    uint32_t status;       // 0 ok, else a px_status (sticky: the shard is dead)
+    uint64_t ctext_off;    // byte offset of the live chunk's text inside the arena text section
+    uint64_t ub_reads;     // out-of-bounds reads the reference would make (UB there)
+};
+
+// per-batch shard work descriptor
+struct GstShard {
+    uint8_t *text;        // arena text section
+    uint32_t *doc_base;   // [doc_cap + 1] doc start relative to the live chunk text base
+    uint4 *nodes;         // [node_cap]
+    uint64_t *hash;       // [hash_mask + 1]
+    uint32_t *root_kids;  // [256]
+    ShardState *st;
+    uint32_t node_cap;
+    uint32_t hash_mask;
+    uint32_t doc_cap;
+    uint32_t r0, r1;      // batch records [r0, r1) belong to this shard, in order
+    uint32_t pad;
+};
+
+// compressed-record slot: what a chunk table entry points at
+struct RecSlot {
+    const uint8_t *comp;  // compressed bytes
+    const uint2 *seg;     // segment index: (src_start, comp_start) x (nseg + 1)
+    uint32_t comp_len;
+    uint32_t nseg;
+};
+
+// decode query
+struct DecodeQuery {
+    uint32_t chunk;       // global chunk id
+    uint32_t idx;         // chunk-local record slot
+    int32_t from, to;     // PiXiuStr::parse(from, to)
+    uint64_t out_off;     // where the output goes
+    uint32_t out_cap;     // consumer stops pulling after this many bytes
+    uint32_t mode;        // 0 compat, 1 exact
+};
+
+// decode frame (scratch, one stack per wave)
+struct Frame {
+    uint32_t rec;     // chunk-local idx of the record being parsed ("self")
+    int32_t from;
+    int32_t len;
+    int32_t ret;      // ret_cursor (relative, the reference's accounting)
+    int32_t src;      // src_cursor (absolute within self)
+    uint32_t seg;     // next segment to visit
+    uint32_t cap;     // absolute output position where this frame's consumer stops
+    uint32_t state;   // 0 run, 1 waiting on a plain child, 2 waiting on a periodic child
+    uint32_t pstart;  // output position where the pending child began
+    int32_t sub_from, sub_to, supply;
+};
+
+enum Status : uint32_t {
+    kOk = 0,
+    kErrInval = 1,      // bad argument / oversize doc / empty key
+    kErrCapacity = 2,   // arena too small (host sizing bug)
+    kErrRefCrash = 3,   // reference would dereference NULL here (SuffixTree.cpp child lookup)
+    kErrCorrupt = 4,    // malformed compressed bytes
+    kErrHang = 5,       // reference decoder would loop forever
+    kErrDepth = 6,      // decode stack exhausted
+    kErrSpace = 7,      // output capacity exceeded (result truncated)
+};
+
+}  // namespace px

@@ -1,0 +1,1133 @@
+// px_runtime.cpp — host runtime behind the C ABI (include/pixiu_amd.h).
+//
+// Owns device memory (a slab heap), the per-shard GST arenas, the compressed
+// record store (chunk slot tables the decoder indexes), and the host-side
+// CritBit index (the north star keeps it on the host).  Every data-path byte is
+// produced by the HIP kernels in px_kernels.hip; the host only moves metadata
+// (lengths, statuses, key prefixes) and runs the CritBit walk.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/pixiu_amd.h"
+#include "px_common.h"
+
+namespace px {
+hipError_t launch_doc_len(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, const uint8_t *,
+                          const uint64_t *, uint32_t *);
+hipError_t launch_doc_write(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, const uint8_t *,
+                            const uint64_t *, uint8_t *const *);
+hipError_t launch_gst_encode(hipStream_t, const GstShard *, uint32_t, const uint32_t *, uint8_t *const *,
+                             uint32_t *, uint32_t *, uint32_t *, uint32_t *);
+hipError_t launch_compact(hipStream_t, uint32_t, uint8_t *const *, const uint32_t *, uint8_t *, const uint64_t *);
+hipError_t launch_tokenize(hipStream_t, uint32_t, const RecSlot *, uint2 *const *, uint32_t *, uint32_t *);
+hipError_t launch_decode(hipStream_t, const DecodeQuery *, uint32_t, const RecSlot *const *, uint8_t *,
+                         uint32_t *, uint32_t *, Frame *, uint32_t, uint32_t);
+hipError_t launch_rehash(hipStream_t, const uint64_t *, uint32_t, uint32_t, uint64_t *, uint32_t);
+}  // namespace px
+
+using namespace px;
+
+namespace {
+
+struct HipFail {
+    hipError_t e;
+};
+inline void hcheck(hipError_t e) {
+    if (e != hipSuccess) throw HipFail{e};
+}
+struct PxFail {
+    int code;
+};
+
+inline uint64_t round_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+inline uint64_t pow2_at_least(uint64_t v) {
+    uint64_t p = 1024;
+    while (p < v) p <<= 1;
+    return p;
+}
+
+// ---------------------------------------------------------------- device heap
+// Slab bump allocator with exact-size free lists: no hipMalloc per shard.
+class DevHeap {
+  public:
+    ~DevHeap() {
+        for (void *s : slabs_) (void)hipFree(s);
+    }
+    void *alloc(uint64_t n) {
+        n = round_up(std::max<uint64_t>(n, 256), 256);
+        auto it = free_.find(n);
+        if (it != free_.end() && !it->second.empty()) {
+            void *p = it->second.back();
+            it->second.pop_back();
+            return p;
+        }
+        if (n > left_) {
+            uint64_t sz = std::max<uint64_t>(n, kSlab);
+            void *s = nullptr;
+            if (hipMalloc(&s, sz) != hipSuccess) throw PxFail{PX_ENOMEM};
+            slabs_.push_back(s);
+            held_ += sz;
+            cur_ = static_cast<char *>(s);
+            left_ = sz;
+        }
+        void *p = cur_;
+        cur_ += n;
+        left_ -= n;
+        return p;
+    }
+    void release(void *p, uint64_t n) {
+        if (!p) return;
+        n = round_up(std::max<uint64_t>(n, 256), 256);
+        free_[n].push_back(p);
+    }
+    uint64_t held() const { return held_; }
+
+  private:
+    static constexpr uint64_t kSlab = 1ull << 30;
+    std::vector<void *> slabs_;
+    char *cur_ = nullptr;
+    uint64_t left_ = 0, held_ = 0;
+    std::map<uint64_t, std::vector<void *>> free_;
+};
+
+// pinned-free scratch buffer that only grows
+struct DevBuf {
+    void *p = nullptr;
+    uint64_t cap = 0;
+    void *get(uint64_t n) {
+        if (n > cap) {
+            if (p) (void)hipFree(p);
+            cap = std::max<uint64_t>(round_up(n, 1 << 20), cap * 2);
+            p = nullptr;
+            if (hipMalloc(&p, cap) != hipSuccess) {
+                cap = 0;
+                throw PxFail{PX_ENOMEM};
+            }
+        }
+        return p;
+    }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+// ---------------------------------------------------------------- crit-bit index
+// Restates CritBitTree.cpp:13-269 over the COMPAT-decoded key prefix of each stored
+// record (computed on the GPU at setitem time).  Walk bytes past a key's end read 0
+// (as getitem does); crit-bit trees are canonical, so this equals the reference's
+// tree whenever the decoded key prefixes equal the true keys.
+struct Leaf {
+    uint32_t chunk, idx;  // global chunk id, slot
+};
+struct CbtRef {
+    int32_t inner = -1;
+    Leaf leaf{0, 0};
+};
+struct CbtInner {
+    CbtRef kid[2];
+    uint16_t diff_at;
+    uint8_t mask;
+};
+inline int crit_dir(uint8_t mask, uint8_t byte) { return (1 + (mask | byte)) >> 8; }
+
+struct Chunk {
+    uint32_t shard = 0;
+    uint32_t n = 0;
+    std::vector<RecSlot> slots;  // host mirror (device pointers inside)
+    RecSlot *dev = nullptr;      // device slot table
+    uint32_t dev_cap = 0;
+    std::vector<uint32_t> doc_len;
+    std::vector<uint8_t> dead;
+    std::string kp;  // concatenated compat key prefixes
+    std::vector<uint64_t> kp_off;
+    std::vector<uint32_t> kp_len;
+};
+
+struct Shard {
+    uint32_t id = 0;
+    // device arena
+    void *arena = nullptr;
+    uint64_t arena_bytes = 0;
+    ShardState *st = nullptr;
+    uint32_t *root_kids = nullptr, *doc_base = nullptr;
+    uint4 *nodes = nullptr;
+    uint64_t *hash = nullptr;
+    uint8_t *text = nullptr;
+    uint32_t node_cap = 0, doc_cap = 0;
+    uint64_t hash_cap = 0, text_cap = 0;
+    ShardState hs{};      // host mirror after the last batch
+    uint64_t text_end = 0;  // end of written text (relative to the arena text section)
+    uint32_t records = 0;
+    std::vector<uint32_t> chunks;  // global chunk ids by chunk_seq
+    // CritBit
+    std::vector<CbtInner> cbt;
+    std::vector<int32_t> cbt_free;
+    bool has_root = false;
+    CbtRef root;
+};
+
+}  // namespace
+
+struct px_ctx {
+    px_opts opts{};
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    DevHeap heap;
+    std::vector<std::unique_ptr<Shard>> shards;
+    std::vector<Chunk> chunks;
+    RecSlot **chunk_tab = nullptr;  // device: chunk id -> slot table
+    uint32_t chunk_tab_cap = 0;
+    std::unordered_map<std::string, uint32_t> keymap;  // raw key -> shard (multi-shard only)
+    DevBuf scratch_frames, dq_buf, dstat_buf, dlen_buf, in_buf, tmp_buf;
+    px_stats stats{};
+    int last_hip = 0;
+
+    // ------------------------------------------------------------ helpers
+    // Host->device copies are staged in buffers owned until the next sync(), so the
+    // caller's (pageable, possibly short-lived) source may go away immediately.
+    std::vector<std::vector<uint8_t>> staged;
+    void sync() {
+        hcheck(hipStreamSynchronize(stream));
+        staged.clear();
+    }
+    void h2d(void *d, const void *h, size_t n) {
+        if (!n) return;
+        const uint8_t *b = static_cast<const uint8_t *>(h);
+        staged.emplace_back(b, b + n);
+        hcheck(hipMemcpyAsync(d, staged.back().data(), n, hipMemcpyHostToDevice, stream));
+    }
+    void d2h(void *h, const void *d, size_t n) {
+        if (n) hcheck(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, stream));
+    }
+
+    Shard &new_shard() {
+        auto s = std::make_unique<Shard>();
+        s->id = (uint32_t)shards.size();
+        shards.push_back(std::move(s));
+        stats.shards = shards.size();
+        return *shards.back();
+    }
+
+    uint32_t new_chunk(uint32_t shard) {
+        chunks.emplace_back();
+        chunks.back().shard = shard;
+        uint32_t id = (uint32_t)chunks.size() - 1;
+        if (chunks.size() > chunk_tab_cap) {
+            uint32_t cap = std::max<uint32_t>(1024, chunk_tab_cap * 2);
+            while (cap < chunks.size()) cap *= 2;
+            auto *nt = (RecSlot **)heap.alloc((uint64_t)cap * sizeof(RecSlot *));
+            if (chunk_tab) {
+                hcheck(hipMemcpyAsync(nt, chunk_tab, (size_t)chunk_tab_cap * sizeof(RecSlot *),
+                                      hipMemcpyDeviceToDevice, stream));
+                heap.release(chunk_tab, (uint64_t)chunk_tab_cap * sizeof(RecSlot *));
+            }
+            chunk_tab = nt;
+            chunk_tab_cap = cap;
+        }
+        stats.chunks = chunks.size();
+        return id;
+    }
+
+    // ensure chunk c's device slot table holds `need` slots
+    void chunk_reserve(uint32_t c, uint32_t need) {
+        Chunk &ch = chunks[c];
+        if (need <= ch.dev_cap) return;
+        uint32_t cap = std::max<uint32_t>(64, ch.dev_cap * 2);
+        while (cap < need) cap *= 2;
+        cap = std::min<uint32_t>(cap, kChunkSlots);
+        auto *nt = (RecSlot *)heap.alloc((uint64_t)cap * sizeof(RecSlot));
+        if (ch.dev) {
+            hcheck(hipMemcpyAsync(nt, ch.dev, (size_t)ch.n * sizeof(RecSlot), hipMemcpyDeviceToDevice, stream));
+            heap.release(ch.dev, (uint64_t)ch.dev_cap * sizeof(RecSlot));
+        }
+        ch.dev = nt;
+        ch.dev_cap = cap;
+        h2d(chunk_tab + c, &ch.dev, sizeof(RecSlot *));
+    }
+
+    // (re)build a shard's arena so the next batch (B new bytes, D new docs) fits
+    void shard_reserve(Shard &s, uint64_t B, uint32_t D) {
+        uint64_t need_nodes = (uint64_t)s.hs.n_nodes + 2 * B + 4;
+        uint64_t need_docs = std::min<uint64_t>((uint64_t)s.hs.n_docs + D, kChunkSlots) + 1;
+        uint64_t need_text = s.text_end + B;
+        uint64_t need_hash = pow2_at_least(2 * need_nodes);
+        if (need_nodes > kMaxNodes) need_nodes = kMaxNodes;
+        bool fits = s.arena && need_nodes <= s.node_cap && need_docs <= s.doc_cap && need_text <= s.text_cap &&
+                    need_hash <= s.hash_cap;
+        if (fits) return;
+        // new capacities (grow geometrically when the shard already exists)
+        uint64_t g = s.arena ? 2 : 1;
+        uint64_t node_cap = std::min<uint64_t>(std::max(need_nodes, (uint64_t)s.node_cap * g), kMaxNodes);
+        uint64_t doc_cap = std::min<uint64_t>(std::max(need_docs, (uint64_t)s.doc_cap * g), kChunkSlots + 1);
+        uint64_t live_text = s.text_end - s.hs.ctext_off;
+        uint64_t text_cap = std::max(live_text + B, s.arena ? (live_text + B) * 3 / 2 : live_text + B);
+        uint64_t hash_cap = pow2_at_least(2 * node_cap);
+        uint64_t off_root = round_up(sizeof(ShardState), 256);
+        uint64_t off_doc = off_root + 1024;
+        uint64_t off_nodes = round_up(off_doc + (doc_cap + 1) * 4, 256);
+        uint64_t off_hash = round_up(off_nodes + node_cap * 16, 256);
+        uint64_t off_text = round_up(off_hash + hash_cap * 8, 256);
+        uint64_t total = round_up(off_text + text_cap + 64, 256);
+        char *a = (char *)heap.alloc(total);
+        Shard o = s;  // old view
+        s.arena = a;
+        s.arena_bytes = total;
+        s.st = (ShardState *)a;
+        s.root_kids = (uint32_t *)(a + off_root);
+        s.doc_base = (uint32_t *)(a + off_doc);
+        s.nodes = (uint4 *)(a + off_nodes);
+        s.hash = (uint64_t *)(a + off_hash);
+        s.text = (uint8_t *)(a + off_text);
+        s.node_cap = (uint32_t)node_cap;
+        s.doc_cap = (uint32_t)doc_cap - 1;
+        s.hash_cap = hash_cap;
+        s.text_cap = text_cap;
+        hcheck(hipMemsetAsync(s.hash, 0, hash_cap * 8, stream));
+        if (!o.arena) {
+            ShardState z{};
+            h2d(s.st, &z, sizeof z);
+            s.text_end = 0;
+            return;
+        }
+        // migrate the live chunk: text moves to offset 0, everything else by copy / rehash
+        hcheck(hipMemcpyAsync(s.root_kids, o.root_kids, 1024, hipMemcpyDeviceToDevice, stream));
+        hcheck(hipMemcpyAsync(s.doc_base, o.doc_base, ((size_t)o.hs.n_docs + 1) * 4, hipMemcpyDeviceToDevice, stream));
+        hcheck(hipMemcpyAsync(s.nodes, o.nodes, (size_t)o.hs.n_nodes * 16, hipMemcpyDeviceToDevice, stream));
+        hcheck(launch_rehash(stream, o.hash, (uint32_t)o.hash_cap, o.hs.epoch, s.hash, (uint32_t)(hash_cap - 1)));
+        hcheck(hipMemcpyAsync(s.text, o.text + o.hs.ctext_off, live_text, hipMemcpyDeviceToDevice, stream));
+        s.hs.ctext_off = 0;
+        s.text_end = live_text;
+        h2d(s.st, &s.hs, sizeof(ShardState));
+        sync();
+        heap.release(o.arena, o.arena_bytes);
+    }
+
+    // ------------------------------------------------------------ key prefixes
+    const uint8_t *kp_of(const Leaf &l, uint32_t *len) const {
+        const Chunk &c = chunks[l.chunk];
+        *len = c.kp_len[l.idx];
+        return reinterpret_cast<const uint8_t *>(c.kp.data()) + c.kp_off[l.idx];
+    }
+
+    // ------------------------------------------------------------ crit-bit ops
+    struct Best {
+        int32_t grand = -1, pa = -1;
+        int dir = 3;
+        Leaf crit{0, 0};
+    };
+    static Best best_match(const Shard &s, const std::string &q) {
+        Best b;
+        CbtRef p = s.root;
+        while (p.inner >= 0) {
+            const CbtInner &n = s.cbt[(size_t)p.inner];
+            uint8_t byte = q.size() > n.diff_at ? (uint8_t)q[n.diff_at] : 0;
+            b.dir = crit_dir(n.mask, byte);
+            b.grand = b.pa;
+            b.pa = p.inner;
+            p = n.kid[b.dir];
+        }
+        b.crit = p.leaf;
+        return b;
+    }
+
+    // CritBitTree::setitem; q = escaped key incl. 251,0.  Returns 1 on replace.
+    int cbt_insert(Shard &s, const std::string &q, Leaf nl) {
+        CbtRef nref;
+        nref.leaf = nl;
+        if (!s.has_root) {
+            s.has_root = true;
+            s.root = nref;
+            return 0;
+        }
+        Best b = best_match(s, q);
+        uint32_t clen;
+        const uint8_t *crit = kp_of(b.crit, &clen);
+        size_t k = 0;
+        uint16_t diff_at = 0;
+        uint8_t crit_rv = 0, src_rv = 0;
+        bool spec = false;
+        for (;;) {
+            if (k >= clen) break;
+            crit_rv = crit[k];
+            if (k >= q.size()) break;
+            src_rv = (uint8_t)q[k];
+            ++k;
+            if (crit_rv != src_rv) break;
+            if (!spec && crit_rv == kEsc) {
+                spec = true;
+            } else if (spec) {
+                if (crit_rv == kKeyEnd) {
+                    chunks[b.crit.chunk].dead[b.crit.idx] = 1;
+                    if (b.pa < 0) s.root = nref;
+                    else s.cbt[(size_t)b.pa].kid[b.dir] = nref;
+                    return 1;
+                }
+                spec = false;
+            }
+            ++diff_at;
+        }
+        if (spec) return 0;
+        uint8_t mask = crit_rv ^ src_rv;
+        mask |= mask >> 1;
+        mask |= mask >> 2;
+        mask |= mask >> 4;
+        mask = (uint8_t)((mask & ~(mask >> 1)) ^ 0xff);
+        uint8_t at = diff_at < q.size() ? (uint8_t)q[diff_at] : 0;
+        int dir = crit_dir(mask, at);
+        int32_t in;
+        if (!s.cbt_free.empty()) {
+            in = s.cbt_free.back();
+            s.cbt_free.pop_back();
+        } else {
+            s.cbt.emplace_back();
+            in = (int32_t)s.cbt.size() - 1;
+        }
+        s.cbt[(size_t)in].diff_at = diff_at;
+        s.cbt[(size_t)in].mask = mask;
+        s.cbt[(size_t)in].kid[dir] = nref;
+        int32_t parent = -1;
+        int pdir = 0;
+        CbtRef p = s.root;
+        while (p.inner >= 0) {
+            const CbtInner &n = s.cbt[(size_t)p.inner];
+            if (n.diff_at > diff_at || (n.diff_at == diff_at && n.mask > mask)) break;
+            uint8_t byte = q.size() > n.diff_at ? (uint8_t)q[n.diff_at] : 0;
+            pdir = crit_dir(n.mask, byte);
+            parent = p.inner;
+            p = n.kid[pdir];
+        }
+        CbtRef iref;
+        iref.inner = in;
+        if (parent < 0) s.root = iref;
+        else s.cbt[(size_t)parent].kid[pdir] = iref;
+        s.cbt[(size_t)in].kid[1 - dir] = p;
+        return 0;
+    }
+
+    // CritBitTree::getitem's key_eq (PiXiuStr.cpp:129-143)
+    bool cbt_lookup(const Shard &s, const std::string &q, Leaf *out) const {
+        if (!s.has_root) return false;
+        Best b = best_match(s, q);
+        uint32_t clen;
+        const uint8_t *crit = kp_of(b.crit, &clen);
+        bool spec = false;
+        for (size_t k = 0; k < clen && k < q.size() && crit[k] == (uint8_t)q[k]; ++k) {
+            uint8_t v = crit[k];
+            if (!spec && v == kEsc) {
+                spec = true;
+            } else if (spec) {
+                if (v == kKeyEnd) {
+                    *out = b.crit;
+                    return true;
+                }
+                spec = false;
+            }
+        }
+        return false;
+    }
+
+    // CritBitTree::contains (CritBitTree.cpp:154-178): crit stream vs the escaped key bytes
+    bool cbt_contains(const Shard &s, const std::string &q) const {
+        if (!s.has_root) return false;
+        Best b = best_match(s, q);
+        uint32_t clen;
+        const uint8_t *crit = kp_of(b.crit, &clen);
+        bool spec = false;
+        for (size_t k = 0; k < clen && k < q.size() && crit[k] == (uint8_t)q[k]; ++k) {
+            uint8_t v = crit[k];
+            if (!spec && v == kEsc) {
+                spec = true;
+            } else if (spec) {
+                if (v == kKeyEnd) return true;
+                spec = false;
+            }
+        }
+        return false;
+    }
+
+    // CritBitTree::delitem (CritBitTree.cpp:107-152)
+    int cbt_delete(Shard &s, const std::string &q) {
+        if (!s.has_root) return 1;
+        Best b = best_match(s, q);
+        uint32_t clen;
+        const uint8_t *crit = kp_of(b.crit, &clen);
+        bool spec = false;
+        for (size_t k = 0; k < clen && k < q.size() && crit[k] == (uint8_t)q[k]; ++k) {
+            uint8_t v = crit[k];
+            if (!spec && v == kEsc) {
+                spec = true;
+            } else if (spec) {
+                if (v == kKeyEnd) {
+                    if (b.pa < 0) {
+                        s.has_root = false;
+                        s.root = CbtRef{};
+                    } else {
+                        const CbtRef other = s.cbt[(size_t)b.pa].kid[1 - b.dir];
+                        if (b.grand < 0) {
+                            s.root = other;
+                        } else {
+                            CbtInner &g = s.cbt[(size_t)b.grand];
+                            int gd = (g.kid[0].inner == b.pa) ? 0 : 1;
+                            g.kid[gd] = other;
+                        }
+                        s.cbt_free.push_back(b.pa);
+                    }
+                    chunks[b.crit.chunk].dead[b.crit.idx] = 1;
+                    return 0;
+                }
+                spec = false;
+            }
+        }
+        return 1;
+    }
+
+    static std::string esc_key(const uint8_t *k, uint64_t n) {
+        std::string q;
+        q.reserve(n + 2);
+        for (uint64_t i = 0; i < n; ++i) {
+            q.push_back((char)k[i]);
+            if (k[i] == kEsc) q.push_back((char)kEsc);
+        }
+        q.push_back((char)kEsc);
+        q.push_back((char)kKeyEnd);
+        return q;
+    }
+
+    Shard *shard_for_key(const std::string &raw) {
+        if (opts.records_per_shard == 0) return shards.empty() ? nullptr : shards[0].get();
+        auto it = keymap.find(raw);
+        return it == keymap.end() ? nullptr : shards[it->second].get();
+    }
+
+    // ------------------------------------------------------------ decode
+    // Runs decode queries; out_dev is a device buffer.  Returns per-query len/status.
+    void run_decode(const std::vector<DecodeQuery> &q, uint8_t *out_dev, std::vector<uint32_t> &len,
+                    std::vector<uint32_t> &st, bool timed) {
+        uint32_t nq = (uint32_t)q.size();
+        len.assign(nq, 0);
+        st.assign(nq, 0);
+        if (!nq) return;
+        uint32_t depth = opts.decode_depth ? opts.decode_depth : 4096;
+        uint32_t waves = opts.decode_waves ? opts.decode_waves : 4096;
+        waves = std::min(waves, nq);
+        auto *frames = (Frame *)scratch_frames.get((uint64_t)waves * depth * sizeof(Frame));
+        auto *dq = (DecodeQuery *)dq_buf.get((uint64_t)nq * sizeof(DecodeQuery));
+        auto *dl = (uint32_t *)dlen_buf.get((uint64_t)nq * 8);
+        uint32_t *ds = dl + nq;
+        h2d(dq, q.data(), (size_t)nq * sizeof(DecodeQuery));
+        if (timed) hcheck(hipEventRecord(ev0, stream));
+        hcheck(launch_decode(stream, dq, nq, (const RecSlot *const *)chunk_tab, out_dev, dl, ds, frames, depth,
+                             waves));
+        if (timed) hcheck(hipEventRecord(ev1, stream));
+        d2h(len.data(), dl, (size_t)nq * 4);
+        d2h(st.data(), ds, (size_t)nq * 4);
+        sync();
+        if (timed) {
+            float ms = 0;
+            hcheck(hipEventElapsedTime(&ms, ev0, ev1));
+            stats.last_decode_kernel_ms = ms;
+        }
+    }
+
+    int set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, const uint8_t *vals,
+                  const uint64_t *voff, int on_device, px_set_result *res);
+    int expand(const std::vector<DecodeQuery> &q0, uint8_t *out, uint64_t out_cap, int out_on_device,
+               uint64_t *out_off, uint32_t *out_len, uint32_t *status, uint64_t *needed,
+               const std::vector<uint32_t> &pre_status);
+};
+
+namespace {
+px_status map_status(uint32_t s) {
+    switch (s) {
+    case kOk: return PX_OK;
+    case kErrInval: return PX_EINVAL;
+    case kErrCapacity: return PX_ECAPACITY;
+    case kErrRefCrash: return PX_EREFCRASH;
+    case kErrCorrupt: return PX_ECORRUPT;
+    case kErrHang: return PX_EHANG;
+    case kErrDepth: return PX_EDEPTH;
+    case kErrSpace: return PX_ESPACE;
+    default: return PX_ECORRUPT;
+    }
+}
+
+// first spec-aware 251,0 in a decoded stream: returns prefix length incl. it, or 0
+uint32_t key_end(const uint8_t *p, uint32_t n) {
+    bool spec = false;
+    for (uint32_t k = 0; k < n; ++k) {
+        if (!spec && p[k] == kEsc) {
+            spec = true;
+        } else if (spec) {
+            if (p[k] == kKeyEnd) return k + 1;
+            spec = false;
+        }
+    }
+    return 0;
+}
+}  // namespace
+
+int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, const uint8_t *vals,
+                      const uint64_t *voff, int on_device, px_set_result *res) {
+    if (n == 0) return PX_OK;
+    // ---- inputs on device; raw keys also on host (the CritBit needs them)
+    std::vector<uint64_t> hkoff(n + 1), hvoff(n + 1);
+    const uint8_t *dkeys, *dvals;
+    const uint64_t *dkoff, *dvoff;
+    std::vector<uint8_t> hkeys;
+    if (on_device) {
+        d2h(hkoff.data(), koff, (n + 1) * 8);
+        d2h(hvoff.data(), voff, (n + 1) * 8);
+        sync();
+        hkeys.resize(hkoff[n] - hkoff[0]);
+        d2h(hkeys.data(), keys + hkoff[0], hkeys.size());
+        sync();
+        for (auto &o : hkoff) o -= hkoff[0];
+        dkeys = keys;
+        dvals = vals;
+        dkoff = koff;
+        dvoff = voff;
+        // (device koff may not start at 0: the kernels use absolute offsets)
+    } else {
+        memcpy(hkoff.data(), koff, (n + 1) * 8);
+        memcpy(hvoff.data(), voff, (n + 1) * 8);
+        uint64_t kb = koff[n] - koff[0], vb = voff[n] - voff[0];
+        hkeys.assign(keys + koff[0], keys + koff[n]);
+        uint64_t tot = kb + vb + (n + 1) * 16 + 512;
+        auto *b = (uint8_t *)in_buf.get(tot);
+        auto *dk = b;
+        auto *dv = b + round_up(kb, 64);
+        auto *dko = (uint64_t *)(dv + round_up(vb, 64));
+        auto *dvo = dko + (n + 1);
+        h2d(dk, keys + koff[0], kb);
+        h2d(dv, vals + voff[0], vb);
+        std::vector<uint64_t> k0(n + 1), v0(n + 1);
+        for (uint32_t i = 0; i <= n; ++i) {
+            k0[i] = koff[i] - koff[0];
+            v0[i] = voff[i] - voff[0];
+        }
+        h2d(dko, k0.data(), (n + 1) * 8);
+        h2d(dvo, v0.data(), (n + 1) * 8);
+        for (auto &o : hkoff) o -= koff[0];
+        for (auto &o : hvoff) o -= voff[0];
+        dkeys = dk;
+        dvals = dv;
+        dkoff = dko;
+        dvoff = dvo;
+    }
+
+    // ---- pass 1: escaped doc lengths
+    auto *tmp = (uint32_t *)tmp_buf.get((uint64_t)n * 24 + 64);
+    uint32_t *d_doclen = tmp, *d_complen = tmp + n, *d_chunk = tmp + 2 * n, *d_idx = tmp + 3 * n,
+             *d_status = tmp + 4 * n, *d_nseg = tmp + 5 * n;
+    hcheck(launch_doc_len(stream, n, dkeys, dkoff, dvals, dvoff, d_doclen));
+    std::vector<uint32_t> doc_len(n);
+    d2h(doc_len.data(), d_doclen, n * 4);
+    sync();
+
+    // ---- shard assignment: contiguous, in arrival order
+    std::vector<uint32_t> rec_shard(n);
+    struct Work {
+        Shard *s;
+        uint32_t r0, r1;
+        uint64_t bytes;
+        uint32_t docs;
+    };
+    std::vector<Work> work;
+    for (uint32_t r = 0; r < n; ++r) {
+        Shard *s;
+        if (opts.records_per_shard == 0) {
+            s = shards.empty() ? &new_shard() : shards[0].get();
+        } else {
+            s = shards.empty() ? &new_shard() : shards.back().get();
+            if (s->records >= opts.records_per_shard) s = &new_shard();
+        }
+        s->records++;
+        rec_shard[r] = s->id;
+        if (work.empty() || work.back().s != s) work.push_back(Work{s, r, r, 0, 0});
+        work.back().r1 = r + 1;
+        if (doc_len[r] != 0xffffffffu) {
+            work.back().bytes += doc_len[r];
+            work.back().docs++;
+        }
+    }
+
+    // ---- arenas, doc destinations, comp scratch
+    std::vector<uint8_t *> dst(n, nullptr), cdst(n, nullptr);
+    uint64_t scratch_bytes = 0;
+    for (uint32_t r = 0; r < n; ++r)
+        if (doc_len[r] != 0xffffffffu) scratch_bytes += round_up(doc_len[r], 16);
+    auto *comp_scratch = (uint8_t *)heap.alloc(scratch_bytes + 256);
+    uint64_t so = 0;
+    std::vector<GstShard> gs;
+    gs.reserve(work.size());
+    for (auto &w : work) {
+        shard_reserve(*w.s, w.bytes, w.docs);
+        uint64_t t = w.s->text_end;
+        for (uint32_t r = w.r0; r < w.r1; ++r) {
+            if (doc_len[r] == 0xffffffffu) continue;
+            dst[r] = w.s->text + t;
+            t += doc_len[r];
+            cdst[r] = comp_scratch + so;
+            so += round_up(doc_len[r], 16);
+        }
+        w.s->text_end = t;
+        GstShard g{};
+        g.text = w.s->text;
+        g.doc_base = w.s->doc_base;
+        g.nodes = w.s->nodes;
+        g.hash = w.s->hash;
+        g.root_kids = w.s->root_kids;
+        g.st = w.s->st;
+        g.node_cap = w.s->node_cap;
+        g.hash_mask = (uint32_t)(w.s->hash_cap - 1);
+        g.doc_cap = w.s->doc_cap;
+        g.r0 = w.r0;
+        g.r1 = w.r1;
+        gs.push_back(g);
+    }
+    auto *d_dst = (uint8_t **)heap.alloc((uint64_t)n * 8);
+    auto *d_cdst = (uint8_t **)heap.alloc((uint64_t)n * 8);
+    auto *d_gs = (GstShard *)heap.alloc(gs.size() * sizeof(GstShard));
+    h2d(d_dst, dst.data(), (size_t)n * 8);
+    h2d(d_cdst, cdst.data(), (size_t)n * 8);
+    h2d(d_gs, gs.data(), gs.size() * sizeof(GstShard));
+    hcheck(launch_doc_write(stream, n, dkeys, dkoff, dvals, dvoff, d_dst));
+
+    // ---- the GST walk + encoder
+    hcheck(hipEventRecord(ev0, stream));
+    hcheck(launch_gst_encode(stream, d_gs, (uint32_t)gs.size(), d_doclen, d_cdst, d_complen, d_chunk, d_idx,
+                             d_status));
+    hcheck(hipEventRecord(ev1, stream));
+    std::vector<uint32_t> comp_len(n), rchunk(n), ridx(n), rstatus(n);
+    d2h(comp_len.data(), d_complen, n * 4);
+    d2h(rchunk.data(), d_chunk, n * 4);
+    d2h(ridx.data(), d_idx, n * 4);
+    d2h(rstatus.data(), d_status, n * 4);
+    for (auto &w : work) d2h(&w.s->hs, w.s->st, sizeof(ShardState));
+    sync();
+    {
+        float ms = 0;
+        hcheck(hipEventElapsedTime(&ms, ev0, ev1));
+        stats.last_set_kernel_ms = ms;
+    }
+
+    // ---- packed store + segment index
+    std::vector<uint64_t> coff(n + 1, 0), soff(n + 1, 0);
+    for (uint32_t r = 0; r < n; ++r) {
+        bool ok = doc_len[r] != 0xffffffffu && rstatus[r] == kOk;
+        coff[r + 1] = coff[r] + (ok ? round_up(comp_len[r], 8) : 0);
+        soff[r + 1] = soff[r] + (ok ? (uint64_t)(comp_len[r] + 2) * 8 : 0);
+    }
+    auto *store = (uint8_t *)heap.alloc(coff[n] + 64);
+    auto *segs = (uint8_t *)heap.alloc(soff[n] + 64);
+    auto *d_coff = (uint64_t *)heap.alloc((uint64_t)n * 8);
+    h2d(d_coff, coff.data(), (size_t)n * 8);
+    hcheck(launch_compact(stream, n, d_cdst, d_complen, store, d_coff));
+    std::vector<RecSlot> slots(n);
+    std::vector<uint2 *> segp(n);
+    for (uint32_t r = 0; r < n; ++r) {
+        slots[r].comp = store + coff[r];
+        slots[r].seg = (const uint2 *)(segs + soff[r]);
+        slots[r].comp_len = (doc_len[r] != 0xffffffffu && rstatus[r] == kOk) ? comp_len[r] : 0;
+        slots[r].nseg = 0;
+        segp[r] = (uint2 *)(segs + soff[r]);
+    }
+    auto *d_slots = (RecSlot *)heap.alloc((uint64_t)n * sizeof(RecSlot));
+    auto *d_segp = (uint2 **)heap.alloc((uint64_t)n * 8);
+    h2d(d_slots, slots.data(), (size_t)n * sizeof(RecSlot));
+    h2d(d_segp, segp.data(), (size_t)n * 8);
+    std::vector<uint32_t> tstat(n);
+    hcheck(launch_tokenize(stream, n, d_slots, d_segp, d_nseg, d_status));
+    std::vector<uint32_t> nseg(n);
+    d2h(nseg.data(), d_nseg, n * 4);
+    d2h(tstat.data(), d_status, n * 4);
+    sync();
+    heap.release(comp_scratch, scratch_bytes + 256);
+    heap.release(d_dst, (uint64_t)n * 8);
+    heap.release(d_cdst, (uint64_t)n * 8);
+    heap.release(d_gs, gs.size() * sizeof(GstShard));
+    heap.release(d_coff, (uint64_t)n * 8);
+    heap.release(d_slots, (uint64_t)n * sizeof(RecSlot));
+    heap.release(d_segp, (uint64_t)n * 8);
+
+    // ---- register records in their chunks
+    std::vector<uint32_t> rgchunk(n, kNone);
+    for (uint32_t r = 0; r < n; ++r) {
+        if (doc_len[r] == 0xffffffffu) rstatus[r] = kErrInval;
+        if (rstatus[r] != kOk) continue;
+        if (tstat[r] != kOk) {
+            rstatus[r] = tstat[r];
+            continue;
+        }
+        Shard &s = *shards[rec_shard[r]];
+        while (s.chunks.size() <= rchunk[r]) s.chunks.push_back(new_chunk(s.id));
+        uint32_t c = s.chunks[rchunk[r]];
+        Chunk &ch = chunks[c];
+        if (ridx[r] != ch.n) {
+            rstatus[r] = kErrCapacity;  // slot order broken: cannot happen
+            continue;
+        }
+        slots[r].nseg = nseg[r];
+        ch.slots.push_back(slots[r]);
+        ch.doc_len.push_back(doc_len[r]);
+        ch.dead.push_back(0);
+        ch.kp_off.push_back(0);
+        ch.kp_len.push_back(0);
+        ch.n++;
+        rgchunk[r] = c;
+        stats.records++;
+        stats.raw_bytes += (hkoff[r + 1] - hkoff[r]) + (hvoff[r + 1] - hvoff[r]);
+        stats.doc_bytes += doc_len[r];
+        stats.comp_bytes += comp_len[r];
+    }
+    // push new slot entries to the device tables (one copy per touched chunk range)
+    {
+        std::map<uint32_t, std::pair<uint32_t, uint32_t>> touched;  // chunk -> [lo, hi)
+        for (uint32_t r = 0; r < n; ++r) {
+            if (rgchunk[r] == kNone) continue;
+            auto it = touched.find(rgchunk[r]);
+            if (it == touched.end()) touched[rgchunk[r]] = {ridx[r], ridx[r] + 1};
+            else it->second.second = ridx[r] + 1;
+        }
+        for (auto &t : touched) {
+            chunk_reserve(t.first, chunks[t.first].n);
+            Chunk &ch = chunks[t.first];
+            h2d(ch.dev + t.second.first, ch.slots.data() + t.second.first,
+                (size_t)(t.second.second - t.second.first) * sizeof(RecSlot));
+        }
+    }
+
+    // ---- compat key prefixes (GPU decode of each new record's key region)
+    std::vector<DecodeQuery> q;
+    std::vector<uint32_t> qrec;
+    uint64_t qo = 0;
+    for (uint32_t r = 0; r < n; ++r) {
+        if (rgchunk[r] == kNone) continue;
+        uint64_t klen = hkoff[r + 1] - hkoff[r];
+        uint32_t cap = (uint32_t)std::min<uint64_t>(doc_len[r] + 64, 2 * klen + 2 + 64);
+        DecodeQuery d{rgchunk[r], ridx[r], 0, kMaxDoc, qo, cap, 0};
+        q.push_back(d);
+        qrec.push_back(r);
+        qo += round_up(cap, 16);
+    }
+    for (int pass = 0; pass < 2 && !q.empty(); ++pass) {
+        auto *kbuf = (uint8_t *)heap.alloc(qo + 64);
+        std::vector<uint32_t> ql, qs;
+        run_decode(q, kbuf, ql, qs, false);
+        std::vector<uint8_t> hk(qo);
+        d2h(hk.data(), kbuf, qo);
+        sync();
+        heap.release(kbuf, qo + 64);
+        std::vector<DecodeQuery> again;
+        std::vector<uint32_t> again_rec;
+        uint64_t ao = 0;
+        for (size_t i = 0; i < q.size(); ++i) {
+            uint32_t r = qrec[i];
+            const uint8_t *p = hk.data() + q[i].out_off;
+            uint32_t ke = key_end(p, ql[i]);
+            if (qs[i] != kOk && qs[i] != kErrSpace) {
+                rstatus[r] = qs[i];
+                continue;
+            }
+            if (ke == 0 && qs[i] == kErrSpace && pass == 0) {  // decoded key ran past the cap
+                DecodeQuery d = q[i];
+                d.out_off = ao;
+                d.out_cap = doc_len[r] + 256;
+                ao += round_up(d.out_cap, 16);
+                again.push_back(d);
+                again_rec.push_back(r);
+                continue;
+            }
+            uint32_t keep = ke ? ke : ql[i];
+            Chunk &ch = chunks[rgchunk[r]];
+            ch.kp_off[ridx[r]] = ch.kp.size();
+            ch.kp_len[ridx[r]] = keep;
+            ch.kp.append(reinterpret_cast<const char *>(p), keep);
+        }
+        q.swap(again);
+        qrec.swap(again_rec);
+        qo = ao;
+    }
+
+    // ---- CritBit inserts (per shard, in arrival order)
+    std::vector<uint32_t> replaced(n, 0);
+    for (uint32_t r = 0; r < n; ++r) {
+        if (rgchunk[r] == kNone || rstatus[r] != kOk) continue;
+        Shard &s = *shards[rec_shard[r]];
+        const uint8_t *kp = hkeys.data() + hkoff[r];
+        uint64_t klen = hkoff[r + 1] - hkoff[r];
+        std::string q = esc_key(kp, klen);
+        if (opts.records_per_shard != 0) {
+            std::string raw(reinterpret_cast<const char *>(kp), klen);
+            auto it = keymap.find(raw);
+            if (it != keymap.end() && it->second != s.id) {
+                cbt_delete(*shards[it->second], q);  // cross-shard replace
+                replaced[r] = 1;
+            }
+            keymap[raw] = s.id;
+        }
+        replaced[r] |= (uint32_t)cbt_insert(s, q, Leaf{rgchunk[r], ridx[r]});
+    }
+
+    // ---- results
+    int rc = PX_OK;
+    uint64_t ub = 0;
+    for (auto &sp : shards) ub += sp->hs.ub_reads;
+    stats.ub_reads = ub;
+    stats.device_bytes = heap.held();
+    for (uint32_t r = 0; r < n; ++r) {
+        px_status st = map_status(rstatus[r]);
+        if (st != PX_OK && rc == PX_OK) rc = st;
+        if (res) {
+            px_set_result &o = res[r];
+            o.status = st;
+            o.replaced = replaced[r];
+            o.shard = rec_shard[r];
+            o.chunk = rchunk[r];
+            o.idx = ridx[r];
+            o.comp_len = st == PX_OK ? comp_len[r] : 0;
+            o.doc_len = doc_len[r] == 0xffffffffu ? 0 : doc_len[r];
+            o.pad = 0;
+        }
+    }
+    return rc;
+}
+
+int px_ctx::expand(const std::vector<DecodeQuery> &q0, uint8_t *out, uint64_t out_cap, int out_on_device,
+                   uint64_t *out_off, uint32_t *out_len, uint32_t *status, uint64_t *needed,
+                   const std::vector<uint32_t> &pre_status) {
+    const uint32_t n = (uint32_t)q0.size();
+    std::vector<DecodeQuery> q = q0;
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        out_off[i] = total;
+        q[i].out_off = total;
+        if (q[i].chunk != kNone) total += q[i].out_cap;
+    }
+    if (needed) *needed = total;
+    if (total > out_cap) return PX_ESPACE;
+    uint8_t *dout = out;
+    if (!out_on_device) dout = (uint8_t *)in_buf.get(total + 64);
+    std::vector<uint32_t> len, st;
+    run_decode(q, dout, len, st, true);
+    // queries that overran their slot: re-run with the exact size they need
+    bool retry = false;
+    for (uint32_t i = 0; i < n; ++i)
+        if (q[i].chunk != kNone && st[i] == kErrSpace && q[i].out_cap < (uint32_t)kMaxDoc * 4) retry = true;
+    if (retry) {
+        // second pass with 4x room for the overflowing ones (over-yield is bounded)
+        uint64_t t2 = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            if (q[i].chunk != kNone && st[i] == kErrSpace) q[i].out_cap = std::max<uint32_t>(q[i].out_cap * 4, 1024);
+            out_off[i] = t2;
+            q[i].out_off = t2;
+            if (q[i].chunk != kNone) t2 += q[i].out_cap;
+        }
+        if (needed) *needed = t2;
+        if (t2 > out_cap) return PX_ESPACE;
+        if (!out_on_device) dout = (uint8_t *)in_buf.get(t2 + 64);
+        run_decode(q, dout, len, st, true);
+        total = t2;
+    }
+    int rc = PX_OK;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (q[i].chunk == kNone) {
+            out_len[i] = 0;
+            status[i] = pre_status[i];
+            continue;
+        }
+        out_len[i] = len[i];
+        status[i] = map_status(st[i]);
+        if (status[i] != PX_OK && rc == PX_OK) rc = (int)status[i];
+    }
+    if (!out_on_device) {
+        d2h(out, dout, total);
+        sync();
+    }
+    return rc;
+}
+
+// ====================================================================== C ABI
+extern "C" {
+
+px_ctx *px_open(const px_opts *opts) {
+    try {
+        auto *c = new px_ctx();
+        if (opts) c->opts = *opts;
+        hcheck(hipSetDevice(c->opts.device));
+        hcheck(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        hcheck(hipEventCreate(&c->ev0));
+        hcheck(hipEventCreate(&c->ev1));
+        return c;
+    } catch (...) {
+        return nullptr;
+    }
+}
+
+void px_close(px_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char *px_strerror(int s) {
+    switch (s) {
+    case PX_OK: return "ok";
+    case PX_EINVAL: return "invalid argument (empty key or escaped doc > 65535 bytes)";
+    case PX_ECAPACITY: return "internal arena capacity exceeded";
+    case PX_EREFCRASH: return "input on which the reference GST dereferences NULL";
+    case PX_ECORRUPT: return "malformed compressed bytes";
+    case PX_EHANG: return "input on which the reference decoder never terminates";
+    case PX_EDEPTH: return "decode nesting exceeds decode_depth";
+    case PX_ESPACE: return "output buffer too small";
+    case PX_ENOTFOUND: return "key not found";
+    case PX_EHIP: return "HIP runtime error";
+    case PX_ENOMEM: return "device allocation failed";
+    default: return "unknown status";
+    }
+}
+
+#define PX_GUARD(...)                                    \
+    try {                                                \
+        __VA_ARGS__                                      \
+    } catch (const HipFail &f) {                         \
+        ctx->last_hip = (int)f.e;                        \
+        return PX_EHIP;                                  \
+    } catch (const PxFail &f) {                          \
+        return f.code;                                   \
+    } catch (const std::bad_alloc &) {                   \
+        return PX_ENOMEM;                                \
+    }
+
+int px_set_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff, const uint8_t *vals,
+                 const uint64_t *voff, int on_device, px_set_result *res) {
+    if (!ctx || (n && (!keys || !koff || !voff))) return PX_EINVAL;
+    PX_GUARD(return ctx->set_batch(n, keys, koff, vals, voff, on_device, res);)
+}
+
+int px_get_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff, int mode, uint8_t *out,
+                 uint64_t out_cap, int out_on_device, uint64_t *out_off, uint32_t *out_len, uint32_t *status,
+                 uint64_t *needed) {
+    if (!ctx || (n && (!keys || !koff || !out_off || !out_len || !status))) return PX_EINVAL;
+    PX_GUARD({
+        std::vector<DecodeQuery> q(n);
+        std::vector<uint32_t> pre(n, PX_OK);
+        for (uint32_t i = 0; i < n; ++i) {
+            std::string raw(reinterpret_cast<const char *>(keys + koff[i]), koff[i + 1] - koff[i]);
+            std::string ek = px_ctx::esc_key(keys + koff[i], koff[i + 1] - koff[i]);
+            Shard *s = ctx->shard_for_key(raw);
+            Leaf l;
+            q[i] = DecodeQuery{kNone, 0, 0, kMaxDoc, 0, 0, (uint32_t)mode};
+            if (!s || !ctx->cbt_lookup(*s, ek, &l)) {
+                pre[i] = PX_ENOTFOUND;
+                continue;
+            }
+            q[i].chunk = l.chunk;
+            q[i].idx = l.idx;
+            q[i].out_cap = (uint32_t)round_up(ctx->chunks[l.chunk].doc_len[l.idx] + 64, 16);
+        }
+        int rc = ctx->expand(q, out, out_cap, out_on_device, out_off, out_len, status, needed, pre);
+        if (rc == PX_OK)
+            for (uint32_t i = 0; i < n; ++i)
+                if (status[i] != PX_OK) {
+                    rc = (int)status[i];
+                    break;
+                }
+        return rc;
+    })
+}
+
+int px_parse_batch(px_ctx *ctx, uint32_t n, const px_rec *recs, int mode, uint8_t *out, uint64_t out_cap,
+                   int out_on_device, uint64_t *out_off, uint32_t *out_len, uint32_t *status, uint64_t *needed) {
+    if (!ctx || (n && (!recs || !out_off || !out_len || !status))) return PX_EINVAL;
+    PX_GUARD({
+        std::vector<DecodeQuery> q(n);
+        std::vector<uint32_t> pre(n, PX_OK);
+        for (uint32_t i = 0; i < n; ++i) {
+            const px_rec &r = recs[i];
+            q[i] = DecodeQuery{kNone, 0, r.from, r.to, 0, 0, (uint32_t)mode};
+            if (r.shard >= ctx->shards.size() || r.chunk >= ctx->shards[r.shard]->chunks.size() ||
+                r.from < 0 || r.to < r.from) {
+                pre[i] = PX_EINVAL;
+                continue;
+            }
+            uint32_t c = ctx->shards[r.shard]->chunks[r.chunk];
+            if (r.idx >= ctx->chunks[c].n) {
+                pre[i] = PX_EINVAL;
+                continue;
+            }
+            q[i].chunk = c;
+            q[i].idx = r.idx;
+            uint64_t span = std::min<uint64_t>((uint64_t)(r.to - r.from), ctx->chunks[c].doc_len[r.idx]);
+            q[i].out_cap = (uint32_t)round_up(span + 64, 16);
+        }
+        return ctx->expand(q, out, out_cap, out_on_device, out_off, out_len, status, needed, pre);
+    })
+}
+
+int px_contains_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff, uint32_t *result) {
+    if (!ctx || (n && (!keys || !koff || !result))) return PX_EINVAL;
+    PX_GUARD({
+        for (uint32_t i = 0; i < n; ++i) {
+            std::string raw(reinterpret_cast<const char *>(keys + koff[i]), koff[i + 1] - koff[i]);
+            Shard *s = ctx->shard_for_key(raw);
+            result[i] = s && ctx->cbt_contains(*s, px_ctx::esc_key(keys + koff[i], koff[i + 1] - koff[i]));
+        }
+        return PX_OK;
+    })
+}
+
+int px_del_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff, uint32_t *result) {
+    if (!ctx || (n && (!keys || !koff || !result))) return PX_EINVAL;
+    PX_GUARD({
+        for (uint32_t i = 0; i < n; ++i) {
+            std::string raw(reinterpret_cast<const char *>(keys + koff[i]), koff[i + 1] - koff[i]);
+            Shard *s = ctx->shard_for_key(raw);
+            result[i] = s ? (uint32_t)ctx->cbt_delete(*s, px_ctx::esc_key(keys + koff[i], koff[i + 1] - koff[i])) : 1u;
+        }
+        return PX_OK;
+    })
+}
+
+int px_export(px_ctx *ctx, uint32_t n, const px_rec *recs, uint8_t *out, uint64_t out_cap, uint64_t *out_off) {
+    if (!ctx || (n && (!recs || !out_off))) return PX_EINVAL;
+    PX_GUARD({
+        out_off[0] = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            const px_rec &r = recs[i];
+            if (r.shard >= ctx->shards.size() || r.chunk >= ctx->shards[r.shard]->chunks.size()) return PX_EINVAL;
+            const Chunk &ch = ctx->chunks[ctx->shards[r.shard]->chunks[r.chunk]];
+            if (r.idx >= ch.n) return PX_EINVAL;
+            const RecSlot &sl = ch.slots[r.idx];
+            if (out_off[i] + sl.comp_len > out_cap) return PX_ESPACE;
+            ctx->d2h(out + out_off[i], sl.comp, sl.comp_len);
+            out_off[i + 1] = out_off[i] + sl.comp_len;
+        }
+        ctx->sync();
+        return PX_OK;
+    })
+}
+
+int px_stats_get(px_ctx *ctx, px_stats *st) {
+    if (!ctx || !st) return PX_EINVAL;
+    *st = ctx->stats;
+    st->device_bytes = ctx->heap.held();
+    return PX_OK;
+}
+
+void *px_stream(px_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+}  // extern "C"

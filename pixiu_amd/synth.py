@@ -1,0 +1,262 @@
+"""Deterministic synthetic corpora for the five BASELINE.json configs.
+
+SURVEY.md §8(d) specifies the shapes; every generator draws from a counter-based
+splitmix64 stream seeded with ``0x5049585500 + config`` so the same corpus is
+rebuilt bit-for-bit on any host (no datasets travel; there is no network).
+
+A corpus is a CSR pair of byte buffers: ``keys[koff[i]:koff[i+1]]`` and
+``vals[voff[i]:voff[i+1]]`` for record ``i``.
+"""
+from __future__ import annotations
+
+import dataclasses
+import functools
+
+import numpy as np
+
+GAMMA = np.uint64(0x9E3779B97F4A7C15)
+_M1 = np.uint64(0xBF58476D1CE4E5B9)
+_M2 = np.uint64(0x94D049BB133111EB)
+SEED_BASE = 0x5049585500
+
+# 40-token HTML/URL vocabulary (visible ASCII only: the README corpus had its
+# invisible characters stripped, README.md:51).
+VOCAB = [
+    "<div", "</div>", "<a", "href=", '"http://', "www.", ".com/", "class=", '"nav"',
+    "<span>", "</span>", "<li>", "</li>", "<ul>", "</ul>", "<p>", "</p>", "<img",
+    "src=", '.jpg"', "/>", "<script", "</script>", "var", "function(){", "return",
+    "question/", "zhihu", "qq", "news", "index", ".htm", "title", "content", "&amp;",
+    "id=", "?", "=", ";", "{",
+]
+
+
+def splitmix64(seed: int, n: int, start: int = 0) -> np.ndarray:
+    """n outputs of splitmix64 at counter positions start+1 .. start+n."""
+    with np.errstate(over="ignore"):
+        x = np.uint64(seed & 0xFFFFFFFFFFFFFFFF) + (
+            np.arange(start + 1, start + n + 1, dtype=np.uint64) * GAMMA)
+        z = (x ^ (x >> np.uint64(30))) * _M1
+        z = (z ^ (z >> np.uint64(27))) * _M2
+        return z ^ (z >> np.uint64(31))
+
+
+class Stream:
+    """Sequential view of one splitmix64 stream."""
+
+    def __init__(self, config: int, tag: int):
+        self.seed = (SEED_BASE + config + tag * 0x1_0000_0000_0000) & 0xFFFFFFFFFFFFFFFF
+        self.pos = 0
+
+    def u64(self, n: int) -> np.ndarray:
+        out = splitmix64(self.seed, n, self.pos)
+        self.pos += n
+        return out
+
+    def uniform(self, n: int) -> np.ndarray:
+        return (self.u64(n) >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
+
+    def randint(self, lo: int, hi: int, n: int) -> np.ndarray:
+        """integers in [lo, hi)"""
+        return (lo + (self.u64(n) % np.uint64(hi - lo))).astype(np.int64)
+
+
+@dataclasses.dataclass
+class Corpus:
+    config: int
+    keys: np.ndarray  # uint8
+    koff: np.ndarray  # int64, n+1
+    vals: np.ndarray  # uint8
+    voff: np.ndarray  # int64, n+1
+
+    @property
+    def n(self) -> int:
+        return len(self.koff) - 1
+
+    def key(self, i: int) -> bytes:
+        return self.keys[self.koff[i]:self.koff[i + 1]].tobytes()
+
+    def val(self, i: int) -> bytes:
+        return self.vals[self.voff[i]:self.voff[i + 1]].tobytes()
+
+    @property
+    def raw_bytes(self) -> int:
+        return int(self.koff[-1] + self.voff[-1])
+
+    def slice(self, a: int, b: int) -> "Corpus":
+        return Corpus(self.config,
+                      self.keys[self.koff[a]:self.koff[b]], self.koff[a:b + 1] - self.koff[a],
+                      self.vals[self.voff[a]:self.voff[b]], self.voff[a:b + 1] - self.voff[a])
+
+
+def _csr(parts: list) -> tuple:
+    lens = np.fromiter((len(p) for p in parts), dtype=np.int64, count=len(parts))
+    off = np.zeros(len(parts) + 1, np.int64)
+    np.cumsum(lens, out=off[1:])
+    buf = np.frombuffer(b"".join(parts), dtype=np.uint8).copy() if parts else np.zeros(0, np.uint8)
+    return buf, off
+
+
+class _TokenTable:
+    """Concatenated token bytes with offsets, for vectorised token -> byte expansion."""
+
+    def __init__(self, tokens: list):
+        enc = [t.encode() if isinstance(t, str) else t for t in tokens]
+        self.lens = np.array([len(t) for t in enc], np.int64)
+        self.offs = np.zeros(len(enc), np.int64)
+        np.cumsum(self.lens[:-1], out=self.offs[1:])
+        self.blob = np.frombuffer(b"".join(enc), np.uint8)
+
+    def expand(self, ids: np.ndarray) -> np.ndarray:
+        lens = self.lens[ids]
+        total = int(lens.sum())
+        starts = np.zeros(len(ids), np.int64)
+        np.cumsum(lens[:-1], out=starts[1:])
+        idx = np.arange(total, dtype=np.int64) + np.repeat(self.offs[ids] - starts, lens)
+        return self.blob[idx]
+
+
+_VOCAB = _TokenTable(VOCAB)
+
+
+@functools.lru_cache(maxsize=None)
+def _numbers(hi: int) -> _TokenTable:
+    return _TokenTable([str(i) for i in range(hi)])
+
+
+def _zipf_ids(st: Stream, n: int, k: int) -> np.ndarray:
+    w = 1.0 / np.arange(1, k + 1)
+    cdf = np.cumsum(w) / w.sum()
+    return np.searchsorted(cdf, st.uniform(n), side="right").clip(0, k - 1)
+
+
+def _soup(st: Stream, nbytes: int, num_hi: int, num_frac: float) -> np.ndarray:
+    """>= nbytes of vocabulary tokens (Zipf-ish) mixed with decimal numbers."""
+    out = []
+    have = 0
+    nums = _numbers(num_hi) if num_hi <= 100_000 else None
+    while have < nbytes:
+        m = max(64, (nbytes - have) // 4)
+        is_num = st.uniform(m) < num_frac
+        vid = _zipf_ids(st, m, len(VOCAB))
+        nid = st.randint(0, num_hi, m)
+        a = _VOCAB.expand(vid[~is_num])
+        b = nums.expand(nid[is_num])
+        # interleave in order: expand each class then merge by token position
+        lv = _VOCAB.lens[vid]
+        ln = nums.lens[nid]
+        tl = np.where(is_num, ln, lv)
+        pos = np.zeros(m, np.int64)
+        np.cumsum(tl[:-1], out=pos[1:])
+        buf = np.empty(int(tl.sum()), np.uint8)
+        ia = np.repeat(pos[~is_num], lv[~is_num]) + (np.arange(len(a)) - np.repeat(
+            np.concatenate([[0], np.cumsum(lv[~is_num])[:-1]]), lv[~is_num]))
+        ib = np.repeat(pos[is_num], ln[is_num]) + (np.arange(len(b)) - np.repeat(
+            np.concatenate([[0], np.cumsum(ln[is_num])[:-1]]), ln[is_num]))
+        buf[ia] = a
+        buf[ib] = b
+        out.append(buf)
+        have += len(buf)
+    return np.concatenate(out)[:nbytes]
+
+
+def config1(n: int = 1000) -> Corpus:
+    st = Stream(1, 0)
+    ids = st.randint(0, 100_000_000, n)
+    keys = [b"http://www.zhihu.com/question/%08d_%d" % (int(ids[i]), i) for i in range(n)]
+    lens = st.randint(60, 80, n)
+    vals = []
+    for i in range(n):
+        body = _soup(st, int(lens[i]), 1000, 0.2)
+        vals.append(b"::" + body.tobytes())
+    kb, ko = _csr(keys)
+    vb, vo = _csr(vals)
+    return Corpus(1, kb, ko, vb, vo)
+
+
+def config2(n: int = 100_000) -> Corpus:
+    st = Stream(2, 0)
+    keys = [b"rec/%08d" % i for i in range(n)]
+    soup = _soup(st, 1000 * n, 1000, 0.2)
+    kb, ko = _csr(keys)
+    vo = np.arange(n + 1, dtype=np.int64) * 1000
+    return Corpus(2, kb, ko, soup, vo)
+
+
+def _templates() -> list:
+    st = Stream(3, 99)
+    return [_soup(st, 8192, 100_000, 0.1) for _ in range(16)]
+
+
+def config3(n: int = 10_000, value_len: int = 60_000) -> Corpus:
+    """HTML-shape pages: a fixed 8 KB boilerplate (one of 16) + tag/word soup + ids."""
+    st = Stream(3, 0)
+    tmpl = _templates()
+    mmdd = st.randint(0, 365, n)
+    tid = st.randint(0, 16, n)
+    keys = []
+    for i in range(n):
+        d = int(mmdd[i])
+        keys.append(b"http://www.qq.com/a/2017%02d%02d/%06d.htm" % (d // 31 + 1, d % 31 + 1, i))
+    vals = np.empty(n * value_len, np.uint8)
+    soup_len = value_len - 8192
+    block = 256
+    for a in range(0, n, block):
+        b = min(n, a + block)
+        soup = _soup(st, soup_len * (b - a), 100_000, 0.1)
+        for i in range(a, b):
+            o = i * value_len
+            vals[o:o + 8192] = tmpl[int(tid[i])]
+            s = (i - a) * soup_len
+            vals[o + 8192:o + value_len] = soup[s:s + soup_len]
+    kb, ko = _csr(keys)
+    vo = np.arange(n + 1, dtype=np.int64) * value_len
+    return Corpus(3, kb, ko, vals, vo)
+
+
+def config4(n: int = 1_000_000, rec_len: int = 256) -> Corpus:
+    st = Stream(4, 0)
+    keys = [b"k%07d" % i for i in range(n)]
+    kb, ko = _csr(keys)
+    vlen = rec_len - 8
+    u = st.uniform(n * vlen)
+    letters = (ord("A") + st.randint(0, 16, n * vlen)).astype(np.uint8)
+    vals = np.where(u < 0.10, np.uint8(251), letters).astype(np.uint8)
+    vo = np.arange(n + 1, dtype=np.int64) * vlen
+    return Corpus(4, kb, ko, vals, vo)
+
+
+def config5(n: int = 10_000, total: int = 65_531) -> Corpus:
+    """Max-size binary records (no byte 251) with planted repeats of earlier records."""
+    st = Stream(5, 0)
+    keys = [b"bin%07d" % i for i in range(n)]
+    kb, ko = _csr(keys)
+    vlen = total - 10
+    vals = np.empty(n * vlen, np.uint8)
+    for i in range(n):
+        o = i * vlen
+        p = 0
+        while p < vlen:
+            r = st.u64(4)
+            if i > 0 and (int(r[0]) >> 11) * (1.0 / (1 << 53)) < 0.25:
+                ln = 32 + int(r[1] % np.uint64(2017))
+                ln = min(ln, vlen - p)
+                j = i - 1 - int(r[2] % np.uint64(min(64, i)))
+                s = int(r[3] % np.uint64(vlen - ln + 1))
+                vals[o + p:o + p + ln] = vals[j * vlen + s:j * vlen + s + ln]
+            else:
+                ln = 256 + int(r[1] % np.uint64(1793))
+                ln = min(ln, vlen - p)
+                b = (st.u64(ln) % np.uint64(255)).astype(np.uint8)
+                b[b >= 251] += 1  # U(0..255) minus {251}
+                vals[o + p:o + p + ln] = b
+            p += ln
+    vo = np.arange(n + 1, dtype=np.int64) * vlen
+    return Corpus(5, kb, ko, vals, vo)
+
+
+GENERATORS = {1: config1, 2: config2, 3: config3, 4: config4, 5: config5}
+FULL_SIZES = {1: 1000, 2: 100_000, 3: 10_000, 4: 1_000_000, 5: 10_000}
+
+
+def make(config: int, n: int | None = None) -> Corpus:
+    return GENERATORS[config](FULL_SIZES[config] if n is None else n)
