@@ -356,6 +356,13 @@ class Gst {
 
     // s_insert_char (SuffixTree.cpp:144-289)
     void step(uint8_t c) {
+        if (g_trace_on) {  // debugging aid: state at each doc position
+            trace(-100 - (int)counter_, (int)act_node_, act_doc_);
+            trace(act_direct_, act_off_, (uint8_t)0);
+            g_trace.back() = remainder_;
+            trace((int)nodes_.size(), pools_, (uint8_t)0);
+            g_trace.back() = used_;
+        }
         ++remainder_;
         if (act_node_ == kRoot && act_off_ == 0) {
             at_root(c, true);

@@ -32,7 +32,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def lib_path() -> str:
-    return os.path.join(_HERE, "libpixiu_amd.so")
+    # PIXIU_AMD_LIB selects a debug build (e.g. libpixiu_amd_trace.so) for tools/
+    return os.environ.get("PIXIU_AMD_LIB") or os.path.join(_HERE, "libpixiu_amd.so")
 
 
 class PxError(RuntimeError):

@@ -25,6 +25,35 @@ using namespace px;
 namespace {
 
 PX_DEV uint32_t lane_id() { return threadIdx.x & 63u; }
+
+#ifdef PX_TRACE
+// debug build only: per-byte encoder message log (cmd, pos, byte) of shard 0
+constexpr uint32_t kTraceCap = 1u << 22;
+__device__ int32_t g_trace[kTraceCap];
+__device__ uint32_t g_trace_n;
+#define PX_TRACE_MSG(cmd, pos, val)                                         \
+    do {                                                                    \
+        if (blockIdx.x == 0 && lane_id() == 0 && g_trace_n + 3 < kTraceCap) { \
+            g_trace[g_trace_n] = (int32_t)(cmd);                            \
+            g_trace[g_trace_n + 1] = (int32_t)(pos);                        \
+            g_trace[g_trace_n + 2] = (int32_t)(val);                        \
+            g_trace_n += 3;                                                 \
+        }                                                                   \
+    } while (0)
+#define PX_TRACE_STATE(k)                                                                     \
+    do {                                                                                        \
+        PX_TRACE_MSG(-100 - (int32_t)(counter + (k)), act_node, act_doc);                       \
+        PX_TRACE_MSG(act_direct, act_off + (k), remainder + (int32_t)(k));                      \
+        PX_TRACE_MSG(n_nodes, pools, used);                                                     \
+    } while (0)
+#else
+#define PX_TRACE_STATE(k) \
+    do {                  \
+    } while (0)
+#define PX_TRACE_MSG(cmd, pos, val) \
+    do {                            \
+    } while (0)
+#endif
 PX_DEV uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 PX_DEV int32_t unii(int32_t v) { return (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)v); }
 PX_DEV uint64_t uni64(uint64_t v) {
@@ -158,8 +187,16 @@ struct GstWave {
         e.flags = uni(v.w) >> 16;
         return e;
     }
-    PX_DEV void store(const Edge &e) {
+    PX_DEV void store(const Edge &e) {  // whole node: only for a node just created
         nodes[e.id] = make_uint4(e.link, e.abs, e.doc | (e.from << 16), e.to | (e.flags << 16));
+    }
+    // label and flags of an existing node.  Never the suffix link: a cached Edge may
+    // hold a stale link (set_link on the same node after it was loaded).
+    PX_DEV void store_label(const Edge &e) {
+        uint32_t *w = reinterpret_cast<uint32_t *>(&nodes[e.id]);
+        w[1] = e.abs;
+        w[2] = e.doc | (e.from << 16);
+        w[3] = e.to | (e.flags << 16);
     }
     PX_DEV void set_link(uint32_t id, uint32_t link) { nodes[id].x = link; }
     PX_DEV uint32_t flags_of(uint32_t id) const { return uni(nodes[id].w) >> 16; }
@@ -347,6 +384,10 @@ struct GstWave {
     }
     // one message for doc byte `b` (2-message 251 look-ahead, PiXiuStr.cpp:33-54)
     PX_DEV void feed(bool is_c, uint32_t idx, uint32_t pos, uint32_t b) {
+        PX_TRACE_MSG(is_c ? (int32_t)idx : -3, is_c ? pos : 0, b);
+        feed_nt(is_c, idx, pos, b);
+    }
+    PX_DEV void feed_nt(bool is_c, uint32_t idx, uint32_t pos, uint32_t b) {
         if (held) {
             held = 0;
             if (h_c && is_c) {
@@ -369,9 +410,12 @@ struct GstWave {
     }
     // m (<= 64) consecutive COMPRESS messages (idx, pos0 + k); m251 = bit k set iff byte k is 251
     PX_DEV void feed_bulk(uint32_t idx, uint32_t pos0, uint32_t m, uint64_t m251) {
+#ifdef PX_TRACE
+        for (uint32_t t = 0; t < m; ++t) PX_TRACE_MSG(idx, pos0 + t, ((m251 >> t) & 1) ? 251 : -1);
+#endif
         uint32_t k = 0;
         if (held) {
-            feed(true, idx, pos0, (m251 & 1) ? kEsc : 0);
+            feed_nt(true, idx, pos0, (m251 & 1) ? kEsc : 0);
             k = 1;
         }
         if (k >= m) return;
@@ -449,7 +493,7 @@ struct GstWave {
             set_child(act_node, tbyte(in.abs), in.id);  // replaces e under its first byte
             e.from = in.to;
             e.abs += act_off;
-            store(e);
+            store_label(e);
             set_child(in.id, tbyte(e.abs), e.id);
             set_child(in.id, tbyte(leaf.abs), leaf.id);
         } else {
@@ -458,7 +502,7 @@ struct GstWave {
             set_child(e.id, tbyte(leaf.abs), leaf.id);
             if (!(e.flags & kFlagKids)) {
                 e.flags |= kFlagKids;
-                store(e);
+                store_label(e);
             }
         }
         return true;
@@ -506,6 +550,7 @@ struct GstWave {
         uint32_t i = 0;
         while (i < len && status == kOk) {
             const uint32_t c = tbyte(cur_base + i);
+            PX_TRACE_STATE(0);
             if (act_node == kRoot && act_off == 0) {
                 ++remainder;
                 at_root(c, true);
@@ -542,6 +587,9 @@ struct GstWave {
                 }
             } else if (e.from + act_off < e.to) {
                 uint32_t m = fast_forward(e, i);
+#ifdef PX_TRACE
+                for (uint32_t k = 1; k < m; ++k) PX_TRACE_STATE(k);
+#endif
                 if (m) {
                     remainder += (int32_t)m;
                     act_off = (act_off + m) & 0xffffu;
@@ -1059,6 +1107,22 @@ hipError_t launch_decode(hipStream_t s, const DecodeQuery *qs, uint32_t nq, cons
     if (!nq) return hipSuccess;
     k_decode<<<n_waves, 64, 0, s>>>(qs, nq, chunk_slots, out, out_len, status, scratch, depth_cap);
     return hipGetLastError();
+}
+
+int debug_trace_take(int32_t *out, uint32_t cap) {
+#ifdef PX_TRACE
+    uint32_t n = 0;
+    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_trace_n), 4) != hipSuccess) return -1;
+    n = n < cap ? n : cap;
+    if (n && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trace), (size_t)n * 4) != hipSuccess) return -1;
+    uint32_t z = 0;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_trace_n), &z, 4);
+    return (int)(n / 3);
+#else
+    (void)out;
+    (void)cap;
+    return -1;
+#endif
 }
 
 hipError_t launch_rehash(hipStream_t s, const uint64_t *old_tab, uint32_t old_cap, uint32_t epoch,

@@ -33,6 +33,7 @@ hipError_t launch_tokenize(hipStream_t, uint32_t, const RecSlot *, uint2 *const 
 hipError_t launch_decode(hipStream_t, const DecodeQuery *, uint32_t, const RecSlot *const *, uint8_t *,
                          uint32_t *, uint32_t *, Frame *, uint32_t, uint32_t);
 hipError_t launch_rehash(hipStream_t, const uint64_t *, uint32_t, uint32_t, uint64_t *, uint32_t);
+int debug_trace_take(int32_t *, uint32_t);
 }  // namespace px
 
 using namespace px;
@@ -1129,5 +1130,8 @@ int px_stats_get(px_ctx *ctx, px_stats *st) {
 }
 
 void *px_stream(px_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+// debug builds (make trace): per-byte encoder messages of the first shard of the last batch
+int px_debug_trace_take(int32_t *out, uint32_t cap) { return px::debug_trace_take(out, cap); }
 
 }  // extern "C"
