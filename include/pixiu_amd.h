@@ -126,6 +126,15 @@ int px_export(px_ctx *ctx, uint32_t n, const px_rec *recs, uint8_t *out, uint64_
 
 int px_stats_get(px_ctx *ctx, px_stats *st);
 
+/* The packed compressed bytes of the last px_set_batch (records in batch order, each
+ * padded to 8 B): the blob multi-GPU runs gather to rank 0 over RCCL.  dst may be
+ * NULL to query *bytes. */
+int px_last_store(px_ctx *ctx, uint8_t *dst, uint64_t cap, int dst_on_device, uint64_t *bytes);
+
+/* Drop every stored record (PiXiuCtrl::free_prop + init_prop, PiXiuCtrl.cpp:77-86) while
+ * keeping the context's device memory for reuse. */
+int px_reset(px_ctx *ctx);
+
 /* HIP stream the context runs on (a hipStream_t), for callers that order their
  * own work against it. */
 void *px_stream(px_ctx *ctx);

@@ -71,7 +71,8 @@ REC_DTYPE = np.dtype([("shard", "<u4"), ("chunk", "<u4"), ("idx", "<u4"), ("from
 
 # every symbol include/pixiu_amd.h declares
 EXPORTS = ["px_open", "px_close", "px_strerror", "px_set_batch", "px_get_batch", "px_parse_batch",
-           "px_contains_batch", "px_del_batch", "px_export", "px_stats_get", "px_stream"]
+           "px_contains_batch", "px_del_batch", "px_export", "px_stats_get", "px_stream", "px_reset",
+           "px_last_store"]
 
 _LIB = None
 
@@ -100,6 +101,8 @@ def load_library() -> C.CDLL:
     lib.px_stats_get.argtypes = [vp, C.POINTER(PxStats)]
     lib.px_stream.restype = vp
     lib.px_stream.argtypes = [vp]
+    lib.px_reset.argtypes = [vp]
+    lib.px_last_store.argtypes = [vp, vp, u64, i32, vp]
     _LIB = lib
     return lib
 
@@ -257,6 +260,24 @@ class Store:
         if rc != PX_OK:
             raise PxError(rc, "px_export")
         return [out[int(off[i]):int(off[i + 1])].tobytes() for i in range(n)]
+
+    def reset(self):
+        """Drop all records, keep device memory (free_prop + init_prop)."""
+        rc = self._lib.px_reset(self._h)
+        if rc != PX_OK:
+            raise PxError(rc, "px_reset")
+
+    def last_store_bytes(self) -> int:
+        b = np.zeros(1, np.uint64)
+        self._lib.px_last_store(self._h, None, 0, 0, _ptr(b))
+        return int(b[0])
+
+    def copy_last_store(self, dst_ptr: int, cap: int, on_device: bool = True) -> int:
+        b = np.zeros(1, np.uint64)
+        rc = self._lib.px_last_store(self._h, dst_ptr, cap, int(on_device), _ptr(b))
+        if rc != PX_OK:
+            raise PxError(rc, "px_last_store")
+        return int(b[0])
 
     def stats(self) -> dict:
         s = PxStats()

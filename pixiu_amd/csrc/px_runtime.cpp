@@ -189,6 +189,9 @@ struct px_ctx {
     RecSlot **chunk_tab = nullptr;  // device: chunk id -> slot table
     uint32_t chunk_tab_cap = 0;
     std::unordered_map<std::string, uint32_t> keymap;  // raw key -> shard (multi-shard only)
+    std::vector<std::pair<void *, uint64_t>> store_blocks;  // packed record stores + segment indexes
+    uint8_t *last_store = nullptr;  // packed compressed bytes of the last set batch
+    uint64_t last_store_bytes = 0;
     DevBuf scratch_frames, dq_buf, dstat_buf, dlen_buf, in_buf, tmp_buf;
     px_stats stats{};
     int last_hip = 0;
@@ -540,6 +543,25 @@ struct px_ctx {
         }
     }
 
+    // drop every record, keep the device memory for reuse
+    void reset() {
+        sync();
+        for (auto &sp : shards)
+            if (sp->arena) heap.release(sp->arena, sp->arena_bytes);
+        for (auto &c : chunks)
+            if (c.dev) heap.release(c.dev, (uint64_t)c.dev_cap * sizeof(RecSlot));
+        for (auto &b : store_blocks) heap.release(b.first, b.second);
+        store_blocks.clear();
+        last_store = nullptr;
+        last_store_bytes = 0;
+        shards.clear();
+        chunks.clear();
+        keymap.clear();
+        uint64_t held = heap.held();
+        stats = px_stats{};
+        stats.device_bytes = held;
+    }
+
     int set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, const uint8_t *vals,
                   const uint64_t *voff, int on_device, px_set_result *res);
     int expand(const std::vector<DecodeQuery> &q0, uint8_t *out, uint64_t out_cap, int out_on_device,
@@ -731,6 +753,10 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     }
     auto *store = (uint8_t *)heap.alloc(coff[n] + 64);
     auto *segs = (uint8_t *)heap.alloc(soff[n] + 64);
+    store_blocks.emplace_back(store, coff[n] + 64);
+    last_store = store;
+    last_store_bytes = coff[n];
+    store_blocks.emplace_back(segs, soff[n] + 64);
     auto *d_coff = (uint64_t *)heap.alloc((uint64_t)n * 8);
     h2d(d_coff, coff.data(), (size_t)n * 8);
     hcheck(launch_compact(stream, n, d_cdst, d_complen, store, d_coff));
@@ -1120,6 +1146,25 @@ int px_export(px_ctx *ctx, uint32_t n, const px_rec *recs, uint8_t *out, uint64_
         ctx->sync();
         return PX_OK;
     })
+}
+
+int px_last_store(px_ctx *ctx, uint8_t *dst, uint64_t cap, int dst_on_device, uint64_t *bytes) {
+    if (!ctx) return PX_EINVAL;
+    PX_GUARD({
+        if (bytes) *bytes = ctx->last_store_bytes;
+        if (!dst) return PX_OK;
+        if (cap < ctx->last_store_bytes) return PX_ESPACE;
+        if (ctx->last_store_bytes)
+            hcheck(hipMemcpyAsync(dst, ctx->last_store, ctx->last_store_bytes,
+                                  dst_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, ctx->stream));
+        ctx->sync();
+        return PX_OK;
+    })
+}
+
+int px_reset(px_ctx *ctx) {
+    if (!ctx) return PX_EINVAL;
+    PX_GUARD(ctx->reset(); return PX_OK;)
 }
 
 int px_stats_get(px_ctx *ctx, px_stats *st) {

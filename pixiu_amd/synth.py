@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import dataclasses
 import functools
+import os
 
 import numpy as np
 
@@ -129,31 +130,31 @@ def _zipf_ids(st: Stream, n: int, k: int) -> np.ndarray:
     return np.searchsorted(cdf, st.uniform(n), side="right").clip(0, k - 1)
 
 
+@functools.lru_cache(maxsize=None)
+def _mixed_table(num_hi: int) -> tuple:
+    """Vocabulary tokens then decimal numbers 0..num_hi-1, padded to a 2-D table."""
+    toks = [t.encode() for t in VOCAB] + [str(i).encode() for i in range(num_hi)]
+    width = max(len(t) for t in toks)
+    tab = np.zeros((len(toks), width), np.uint8)
+    lens = np.array([len(t) for t in toks], np.int64)
+    for i, t in enumerate(toks):
+        tab[i, :len(t)] = np.frombuffer(t, np.uint8)
+    mask = np.arange(width)[None, :] < lens[:, None]
+    return tab, mask, lens
+
+
 def _soup(st: Stream, nbytes: int, num_hi: int, num_frac: float) -> np.ndarray:
     """>= nbytes of vocabulary tokens (Zipf-ish) mixed with decimal numbers."""
+    tab, mask, lens = _mixed_table(num_hi)
     out = []
     have = 0
-    nums = _numbers(num_hi) if num_hi <= 100_000 else None
     while have < nbytes:
         m = max(64, (nbytes - have) // 4)
         is_num = st.uniform(m) < num_frac
         vid = _zipf_ids(st, m, len(VOCAB))
         nid = st.randint(0, num_hi, m)
-        a = _VOCAB.expand(vid[~is_num])
-        b = nums.expand(nid[is_num])
-        # interleave in order: expand each class then merge by token position
-        lv = _VOCAB.lens[vid]
-        ln = nums.lens[nid]
-        tl = np.where(is_num, ln, lv)
-        pos = np.zeros(m, np.int64)
-        np.cumsum(tl[:-1], out=pos[1:])
-        buf = np.empty(int(tl.sum()), np.uint8)
-        ia = np.repeat(pos[~is_num], lv[~is_num]) + (np.arange(len(a)) - np.repeat(
-            np.concatenate([[0], np.cumsum(lv[~is_num])[:-1]]), lv[~is_num]))
-        ib = np.repeat(pos[is_num], ln[is_num]) + (np.arange(len(b)) - np.repeat(
-            np.concatenate([[0], np.cumsum(ln[is_num])[:-1]]), ln[is_num]))
-        buf[ia] = a
-        buf[ib] = b
+        ids = np.where(is_num, len(VOCAB) + nid, vid)
+        buf = tab[ids][mask[ids]]
         out.append(buf)
         have += len(buf)
     return np.concatenate(out)[:nbytes]
@@ -187,27 +188,40 @@ def _templates() -> list:
     return [_soup(st, 8192, 100_000, 0.1) for _ in range(16)]
 
 
-def config3(n: int = 10_000, value_len: int = 60_000) -> Corpus:
-    """HTML-shape pages: a fixed 8 KB boilerplate (one of 16) + tag/word soup + ids."""
-    st = Stream(3, 0)
+def _config3_block(args) -> np.ndarray:
+    b, count, soup_len, part = args
+    return _soup(Stream(3, 1000 + b + part * 1_000_000), soup_len * count, 100_000, 0.1)
+
+
+def config3(n: int = 10_000, value_len: int = 60_000, workers: int = 0, part: int = 0) -> Corpus:
+    """HTML-shape pages: a fixed 8 KB boilerplate (one of 16) + tag/word soup + ids.
+    Blocks of 256 pages draw from independent streams, so they can be built in parallel."""
+    st = Stream(3, part * 1_000_000)
     tmpl = _templates()
     mmdd = st.randint(0, 365, n)
     tid = st.randint(0, 16, n)
     keys = []
     for i in range(n):
         d = int(mmdd[i])
-        keys.append(b"http://www.qq.com/a/2017%02d%02d/%06d.htm" % (d // 31 + 1, d % 31 + 1, i))
+        keys.append(b"http://www.qq.com/a/2017%02d%02d/%06d.htm" % (d // 31 + 1, d % 31 + 1, i + part * n))
     vals = np.empty(n * value_len, np.uint8)
     soup_len = value_len - 8192
     block = 256
-    for a in range(0, n, block):
-        b = min(n, a + block)
-        soup = _soup(st, soup_len * (b - a), 100_000, 0.1)
-        for i in range(a, b):
+    jobs = [(b, min(n, (b + 1) * block) - b * block, soup_len, part) for b in range((n + block - 1) // block)]
+    if workers == 0:
+        workers = min(8, os.cpu_count() or 1) if len(jobs) > 4 else 1
+    if workers > 1:
+        import concurrent.futures as cf
+        with cf.ProcessPoolExecutor(workers) as ex:
+            soups = list(ex.map(_config3_block, jobs))
+    else:
+        soups = [_config3_block(j) for j in jobs]
+    for (b, count, _, _), soup in zip(jobs, soups):
+        for k in range(count):
+            i = b * block + k
             o = i * value_len
             vals[o:o + 8192] = tmpl[int(tid[i])]
-            s = (i - a) * soup_len
-            vals[o + 8192:o + value_len] = soup[s:s + soup_len]
+            vals[o + 8192:o + value_len] = soup[k * soup_len:(k + 1) * soup_len]
     kb, ko = _csr(keys)
     vo = np.arange(n + 1, dtype=np.int64) * value_len
     return Corpus(3, kb, ko, vals, vo)
@@ -258,5 +272,11 @@ GENERATORS = {1: config1, 2: config2, 3: config3, 4: config4, 5: config5}
 FULL_SIZES = {1: 1000, 2: 100_000, 3: 10_000, 4: 1_000_000, 5: 10_000}
 
 
-def make(config: int, n: int | None = None) -> Corpus:
-    return GENERATORS[config](FULL_SIZES[config] if n is None else n)
+def make(config: int, n: int | None = None, part: int = 0) -> Corpus:
+    """Corpus of `config`; `part` selects an independent, same-shaped corpus (per rank)."""
+    n = FULL_SIZES[config] if n is None else n
+    if config == 3:
+        return config3(n, part=part)
+    if part:
+        raise ValueError("part is only implemented for config 3")
+    return GENERATORS[config](n)
