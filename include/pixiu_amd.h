@@ -131,6 +131,11 @@ int px_stats_get(px_ctx *ctx, px_stats *st);
  * NULL to query *bytes. */
 int px_last_store(px_ctx *ctx, uint8_t *dst, uint64_t cap, int dst_on_device, uint64_t *bytes);
 
+/* Import n compressed records (host CSR: comp[off[i] .. off[i+1])) as one chunk of a
+ * new read-only shard (chunk 0, slots 0..n-1), e.g. records exported by px_export.
+ * They can then be expanded with px_parse_batch. */
+int px_import_chunk(px_ctx *ctx, uint32_t n, const uint8_t *comp, const uint64_t *off, uint32_t *shard);
+
 /* Drop every stored record (PiXiuCtrl::free_prop + init_prop, PiXiuCtrl.cpp:77-86) while
  * keeping the context's device memory for reuse. */
 int px_reset(px_ctx *ctx);

@@ -766,6 +766,49 @@ struct pxo_shard {
         return 0;
     }
 
+    // CritBitTree::contains / delitem (CritBitTree.cpp:107-178): the crit record's decoded
+    // stream is compared with the escaped key bytes until the key terminator.
+    bool key_matches(const Bytes &q, const Leaf &l) {
+        Bytes crit = key_prefix(l);
+        bool spec = false;
+        for (size_t k = 0; k < crit.size() && k < q.size() && crit[k] == q[k]; ++k) {
+            uint8_t v = crit[k];
+            if (!spec && v == kEsc) {
+                spec = true;
+            } else if (spec) {
+                if (v == kKeyEnd) return true;
+                spec = false;
+            }
+        }
+        return false;
+    }
+
+    bool contains(const Bytes &q) {
+        if (!has_root) return false;
+        return key_matches(q, best_match(q).crit);
+    }
+
+    int remove(const Bytes &q) {  // 0 deleted, 1 CBT_DEL_NOT_FOUND
+        if (!has_root) return 1;
+        Best b = best_match(q);
+        if (!key_matches(q, b.crit)) return 1;
+        if (b.pa < 0) {
+            has_root = false;
+            root = CbtRef{};
+        } else {
+            CbtRef other = cbt[(size_t)b.pa].kid[1 - b.dir];
+            if (b.grand < 0) {
+                root = other;
+            } else {
+                CbtInner &g = cbt[(size_t)b.grand];
+                g.kid[g.kid[0].inner == b.pa ? 0 : 1] = other;
+            }
+            cbt_free.push_back(b.pa);
+        }
+        mark_dead(b.crit);
+        return 0;
+    }
+
     // CritBitTree::getitem + key_eq (CritBitTree.cpp:180-196; PiXiuStr.cpp:129-143)
     bool lookup(const Bytes &q, Leaf *out) {
         if (!has_root) return false;
@@ -815,6 +858,26 @@ int pxo_set(pxo_shard *s, const uint8_t *k, int klen, const uint8_t *v, int vlen
     }
 }
 
+int pxo_contains(pxo_shard *s, const uint8_t *k, int klen) {
+    try {
+        Bytes key;
+        escape_append(k, klen, true, key);
+        return s->contains(key) ? 1 : 0;
+    } catch (const Fail &f) {
+        return f.code;
+    }
+}
+
+int pxo_delete(pxo_shard *s, const uint8_t *k, int klen) {
+    try {
+        Bytes key;
+        escape_append(k, klen, true, key);
+        return s->remove(key);
+    } catch (const Fail &f) {
+        return f.code;
+    }
+}
+
 int pxo_comp(pxo_shard *s, uint32_t chunk, uint32_t idx, uint8_t *out, int cap) {
     if (chunk >= s->chunks.size() || idx >= s->chunks[chunk].recs.size()) return PXO_EINVAL;
     return copy_out(s->chunks[chunk].recs[idx], out, cap);
@@ -841,6 +904,28 @@ int pxo_get(pxo_shard *s, const uint8_t *k, int klen, int mode, uint8_t *out, in
         if (!s->lookup(key, &l)) return PXO_NOTFOUND;
         Sink sk;
         s->decode_into(l.chunk, l.idx, 0, kMaxDoc, mode, sk);
+        return copy_out(sk.out, out, cap);
+    } catch (const Fail &f) {
+        return f.code;
+    }
+}
+
+// Decode against a caller-supplied chunk of compressed records (decoder KATs).
+int pxo_decode_chunk(int n, const uint8_t *comp, const uint64_t *off, int idx, int from, int to, int mode,
+                     uint8_t *out, int cap) {
+    try {
+        Chunk ch;
+        for (int i = 0; i < n; ++i) ch.recs.emplace_back(comp + off[i], comp + off[i + 1]);
+        ch.dead.assign((size_t)n, 0);
+        if (idx < 0 || idx >= n || from < 0 || to < from) return PXO_EINVAL;
+        Sink sk;
+        if (mode == PXO_COMPAT) {
+            compat_parse(ch, (uint32_t)idx, from, to, sk, (size_t)-1, 0);
+        } else {
+            const Bytes &e = exact_expand(ch, (uint32_t)idx, 0);
+            size_t a = std::min((size_t)from, e.size()), b = std::min((size_t)to, e.size());
+            sk.out.assign(e.begin() + a, e.begin() + b);
+        }
         return copy_out(sk.out, out, cap);
     } catch (const Fail &f) {
         return f.code;

@@ -49,6 +49,10 @@ int pxo_parse(pxo_shard *s, uint32_t chunk, uint32_t idx, int from, int to, int 
 #define PXO_NOTFOUND -5
 int pxo_get(pxo_shard *s, const uint8_t *k, int klen, int mode, uint8_t *out, int cap);
 
+/* PiXiuCtrl::contains (1/0) and ::delitem (0 deleted, 1 not found) */
+int pxo_contains(pxo_shard *s, const uint8_t *k, int klen);
+int pxo_delete(pxo_shard *s, const uint8_t *k, int klen);
+
 uint32_t pxo_num_chunks(pxo_shard *s);
 uint32_t pxo_chunk_records(pxo_shard *s, uint32_t chunk);
 /* pool counters of the live GST (MemPool.h:14-22: nth, used_num) */
@@ -74,6 +78,10 @@ int pxo_run(int n, const uint8_t *keys, const uint64_t *koff, const uint32_t *kl
 int pxo_encode_docs(int n, const uint8_t *docs, const uint64_t *doc_off,
                     uint8_t *comp, uint64_t comp_cap, uint64_t *comp_off,
                     uint32_t *chunk_no, uint32_t *idx);
+
+/* decode (idx, from, to) against a caller-supplied chunk of n compressed records */
+int pxo_decode_chunk(int n, const uint8_t *comp, const uint64_t *off, int idx, int from, int to, int mode,
+                     uint8_t *out, int cap);
 
 #ifdef __cplusplus
 }

@@ -177,3 +177,21 @@ extern "C" int refx_dump_tree(char *out, int cap) {
     memcpy(out, s.c_str(), s.size() + 1);
     return (int)s.size();
 }
+
+// Decode queries against a caller-supplied chunk of compressed records (for the
+// decoder known-answer tests, e.g. PiXiuStr.cpp:356-413, which build chunks by hand).
+extern "C" int refx_decode_chunk(int n, const uint8_t *comp, const uint64_t *off, int idx, int from, int to,
+                                 uint8_t *out, int cap) {
+    PiXiuChunk *c = PiXiuChunk_init();
+    for (int i = 0; i < n; ++i) {
+        int len = (int)(off[i + 1] - off[i]);
+        PiXiuStr *p = (PiXiuStr *)malloc(sizeof(PiXiuStr) + (size_t)len + 8);
+        p->len = (uint16_t)len;
+        memcpy(p->data, comp + off[i], (size_t)len);
+        c->strs[i] = p;
+    }
+    c->used_num = (uint16_t)n;
+    int r = drain(c->getitem(idx)->parse(from, to, c), out, cap);
+    PiXiuChunk_free(c);
+    return r;
+}

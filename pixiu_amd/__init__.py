@@ -72,7 +72,7 @@ REC_DTYPE = np.dtype([("shard", "<u4"), ("chunk", "<u4"), ("idx", "<u4"), ("from
 # every symbol include/pixiu_amd.h declares
 EXPORTS = ["px_open", "px_close", "px_strerror", "px_set_batch", "px_get_batch", "px_parse_batch",
            "px_contains_batch", "px_del_batch", "px_export", "px_stats_get", "px_stream", "px_reset",
-           "px_last_store"]
+           "px_last_store", "px_import_chunk"]
 
 _LIB = None
 
@@ -103,6 +103,7 @@ def load_library() -> C.CDLL:
     lib.px_stream.argtypes = [vp]
     lib.px_reset.argtypes = [vp]
     lib.px_last_store.argtypes = [vp, vp, u64, i32, vp]
+    lib.px_import_chunk.argtypes = [vp, u32, vp, vp, vp]
     _LIB = lib
     return lib
 
@@ -260,6 +261,15 @@ class Store:
         if rc != PX_OK:
             raise PxError(rc, "px_export")
         return [out[int(off[i]):int(off[i + 1])].tobytes() for i in range(n)]
+
+    def import_chunk(self, recs: list) -> int:
+        """Load compressed records as one chunk of a new read-only shard; returns the shard id."""
+        buf, off = csr(recs)
+        sid = np.zeros(1, np.uint32)
+        rc = self._lib.px_import_chunk(self._h, len(recs), _ptr(buf), _ptr(off), _ptr(sid))
+        if rc != PX_OK:
+            raise PxError(rc, "px_import_chunk")
+        return int(sid[0])
 
     def reset(self):
         """Drop all records, keep device memory (free_prop + init_prop)."""

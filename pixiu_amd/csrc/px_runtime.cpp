@@ -1162,6 +1162,70 @@ int px_last_store(px_ctx *ctx, uint8_t *dst, uint64_t cap, int dst_on_device, ui
     })
 }
 
+// Import a chunk of compressed records (e.g. exported earlier, or hand-built for the
+// decoder known-answer tests) as a new read-only shard; returns its shard id.
+int px_import_chunk(px_ctx *ctx, uint32_t n, const uint8_t *comp, const uint64_t *off, uint32_t *shard_out) {
+    if (!ctx || !n || n > (uint32_t)kChunkSlots || !comp || !off) return PX_EINVAL;
+    PX_GUARD({
+        std::vector<uint64_t> coff(n + 1, 0), soff(n + 1, 0);
+        for (uint32_t r = 0; r < n; ++r) {
+            uint64_t l = off[r + 1] - off[r];
+            if (l > (uint64_t)kMaxDoc) return PX_EINVAL;
+            coff[r + 1] = coff[r] + round_up(l, 8);
+            soff[r + 1] = soff[r] + (l + 2) * 8;
+        }
+        auto *store = (uint8_t *)ctx->heap.alloc(coff[n] + 64);
+        auto *segs = (uint8_t *)ctx->heap.alloc(soff[n] + 64);
+        ctx->store_blocks.emplace_back(store, coff[n] + 64);
+        ctx->store_blocks.emplace_back(segs, soff[n] + 64);
+        std::vector<RecSlot> slots(n);
+        std::vector<uint2 *> segp(n);
+        for (uint32_t r = 0; r < n; ++r) {
+            uint64_t l = off[r + 1] - off[r];
+            ctx->h2d(store + coff[r], comp + off[r], l);
+            slots[r] = RecSlot{store + coff[r], (const uint2 *)(segs + soff[r]), (uint32_t)l, 0};
+            segp[r] = (uint2 *)(segs + soff[r]);
+        }
+        auto *d_slots = (RecSlot *)ctx->heap.alloc((uint64_t)n * sizeof(RecSlot));
+        auto *d_segp = (uint2 **)ctx->heap.alloc((uint64_t)n * 8);
+        auto *d_tmp = (uint32_t *)ctx->heap.alloc((uint64_t)n * 8);
+        ctx->h2d(d_slots, slots.data(), (size_t)n * sizeof(RecSlot));
+        ctx->h2d(d_segp, segp.data(), (size_t)n * 8);
+        hcheck(launch_tokenize(ctx->stream, n, d_slots, d_segp, d_tmp, d_tmp + n));
+        std::vector<uint32_t> nseg(n), tst(n);
+        ctx->d2h(nseg.data(), d_tmp, (size_t)n * 4);
+        ctx->d2h(tst.data(), d_tmp + n, (size_t)n * 4);
+        ctx->sync();
+        std::vector<uint2> sentinel(n);
+        for (uint32_t r = 0; r < n; ++r) ctx->d2h(&sentinel[r], segp[r] + nseg[r], sizeof(uint2));
+        ctx->sync();
+        ctx->heap.release(d_slots, (uint64_t)n * sizeof(RecSlot));
+        ctx->heap.release(d_segp, (uint64_t)n * 8);
+        ctx->heap.release(d_tmp, (uint64_t)n * 8);
+        for (uint32_t r = 0; r < n; ++r)
+            if (tst[r] != kOk) return (int)map_status(tst[r]);
+        Shard &sh = ctx->new_shard();
+        sh.records = n;
+        uint32_t c = ctx->new_chunk(sh.id);
+        sh.chunks.push_back(c);
+        Chunk &ch = ctx->chunks[c];
+        for (uint32_t r = 0; r < n; ++r) {
+            slots[r].nseg = nseg[r];
+            ch.slots.push_back(slots[r]);
+            ch.doc_len.push_back(std::min<uint32_t>(sentinel[r].x, (uint32_t)kMaxDoc * 4));
+            ch.dead.push_back(0);
+            ch.kp_off.push_back(0);
+            ch.kp_len.push_back(0);
+        }
+        ch.n = n;
+        ctx->chunk_reserve(c, n);
+        ctx->h2d(ctx->chunks[c].dev, ctx->chunks[c].slots.data(), (size_t)n * sizeof(RecSlot));
+        ctx->sync();
+        if (shard_out) *shard_out = sh.id;
+        return PX_OK;
+    })
+}
+
 int px_reset(px_ctx *ctx) {
     if (!ctx) return PX_EINVAL;
     PX_GUARD(ctx->reset(); return PX_OK;)

@@ -268,6 +268,12 @@ def config5(n: int = 10_000, total: int = 65_531) -> Corpus:
     return Corpus(5, kb, ko, vals, vo)
 
 
+def tiny_keys(n: int) -> Corpus:
+    """n key-only records "s%06d" (exercises the 65,535-slot chunk rotation)."""
+    kb, ko = _csr([b"s%06d" % i for i in range(n)])
+    return Corpus(0, kb, ko, np.zeros(0, np.uint8), np.zeros(n + 1, np.int64))
+
+
 GENERATORS = {1: config1, 2: config2, 3: config3, 4: config4, 5: config5}
 FULL_SIZES = {1: 1000, 2: 100_000, 3: 10_000, 4: 1_000_000, 5: 10_000}
 

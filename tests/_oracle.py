@@ -156,6 +156,12 @@ class _Shard:
             raise RuntimeError(f"pxo_parse: {n}")
         return out.raw[:n]
 
+    def contains(self, k: bytes) -> int:
+        return self.lib.pxo_contains(self.h, k, len(k))
+
+    def delete(self, k: bytes) -> int:
+        return self.lib.pxo_delete(self.h, k, len(k))
+
     def comp(self, chunk, idx):
         out = C.create_string_buffer(1 << 17)
         n = self.lib.pxo_comp(self.h, chunk, idx, out, len(out))
