@@ -93,6 +93,7 @@ def main():
 
     import pixiu_amd as px
     from pixiu_amd import synth
+    from pixiu_amd.dist import gather_blobs
 
     corpus = synth.make(a.config, a.records, part=rank) if a.config == 3 else synth.make(a.config, a.records)
     n = corpus.n
@@ -124,15 +125,10 @@ def main():
             nonlocal gather_buf
             tg = time.perf_counter()
             nb = st.last_store_bytes()
-            sizes = torch.tensor([nb], dtype=torch.int64, device=dev)
-            all_sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-            dist.all_gather(all_sizes, sizes)
-            mx = int(max(int(x.item()) for x in all_sizes))
-            if gather_buf is None or gather_buf.numel() < mx:
-                gather_buf = torch.empty(mx, dtype=torch.uint8, device=dev)
+            if gather_buf is None or gather_buf.numel() < nb:
+                gather_buf = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
             st.copy_last_store(gather_buf.data_ptr(), gather_buf.numel(), True)
-            recv = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(world)] if rank == 0 else None
-            dist.gather(gather_buf[:mx], recv, dst=0)
+            gather_blobs(gather_buf[:nb], dst=0)
             torch.cuda.synchronize()
             g_ms = (time.perf_counter() - tg) * 1e3
         if rc != px.PX_OK or int(res["status"].max()) != 0:
@@ -157,9 +153,12 @@ def main():
     set_s = sum(r["set_s"] for r in runs)
     get_s = sum(r["get_s"] for r in runs)
     tot = torch.tensor([elapsed, set_s, get_s], dtype=torch.float64, device=dev)
-    if world > 1:
+    vol = torch.tensor([raw_bytes, runs[-1]["comp"], runs[-1]["exp"]], dtype=torch.float64, device=dev)
+    if world > 1:  # slowest rank's clock, every rank's bytes
         dist.all_reduce(tot, op=dist.ReduceOp.MAX)
+        dist.all_reduce(vol, op=dist.ReduceOp.SUM)
     elapsed, set_s, get_s = (float(x) for x in tot.tolist())
+    job_raw, job_comp, job_exp = (float(x) for x in vol.tolist())
     comp = runs[-1]["comp"]
     exp = runs[-1]["exp"]
     set_kms = float(np.mean([r["set_kms"] for r in runs]))
@@ -172,8 +171,8 @@ def main():
         return
 
     K = a.steps
-    set_MBps = world * raw_bytes * K / set_s / 1e6
-    get_MBps = world * exp * K / get_s / 1e6
+    set_MBps = job_raw * K / set_s / 1e6
+    get_MBps = job_exp * K / get_s / 1e6
     # roofline: algorithmic bytes per launch / avg launch time
     set_alg = raw_bytes + comp                  # raw in + compressed out
     dec_alg = comp + exp                        # compressed in + expanded out
@@ -210,7 +209,7 @@ def main():
                    "parallelism": f"dp{world} (record-range shards, no cross-GPU refs)"},
         "setitem_MBps": round(set_MBps, 3),
         "getitem_MBps": round(get_MBps, 3),
-        "compression_ratio": round(comp / raw_bytes, 4),
+        "compression_ratio": round(job_comp / job_raw, 4),
         "kernel_ms": {"k_gst_encode": round(set_kms, 3), "k_decode": round(dec_kms, 3)},
         "gather_ms": round(float(np.mean([r["gather_ms"] for r in runs])), 3),
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 3), "peak": PEAK_HBM_GBPS,

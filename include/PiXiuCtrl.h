@@ -1,0 +1,189 @@
+// PiXiuCtrl.h — source-compatible C++ facade of the reference's PiXiuCtrl
+// (reference src/proj/PiXiuCtrl.h:7-26, README.md:100-150), implemented over the
+// C ABI in pixiu_amd.h.  Header-only; link against libpixiu_amd.so.
+//
+// Client code written for the reference keeps compiling:
+//
+//     PiXiuCtrl ctrl; ctrl.init_prop();
+//     ctrl.setitem((uint8_t *)k, klen, (uint8_t *)v, vlen);
+//     PXSGen *gen = ctrl.getitem((uint8_t *)k, klen);
+//     uint8_t rv; while (gen->operator()(rv)) putchar(rv);
+//     PXSGen_free(gen);
+//     ctrl.free_prop();
+//
+// including the CLI's `ctrl.st.cbt_chunk->getitem(ctrl.st.local_chunk.used_num - 1)->len`
+// (main.cpp:67).  Semantics are the reference's single instance (one shard);
+// getitem streams the compat expansion (PXSGen byte-for-byte).  Differences:
+// `iter` returns NULL (prefix iteration is not on the ported path yet) and
+// `reinsert` is a no-op (compaction policy out of scope).
+#ifndef PIXIU_CTRL_FACADE_H
+#define PIXIU_CTRL_FACADE_H
+
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "pixiu_amd.h"
+
+#define CBT_SET_REPLACE 1
+#define CBT_DEL_NOT_FOUND 1
+#define PXSG_MAX_TO 65535
+#define PXC_STR_NUM 65535
+
+struct PiXiuStr {  // compressed record as the reference lays it out (PiXiuStr.h:61-64)
+    uint16_t len;
+    uint8_t data[1];
+};
+
+// A generator over an already-expanded buffer (the GPU expands the whole record).
+struct PXSGen {
+    std::vector<uint8_t> buf;
+    size_t cur = 0;
+
+    bool operator()(uint8_t &rv) {
+        if (cur >= buf.size()) return false;
+        rv = buf[cur++];
+        return true;
+    }
+
+    // PiXiuStr.h:200-211: drain, keep visible bytes 33..126, NUL-terminate, free the gen
+    char *consume_repr(void);
+};
+
+struct CBTGen {
+    bool operator()(PXSGen *&) { return false; }
+};
+
+inline void PXSGen_free(PXSGen *gen) { delete gen; }
+inline void CBTGen_free(CBTGen *gen) { delete gen; }
+
+inline char *PXSGen::consume_repr(void) {
+    std::vector<char> out;
+    uint8_t rv;
+    while ((*this)(rv))
+        if (33 <= rv && rv <= 126) out.push_back((char)rv);
+    char *s = (char *)malloc(out.size() + 1);
+    if (!out.empty()) memcpy(s, out.data(), out.size());
+    s[out.size()] = '\0';
+    PXSGen_free(this);
+    return s;
+}
+
+struct PiXiuCtrl;
+
+// The part of the reference's SuffixTree / PiXiuChunk that client code touches.
+struct PiXiuChunk {
+    PiXiuCtrl *owner = nullptr;
+    uint32_t chunk = 0;
+    std::vector<std::vector<uint8_t>> cache;
+    PiXiuStr *getitem(int idx);
+};
+
+struct PiXiuLocalChunk {
+    uint16_t used_num = 0;
+};
+
+struct SuffixTree {
+    PiXiuChunk *cbt_chunk = nullptr;
+    PiXiuLocalChunk local_chunk;
+};
+
+struct CritBitTree {};
+
+struct PiXiuCtrl {
+    CritBitTree cbt;
+    SuffixTree st;
+    px_ctx *ctx = nullptr;
+    PiXiuChunk chunk_view;
+    int device = 0;
+
+    int setitem(uint8_t k[], int k_len, uint8_t v[], int v_len, bool = false) {
+        uint64_t koff[2] = {0, (uint64_t)k_len}, voff[2] = {0, (uint64_t)(v_len > 0 ? v_len : 0)};
+        uint8_t dummy = 0;
+        px_set_result r;
+        int rc = px_set_batch(ctx, 1, k, koff, v ? v : &dummy, voff, 0, &r);
+        if (rc != PX_OK) return -rc;
+        if (r.chunk != chunk_view.chunk) {  // chunk rotation (PiXiuCtrl.cpp:13-25)
+            chunk_view.chunk = r.chunk;
+            chunk_view.cache.clear();
+        }
+        st.local_chunk.used_num = (uint16_t)(r.idx + 1);
+        return (int)r.replaced;
+    }
+
+    bool contains(uint8_t k[], int k_len) {
+        uint64_t off[2] = {0, (uint64_t)k_len};
+        uint32_t res = 0;
+        return px_contains_batch(ctx, 1, k, off, &res) == PX_OK && res;
+    }
+
+    PXSGen *getitem(uint8_t k[], int k_len) {
+        uint64_t koff[2] = {0, (uint64_t)k_len};
+        std::vector<uint8_t> out(4 * PXSG_MAX_TO + 1024);
+        uint64_t off = 0, need = 0;
+        uint32_t len = 0, status = 0;
+        int rc = px_get_batch(ctx, 1, k, koff, PX_COMPAT, out.data(), out.size(), 0, &off, &len, &status, &need);
+        if (rc == PX_ESPACE) {
+            out.resize(need);
+            rc = px_get_batch(ctx, 1, k, koff, PX_COMPAT, out.data(), out.size(), 0, &off, &len, &status, &need);
+        }
+        if (rc != PX_OK || status != PX_OK) return nullptr;
+        PXSGen *g = new PXSGen();
+        g->buf.assign(out.begin() + (long)off, out.begin() + (long)(off + len));
+        return g;
+    }
+
+    CBTGen *iter(uint8_t[], int) { return nullptr; }
+
+    int delitem(uint8_t k[], int k_len) {
+        uint64_t off[2] = {0, (uint64_t)k_len};
+        uint32_t res = CBT_DEL_NOT_FOUND;
+        px_del_batch(ctx, 1, k, off, &res);
+        return (int)res;
+    }
+
+    void init_prop(void) {
+        if (!ctx) {
+            px_opts o;
+            memset(&o, 0, sizeof o);
+            o.device = device;
+            o.records_per_shard = 0;  // one shard: the reference's single instance
+            ctx = px_open(&o);
+        } else {
+            px_reset(ctx);
+        }
+        chunk_view = PiXiuChunk();
+        chunk_view.owner = this;
+        st.cbt_chunk = &chunk_view;
+        st.local_chunk.used_num = 0;
+    }
+
+    void free_prop(void) {
+        if (ctx) px_close(ctx);
+        ctx = nullptr;
+        st.cbt_chunk = nullptr;
+    }
+
+    void reinsert(PiXiuChunk *&) {}
+};
+
+inline PiXiuStr *PiXiuChunk::getitem(int idx) {
+    if (idx < 0) return nullptr;
+    if ((size_t)idx >= cache.size()) cache.resize((size_t)idx + 1);
+    std::vector<uint8_t> &c = cache[(size_t)idx];
+    if (c.empty()) {
+        px_rec r = {0, chunk, (uint32_t)idx, 0, PXSG_MAX_TO};
+        std::vector<uint8_t> buf(PXSG_MAX_TO + 8);
+        uint64_t off[2] = {0, 0};
+        if (px_export(owner->ctx, 1, &r, buf.data(), buf.size(), off) != PX_OK) return nullptr;
+        c.resize(2 + off[1]);
+        uint16_t len = (uint16_t)off[1];
+        memcpy(c.data(), &len, 2);
+        memcpy(c.data() + 2, buf.data(), off[1]);
+    }
+    return reinterpret_cast<PiXiuStr *>(c.data());
+}
+
+#endif
