@@ -21,16 +21,23 @@ constexpr int kEdgeBlocks = 3;   // sizeof(SGTNode<STNode>) = 24 B
 constexpr int kRotatePools = 2048;
 
 // ---- GST arena ----
-// Node (16 B):  x = suffix link, y = label start relative to the chunk's text base,
-//               z = doc | from << 16,  w = to | flags << 16
+// A node is just its suffix link (u32).  Every edge lives in its parent's child
+// map as a 16-byte entry that carries the child's label, so one probe yields the
+// child's id AND label (no second dependent load):
+//   x = parent:26 | epoch:4 << 26      (epoch 0 == empty; rotation bumps the epoch)
+//   y = child:26  | kids:1 << 26       (kids: the child has >= 1 child itself)
+//   z = doc | from << 16               (label in the chunk-local doc `doc`)
+//   w = to  | byte << 16               (byte = the key, the label's first byte)
+// The root's 256 entries live in a direct table (LDS while a kernel runs).
+// Non-root entries: open addressing over 64-byte buckets of 4 entries.
 constexpr uint32_t kRoot = 0;
 constexpr uint32_t kNone = 0xffffffffu;
-constexpr uint32_t kFlagKids = 1;  // node has >= 1 child (STNode::is_inner for non-root)
-// child-map hash entry (u64): epoch:4 | parent:26 | byte:8 | child:26; epoch 0 == empty
 constexpr int kNodeBits = 26;
-constexpr uint32_t kMaxNodes = (1u << kNodeBits) - 1;
+constexpr uint32_t kNodeMask = (1u << kNodeBits) - 1;
+constexpr uint32_t kMaxNodes = kNodeMask;
+constexpr uint32_t kKidsBit = 1u << 26;
 constexpr int kMaxEpoch = 15;
-constexpr int kProbe = 16;  // lanes per hash probe window
+constexpr int kBucket = 4;  // entries per 64-byte bucket
 
 // persistent per-shard GST state (device resident between batches)
 struct ShardState {
@@ -50,12 +57,12 @@ struct ShardState {
 struct GstShard {
     uint8_t *text;        // arena text section
     uint32_t *doc_base;   // [doc_cap + 1] doc start relative to the live chunk text base
-    uint4 *nodes;         // [node_cap]
-    uint64_t *hash;       // [hash_mask + 1]
-    uint32_t *root_kids;  // [256]
+    uint4 *nodes;         // [2 * node_cap] node records (link, child count, two inline children)
+    uint4 *hash;          // [hash_mask + 1] child-map entries
+    uint4 *root;          // [256] root entries (y == kNone: absent)
     ShardState *st;
     uint32_t node_cap;
-    uint32_t hash_mask;
+    uint32_t hash_mask;   // entries - 1 (a multiple of kBucket minus 1)
     uint32_t doc_cap;
     uint32_t r0, r1;      // batch records [r0, r1) belong to this shard, in order
     uint32_t pad;

@@ -66,6 +66,20 @@ PX_DEV uint32_t ffs64(uint64_t m) { return (uint32_t)__ffsll((unsigned long long
 PX_DEV uint32_t readlane(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
 PX_DEV uint32_t rd16(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
 
+#ifdef PX_PROFILE
+// debug build only: per-category counters and shader-clock cycles of k_gst_encode
+enum { P_BYTES, P_FF_CALLS, P_FF_BYTES, P_PASS, P_ITERS, P_LOOKUPS, P_PROBES, P_ROOT, P_WALK, P_LINK, P_CANON_LVL,
+       P_T_TOTAL, P_T_FF, P_T_DERIVE, P_T_WALK, P_T_SPLIT, P_T_GROW, P_T_CANON, P_T_END, P_T_ROOT, P_T_ENC, P_N };
+__device__ unsigned long long g_prof[P_N];
+#define PX_CNT(k, v) (prof[k] += (v))
+#define PX_T0() uint64_t _t0 = __builtin_amdgcn_s_memtime()
+#define PX_T1(k) (prof[k] += __builtin_amdgcn_s_memtime() - _t0)
+#else
+#define PX_CNT(k, v) ((void)0)
+#define PX_T0() ((void)0)
+#define PX_T1(k) ((void)0)
+#endif
+
 // ====================================================================== escape
 // One wave per record (grid-stride).  doc_len = esc(k)+2 (+ esc(v)+2 when vlen>0).
 __global__ void __launch_bounds__(256) k_doc_len(uint32_t n, const uint8_t *keys, const uint64_t *koff,
@@ -135,8 +149,17 @@ __global__ void __launch_bounds__(256) k_doc_write(uint32_t n, const uint8_t *ke
 }
 
 // ====================================================================== GST
-constexpr uint32_t kObuf = 2048;   // per-wave output staging (LDS)
+// One wave per shard.  The serial Ukkonen walk (SuffixTree.cpp:144-289) and the
+// stream encoder (PiXiuStr.cpp:16-118) run on wave-uniform values; the lanes are
+// used for wide work: 64-byte edge-label fast-forward compares, 4-entry bucket
+// probes (one 64-byte line per probe), the current doc's 256-byte byte window,
+// and the encoder's output staging.  Per shard, LDS holds the root's 256 child
+// entries, the first 256 doc starts and the output staging buffer.
+constexpr uint32_t kObuf = 1024;  // per-wave output staging (LDS)
 constexpr uint32_t kFlushAt = kObuf - 64;
+constexpr uint32_t kDocCache = 256;  // doc starts cached in LDS
+constexpr uint32_t kRootSlot = 0x80000000u;
+constexpr uint32_t kWin = 256;  // current-doc window (4 bytes per lane)
 
 PX_DEV uint32_t hslot(uint32_t parent, uint32_t c) {
     uint32_t h = parent * 0x9E3779B1u ^ (c + 1u) * 0x85EBCA77u;
@@ -146,60 +169,45 @@ PX_DEV uint32_t hslot(uint32_t parent, uint32_t c) {
     return h;
 }
 
+// an edge = the child's entry in its parent's map.  cnt = the child's own child
+// count, saturated at 3; slot = where the entry lives (root table, one of the
+// parent's two inline slots, or a hash slot).
 struct Edge {
-    uint32_t id, link, abs, doc, from, to, flags;
+    uint32_t id, doc, from, to, cnt, slot, key;
+};
+constexpr uint32_t kInlineSlot = 0x40000000u;  // | which << 26 | parent
+
+struct GstLds {
+    uint4 root[256];
+    uint32_t doc_base[kDocCache + 1];
+    uint8_t obuf[kObuf];
 };
 
 struct GstWave {
     // shard arena
-    const GstShard *sh;
     uint8_t *text;  // live chunk text base
     uint32_t *doc_base;
-    uint4 *nodes;
-    uint64_t *hash;
-    uint32_t *root_kids;
+    uint4 *nodes;   // 2 x uint4 per node: {link, cnt, e0.w0, e0.w1}, {e0.w2, e1.w0, e1.w1, e1.w2}
+    uint4 *hash;
     uint32_t node_cap, hash_mask, doc_cap;
+    GstLds *lds;
     // persistent counters
     uint32_t n_nodes, n_docs, chunk_seq, epoch, status;
     int32_t pools, used, pool_open;
     uint64_t ctext_off, ub;
-    // current doc
-    uint32_t cur, cur_base, cur_len;
-    // active point (SuffixTree.h:33-40)
-    uint32_t act_node, act_doc, act_direct, act_off, counter;
+    // current doc + its byte window (lane l holds bytes [wb + 4l, wb + 4l + 4))
+    uint32_t cur, cur_base, cur_len, wb, win;
+    // active point (SuffixTree.h:33-40); act_base/act_len: text extent of act_doc
+    uint32_t act_node, act_doc, act_direct, act_off, counter, act_base, act_len;
     int32_t remainder;
-    // encoder (PiXiuStr.cpp:17-26 statics, per wave here)
+    // encoder (the reference keeps these as statics, PiXiuStr.cpp:17-26)
     uint32_t out, flushed, run, run_idx, run_to, applied, held, h_c, h_idx, h_pos;
     uint8_t *out_dst;
-    uint8_t *obuf;  // LDS
+#ifdef PX_PROFILE
+    uint64_t prof[P_N];
+#endif
 
     PX_DEV uint32_t tbyte(uint32_t rel) const { return uni(text[rel]); }
-
-    PX_DEV Edge load(uint32_t id) const {
-        uint4 v = nodes[id];
-        Edge e;
-        e.id = id;
-        e.link = uni(v.x);
-        e.abs = uni(v.y);
-        e.doc = uni(v.z) & 0xffffu;
-        e.from = uni(v.z) >> 16;
-        e.to = uni(v.w) & 0xffffu;
-        e.flags = uni(v.w) >> 16;
-        return e;
-    }
-    PX_DEV void store(const Edge &e) {  // whole node: only for a node just created
-        nodes[e.id] = make_uint4(e.link, e.abs, e.doc | (e.from << 16), e.to | (e.flags << 16));
-    }
-    // label and flags of an existing node.  Never the suffix link: a cached Edge may
-    // hold a stale link (set_link on the same node after it was loaded).
-    PX_DEV void store_label(const Edge &e) {
-        uint32_t *w = reinterpret_cast<uint32_t *>(&nodes[e.id]);
-        w[1] = e.abs;
-        w[2] = e.doc | (e.from << 16);
-        w[3] = e.to | (e.flags << 16);
-    }
-    PX_DEV void set_link(uint32_t id, uint32_t link) { nodes[id].x = link; }
-    PX_DEV uint32_t flags_of(uint32_t id) const { return uni(nodes[id].w) >> 16; }
 
     PX_DEV void fail(uint32_t code) {
         if (status == kOk) status = code;
@@ -219,124 +227,197 @@ struct GstWave {
         used += blocks;
     }
 
-    PX_DEV uint32_t doc_len_of(uint32_t d) const { return uni(doc_base[d + 1]) - uni(doc_base[d]); }
+    // ---- doc extents: LDS cache for the first kDocCache docs
+    PX_DEV uint32_t docbase(uint32_t d) const {
+        return d <= kDocCache ? uni(lds->doc_base[d]) : uni(doc_base[d]);
+    }
+    PX_DEV void set_docbase(uint32_t d, uint32_t v) {
+        doc_base[d] = v;
+        if (d <= kDocCache) lds->doc_base[d] = v;
+    }
+    PX_DEV void set_act_doc(uint32_t d) {
+        act_doc = d;
+        act_base = docbase(d);
+        act_len = docbase(d + 1) - act_base;
+    }
 
-    // byte the reference reads through strs[doc]->data[pos]; past the end it reads
-    // heap bytes (UB) -> modelled as a value matching nothing, counted.
-    PX_DEV int32_t stale_byte(uint32_t doc, uint32_t pos) {
-        uint32_t base = uni(doc_base[doc]);
-        uint32_t len = uni(doc_base[doc + 1]) - base;
-        if (pos >= len) {
+    // ---- current doc window
+    PX_DEV void load_window(uint32_t at) {
+        uint32_t abs0 = (cur_base + at) & ~3u;  // 4-byte aligned window start
+        wb = abs0 - cur_base;                    // may wrap below 0 (unsigned): range tests cope
+        win = *reinterpret_cast<const uint32_t *>(text + abs0 + 4 * lane_id());
+    }
+    PX_DEV uint32_t curchar(uint32_t p) {  // byte p of the current doc
+        uint32_t d = p - wb;
+        if (d < kWin) return (readlane(win, d >> 2) >> ((d & 3) * 8)) & 0xffu;
+        return tbyte(cur_base + p);
+    }
+
+    // byte the reference reads through strs[act_doc]->data[pos]; past the end it
+    // reads heap bytes (UB) -> modelled as a value matching nothing, counted.
+    PX_DEV int32_t stale_byte(uint32_t pos) {
+        if (pos >= act_len) {
             ++ub;
             return -1;
         }
-        return (int32_t)tbyte(base + pos);
+        return (int32_t)tbyte(act_base + pos);
     }
 
-    // ---- child map: root = direct table, others = 16-wide linear-probe hash ----
-    PX_DEV uint32_t child(uint32_t n, uint32_t c, uint32_t *slot_out, bool *found) {
+    // ---- child map
+    PX_DEV static void unpack(uint32_t w0, uint32_t w1, uint32_t w2, Edge &e) {
+        e.id = w0 & kNodeMask;
+        e.cnt = (w0 >> 26) & 3u;
+        e.doc = w1 & 0xffffu;
+        e.from = w1 >> 16;
+        e.to = w2 & 0xffffu;
+        e.key = (w2 >> 16) & 0xffu;
+    }
+    PX_DEV static uint32_t pk0(const Edge &e) { return e.id | (min(e.cnt, 3u) << 26); }
+    PX_DEV static uint32_t pk1(const Edge &e) { return e.doc | (e.from << 16); }
+    PX_DEV static uint32_t pk2(const Edge &e) { return e.to | (e.key << 16); }
+
+    // child of n keyed by byte c.  found: fills e.  not found: slot = where a new
+    // child goes (kNone: a hash slot must still be probed) and ncnt = n's count.
+    PX_DEV bool lookup(uint32_t n, uint32_t c, Edge &e, uint32_t &slot, uint32_t &ncnt) {
         if (n == kRoot) {
-            uint32_t v = uni(root_kids[c]);
-            *found = v != kNone;
-            *slot_out = c;
-            return v;
+            uint4 v = lds->root[c];
+            slot = kRootSlot | c;
+            ncnt = 3;
+            if (uni(v.y) == kNone) return false;
+            unpack(uni(v.y), uni(v.z), uni(v.w), e);
+            e.slot = slot;
+            return true;
         }
+        PX_CNT(P_LOOKUPS, 1);
         const uint32_t lane = lane_id();
-        const uint64_t want = ((uint64_t)n << 8) | c;
-        uint32_t h = hslot(n, c);
-        for (;;) {
-            uint32_t s = (h + lane) & hash_mask;
-            uint64_t e = lane < kProbe ? hash[s] : 0;
-            bool valid = (uint32_t)(e >> 60) == epoch;
-            bool match = lane < kProbe && valid && ((e >> 26) & 0x3ffffffffull) == want;
-            bool empty = lane < kProbe && !valid;
+        const uint32_t nb = (hash_mask >> 2);
+        uint32_t b = hslot(n, c) & nb;
+        // the node record and the first hash bucket, issued together
+        uint4 r0 = nodes[2 * n], r1 = nodes[2 * n + 1];
+        uint4 v = lane < kBucket ? hash[b * kBucket + lane] : make_uint4(0, 0, 0, 0);
+        ncnt = uni(r0.y);
+        if (ncnt >= 1 && ((uni(r1.x) >> 16) & 0xffu) == c) {
+            unpack(uni(r0.z), uni(r0.w), uni(r1.x), e);
+            e.slot = slot = kInlineSlot | n;
+            return true;
+        }
+        if (ncnt >= 2 && ((uni(r1.w) >> 16) & 0xffu) == c) {
+            unpack(uni(r1.y), uni(r1.z), uni(r1.w), e);
+            e.slot = slot = kInlineSlot | (1u << 26) | n;
+            return true;
+        }
+        if (ncnt < 2) {
+            slot = kInlineSlot | (ncnt << 26) | n;
+            return false;
+        }
+        if (ncnt == 2) {
+            slot = kNone;
+            return false;
+        }
+        const uint32_t want = n | (epoch << 26);
+        for (uint32_t guard = 0; guard <= nb; ++guard) {
+            PX_CNT(P_PROBES, 1);
+            bool valid = (v.x >> 26) == epoch;
+            bool match = lane < kBucket && v.x == want && ((v.w >> 16) & 0xffu) == c;
+            bool empty = lane < kBucket && !valid;
             uint64_t mm = ballot(match), me = ballot(empty);
             if (mm) {
                 uint32_t l = ffs64(mm);
-                *found = true;
-                *slot_out = (h + l) & hash_mask;
-                return uni(readlane((uint32_t)e & ((1u << kNodeBits) - 1u), l));
+                unpack(readlane(v.y, l), readlane(v.z, l), readlane(v.w, l), e);
+                e.slot = slot = b * kBucket + l;
+                return true;
             }
             if (me) {
-                *found = false;
-                *slot_out = (h + ffs64(me)) & hash_mask;
-                return kNone;
+                slot = b * kBucket + ffs64(me);
+                return false;
             }
-            h += kProbe;
+            b = (b + 1) & nb;
+            v = lane < kBucket ? hash[b * kBucket + lane] : make_uint4(0, 0, 0, 0);
+        }
+        fail(kErrCapacity);
+        slot = kNone;
+        return false;
+    }
+    PX_DEV bool lookup(uint32_t n, uint32_t c, Edge &e) {
+        uint32_t slot, ncnt;
+        return lookup(n, c, e, slot, ncnt);
+    }
+    // a free hash slot for a new child of n (n already has >= 2 children)
+    PX_DEV uint32_t hash_free_slot(uint32_t n, uint32_t c) {
+        const uint32_t lane = lane_id();
+        const uint32_t nb = (hash_mask >> 2);
+        uint32_t b = hslot(n, c) & nb;
+        for (uint32_t guard = 0; guard <= nb; ++guard) {
+            PX_CNT(P_PROBES, 1);
+            uint4 v = lane < kBucket ? hash[b * kBucket + lane] : make_uint4(0, 0, 0, 0);
+            uint64_t me = ballot(lane < kBucket && (v.x >> 26) != epoch);
+            if (me) return b * kBucket + ffs64(me);
+            b = (b + 1) & nb;
+        }
+        fail(kErrCapacity);
+        return kNone;
+    }
+    PX_DEV void write_entry(uint32_t slot, uint32_t parent, const Edge &e) {
+        if (slot & kRootSlot) {
+            lds->root[slot & 0xffu] = make_uint4(0, pk0(e), pk1(e), pk2(e));
+        } else if (slot & kInlineSlot) {
+            uint32_t n = slot & kNodeMask;
+            uint32_t *rec = reinterpret_cast<uint32_t *>(&nodes[2 * n]);
+            uint32_t o = (slot >> 26) & 1u ? 5 : 2;  // e1 at words 5..7, e0 at words 2..4
+            rec[o] = pk0(e);
+            rec[o + 1] = pk1(e);
+            rec[o + 2] = pk2(e);
+        } else if (slot != kNone) {
+            hash[slot] = make_uint4(parent | (epoch << 26), pk0(e), pk1(e), pk2(e));
         }
     }
-    PX_DEV uint32_t child(uint32_t n, uint32_t c) {
-        uint32_t s;
-        bool f;
-        return child(n, c, &s, &f);
-    }
-    PX_DEV bool must_child(uint32_t n, uint32_t c, uint32_t *out) {
-        uint32_t v = child(n, c);
-        if (v == kNone) {
-            fail(kErrRefCrash);  // the reference dereferences NULL here
-            return false;
-        }
-        *out = v;
-        return true;
-    }
-    // STNode::set_sub: insert (charges one map entry) or replace an equal key
-    PX_DEV void set_child(uint32_t n, uint32_t c, uint32_t kid) {
-        uint32_t slot;
-        bool found;
-        child(n, c, &slot, &found);
-        if (!found) charge(kEdgeBlocks);
-        if (n == kRoot) {
-            root_kids[c] = kid;
-        } else {
-            hash[slot] = ((uint64_t)epoch << 60) | ((uint64_t)n << 34) | ((uint64_t)c << 26) | kid;
-        }
+    // add a child that is known to be absent (charges one map entry)
+    PX_DEV void add_child(uint32_t parent, uint32_t pcnt, const Edge &kid) {
+        charge(kEdgeBlocks);
+        uint32_t slot = pcnt < 2 ? (kInlineSlot | (pcnt << 26) | parent) : hash_free_slot(parent, kid.key);
+        write_entry(slot, parent, kid);
+        if (parent != kRoot && pcnt < 3) reinterpret_cast<uint32_t *>(&nodes[2 * parent])[1] = pcnt + 1;
     }
 
-    PX_DEV bool new_node(Edge &e, uint32_t abs, uint32_t doc, uint32_t from, uint32_t to, uint32_t flags) {
+    PX_DEV bool new_node(uint32_t &id) {
         if (n_nodes >= node_cap || n_nodes >= kMaxNodes) {
             fail(kErrCapacity);
             return false;
         }
         charge(kNodeBlocks);
-        e.id = n_nodes++;
-        e.link = kRoot;
-        e.abs = abs;
-        e.doc = doc;
-        e.from = from;
-        e.to = to;
-        e.flags = flags;
-        store(e);
+        id = n_nodes++;
         return true;
     }
 
-    // ---- fresh chunk (SuffixTree::init_prop, SuffixTree.cpp:61-78) ----
+    // ---- fresh chunk (SuffixTree::init_prop, SuffixTree.cpp:61-78)
     PX_DEV void clear_tree() {
         const uint32_t lane = lane_id();
         n_nodes = 0;
         pools = 0;
         used = 0;
         pool_open = 0;
-        for (uint32_t c = lane; c < 256; c += 64) root_kids[c] = kNone;
+        for (uint32_t c = lane; c < 256; c += 64) lds->root[c] = make_uint4(0, kNone, 0, 0);
         if (++epoch > (uint32_t)kMaxEpoch) {  // epochs exhausted: really clear
-            for (uint32_t s = lane; s <= hash_mask; s += 64) hash[s] = 0;
+            for (uint32_t s = lane; s <= hash_mask; s += 64) hash[s] = make_uint4(0, 0, 0, 0);
             epoch = 1;
         }
-        Edge root;
-        new_node(root, 0, 0, 0, 0, 0);
+        __syncthreads();
+        uint32_t root;
+        if (new_node(root)) nodes[2 * root] = make_uint4(kRoot, 0, 0, 0);
     }
 
-    // ---- stream encoder (PiXiuStr_init_stream) ----
+    // ---- stream encoder (PiXiuStr_init_stream)
     PX_DEV void flush_obuf(bool all) {
         const uint32_t lane = lane_id();
         uint32_t n = out - flushed;
         if (!all && n < kFlushAt) return;
         __syncthreads();
-        for (uint32_t o = lane; o < n; o += 64) out_dst[flushed + o] = obuf[o];
+        for (uint32_t o = lane; o < n; o += 64) out_dst[flushed + o] = lds->obuf[o];
         __syncthreads();
         flushed = out;
     }
     PX_DEV void put(uint32_t b) {
-        obuf[out - flushed] = (uint8_t)b;
+        lds->obuf[out - flushed] = (uint8_t)b;
         ++out;
         flush_obuf(false);
     }
@@ -363,8 +444,12 @@ struct GstWave {
         } else {
             const uint32_t lane = lane_id();
             // the run's bytes were appended literally: they are the doc bytes just consumed
-            uint8_t b = lane < run ? text[cur_base + applied - run + lane] : 0;
-            if (lane < run) obuf[out - flushed + lane] = b;
+            uint32_t b = 0;
+            for (uint32_t k = 0; k < run; ++k) {
+                uint32_t v = curchar(applied - run + k);
+                if (lane == k) b = v;
+            }
+            if (lane < run) lds->obuf[out - flushed + lane] = (uint8_t)b;
             __syncthreads();
             out += run;
             flush_obuf(false);
@@ -379,7 +464,7 @@ struct GstWave {
     }
     PX_DEV void apply_p() {
         flush_run();
-        put(tbyte(cur_base + applied));
+        put(curchar(applied));
         ++applied;
     }
     // one message for doc byte `b` (2-message 251 look-ahead, PiXiuStr.cpp:33-54)
@@ -442,67 +527,97 @@ struct GstWave {
         }
     }
 
-    // ---- Ukkonen step pieces (SuffixTree.cpp:144-289) ----
-    PX_DEV void at_root(uint32_t c, bool send) {
-        uint32_t e = uni(root_kids[c]);
-        if (e == kNone) {
-            Edge leaf;
-            if (!new_node(leaf, cur_base + counter, cur, counter, cur_len, 0)) return;
-            set_child(kRoot, c, leaf.id);
-            --remainder;
-            if (send) feed(false, 0, 0, c);
-        } else {
-            Edge ed = load(e);
-            act_doc = ed.doc;
-            act_direct = ed.from;
-            act_off = (act_off + 1) & 0xffffu;
-            if (send) feed(true, ed.doc, ed.from, c);
-        }
+    // ---- Ukkonen step pieces (SuffixTree.cpp:144-289)
+    PX_DEV bool new_leaf(Edge &leaf, uint32_t c) {
+        if (!new_node(leaf.id)) return false;
+        nodes[2 * leaf.id] = make_uint4(kRoot, 0, 0, 0);  // link, child count
+        leaf.doc = cur;
+        leaf.from = counter;
+        leaf.to = cur_len;
+        leaf.cnt = 0;
+        leaf.key = c;
+        return true;
     }
 
-    // overflow_fix: canonise the active point along the current text
-    PX_DEV bool canonise(Edge &e) {
-        int32_t end = (int32_t)counter;
-        int32_t begin = end - (int32_t)act_off;
-        uint32_t id;
-        if (!must_child(act_node, tbyte(cur_base + counter - act_off), &id)) return false;
-        e = load(id);
-        int32_t supply;
-        while (end - begin > (supply = (int32_t)e.to - (int32_t)e.from)) {
-            act_node = e.id;
-            begin += supply;
-            act_off = (act_off - (uint32_t)supply) & 0xffffu;
-            if (!must_child(act_node, tbyte(cur_base + (uint32_t)begin), &id)) return false;
-            e = load(id);
-            act_direct = e.from;
+    // case_root: returns true (and the edge) when the byte exists under the root
+    PX_DEV bool at_root(uint32_t c, bool send, Edge &e) {
+        uint32_t slot, ncnt;
+        if (!lookup(kRoot, c, e, slot, ncnt)) {
+            Edge leaf;
+            if (!new_leaf(leaf, c)) return false;
+            charge(kEdgeBlocks);
+            write_entry(slot, kRoot, leaf);
+            --remainder;
+            if (send) feed(false, 0, 0, c);
+            return false;
+        }
+        set_act_doc(e.doc);
+        act_direct = e.from;
+        act_off = (act_off + 1) & 0xffffu;
+        if (send) feed(true, e.doc, e.from, c);
+        return true;
+    }
+
+    PX_DEV bool must_lookup(uint32_t n, uint32_t c, Edge &e) {
+        if (!lookup(n, c, e)) {
+            if (status == kOk) fail(kErrRefCrash);  // the reference dereferences NULL here
+            return false;
         }
         return true;
     }
 
-    // split_grow
-    PX_DEV bool grow(Edge &e, uint32_t &last_inner) {
+    // overflow_fix: canonise the active point along the current text
+    PX_DEV bool canonise(Edge &e) {
+        if (!must_lookup(act_node, curchar(counter - act_off), e)) return false;
+        uint32_t supply;
+        while (act_off > (supply = e.to - e.from)) {
+            act_node = e.id;
+            act_off = (act_off - supply) & 0xffffu;
+            if (!must_lookup(act_node, curchar(counter - act_off), e)) return false;
+            act_direct = e.from;
+            PX_CNT(P_CANON_LVL, 1);
+        }
+        return true;
+    }
+
+    // split_grow: `split` and the byte of e at the split point were computed by
+    // the caller (their loads were issued before this function's stores)
+    PX_DEV bool grow(Edge &e, uint32_t &last_inner, uint32_t c, bool split, uint32_t key_e) {
         Edge leaf;
-        if (!new_node(leaf, cur_base + counter, cur, counter, cur_len, 0)) return false;
+        if (!new_leaf(leaf, c)) return false;
         --remainder;
-        bool e_leaf = e.id != kRoot && !(e.flags & kFlagKids);
-        if ((e_leaf || e.to - e.from > 1) && e.from + act_off != e.to) {
+        if (split) {
             Edge in;
-            if (!new_node(in, e.abs, e.doc, e.from, (e.from + act_off) & 0xffffu, kFlagKids)) return false;
-            if (last_inner != kNone) set_link(last_inner, in.id);
+            if (!new_node(in.id)) return false;
+            if (last_inner != kNone) nodes[2 * last_inner].x = in.id;
             last_inner = in.id;
-            set_child(act_node, tbyte(in.abs), in.id);  // replaces e under its first byte
+            in.doc = e.doc;
+            in.from = e.from;
+            in.to = (e.from + act_off) & 0xffffu;
+            in.key = e.key;
+            in.cnt = key_e != c ? 2 : 1;
+            write_entry(e.slot, act_node, in);  // replaces e under its first byte: no charge
             e.from = in.to;
-            e.abs += act_off;
-            store_label(e);
-            set_child(in.id, tbyte(e.abs), e.id);
-            set_child(in.id, tbyte(leaf.abs), leaf.id);
+            e.key = key_e;
+            // inner->set_sub(edge); inner->set_sub(leaf): an equal key replaces
+            charge(kEdgeBlocks);
+            if (key_e != c) {
+                charge(kEdgeBlocks);
+                nodes[2 * in.id] = make_uint4(kRoot, 2, pk0(e), pk1(e));
+                nodes[2 * in.id + 1] = make_uint4(pk2(e), pk0(leaf), pk1(leaf), pk2(leaf));
+                e.slot = kInlineSlot | in.id;
+            } else {
+                nodes[2 * in.id] = make_uint4(kRoot, 1, pk0(leaf), pk1(leaf));
+                reinterpret_cast<uint32_t *>(&nodes[2 * in.id])[4] = pk2(leaf);
+                e.slot = kNone;  // e fell out of the tree (replaced under the same byte)
+            }
         } else {
-            if (last_inner != kNone) set_link(last_inner, e.id);
+            if (last_inner != kNone) nodes[2 * last_inner].x = e.id;
             last_inner = e.id;
-            set_child(e.id, tbyte(leaf.abs), leaf.id);
-            if (!(e.flags & kFlagKids)) {
-                e.flags |= kFlagKids;
-                store_label(e);
+            add_child(e.id, e.cnt, leaf);
+            if (e.cnt < 3) {
+                ++e.cnt;
+                write_entry(e.slot, act_node, e);
             }
         }
         return true;
@@ -513,8 +628,6 @@ struct GstWave {
     // matching prefix as COMPRESS messages in bulk.  Returns matched length.
     PX_DEV uint32_t fast_forward(const Edge &e, uint32_t i) {
         const uint32_t lane = lane_id();
-        uint32_t base_a = uni(doc_base[act_doc]);
-        uint32_t len_a = uni(doc_base[act_doc + 1]) - base_a;
         uint32_t limit = min(e.to - e.from - act_off, cur_len - i);
         uint32_t m = 0;
         while (m < limit) {
@@ -522,15 +635,15 @@ struct GstWave {
             uint32_t t = e.from + act_off + m + lane;  // position in the active doc
             bool live = lane < w;
             uint32_t a = live ? text[cur_base + i + m + lane] : 0;
-            bool oob = live && t >= len_a;
-            uint32_t b = (live && !oob) ? text[base_a + t] : 0x100u;
+            bool oob = live && t >= act_len;
+            uint32_t b = (live && !oob) ? text[act_base + t] : 0x100u;
             uint64_t mism = ballot(live && (oob || a != b));
             uint64_t m251 = ballot(live && a == kEsc);
             uint32_t got = mism ? ffs64(mism) : w;
             if (got) feed_bulk(e.doc, e.from + act_off + m, got, m251);
             m += got;
             if (mism) {
-                if ((mism >> got) & 1ull && readlane((uint32_t)oob, got)) ++ub;
+                if (readlane((uint32_t)oob, got)) ++ub;
                 break;
             }
         }
@@ -544,39 +657,49 @@ struct GstWave {
         counter = 0;
         act_node = kRoot;
         act_doc = act_direct = act_off = 0;
+        act_base = docbase(0);
+        act_len = docbase(1) - act_base;
         out = flushed = run = applied = held = 0;
+        load_window(0);
         bool have_e = false;
         Edge e;
         uint32_t i = 0;
         while (i < len && status == kOk) {
-            const uint32_t c = tbyte(cur_base + i);
+            if (i - wb >= kWin - 64 && i - wb < 0x80000000u) load_window(i >= 64 ? i - 64 : 0);
+            const uint32_t c = curchar(i);
             PX_TRACE_STATE(0);
+            PX_CNT(P_BYTES, 1);
             if (act_node == kRoot && act_off == 0) {
+                PX_T0();
                 ++remainder;
-                at_root(c, true);
+                have_e = at_root(c, true, e);
                 ++counter;
                 ++i;
-                have_e = false;
+                PX_CNT(P_ROOT, 1);
+                PX_T1(P_T_ROOT);
                 continue;
             }
             if (!have_e) {
-                int32_t key = stale_byte(act_doc, act_direct);
-                uint32_t id;
+                PX_T0();
+                int32_t key = stale_byte(act_direct);
                 if (key < 0) {
                     fail(kErrRefCrash);  // get_sub(garbage) -> NULL deref in the reference
                     break;
                 }
-                if (!must_child(act_node, (uint32_t)key, &id)) break;
-                e = load(id);
+                if (!must_lookup(act_node, (uint32_t)key, e)) break;
                 have_e = true;
+                PX_T1(P_T_DERIVE);
             }
             if (e.from + act_off == e.to) {
-                uint32_t nx = (e.flags & kFlagKids) ? child(e.id, c) : kNone;
-                if (nx != kNone) {
+                Edge n;
+                PX_T0();
+                bool wd = e.cnt && lookup(e.id, c, n);
+                PX_T1(P_T_WALK);
+                if (wd) {
+                    PX_CNT(P_WALK, 1);
                     ++remainder;
-                    Edge n = load(nx);
                     act_node = e.id;
-                    act_doc = n.doc;
+                    set_act_doc(n.doc);
                     act_direct = n.from;
                     act_off = 1;
                     feed(true, n.doc, n.from, c);
@@ -586,7 +709,11 @@ struct GstWave {
                     continue;
                 }
             } else if (e.from + act_off < e.to) {
+                PX_T0();
                 uint32_t m = fast_forward(e, i);
+                PX_T1(P_T_FF);
+                PX_CNT(P_FF_CALLS, 1);
+                PX_CNT(P_FF_BYTES, m);
 #ifdef PX_TRACE
                 for (uint32_t k = 1; k < m; ++k) PX_TRACE_STATE(k);
 #endif
@@ -599,40 +726,69 @@ struct GstWave {
                 }
             }
             // mismatch: emit PASS, then split/grow along suffix links
+            PX_CNT(P_PASS, 1);
+            PX_T0();
             ++remainder;
             feed(false, 0, 0, c);
             uint32_t last_inner = kNone;
+            // e's own byte at the split point, when an earlier read already has it
+            int32_t e_next = -1;
+            // the suffix link of act_node is loaded one iteration ahead (next to the
+            // previous end check), so an iteration costs two dependent round trips
+            uint32_t lraw = act_node != kRoot ? nodes[2 * act_node].x : 0u;
             while (remainder > 0 && status == kOk) {
-                if (!grow(e, last_inner)) break;
-                if (act_node == kRoot || !(flags_of(act_node) & kFlagKids)) {
+                PX_CNT(P_ITERS, 1);
+#ifdef PX_PROFILE
+                uint64_t tg = __builtin_amdgcn_s_memtime();
+#endif
+                const bool split = (!e.cnt || e.to - e.from > 1) && e.from + act_off != e.to;
+                uint32_t key_e = 0;
+                if (split) key_e = e_next >= 0 ? (uint32_t)e_next : tbyte(docbase(e.doc) + e.from + act_off);
+                if (!grow(e, last_inner, c, split, key_e)) break;
+#ifdef PX_PROFILE
+                prof[P_T_GROW] += __builtin_amdgcn_s_memtime() - tg;
+                tg = __builtin_amdgcn_s_memtime();
+#endif
+                e_next = -1;
+                if (act_node == kRoot) {  // STNode::is_inner(act_node) == (act_node != root) here
                     act_off = (act_off - 1) & 0xffffu;
                     act_direct = (act_direct + 1) & 0xffffu;
                     if (act_off > 0) {
                         if (!canonise(e)) break;
                     } else {
-                        at_root(c, false);
+                        at_root(c, false, e);
                         break;
                     }
                 } else {
-                    act_node = load(act_node).link;
+                    PX_CNT(P_LINK, 1);
+                    act_node = uni(lraw);
                     if (!canonise(e)) break;
                 }
+#ifdef PX_PROFILE
+                prof[P_T_CANON] += __builtin_amdgcn_s_memtime() - tg;
+#endif
+                // next iteration's suffix link, issued before this end check's wait
+                lraw = act_node != kRoot ? nodes[2 * act_node].x : 0u;
                 if (e.from + act_off == e.to) {
-                    uint32_t nx = (e.flags & kFlagKids) ? child(e.id, c) : kNone;
-                    if (nx != kNone) {
-                        Edge n = load(nx);
+                    Edge n;
+                    if (e.cnt && lookup(e.id, c, n)) {
                         act_node = e.id;
-                        act_doc = n.doc;
+                        set_act_doc(n.doc);
                         act_direct = n.from;
                         act_off = 1;
-                        if (last_inner != kNone) set_link(last_inner, act_node);
+                        if (last_inner != kNone) nodes[2 * last_inner].x = act_node;
                         break;
                     }
-                } else if (e.from + act_off < e.to && c == tbyte(e.abs + act_off)) {
-                    act_off = (act_off + 1) & 0xffffu;
-                    break;
+                } else if (e.from + act_off < e.to) {
+                    uint32_t ch = tbyte(docbase(e.doc) + e.from + act_off);
+                    if (c == ch) {
+                        act_off = (act_off + 1) & 0xffffu;
+                        break;
+                    }
+                    e_next = (int32_t)ch;
                 }
             }
+            PX_T1(P_T_SPLIT);
             have_e = false;
             ++counter;
             ++i;
@@ -649,20 +805,20 @@ __global__ void __launch_bounds__(64) k_gst_encode(const GstShard *shards, uint3
                                                    const uint32_t *doc_len, uint8_t *const *comp_dst,
                                                    uint32_t *comp_len, uint32_t *rec_chunk,
                                                    uint32_t *rec_idx, uint32_t *rec_status) {
-    __shared__ uint8_t obuf[kObuf];
+    __shared__ GstLds lds;
     const uint32_t s = blockIdx.x;
     if (s >= n_shards) return;
+    const uint32_t lane = lane_id();
     const GstShard sh = shards[s];
     ShardState st = *sh.st;
     GstWave g;
-    g.sh = &shards[s];
     g.doc_base = sh.doc_base;
     g.nodes = sh.nodes;
     g.hash = sh.hash;
-    g.root_kids = sh.root_kids;
     g.node_cap = sh.node_cap;
     g.hash_mask = sh.hash_mask;
     g.doc_cap = sh.doc_cap;
+    g.lds = &lds;
     g.n_nodes = uni(st.n_nodes);
     g.n_docs = uni(st.n_docs);
     g.chunk_seq = uni(st.chunk_seq);
@@ -674,17 +830,23 @@ __global__ void __launch_bounds__(64) k_gst_encode(const GstShard *shards, uint3
     g.ctext_off = uni64(st.ctext_off);
     g.ub = uni64(st.ub_reads);
     g.text = sh.text + g.ctext_off;
-    g.obuf = obuf;
+#ifdef PX_PROFILE
+    for (int k = 0; k < P_N; ++k) g.prof[k] = 0;
+    uint64_t t_kernel0 = __builtin_amdgcn_s_memtime();
+#endif
+    // stage the persistent root entries and doc starts into LDS
+    for (uint32_t c = lane; c < 256; c += 64) lds.root[c] = sh.root[c];
+    for (uint32_t d = lane; d <= kDocCache; d += 64) lds.doc_base[d] = d <= g.n_docs ? sh.doc_base[d] : 0;
+    __syncthreads();
     if (g.epoch == 0) {  // brand-new shard
-        g.epoch = 0;
         g.clear_tree();
-        g.doc_base[0] = 0;
+        g.set_docbase(0, 0);
         g.n_docs = 0;
     }
     for (uint32_t r = sh.r0; r < sh.r1; ++r) {
         const uint32_t len = uni(doc_len[r]);
         if (g.status != kOk || len == 0xffffffffu) {
-            if (lane_id() == 0) {
+            if (lane == 0) {
                 rec_status[r] = g.status != kOk ? g.status : (uint32_t)kErrInval;
                 comp_len[r] = 0;
             }
@@ -692,33 +854,41 @@ __global__ void __launch_bounds__(64) k_gst_encode(const GstShard *shards, uint3
         }
         // rotation (PiXiuCtrl.cpp:13-25): before the doc, by pool count or slot count
         if (g.pools >= kRotatePools || g.n_docs == (uint32_t)kChunkSlots) {
-            uint32_t shift = uni(g.doc_base[g.n_docs]);
+            uint32_t shift = g.docbase(g.n_docs);
             g.ctext_off += shift;
             g.text = sh.text + g.ctext_off;
             g.n_docs = 0;
-            g.doc_base[0] = 0;
+            g.set_docbase(0, 0);
             ++g.chunk_seq;
             g.clear_tree();
         }
         if (g.n_docs >= g.doc_cap) {
             g.fail(kErrCapacity);
-            if (lane_id() == 0) rec_status[r] = g.status;
+            if (lane == 0) rec_status[r] = g.status;
             continue;
         }
         g.cur = g.n_docs;
-        g.cur_base = uni(g.doc_base[g.cur]);
-        g.doc_base[g.cur + 1] = g.cur_base + len;
+        g.cur_base = g.docbase(g.cur);
+        g.set_docbase(g.cur + 1, g.cur_base + len);
+        __syncthreads();
         g.out_dst = comp_dst[r];
         g.encode_doc(len);
         ++g.n_docs;
-        if (lane_id() == 0) {
+        if (lane == 0) {
             comp_len[r] = g.out;
             rec_chunk[r] = g.chunk_seq;
             rec_idx[r] = g.cur;
             rec_status[r] = g.status;
         }
     }
-    if (lane_id() == 0) {
+    __syncthreads();
+#ifdef PX_PROFILE
+    g.prof[P_T_TOTAL] = __builtin_amdgcn_s_memtime() - t_kernel0;
+    if (lane == 0)
+        for (int k = 0; k < P_N; ++k) atomicAdd(&g_prof[k], (unsigned long long)g.prof[k]);
+#endif
+    for (uint32_t c = lane; c < 256; c += 64) sh.root[c] = lds.root[c];
+    if (lane == 0) {
         ShardState o;
         o.n_nodes = g.n_nodes;
         o.pools = g.pools;
@@ -1038,20 +1208,28 @@ __global__ void __launch_bounds__(64) k_decode(const DecodeQuery *qs, uint32_t n
 }
 
 // ====================================================================== migrate
-__global__ void __launch_bounds__(256) k_rehash(const uint64_t *old_tab, uint32_t old_cap, uint32_t epoch,
-                                                uint64_t *new_tab, uint32_t new_mask) {
+// Re-insert the live-epoch entries of a child map into a larger (zeroed) table.
+__global__ void __launch_bounds__(256) k_rehash(const uint4 *old_tab, uint32_t old_n, uint32_t epoch,
+                                                uint4 *new_tab, uint32_t new_mask) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= old_cap) return;
-    uint64_t e = old_tab[i];
-    if ((uint32_t)(e >> 60) != epoch) return;
-    uint32_t parent = (uint32_t)(e >> 34) & ((1u << kNodeBits) - 1u);
-    uint32_t c = (uint32_t)(e >> 26) & 0xffu;
-    uint32_t h = hslot(parent, c);
+    if (i >= old_n) return;
+    uint4 e = old_tab[i];
+    if ((e.x >> 26) != epoch) return;
+    uint32_t parent = e.x & kNodeMask;
+    uint32_t c = (e.w >> 16) & 0xffu;
+    uint32_t nb = (new_mask + 1) / kBucket;
+    uint32_t b = hslot(parent, c) & (nb - 1);
     for (;;) {
-        uint32_t s = h & new_mask;
-        unsigned long long prev = atomicCAS((unsigned long long *)&new_tab[s], 0ull, (unsigned long long)e);
-        if (prev == 0ull) return;
-        ++h;
+        for (uint32_t l = 0; l < kBucket; ++l) {
+            uint32_t *slot = reinterpret_cast<uint32_t *>(&new_tab[b * kBucket + l]);
+            if (atomicCAS(slot, 0u, e.x) == 0u) {
+                slot[1] = e.y;
+                slot[2] = e.z;
+                slot[3] = e.w;
+                return;
+            }
+        }
+        b = (b + 1) & (nb - 1);
     }
 }
 
@@ -1109,6 +1287,20 @@ hipError_t launch_decode(hipStream_t s, const DecodeQuery *qs, uint32_t nq, cons
     return hipGetLastError();
 }
 
+int debug_prof_take(unsigned long long *out, uint32_t cap) {
+#ifdef PX_PROFILE
+    uint32_t n = cap < (uint32_t)P_N ? cap : (uint32_t)P_N;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), n * 8) != hipSuccess) return -1;
+    unsigned long long z[P_N] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof z);
+    return (int)n;
+#else
+    (void)out;
+    (void)cap;
+    return -1;
+#endif
+}
+
 int debug_trace_take(int32_t *out, uint32_t cap) {
 #ifdef PX_TRACE
     uint32_t n = 0;
@@ -1125,8 +1317,8 @@ int debug_trace_take(int32_t *out, uint32_t cap) {
 #endif
 }
 
-hipError_t launch_rehash(hipStream_t s, const uint64_t *old_tab, uint32_t old_cap, uint32_t epoch,
-                         uint64_t *new_tab, uint32_t new_mask) {
+hipError_t launch_rehash(hipStream_t s, const uint4 *old_tab, uint32_t old_cap, uint32_t epoch,
+                         uint4 *new_tab, uint32_t new_mask) {
     if (!old_cap) return hipSuccess;
     k_rehash<<<(old_cap + 255) / 256, 256, 0, s>>>(old_tab, old_cap, epoch, new_tab, new_mask);
     return hipGetLastError();

@@ -32,8 +32,9 @@ hipError_t launch_compact(hipStream_t, uint32_t, uint8_t *const *, const uint32_
 hipError_t launch_tokenize(hipStream_t, uint32_t, const RecSlot *, uint2 *const *, uint32_t *, uint32_t *);
 hipError_t launch_decode(hipStream_t, const DecodeQuery *, uint32_t, const RecSlot *const *, uint8_t *,
                          uint32_t *, uint32_t *, Frame *, uint32_t, uint32_t);
-hipError_t launch_rehash(hipStream_t, const uint64_t *, uint32_t, uint32_t, uint64_t *, uint32_t);
+hipError_t launch_rehash(hipStream_t, const uint4 *, uint32_t, uint32_t, uint4 *, uint32_t);
 int debug_trace_take(int32_t *, uint32_t);
+int debug_prof_take(unsigned long long *, uint32_t);
 }  // namespace px
 
 using namespace px;
@@ -160,9 +161,10 @@ struct Shard {
     void *arena = nullptr;
     uint64_t arena_bytes = 0;
     ShardState *st = nullptr;
-    uint32_t *root_kids = nullptr, *doc_base = nullptr;
+    uint4 *root_tab = nullptr;
+    uint32_t *doc_base = nullptr;
     uint4 *nodes = nullptr;
-    uint64_t *hash = nullptr;
+    uint4 *hash = nullptr;
     uint8_t *text = nullptr;
     uint32_t node_cap = 0, doc_cap = 0;
     uint64_t hash_cap = 0, text_cap = 0;
@@ -264,7 +266,7 @@ struct px_ctx {
         uint64_t need_nodes = (uint64_t)s.hs.n_nodes + 2 * B + 4;
         uint64_t need_docs = std::min<uint64_t>((uint64_t)s.hs.n_docs + D, kChunkSlots) + 1;
         uint64_t need_text = s.text_end + B;
-        uint64_t need_hash = pow2_at_least(2 * need_nodes);
+        uint64_t need_hash = pow2_at_least(need_nodes);  // only 3rd+ children live in the hash
         if (need_nodes > kMaxNodes) need_nodes = kMaxNodes;
         bool fits = s.arena && need_nodes <= s.node_cap && need_docs <= s.doc_cap && need_text <= s.text_cap &&
                     need_hash <= s.hash_cap;
@@ -275,28 +277,28 @@ struct px_ctx {
         uint64_t doc_cap = std::min<uint64_t>(std::max(need_docs, (uint64_t)s.doc_cap * g), kChunkSlots + 1);
         uint64_t live_text = s.text_end - s.hs.ctext_off;
         uint64_t text_cap = std::max(live_text + B, s.arena ? (live_text + B) * 3 / 2 : live_text + B);
-        uint64_t hash_cap = pow2_at_least(2 * node_cap);
+        uint64_t hash_cap = pow2_at_least(node_cap);
         uint64_t off_root = round_up(sizeof(ShardState), 256);
-        uint64_t off_doc = off_root + 1024;
+        uint64_t off_doc = off_root + 256 * 16;
         uint64_t off_nodes = round_up(off_doc + (doc_cap + 1) * 4, 256);
-        uint64_t off_hash = round_up(off_nodes + node_cap * 16, 256);
-        uint64_t off_text = round_up(off_hash + hash_cap * 8, 256);
-        uint64_t total = round_up(off_text + text_cap + 64, 256);
+        uint64_t off_hash = round_up(off_nodes + node_cap * 32, 256);
+        uint64_t off_text = round_up(off_hash + hash_cap * 16, 256);
+        uint64_t total = round_up(off_text + text_cap + 1024, 256);  // slack: the kernel's 256-byte doc window
         char *a = (char *)heap.alloc(total);
         Shard o = s;  // old view
         s.arena = a;
         s.arena_bytes = total;
         s.st = (ShardState *)a;
-        s.root_kids = (uint32_t *)(a + off_root);
+        s.root_tab = (uint4 *)(a + off_root);
         s.doc_base = (uint32_t *)(a + off_doc);
         s.nodes = (uint4 *)(a + off_nodes);
-        s.hash = (uint64_t *)(a + off_hash);
+        s.hash = (uint4 *)(a + off_hash);
         s.text = (uint8_t *)(a + off_text);
         s.node_cap = (uint32_t)node_cap;
         s.doc_cap = (uint32_t)doc_cap - 1;
         s.hash_cap = hash_cap;
         s.text_cap = text_cap;
-        hcheck(hipMemsetAsync(s.hash, 0, hash_cap * 8, stream));
+        hcheck(hipMemsetAsync(s.hash, 0, hash_cap * 16, stream));
         if (!o.arena) {
             ShardState z{};
             h2d(s.st, &z, sizeof z);
@@ -304,9 +306,9 @@ struct px_ctx {
             return;
         }
         // migrate the live chunk: text moves to offset 0, everything else by copy / rehash
-        hcheck(hipMemcpyAsync(s.root_kids, o.root_kids, 1024, hipMemcpyDeviceToDevice, stream));
+        hcheck(hipMemcpyAsync(s.root_tab, o.root_tab, 256 * 16, hipMemcpyDeviceToDevice, stream));
         hcheck(hipMemcpyAsync(s.doc_base, o.doc_base, ((size_t)o.hs.n_docs + 1) * 4, hipMemcpyDeviceToDevice, stream));
-        hcheck(hipMemcpyAsync(s.nodes, o.nodes, (size_t)o.hs.n_nodes * 16, hipMemcpyDeviceToDevice, stream));
+        hcheck(hipMemcpyAsync(s.nodes, o.nodes, (size_t)o.hs.n_nodes * 32, hipMemcpyDeviceToDevice, stream));
         hcheck(launch_rehash(stream, o.hash, (uint32_t)o.hash_cap, o.hs.epoch, s.hash, (uint32_t)(hash_cap - 1)));
         hcheck(hipMemcpyAsync(s.text, o.text + o.hs.ctext_off, live_text, hipMemcpyDeviceToDevice, stream));
         s.hs.ctext_off = 0;
@@ -709,7 +711,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         g.doc_base = w.s->doc_base;
         g.nodes = w.s->nodes;
         g.hash = w.s->hash;
-        g.root_kids = w.s->root_kids;
+        g.root = w.s->root_tab;
         g.st = w.s->st;
         g.node_cap = w.s->node_cap;
         g.hash_mask = (uint32_t)(w.s->hash_cap - 1);
@@ -1242,5 +1244,7 @@ void *px_stream(px_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
 
 // debug builds (make trace): per-byte encoder messages of the first shard of the last batch
 int px_debug_trace_take(int32_t *out, uint32_t cap) { return px::debug_trace_take(out, cap); }
+// debug builds (make prof): k_gst_encode counters/cycles accumulated since the last call
+int px_debug_prof_take(unsigned long long *out, uint32_t cap) { return px::debug_prof_take(out, cap); }
 
 }  // extern "C"
