@@ -69,12 +69,17 @@ struct GstShard {
 };
 
 // compressed-record slot: what a chunk table entry points at
-struct RecSlot {
-    const uint8_t *comp;  // compressed bytes
-    const uint2 *seg;     // segment index: (src_start, comp_start) x (nseg + 1)
+struct alignas(16) RecSlot {
+    const uint8_t *comp;    // compressed bytes
+    const uint4 *seg;       // segment index, nseg entries + a sentinel (see k_tokenize)
+    const uint16_t *pidx;   // position index: pidx[b] = segment holding source position 16b
     uint32_t comp_len;
     uint32_t nseg;
+    uint32_t pidx_n;        // blocks in pidx (0: no position index, serial decode only)
+    uint32_t pad;
+    uint64_t pad2;          // 48 bytes: three 16-byte loads on the device
 };
+static_assert(sizeof(RecSlot) == 48, "RecSlot is loaded as three 16-byte vectors");
 
 // decode query
 struct DecodeQuery {
@@ -84,10 +89,12 @@ struct DecodeQuery {
     uint64_t out_off;     // where the output goes
     uint32_t out_cap;     // consumer stops pulling after this many bytes
     uint32_t mode;        // 0 compat, 1 exact
+    uint32_t nrec;        // records in the chunk (record tokens are bounds-checked against it)
+    uint32_t pad;
 };
 
 // decode frame (scratch, one stack per wave)
-struct Frame {
+struct alignas(16) Frame {
     uint32_t rec;     // chunk-local idx of the record being parsed ("self")
     int32_t from;
     int32_t len;
@@ -99,6 +106,7 @@ struct Frame {
     uint32_t pstart;  // output position where the pending child began
     int32_t sub_from, sub_to, supply;
 };
+static_assert(sizeof(Frame) == 48, "Frame is moved as three 16-byte vectors");
 
 enum Status : uint32_t {
     kOk = 0,

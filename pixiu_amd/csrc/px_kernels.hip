@@ -21,10 +21,16 @@
 using namespace px;
 
 #define PX_DEV __device__ __forceinline__
+// explicit address spaces: pointers reached through structs would otherwise be
+// flat, and every flat access waits for all outstanding vector-memory AND LDS ops
+#define PX_GAS __attribute__((address_space(1)))
+#define PX_LAS __attribute__((address_space(3)))
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
 PX_DEV uint32_t lane_id() { return threadIdx.x & 63u; }
+PX_DEV u32x4 mk4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return u32x4{a, b, c, d}; }
 
 #ifdef PX_TRACE
 // debug build only: per-byte encoder message log (cmd, pos, byte) of shard 0
@@ -69,7 +75,8 @@ PX_DEV uint32_t rd16(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1]
 #ifdef PX_PROFILE
 // debug build only: per-category counters and shader-clock cycles of k_gst_encode
 enum { P_BYTES, P_FF_CALLS, P_FF_BYTES, P_PASS, P_ITERS, P_LOOKUPS, P_PROBES, P_ROOT, P_WALK, P_LINK, P_CANON_LVL,
-       P_T_TOTAL, P_T_FF, P_T_DERIVE, P_T_WALK, P_T_SPLIT, P_T_GROW, P_T_CANON, P_T_END, P_T_ROOT, P_T_ENC, P_N };
+       P_T_TOTAL, P_T_FF, P_T_DERIVE, P_T_WALK, P_T_SPLIT, P_T_GROW, P_T_CANON, P_T_END, P_T_ROOT, P_T_ENC,
+       P_KEYMISS, P_T_KEY, P_T_LOOK, P_N };
 __device__ unsigned long long g_prof[P_N];
 #define PX_CNT(k, v) (prof[k] += (v))
 #define PX_T0() uint64_t _t0 = __builtin_amdgcn_s_memtime()
@@ -161,6 +168,11 @@ constexpr uint32_t kDocCache = 256;  // doc starts cached in LDS
 constexpr uint32_t kRootSlot = 0x80000000u;
 constexpr uint32_t kWin = 256;  // current-doc window (4 bytes per lane)
 
+// GST blocks are exactly one wave: LDS ops of a wave execute in order, so lanes
+// exchanging data through LDS need only a compiler barrier, not s_barrier (whose
+// fence would also wait for every outstanding global load and store)
+PX_DEV void wave_sync() { asm volatile("" ::: "memory"); }
+
 PX_DEV uint32_t hslot(uint32_t parent, uint32_t c) {
     uint32_t h = parent * 0x9E3779B1u ^ (c + 1u) * 0x85EBCA77u;
     h ^= h >> 15;
@@ -178,19 +190,19 @@ struct Edge {
 constexpr uint32_t kInlineSlot = 0x40000000u;  // | which << 26 | parent
 
 struct GstLds {
-    uint4 root[256];
+    u32x4 root[256];
     uint32_t doc_base[kDocCache + 1];
     uint8_t obuf[kObuf];
 };
 
 struct GstWave {
     // shard arena
-    uint8_t *text;  // live chunk text base
-    uint32_t *doc_base;
-    uint4 *nodes;   // 2 x uint4 per node: {link, cnt, e0.w0, e0.w1}, {e0.w2, e1.w0, e1.w1, e1.w2}
-    uint4 *hash;
+    PX_GAS uint8_t *text;  // live chunk text base
+    PX_GAS uint32_t *doc_base;
+    PX_GAS u32x4 *nodes;   // 2 x uint4 per node: {link, cnt, e0.w0, e0.w1}, {e0.w2, e1.w0, e1.w1, e1.w2}
+    PX_GAS u32x4 *hash;
     uint32_t node_cap, hash_mask, doc_cap;
-    GstLds *lds;
+    PX_LAS GstLds *lds;
     // persistent counters
     uint32_t n_nodes, n_docs, chunk_seq, epoch, status;
     int32_t pools, used, pool_open;
@@ -202,7 +214,7 @@ struct GstWave {
     int32_t remainder;
     // encoder (the reference keeps these as statics, PiXiuStr.cpp:17-26)
     uint32_t out, flushed, run, run_idx, run_to, applied, held, h_c, h_idx, h_pos;
-    uint8_t *out_dst;
+    PX_GAS uint8_t *out_dst;
 #ifdef PX_PROFILE
     uint64_t prof[P_N];
 #endif
@@ -245,7 +257,7 @@ struct GstWave {
     PX_DEV void load_window(uint32_t at) {
         uint32_t abs0 = (cur_base + at) & ~3u;  // 4-byte aligned window start
         wb = abs0 - cur_base;                    // may wrap below 0 (unsigned): range tests cope
-        win = *reinterpret_cast<const uint32_t *>(text + abs0 + 4 * lane_id());
+        win = *(const PX_GAS uint32_t *)(text + abs0 + 4 * lane_id());
     }
     PX_DEV uint32_t curchar(uint32_t p) {  // byte p of the current doc
         uint32_t d = p - wb;
@@ -262,6 +274,8 @@ struct GstWave {
         }
         return (int32_t)tbyte(act_base + pos);
     }
+
+    PX_DEV PX_GAS uint32_t *nrec(uint32_t n) const { return (PX_GAS uint32_t *)&nodes[2 * n]; }
 
     // ---- child map
     PX_DEV static void unpack(uint32_t w0, uint32_t w1, uint32_t w2, Edge &e) {
@@ -280,7 +294,7 @@ struct GstWave {
     // child goes (kNone: a hash slot must still be probed) and ncnt = n's count.
     PX_DEV bool lookup(uint32_t n, uint32_t c, Edge &e, uint32_t &slot, uint32_t &ncnt) {
         if (n == kRoot) {
-            uint4 v = lds->root[c];
+            u32x4 v = lds->root[c];
             slot = kRootSlot | c;
             ncnt = 3;
             if (uni(v.y) == kNone) return false;
@@ -293,8 +307,8 @@ struct GstWave {
         const uint32_t nb = (hash_mask >> 2);
         uint32_t b = hslot(n, c) & nb;
         // the node record and the first hash bucket, issued together
-        uint4 r0 = nodes[2 * n], r1 = nodes[2 * n + 1];
-        uint4 v = lane < kBucket ? hash[b * kBucket + lane] : make_uint4(0, 0, 0, 0);
+        u32x4 r0 = nodes[2 * n], r1 = nodes[2 * n + 1];
+        u32x4 v = lane < kBucket ? hash[b * kBucket + lane] : mk4(0, 0, 0, 0);
         ncnt = uni(r0.y);
         if (ncnt >= 1 && ((uni(r1.x) >> 16) & 0xffu) == c) {
             unpack(uni(r0.z), uni(r0.w), uni(r1.x), e);
@@ -332,7 +346,7 @@ struct GstWave {
                 return false;
             }
             b = (b + 1) & nb;
-            v = lane < kBucket ? hash[b * kBucket + lane] : make_uint4(0, 0, 0, 0);
+            v = lane < kBucket ? hash[b * kBucket + lane] : mk4(0, 0, 0, 0);
         }
         fail(kErrCapacity);
         slot = kNone;
@@ -349,7 +363,7 @@ struct GstWave {
         uint32_t b = hslot(n, c) & nb;
         for (uint32_t guard = 0; guard <= nb; ++guard) {
             PX_CNT(P_PROBES, 1);
-            uint4 v = lane < kBucket ? hash[b * kBucket + lane] : make_uint4(0, 0, 0, 0);
+            u32x4 v = lane < kBucket ? hash[b * kBucket + lane] : mk4(0, 0, 0, 0);
             uint64_t me = ballot(lane < kBucket && (v.x >> 26) != epoch);
             if (me) return b * kBucket + ffs64(me);
             b = (b + 1) & nb;
@@ -359,16 +373,16 @@ struct GstWave {
     }
     PX_DEV void write_entry(uint32_t slot, uint32_t parent, const Edge &e) {
         if (slot & kRootSlot) {
-            lds->root[slot & 0xffu] = make_uint4(0, pk0(e), pk1(e), pk2(e));
+            lds->root[slot & 0xffu] = mk4(0, pk0(e), pk1(e), pk2(e));
         } else if (slot & kInlineSlot) {
             uint32_t n = slot & kNodeMask;
-            uint32_t *rec = reinterpret_cast<uint32_t *>(&nodes[2 * n]);
+            PX_GAS uint32_t *rec = nrec(n);
             uint32_t o = (slot >> 26) & 1u ? 5 : 2;  // e1 at words 5..7, e0 at words 2..4
             rec[o] = pk0(e);
             rec[o + 1] = pk1(e);
             rec[o + 2] = pk2(e);
         } else if (slot != kNone) {
-            hash[slot] = make_uint4(parent | (epoch << 26), pk0(e), pk1(e), pk2(e));
+            hash[slot] = mk4(parent | (epoch << 26), pk0(e), pk1(e), pk2(e));
         }
     }
     // add a child that is known to be absent (charges one map entry)
@@ -376,7 +390,7 @@ struct GstWave {
         charge(kEdgeBlocks);
         uint32_t slot = pcnt < 2 ? (kInlineSlot | (pcnt << 26) | parent) : hash_free_slot(parent, kid.key);
         write_entry(slot, parent, kid);
-        if (parent != kRoot && pcnt < 3) reinterpret_cast<uint32_t *>(&nodes[2 * parent])[1] = pcnt + 1;
+        if (parent != kRoot && pcnt < 3) nrec(parent)[1] = pcnt + 1;
     }
 
     PX_DEV bool new_node(uint32_t &id) {
@@ -396,14 +410,14 @@ struct GstWave {
         pools = 0;
         used = 0;
         pool_open = 0;
-        for (uint32_t c = lane; c < 256; c += 64) lds->root[c] = make_uint4(0, kNone, 0, 0);
+        for (uint32_t c = lane; c < 256; c += 64) lds->root[c] = mk4(0, kNone, 0, 0);
         if (++epoch > (uint32_t)kMaxEpoch) {  // epochs exhausted: really clear
-            for (uint32_t s = lane; s <= hash_mask; s += 64) hash[s] = make_uint4(0, 0, 0, 0);
+            for (uint32_t s = lane; s <= hash_mask; s += 64) hash[s] = mk4(0, 0, 0, 0);
             epoch = 1;
         }
-        __syncthreads();
+        wave_sync();
         uint32_t root;
-        if (new_node(root)) nodes[2 * root] = make_uint4(kRoot, 0, 0, 0);
+        if (new_node(root)) nodes[2 * root] = mk4(kRoot, 0, 0, 0);
     }
 
     // ---- stream encoder (PiXiuStr_init_stream)
@@ -411,49 +425,49 @@ struct GstWave {
         const uint32_t lane = lane_id();
         uint32_t n = out - flushed;
         if (!all && n < kFlushAt) return;
-        __syncthreads();
+        wave_sync();
+#pragma unroll 1
         for (uint32_t o = lane; o < n; o += 64) out_dst[flushed + o] = lds->obuf[o];
-        __syncthreads();
+        wave_sync();
         flushed = out;
     }
-    PX_DEV void put(uint32_t b) {
-        lds->obuf[out - flushed] = (uint8_t)b;
-        ++out;
+    // append n (<= 64) bytes; lane k holds byte k
+    PX_DEV void put_lanes(uint32_t n, uint32_t b) {
+        if (lane_id() < n) lds->obuf[out - flushed + lane_id()] = (uint8_t)b;
+        wave_sync();
+        out += n;
         flush_obuf(false);
     }
+    PX_DEV void put(uint32_t b) { put_lanes(1, b); }
     PX_DEV void flush_run() {
         if (run == 0) return;
+        const uint32_t lane = lane_id();
+        uint32_t n, b;
         if (run > 6) {
-            put(kEsc);
+            // [251, run, idx:2, to:2] or, past 255, [251, 1, idx:2, to:2, from:2];
+            // run == 251 aliases the escape (PiXiuStr.cpp:72): kept
+            uint32_t w0, w1;
             if (run > 255) {
                 uint32_t from = (run_to - run) & 0xffffu;
-                put(kBigSign);
-                put(run_idx & 0xff);
-                put((run_idx >> 8) & 0xff);
-                put(run_to & 0xff);
-                put((run_to >> 8) & 0xff);
-                put(from & 0xff);
-                put(from >> 8);
+                w0 = kEsc | (uint32_t)kBigSign << 8 | (run_idx & 0xffffu) << 16;
+                w1 = (run_to & 0xffffu) | from << 16;
+                n = 8;
             } else {
-                put(run);  // run == 251 aliases the escape (PiXiuStr.cpp:72): kept
-                put(run_idx & 0xff);
-                put((run_idx >> 8) & 0xff);
-                put(run_to & 0xff);
-                put((run_to >> 8) & 0xff);
+                w0 = kEsc | run << 8 | (run_idx & 0xffffu) << 16;
+                w1 = run_to & 0xffffu;
+                n = 6;
             }
+            b = ((lane < 4 ? w0 : w1) >> ((lane & 3) * 8)) & 0xffu;
         } else {
-            const uint32_t lane = lane_id();
             // the run's bytes were appended literally: they are the doc bytes just consumed
-            uint32_t b = 0;
-            for (uint32_t k = 0; k < run; ++k) {
-                uint32_t v = curchar(applied - run + k);
-                if (lane == k) b = v;
-            }
-            if (lane < run) lds->obuf[out - flushed + lane] = (uint8_t)b;
-            __syncthreads();
-            out += run;
-            flush_obuf(false);
+            uint32_t p = applied - run + lane;
+            uint32_t d = p - wb;
+            uint32_t wv = __shfl(win, (int)((d >> 2) & 63u));
+            b = (wv >> ((d & 3) * 8)) & 0xffu;
+            if (lane < run && d >= kWin) b = text[cur_base + p];
+            n = run;
         }
+        put_lanes(n, b);
         run = 0;
     }
     PX_DEV void apply_c(uint32_t idx, uint32_t pos) {
@@ -479,8 +493,8 @@ struct GstWave {
                 apply_c(h_idx, h_pos);
                 apply_c(idx, pos);
             } else {
-                apply_p();
-                apply_p();
+#pragma unroll 1
+                for (int k = 0; k < 2; ++k) apply_p();
             }
         } else if (b == kEsc) {
             held = 1;
@@ -530,7 +544,7 @@ struct GstWave {
     // ---- Ukkonen step pieces (SuffixTree.cpp:144-289)
     PX_DEV bool new_leaf(Edge &leaf, uint32_t c) {
         if (!new_node(leaf.id)) return false;
-        nodes[2 * leaf.id] = make_uint4(kRoot, 0, 0, 0);  // link, child count
+        nodes[2 * leaf.id] = mk4(kRoot, 0, 0, 0);  // link, child count
         leaf.doc = cur;
         leaf.from = counter;
         leaf.to = cur_len;
@@ -568,7 +582,18 @@ struct GstWave {
 
     // overflow_fix: canonise the active point along the current text
     PX_DEV bool canonise(Edge &e) {
+#ifdef PX_PROFILE
+        uint64_t tk = __builtin_amdgcn_s_memtime();
+        if ((counter - act_off) - wb >= kWin) PX_CNT(P_KEYMISS, 1);
+        uint32_t key0 = curchar(counter - act_off);
+        uint64_t tl = __builtin_amdgcn_s_memtime();
+        prof[P_T_KEY] += tl - tk;
+        bool ok0 = must_lookup(act_node, key0, e);
+        prof[P_T_LOOK] += __builtin_amdgcn_s_memtime() - tl;
+        if (!ok0) return false;
+#else
         if (!must_lookup(act_node, curchar(counter - act_off), e)) return false;
+#endif
         uint32_t supply;
         while (act_off > (supply = e.to - e.from)) {
             act_node = e.id;
@@ -603,12 +628,12 @@ struct GstWave {
             charge(kEdgeBlocks);
             if (key_e != c) {
                 charge(kEdgeBlocks);
-                nodes[2 * in.id] = make_uint4(kRoot, 2, pk0(e), pk1(e));
-                nodes[2 * in.id + 1] = make_uint4(pk2(e), pk0(leaf), pk1(leaf), pk2(leaf));
+                nodes[2 * in.id] = mk4(kRoot, 2, pk0(e), pk1(e));
+                nodes[2 * in.id + 1] = mk4(pk2(e), pk0(leaf), pk1(leaf), pk2(leaf));
                 e.slot = kInlineSlot | in.id;
             } else {
-                nodes[2 * in.id] = make_uint4(kRoot, 1, pk0(leaf), pk1(leaf));
-                reinterpret_cast<uint32_t *>(&nodes[2 * in.id])[4] = pk2(leaf);
+                nodes[2 * in.id] = mk4(kRoot, 1, pk0(leaf), pk1(leaf));
+                nrec(in.id)[4] = pk2(leaf);
                 e.slot = kNone;  // e fell out of the tree (replaced under the same byte)
             }
         } else {
@@ -767,6 +792,9 @@ struct GstWave {
 #ifdef PX_PROFILE
                 prof[P_T_CANON] += __builtin_amdgcn_s_memtime() - tg;
 #endif
+#ifdef PX_PROFILE
+                tg = __builtin_amdgcn_s_memtime();
+#endif
                 // next iteration's suffix link, issued before this end check's wait
                 lraw = act_node != kRoot ? nodes[2 * act_node].x : 0u;
                 if (e.from + act_off == e.to) {
@@ -787,6 +815,9 @@ struct GstWave {
                     }
                     e_next = (int32_t)ch;
                 }
+#ifdef PX_PROFILE
+                prof[P_T_END] += __builtin_amdgcn_s_memtime() - tg;
+#endif
             }
             PX_T1(P_T_SPLIT);
             have_e = false;
@@ -812,13 +843,13 @@ __global__ void __launch_bounds__(64) k_gst_encode(const GstShard *shards, uint3
     const GstShard sh = shards[s];
     ShardState st = *sh.st;
     GstWave g;
-    g.doc_base = sh.doc_base;
-    g.nodes = sh.nodes;
-    g.hash = sh.hash;
+    g.doc_base = (PX_GAS uint32_t *)sh.doc_base;
+    g.nodes = (PX_GAS u32x4 *)sh.nodes;
+    g.hash = (PX_GAS u32x4 *)sh.hash;
     g.node_cap = sh.node_cap;
     g.hash_mask = sh.hash_mask;
     g.doc_cap = sh.doc_cap;
-    g.lds = &lds;
+    g.lds = (PX_LAS GstLds *)&lds;
     g.n_nodes = uni(st.n_nodes);
     g.n_docs = uni(st.n_docs);
     g.chunk_seq = uni(st.chunk_seq);
@@ -829,15 +860,15 @@ __global__ void __launch_bounds__(64) k_gst_encode(const GstShard *shards, uint3
     g.pool_open = unii(st.pool_open);
     g.ctext_off = uni64(st.ctext_off);
     g.ub = uni64(st.ub_reads);
-    g.text = sh.text + g.ctext_off;
+    g.text = (PX_GAS uint8_t *)sh.text + g.ctext_off;
 #ifdef PX_PROFILE
     for (int k = 0; k < P_N; ++k) g.prof[k] = 0;
     uint64_t t_kernel0 = __builtin_amdgcn_s_memtime();
 #endif
     // stage the persistent root entries and doc starts into LDS
-    for (uint32_t c = lane; c < 256; c += 64) lds.root[c] = sh.root[c];
+    for (uint32_t c = lane; c < 256; c += 64) lds.root[c] = ((const PX_GAS u32x4 *)sh.root)[c];
     for (uint32_t d = lane; d <= kDocCache; d += 64) lds.doc_base[d] = d <= g.n_docs ? sh.doc_base[d] : 0;
-    __syncthreads();
+    wave_sync();
     if (g.epoch == 0) {  // brand-new shard
         g.clear_tree();
         g.set_docbase(0, 0);
@@ -856,7 +887,7 @@ __global__ void __launch_bounds__(64) k_gst_encode(const GstShard *shards, uint3
         if (g.pools >= kRotatePools || g.n_docs == (uint32_t)kChunkSlots) {
             uint32_t shift = g.docbase(g.n_docs);
             g.ctext_off += shift;
-            g.text = sh.text + g.ctext_off;
+            g.text = (PX_GAS uint8_t *)sh.text + g.ctext_off;
             g.n_docs = 0;
             g.set_docbase(0, 0);
             ++g.chunk_seq;
@@ -870,8 +901,8 @@ __global__ void __launch_bounds__(64) k_gst_encode(const GstShard *shards, uint3
         g.cur = g.n_docs;
         g.cur_base = g.docbase(g.cur);
         g.set_docbase(g.cur + 1, g.cur_base + len);
-        __syncthreads();
-        g.out_dst = comp_dst[r];
+        wave_sync();
+        g.out_dst = (PX_GAS uint8_t *)comp_dst[r];
         g.encode_doc(len);
         ++g.n_docs;
         if (lane == 0) {
@@ -881,13 +912,13 @@ __global__ void __launch_bounds__(64) k_gst_encode(const GstShard *shards, uint3
             rec_status[r] = g.status;
         }
     }
-    __syncthreads();
+    wave_sync();
 #ifdef PX_PROFILE
     g.prof[P_T_TOTAL] = __builtin_amdgcn_s_memtime() - t_kernel0;
     if (lane == 0)
         for (int k = 0; k < P_N; ++k) atomicAdd(&g_prof[k], (unsigned long long)g.prof[k]);
 #endif
-    for (uint32_t c = lane; c < 256; c += 64) sh.root[c] = lds.root[c];
+    for (uint32_t c = lane; c < 256; c += 64) ((PX_GAS u32x4 *)sh.root)[c] = lds.root[c];
     if (lane == 0) {
         ShardState o;
         o.n_nodes = g.n_nodes;
@@ -918,22 +949,50 @@ __global__ void __launch_bounds__(256) k_compact(uint32_t n, uint8_t *const *src
     }
 }
 
-// Segment index over the token grammar of PXSGen (PiXiuStr.h:139-192):
-// entries (src_start, comp_start | kind << 30) + a sentinel (src_total, comp_len).
-// kind 0 plain (literals and 251-pairs, copied verbatim), 2 record, 1 skip (251 + 3..6).
+// Segment index over the token grammar of PXSGen (PiXiuStr.h:139-192): one 16-byte
+// entry per segment, then a sentinel (src_total, src_total, comp_len, 0):
+//   x = source start          y = source end (= the next segment's start)
+//   z = comp offset | kind << 30   kind 0 plain (literals and 251-pairs, copied
+//       verbatim), 2 record, 1 skip (251 + 3..6: no source bytes)
+//   w = record: idx | from << 16   (to = from + (y - x))
+// pidx[b] = the segment holding source position 16b.  A record whose source
+// positions are not monotone (a record token with to < from) gets no position
+// index (nseg_out bit 31) and is only ever decoded by the serial path.
 constexpr uint32_t kSegRecord = 2u << 30, kSegSkip = 1u << 30, kSegMask = (1u << 30) - 1;
+constexpr uint32_t kNoPidx = 1u << 31;
 
-__global__ void __launch_bounds__(256) k_tokenize(uint32_t n, const RecSlot *slots_in, uint2 *const *seg_out,
-                                                  uint32_t *nseg_out, uint32_t *status) {
+__global__ void __launch_bounds__(256) k_tokenize(uint32_t n, const RecSlot *slots_in, uint32_t *nseg_out,
+                                                  uint32_t *status) {
     const uint32_t lane = lane_id();
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);
     for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < n; r += waves) {
-        const uint8_t *comp = slots_in[r].comp;
-        const uint32_t len = slots_in[r].comp_len;
-        uint2 *seg = seg_out[r];
+        const RecSlot sl = slots_in[r];
+        const PX_GAS uint8_t *comp = (const PX_GAS uint8_t *)sl.comp;
+        const uint32_t len = sl.comp_len;
+        PX_GAS u32x4 *seg = (PX_GAS u32x4 *)sl.seg;
+        PX_GAS uint16_t *pidx = (PX_GAS uint16_t *)sl.pidx;
+        const uint32_t pidx_n = sl.pidx_n;
         uint32_t ns = 0, p = 0, wb = 0, err = 0, plain_start = 0;
-        int32_t src = 0;
-        bool plain_open = false;
+        int32_t src = 0, plain_src = 0;
+        bool plain_open = false, mono = true, have = false;
+        uint32_t pend_x = 0, pend_z = 0, pend_w = 0;
+        // the pending segment is written once the next one starts (its end is then known)
+        auto emit = [&](int32_t x, uint32_t z, uint32_t w) {
+            if (have) {
+                if (lane == 0) seg[ns] = mk4(pend_x, (uint32_t)x, pend_z, pend_w);
+                if (x < (int32_t)pend_x) {
+                    mono = false;
+                } else if (mono && pidx_n) {
+                    uint32_t b0 = (pend_x + 15) >> 4, b1 = min(((uint32_t)x + 15) >> 4, pidx_n);
+                    for (uint32_t b = b0 + lane; b < b1; b += 64) pidx[b] = (uint16_t)ns;
+                }
+                ++ns;
+            }
+            pend_x = (uint32_t)x;
+            pend_z = z;
+            pend_w = w;
+            have = true;
+        };
         uint32_t b = lane < len ? comp[lane] : 0;
         while (p < len) {
             if (p >= wb + 64 || (p + 8 > wb + 64 && wb + 64 < len)) {
@@ -941,10 +1000,9 @@ __global__ void __launch_bounds__(256) k_tokenize(uint32_t n, const RecSlot *slo
                 b = wb + lane < len ? comp[wb + lane] : 0;
             }
             if (!plain_open) {
-                if (lane == 0) seg[ns] = make_uint2((uint32_t)src, p);
-                ++ns;
                 plain_open = true;
                 plain_start = p;
+                plain_src = src;
             }
             uint32_t lim = min(64u, len - wb);
             uint64_t m = ballot(lane >= p - wb && lane < lim && b == kEsc);
@@ -969,51 +1027,174 @@ __global__ void __launch_bounds__(256) k_tokenize(uint32_t n, const RecSlot *slo
                 continue;
             }
             // record or skip token: closes the plain segment (dropped if empty)
-            if (plain_start == p) --ns;
+            if (plain_start < p) emit(plain_src, plain_start, 0);
             if (nx == kBigSign || nx > 6) {
                 uint32_t size = nx == kBigSign ? 8u : 6u;
                 if (p + size > len) {
                     err = kErrCorrupt;
                     break;
                 }
+                uint32_t idx = readlane(b, p + 2 - wb) | (readlane(b, p + 3 - wb) << 8);
                 uint32_t to = readlane(b, p + 4 - wb) | (readlane(b, p + 5 - wb) << 8);
                 uint32_t from = nx == kBigSign ? (readlane(b, p + 6 - wb) | (readlane(b, p + 7 - wb) << 8))
                                                : ((to - nx) & 0xffffu);
-                if (lane == 0) seg[ns] = make_uint2((uint32_t)src, p | kSegRecord);
-                ++ns;
+                emit(src, p | kSegRecord, idx | from << 16);
                 src += (int32_t)to - (int32_t)from;
                 p += size;
             } else {
-                if (lane == 0) seg[ns] = make_uint2((uint32_t)src, p | kSegSkip);
-                ++ns;
+                emit(src, p | kSegSkip, 0);
                 p += 1;
             }
             plain_open = false;
         }
         if (!err) {
-            if (plain_open && plain_start == len) --ns;
-            if (lane == 0) seg[ns] = make_uint2((uint32_t)src, len);
+            if (plain_open && plain_start < len) emit(plain_src, plain_start, 0);
+            emit(src, len, 0);  // closes the last segment; the sentinel stays pending
+            if (lane == 0) seg[ns] = mk4((uint32_t)src, (uint32_t)src, len, 0);
+            // blocks past the source end: no segment
+            if (mono && pidx_n)
+                for (uint32_t k = ((uint32_t)max(src, 0) + 15) / 16 + lane; k < pidx_n; k += 64) pidx[k] = (uint16_t)min(ns, 65535u);
         }
         if (lane == 0) {
-            nseg_out[r] = err ? 0 : ns;
+            nseg_out[r] = err ? 0 : (ns | (mono && pidx_n ? 0u : kNoPidx));
             status[r] = err;
         }
     }
 }
 
 // ====================================================================== decode
-PX_DEV void wave_copy(uint8_t *dst, const uint8_t *src, uint32_t n) {
-    for (uint32_t o = lane_id(); o < n; o += 64) dst[o] = src[o];
+// One wave per query.  A frame (the reference's PXSGen over one record range) is
+// consumed 64 segments at a time: lane l takes segment f.seg + l, a prefix scan of
+// the requested sizes gives every lane its ret cursor and its output offset, and
+// each lane expands its own record reference depth-first through a small per-lane
+// stack in LDS, writing straight to the output.  A lane whose work leaves the
+// simple case (a periodic self reference, deeper nesting, an output that would
+// reach the consumer's cap or differ from what it asked for, a record without a
+// position index) ends the batch; that one segment then goes through the serial
+// frame machine (a stack of Frames in scratch memory), which is the reference's
+// generator nesting restated.
+constexpr uint32_t kLaneDepth = 8;
+
+struct SlotV {
+    const PX_GAS uint8_t *comp;
+    const PX_GAS u32x4 *seg;
+    const PX_GAS uint16_t *pidx;
+    uint32_t nseg, pidx_n;
+};
+
+// 48-byte records moved as three 16-byte vectors (struct copies cannot cross address spaces)
+template <class T>
+PX_DEV T load48(const PX_GAS T *p) {
+    static_assert(sizeof(T) == 48, "48-byte record");
+    const PX_GAS u32x4 *v = (const PX_GAS u32x4 *)p;
+    u32x4 w[3] = {v[0], v[1], v[2]};
+    T t;
+    __builtin_memcpy(&t, w, 48);
+    return t;
+}
+template <class T>
+PX_DEV void store48(PX_GAS T *p, const T &t) {
+    u32x4 w[3];
+    __builtin_memcpy(w, &t, 48);
+    PX_GAS u32x4 *v = (PX_GAS u32x4 *)p;
+    v[0] = w[0];
+    v[1] = w[1];
+    v[2] = w[2];
 }
 
-// first segment whose end is beyond `from` (64-ary search)
-PX_DEV uint32_t seg_search(const uint2 *seg, uint32_t nseg, int32_t from) {
+PX_DEV SlotV slot_at(const PX_GAS RecSlot *slots, uint32_t r) {
+    const RecSlot s = load48(slots + r);
+    SlotV v;
+    v.comp = (const PX_GAS uint8_t *)s.comp;
+    v.seg = (const PX_GAS u32x4 *)s.seg;
+    v.pidx = (const PX_GAS uint16_t *)s.pidx;
+    v.nseg = s.nseg;
+    v.pidx_n = s.pidx_n;
+    return v;
+}
+PX_DEV SlotV slot_uniform(const PX_GAS RecSlot *slots, uint32_t r) {
+    SlotV v = slot_at(slots, r);
+    v.comp = (const PX_GAS uint8_t *)uni64((uint64_t)v.comp);
+    v.seg = (const PX_GAS u32x4 *)uni64((uint64_t)v.seg);
+    v.pidx = (const PX_GAS uint16_t *)uni64((uint64_t)v.pidx);
+    v.nseg = uni(v.nseg);
+    v.pidx_n = uni(v.pidx_n);
+    return v;
+}
+
+PX_DEV void wave_copy(PX_GAS uint8_t *dst, const PX_GAS uint8_t *src, uint32_t n) {
     const uint32_t lane = lane_id();
-    uint32_t lo = 0, hi = nseg;  // answer in [lo, hi]; seg[k+1].x > from
+    uint32_t o = 0;
+    for (; o + 256 <= n; o += 256) {  // four loads in flight per lane
+        uint8_t a0 = src[o + lane], a1 = src[o + 64 + lane], a2 = src[o + 128 + lane], a3 = src[o + 192 + lane];
+        dst[o + lane] = a0;
+        dst[o + 64 + lane] = a1;
+        dst[o + 128 + lane] = a2;
+        dst[o + 192 + lane] = a3;
+    }
+    for (uint32_t k = o + lane; k < n; k += 64) dst[k] = src[k];
+}
+
+// one lane copies its own n bytes
+PX_DEV void lane_copy(PX_GAS uint8_t *dst, const PX_GAS uint8_t *src, uint32_t n) {
+    uint32_t i = 0;
+    for (; i + 4 <= n; i += 4) {
+        uint8_t a = src[i], b = src[i + 1], c = src[i + 2], d = src[i + 3];
+        dst[i] = a;
+        dst[i + 1] = b;
+        dst[i + 2] = c;
+        dst[i + 3] = d;
+    }
+    for (; i < n; ++i) dst[i] = src[i];
+}
+
+PX_DEV int32_t wave_excl_scan(int32_t v) {
+    int32_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        int32_t y = __shfl_up(x, o);
+        if ((int)lane_id() >= o) x += y;
+    }
+    return x - v;
+}
+
+// length of the run of 251 bytes ending at comp[ci], not looking below comp[lo]
+PX_DEV uint32_t esc_run_lane(const PX_GAS uint8_t *comp, uint32_t lo, uint32_t ci) {
+    uint32_t run = 0;
+    while (run <= ci - lo && comp[ci - run] == kEsc) ++run;
+    return run;
+}
+PX_DEV uint32_t esc_run_wave(const PX_GAS uint8_t *comp, uint32_t lo, uint32_t ci) {
+    const uint32_t lane = lane_id();
+    uint32_t run = 0;
+    for (;;) {
+        uint32_t top = ci + 1 - run;  // scan [top-64, top)
+        uint32_t span = min(64u, top - lo);
+        bool is_e = lane < span && comp[top - 1 - lane] == kEsc;
+        uint64_t nm = ballot(lane < span && !is_e);
+        if (nm) return run + ffs64(nm);
+        run += span;
+        if (span < 64) return run;
+    }
+}
+
+// first segment of s whose end is beyond `from` (wave-uniform)
+PX_DEV uint32_t seg_find(const SlotV &s, int32_t from) {
+    const uint32_t lane = lane_id();
+    uint32_t lo = 0, hi = s.nseg;  // answer in [lo, hi]
+    if (s.pidx_n && from >= 0 && ((uint32_t)from >> 4) < s.pidx_n) {
+        lo = min((uint32_t)uni(s.pidx[(uint32_t)from >> 4]), hi);
+        for (;;) {  // at most 16 source bytes past a segment start: one probe, almost always
+            uint32_t k = lo + lane;
+            uint64_t m = ballot(k < hi && (int32_t)s.seg[k].y > from);
+            if (m) return lo + ffs64(m);
+            if (hi - lo <= 64) return hi;
+            lo += 64;
+        }
+    }
     while (hi - lo > 64) {
         uint32_t step = (hi - lo + 63) / 64;
         uint32_t k = lo + lane * step;
-        bool le = k < hi && (int32_t)seg[k + 1].x <= from;  // segment k ends at or before from
+        bool le = k < hi && (int32_t)s.seg[k].y <= from;  // segment k ends at or before from
         uint64_t m = ballot(le);
         uint32_t cnt = (uint32_t)__popcll(m);  // prefix of lanes with le (monotone)
         uint32_t nlo = cnt ? lo + (cnt - 1) * step + 1 : lo;
@@ -1022,49 +1203,222 @@ PX_DEV uint32_t seg_search(const uint2 *seg, uint32_t nseg, int32_t from) {
         hi = uni(nhi);
     }
     uint32_t k = lo + lane;
-    bool le = k < hi && (int32_t)seg[k + 1].x <= from;
+    bool le = k < hi && (int32_t)s.seg[k].y <= from;
     return uni(lo + (uint32_t)__popcll(ballot(le)));
 }
 
+// per-lane version through the position index; flag when there is none
+PX_DEV uint32_t lane_find(const SlotV &s, int32_t a, bool &flag) {
+    uint32_t b = (uint32_t)a >> 4;
+    if (a < 0 || b >= s.pidx_n) {
+        flag = true;
+        return 0;
+    }
+    uint32_t k = s.pidx[b];
+    while (k < s.nseg && (int32_t)s.seg[k].y <= a) ++k;
+    return k;
+}
+
+struct DecLds {
+    uint32_t stk[kLaneDepth * 5][64];  // per-lane frames: rec, from, len, ret, seg
+};
+
 __global__ void __launch_bounds__(64) k_decode(const DecodeQuery *qs, uint32_t nq, const RecSlot *const *chunk_slots,
-                                               uint8_t *out, uint32_t *out_len, uint32_t *status,
+                                               uint8_t *out_, uint32_t *out_len, uint32_t *status,
                                                Frame *scratch, uint32_t depth_cap) {
+    __shared__ DecLds lds;
     const uint32_t lane = lane_id();
-    Frame *stk = scratch + (size_t)blockIdx.x * depth_cap;
+    PX_GAS Frame *stk = (PX_GAS Frame *)scratch + (size_t)blockIdx.x * depth_cap;
     for (uint32_t qi = blockIdx.x; qi < nq; qi += gridDim.x) {
         const DecodeQuery q = qs[qi];
-        const RecSlot *slots = uni(q.chunk) == kNone ? nullptr : chunk_slots[uni(q.chunk)];
+        const uint32_t qchunk = uni(q.chunk);
+        const PX_GAS RecSlot *slots = qchunk == kNone ? nullptr : (const PX_GAS RecSlot *)chunk_slots[qchunk];
         const bool compat = uni(q.mode) == 0;
-        uint8_t *o = out + uni64(q.out_off);
+        const uint32_t nrec = uni(q.nrec);
+        PX_GAS uint8_t *o = (PX_GAS uint8_t *)out_ + uni64(q.out_off);
         const uint32_t qcap = uni(q.out_cap);
         uint32_t outp = 0, err = 0, depth = 0;
         bool capped = false;
 
-        // push helper (inline): frame for record `r`, range [from, to), cap
         auto push = [&](uint32_t r, int32_t from, int32_t to, uint32_t cap) -> bool {
+            if (r >= nrec) {
+                err = kErrCorrupt;  // PiXiuChunk::getitem past the chunk (the oracle's ECORRUPT)
+                return false;
+            }
             if (depth >= depth_cap) {
                 err = kErrDepth;
                 return false;
             }
-            const RecSlot sl = slots[r];
-            uint32_t nseg = uni(sl.nseg);
+            const SlotV sv = slot_uniform(slots, r);
             Frame f;
             f.rec = r;
             f.from = from;
             f.len = to - from;
             f.ret = 0;
-            f.seg = nseg ? seg_search(sl.seg, nseg, from) : 0;
-            f.src = f.seg < nseg ? unii((int32_t)sl.seg[f.seg].x) : 0;
+            f.src = 0;
+            f.seg = sv.nseg ? seg_find(sv, from) : 0;
             f.cap = cap;
             f.state = 0;
             f.pstart = 0;
             f.sub_from = f.sub_to = f.supply = 0;
-            stk[depth] = f;
+            store48(stk + depth, f);
             ++depth;
             return true;
         };
 
-        if (uni(q.chunk) == kNone || !push(uni(q.idx), unii(q.from), unii(q.to), qcap)) {
+        // Consume up to 64 segments of frame f in parallel.  Returns true when the
+        // segment at f.seg must go through the serial path next.
+        auto batch = [&](Frame &f, const SlotV &sv) -> bool {
+            const uint32_t k = f.seg + lane;
+            const bool valid = k < sv.nseg;
+            const u32x4 E = valid ? sv.seg[k] : mk4(0, 0, 0, 0);
+            const int32_t sx = (int32_t)E.x, ex = (int32_t)E.y;
+            const uint32_t kind = E.z >> 30, cs = E.z & kSegMask;
+            const uint32_t ridx = E.w & 0xffffu;
+            const int32_t rfrom = (int32_t)(E.w >> 16), supply = ex - sx, rto = rfrom + supply;
+            const int32_t p0 = max(sx, f.from);
+            const int32_t sub_from = rfrom + max(0, f.from - sx);
+            const bool enter = kind == 2 && sx - 1 + supply >= f.from;
+            int32_t req = 0;  // requested size, unclamped (ret grows by it)
+            if (valid && kind == 0 && p0 < ex) req = ex - p0;
+            if (valid && enter) req = rto - sub_from;
+            const int32_t ret_l = f.ret + wave_excl_scan(req);
+            const bool active = valid && ret_l < f.len;  // a prefix of the lanes
+            const int32_t need = f.len - ret_l;
+            bool flag = false, child = false;
+            int32_t reqc = 0, sub_to = 0;
+            uint32_t csrc = 0;
+            if (active && kind == 0 && p0 < ex) {
+                const int32_t avail = ex - p0;
+                reqc = min(avail, need);
+                csrc = cs + (uint32_t)(p0 - sx);
+                // the range ends here: if its last byte opens a 251 pair, the pair is
+                // written whole (per-token length check, PiXiuStr.h:136,142-147)
+                if (avail > need && compat && (esc_run_lane(sv.comp, cs, csrc + (uint32_t)reqc - 1) & 1)) ++reqc;
+            } else if (active && enter) {
+                sub_to = min(rto, sub_from + need);
+                const int32_t stop = compat ? ret_l : max(sx, f.from);
+                if (ridx >= nrec || (sub_from < stop && stop < sub_to && ridx == f.rec)) flag = true;
+                reqc = sub_to - sub_from;
+                child = true;
+            }
+            const uint32_t base = outp + (uint32_t)wave_excl_scan(active ? reqc : 0);
+            if (active && (uint64_t)base + (uint64_t)reqc >= f.cap) flag = true;
+            // short plain pieces: copied by their lane now; long ones cooperatively below
+            uint32_t w = 0;
+            if (active && !flag && kind == 0) {
+                if (reqc <= 64) lane_copy(o + base, sv.comp + csrc, (uint32_t)reqc);
+                w = (uint32_t)reqc;
+            }
+            // record references: each lane expands its own range depth-first
+            bool busy = active && !flag && child;
+            if (ballot(busy)) {
+                uint32_t rec = ridx, kk = 0, d = 0;
+                int32_t from = sub_from, len = reqc, ret = 0;
+                const uint32_t wmax = (uint32_t)reqc;
+                SlotV s{};
+                if (busy) {
+                    s = slot_at(slots, rec);
+                    kk = lane_find(s, from, flag);
+                    busy = !flag;
+                }
+                while (ballot(busy)) {
+                    if (busy) {
+                        if (ret >= len || kk >= s.nseg) {
+                            if (d == 0) {
+                                busy = false;
+                            } else {
+                                --d;
+                                rec = lds.stk[d * 5 + 0][lane];
+                                from = (int32_t)lds.stk[d * 5 + 1][lane];
+                                len = (int32_t)lds.stk[d * 5 + 2][lane];
+                                ret = (int32_t)lds.stk[d * 5 + 3][lane];
+                                kk = lds.stk[d * 5 + 4][lane];
+                                s = slot_at(slots, rec);
+                            }
+                        } else {
+                            const u32x4 F = s.seg[kk];
+                            const int32_t x = (int32_t)F.x, y = (int32_t)F.y;
+                            const uint32_t kd = F.z >> 30, c0 = F.z & kSegMask;
+                            if (kd == 0) {
+                                const int32_t q0 = max(x, from);
+                                if (q0 < y) {
+                                    const int32_t avail = y - q0, nd = len - ret;
+                                    int32_t nb = min(avail, nd);
+                                    const uint32_t ci = c0 + (uint32_t)(q0 - x);
+                                    if (avail > nd && compat && (esc_run_lane(s.comp, c0, ci + (uint32_t)nb - 1) & 1)) ++nb;
+                                    if (w + (uint32_t)nb > wmax) {
+                                        flag = true;  // over-yield past the lane's slot
+                                        busy = false;
+                                    } else {
+                                        lane_copy(o + base + w, s.comp + ci, (uint32_t)nb);
+                                        w += (uint32_t)nb;
+                                        ret += nb;
+                                    }
+                                }
+                                ++kk;
+                            } else if (kd == 2) {
+                                const int32_t sup = y - x;
+                                if (x - 1 + sup >= from) {
+                                    const uint32_t ri = F.w & 0xffffu;
+                                    const int32_t rf = (int32_t)(F.w >> 16), rt = rf + sup;
+                                    const int32_t sf = rf + max(0, from - x);
+                                    const int32_t st = min(rt, sf + (len - ret));
+                                    const int32_t stop = compat ? ret : max(x, from);
+                                    if (ri >= nrec || (ri == rec && sf < stop && stop < st) || d + 1 >= kLaneDepth) {
+                                        flag = true;
+                                        busy = false;
+                                    } else {
+                                        lds.stk[d * 5 + 0][lane] = rec;
+                                        lds.stk[d * 5 + 1][lane] = (uint32_t)from;
+                                        lds.stk[d * 5 + 2][lane] = (uint32_t)len;
+                                        lds.stk[d * 5 + 3][lane] = (uint32_t)(ret + (st - sf));
+                                        lds.stk[d * 5 + 4][lane] = kk + 1;
+                                        ++d;
+                                        rec = ri;
+                                        from = sf;
+                                        len = st - sf;
+                                        ret = 0;
+                                        s = slot_at(slots, rec);
+                                        kk = lane_find(s, from, flag);
+                                        if (flag) busy = false;
+                                    }
+                                } else {
+                                    ++kk;
+                                }
+                            } else {
+                                ++kk;
+                            }
+                        }
+                    }
+                }
+            }
+            // commit the lanes before the first flagged one; a lane that produced fewer
+            // bytes than it asked for (its record ran out) is committed but ends the batch
+            const uint64_t fm = ballot(active && flag);
+            const uint64_t sm = ballot(active && !flag && w != (uint32_t)reqc);
+            const uint64_t am = ballot(active);
+            const uint32_t L = (uint32_t)__popcll(am);
+            const uint32_t first_flag = fm ? ffs64(fm) : 64u;
+            const uint32_t first_short = sm ? ffs64(sm) : 64u;
+            const uint32_t C = min(L, min(first_flag, first_short + 1));
+            uint64_t lm = ballot(active && !flag && kind == 0 && reqc > 64 && lane < C);
+            while (lm) {
+                const uint32_t j = ffs64(lm);
+                lm &= lm - 1;
+                wave_copy(o + readlane(base, j), sv.comp + readlane(csrc, j), readlane((uint32_t)reqc, j));
+            }
+            const int32_t rsum = wave_excl_scan(lane < C ? reqc : 0) + (lane < C ? reqc : 0);
+            const int32_t wsum = wave_excl_scan(lane < C ? (int32_t)w : 0) + (lane < C ? (int32_t)w : 0);
+            if (C) {
+                f.ret += unii(readlane((uint32_t)rsum, C - 1));
+                outp += (uint32_t)uni(readlane((uint32_t)wsum, C - 1));
+                f.seg += C;
+            }
+            return first_flag == C && C < L;
+        };
+
+        if (qchunk == kNone || !push(uni(q.idx), unii(q.from), unii(q.to), qcap)) {
             if (lane == 0) {
                 out_len[qi] = 0;
                 status[qi] = err ? err : kErrInval;
@@ -1073,12 +1427,11 @@ __global__ void __launch_bounds__(64) k_decode(const DecodeQuery *qs, uint32_t n
         }
         while (depth > 0 && !err) {
             __builtin_amdgcn_wave_barrier();
-            Frame f = stk[depth - 1];
+            Frame f = load48(stk + (depth - 1));
             f.rec = uni(f.rec);
             f.from = unii(f.from);
             f.len = unii(f.len);
             f.ret = unii(f.ret);
-            f.src = unii(f.src);
             f.seg = uni(f.seg);
             f.cap = uni(f.cap);
             f.state = uni(f.state);
@@ -1086,10 +1439,7 @@ __global__ void __launch_bounds__(64) k_decode(const DecodeQuery *qs, uint32_t n
             f.sub_from = unii(f.sub_from);
             f.sub_to = unii(f.sub_to);
             f.supply = unii(f.supply);
-            const RecSlot sl = slots[f.rec];
-            const uint8_t *comp = sl.comp;
-            const uint2 *seg = sl.seg;
-            const uint32_t nseg = uni(sl.nseg);
+            const SlotV sv = slot_uniform(slots, f.rec);
             bool pop = false;
 
             if (f.state != 0) {  // a child just returned
@@ -1114,27 +1464,28 @@ __global__ void __launch_bounds__(64) k_decode(const DecodeQuery *qs, uint32_t n
                     }
                     if (!pop) {
                         f.ret += f.sub_to - f.sub_from;
-                        f.src += f.supply;
                         ++f.seg;
                         f.state = 0;
                     }
                 }
             }
             bool pushed = false;
-            while (!pop && !pushed && f.ret < f.len && f.seg < nseg) {
-                const uint32_t sx = uni(seg[f.seg].x), sy = uni(seg[f.seg].y);
-                const uint32_t cs = sy & kSegMask;
-                if (sy & kSegRecord) {
-                    const uint8_t *t = comp + cs;
-                    uint32_t sign = uni(t[1]);
-                    int32_t ridx = (int32_t)uni(rd16(t + 2));
-                    int32_t rto = (int32_t)uni(rd16(t + 4));
-                    int32_t rfrom = sign == kBigSign ? (int32_t)uni(rd16(t + 6)) : ((rto - (int32_t)sign) & 0xffff);
-                    int32_t supply = rto - rfrom;
-                    if (f.src - 1 + supply >= f.from) {
-                        int32_t sub_from = rfrom + max(0, f.from - f.src);
+            while (!pop && !pushed && !err && f.ret < f.len && f.seg < sv.nseg) {
+                if (!batch(f, sv)) continue;
+                // one segment through the serial machine
+                const u32x4 E = sv.seg[f.seg];
+                const int32_t sx = (int32_t)uni(E.x), ex = (int32_t)uni(E.y);
+                const uint32_t sz = uni(E.z), sw = uni(E.w);
+                const uint32_t cs = sz & kSegMask;
+                if (sz & kSegRecord) {
+                    const int32_t ridx = (int32_t)(sw & 0xffffu);
+                    const int32_t rfrom = (int32_t)(sw >> 16);
+                    const int32_t supply = ex - sx;
+                    const int32_t rto = rfrom + supply;
+                    if (sx - 1 + supply >= f.from) {
+                        int32_t sub_from = rfrom + max(0, f.from - sx);
                         int32_t sub_to = min(rto, sub_from + (f.len - f.ret));
-                        int32_t stop = compat ? f.ret : max(f.src, f.from);
+                        int32_t stop = compat ? f.ret : max(sx, f.from);
                         bool periodic = sub_from < stop && stop < sub_to && (uint32_t)ridx == f.rec;
                         f.state = periodic ? 2 : 1;
                         f.pstart = outp;
@@ -1142,46 +1493,29 @@ __global__ void __launch_bounds__(64) k_decode(const DecodeQuery *qs, uint32_t n
                         f.sub_to = sub_to;
                         f.supply = supply;
                         __builtin_amdgcn_wave_barrier();
-                        stk[depth - 1] = f;
+                        store48(stk + (depth - 1), f);
                         uint32_t ccap = periodic ? min(f.cap, outp + (uint32_t)(sub_to - sub_from)) : f.cap;
                         bool ok = periodic ? push(f.rec, sub_from, stop, ccap) : push((uint32_t)ridx, sub_from, sub_to, ccap);
                         if (!ok) break;
                         pushed = true;
                         break;
                     }
-                    f.src += supply;
                     ++f.seg;
-                } else if (sy & kSegSkip) {
+                } else if (sz & kSegSkip) {
                     ++f.seg;
                 } else {
-                    const int32_t e = (int32_t)uni(seg[f.seg + 1].x);
-                    const int32_t p0 = max((int32_t)sx, f.from);
-                    if (p0 < e) {
-                        uint32_t avail = (uint32_t)(e - p0);
+                    const int32_t p0 = max(sx, f.from);
+                    if (p0 < ex) {
+                        uint32_t avail = (uint32_t)(ex - p0);
                         uint32_t need = (uint32_t)(f.len - f.ret);
                         uint32_t nb = min(avail, need);
                         if (avail > need && compat) {
-                            // the range ends here: if the last byte opens a 251 pair, the pair
-                            // is written whole (per-token length check, PiXiuStr.h:136,142-147)
-                            uint32_t ci = cs + (uint32_t)(p0 - (int32_t)sx) + nb - 1;
-                            uint32_t run = 0;
-                            for (;;) {
-                                uint32_t lo = ci + 1 - run;  // scan [lo-64, lo)
-                                uint32_t span = min(64u, lo - cs);
-                                bool is_e = lane < span && comp[lo - 1 - lane] == kEsc;
-                                uint64_t nm = ballot(lane < span && !is_e);
-                                if (nm) {
-                                    run += ffs64(nm);
-                                    break;
-                                }
-                                run += span;
-                                if (span < 64) break;
-                            }
-                            if (run & 1) nb += 1;
+                            uint32_t ci = cs + (uint32_t)(p0 - sx) + nb - 1;
+                            if (esc_run_wave(sv.comp, cs, ci) & 1) nb += 1;
                         }
                         uint32_t room = f.cap > outp ? f.cap - outp : 0;
                         uint32_t w = min(nb, room);
-                        wave_copy(o + outp, comp + cs + (uint32_t)(p0 - (int32_t)sx), w);
+                        wave_copy(o + outp, sv.comp + cs + (uint32_t)(p0 - sx), w);
                         outp += w;
                         f.ret += (int32_t)nb;
                         if (w < nb || outp >= f.cap) {
@@ -1189,7 +1523,6 @@ __global__ void __launch_bounds__(64) k_decode(const DecodeQuery *qs, uint32_t n
                             break;
                         }
                     }
-                    f.src = e;
                     ++f.seg;
                 }
             }
@@ -1271,11 +1604,10 @@ hipError_t launch_compact(hipStream_t s, uint32_t n, uint8_t *const *src, const 
     return hipGetLastError();
 }
 
-hipError_t launch_tokenize(hipStream_t s, uint32_t n, const RecSlot *slots, uint2 *const *seg_out,
-                           uint32_t *nseg_out, uint32_t *status) {
+hipError_t launch_tokenize(hipStream_t s, uint32_t n, const RecSlot *slots, uint32_t *nseg_out, uint32_t *status) {
     if (!n) return hipSuccess;
     uint32_t blocks = min((n + 3) / 4, 8192u);
-    k_tokenize<<<blocks, 256, 0, s>>>(n, slots, seg_out, nseg_out, status);
+    k_tokenize<<<blocks, 256, 0, s>>>(n, slots, nseg_out, status);
     return hipGetLastError();
 }
 

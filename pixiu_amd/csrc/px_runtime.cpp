@@ -29,7 +29,7 @@ hipError_t launch_doc_write(hipStream_t, uint32_t, const uint8_t *, const uint64
 hipError_t launch_gst_encode(hipStream_t, const GstShard *, uint32_t, const uint32_t *, uint8_t *const *,
                              uint32_t *, uint32_t *, uint32_t *, uint32_t *);
 hipError_t launch_compact(hipStream_t, uint32_t, uint8_t *const *, const uint32_t *, uint8_t *, const uint64_t *);
-hipError_t launch_tokenize(hipStream_t, uint32_t, const RecSlot *, uint2 *const *, uint32_t *, uint32_t *);
+hipError_t launch_tokenize(hipStream_t, uint32_t, const RecSlot *, uint32_t *, uint32_t *);
 hipError_t launch_decode(hipStream_t, const DecodeQuery *, uint32_t, const RecSlot *const *, uint8_t *,
                          uint32_t *, uint32_t *, Frame *, uint32_t, uint32_t);
 hipError_t launch_rehash(hipStream_t, const uint4 *, uint32_t, uint32_t, uint4 *, uint32_t);
@@ -52,6 +52,13 @@ struct PxFail {
 };
 
 inline uint64_t round_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+// position-index blocks for a record of `src_len` source bytes (k_tokenize)
+inline uint32_t pidx_blocks(uint32_t src_len) { return src_len / 16 + 2; }
+constexpr uint32_t kNoPidxBit = 1u << 31;  // k_tokenize: record has no position index
+inline void set_nseg(RecSlot &s, uint32_t tok) {
+    s.nseg = tok & ~kNoPidxBit;
+    if (tok & kNoPidxBit) s.pidx_n = 0;
+}
 inline uint64_t pow2_at_least(uint64_t v) {
     uint64_t p = 1024;
     while (p < v) p <<= 1;
@@ -530,7 +537,9 @@ struct px_ctx {
         auto *dq = (DecodeQuery *)dq_buf.get((uint64_t)nq * sizeof(DecodeQuery));
         auto *dl = (uint32_t *)dlen_buf.get((uint64_t)nq * 8);
         uint32_t *ds = dl + nq;
-        h2d(dq, q.data(), (size_t)nq * sizeof(DecodeQuery));
+        std::vector<DecodeQuery> qn(q);
+        for (auto &d : qn) d.nrec = d.chunk == kNone ? 0 : chunks[d.chunk].n;
+        h2d(dq, qn.data(), (size_t)nq * sizeof(DecodeQuery));
         if (timed) hcheck(hipEventRecord(ev0, stream));
         hcheck(launch_decode(stream, dq, nq, (const RecSlot *const *)chunk_tab, out_dev, dl, ds, frames, depth,
                              waves));
@@ -747,36 +756,37 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     }
 
     // ---- packed store + segment index
-    std::vector<uint64_t> coff(n + 1, 0), soff(n + 1, 0);
+    std::vector<uint64_t> coff(n + 1, 0), soff(n + 1, 0), poff(n + 1, 0);
     for (uint32_t r = 0; r < n; ++r) {
         bool ok = doc_len[r] != 0xffffffffu && rstatus[r] == kOk;
         coff[r + 1] = coff[r] + (ok ? round_up(comp_len[r], 8) : 0);
-        soff[r + 1] = soff[r] + (ok ? (uint64_t)(comp_len[r] + 2) * 8 : 0);
+        soff[r + 1] = soff[r] + (ok ? (uint64_t)(comp_len[r] + 2) * sizeof(uint4) : 0);
+        poff[r + 1] = poff[r] + (ok ? round_up(pidx_blocks(doc_len[r]) * 2, 16) : 0);
     }
     auto *store = (uint8_t *)heap.alloc(coff[n] + 64);
-    auto *segs = (uint8_t *)heap.alloc(soff[n] + 64);
+    auto *segs = (uint8_t *)heap.alloc(soff[n] + poff[n] + 64);
     store_blocks.emplace_back(store, coff[n] + 64);
     last_store = store;
     last_store_bytes = coff[n];
-    store_blocks.emplace_back(segs, soff[n] + 64);
+    store_blocks.emplace_back(segs, soff[n] + poff[n] + 64);
     auto *d_coff = (uint64_t *)heap.alloc((uint64_t)n * 8);
     h2d(d_coff, coff.data(), (size_t)n * 8);
     hcheck(launch_compact(stream, n, d_cdst, d_complen, store, d_coff));
     std::vector<RecSlot> slots(n);
-    std::vector<uint2 *> segp(n);
     for (uint32_t r = 0; r < n; ++r) {
+        bool ok = doc_len[r] != 0xffffffffu && rstatus[r] == kOk;
         slots[r].comp = store + coff[r];
-        slots[r].seg = (const uint2 *)(segs + soff[r]);
-        slots[r].comp_len = (doc_len[r] != 0xffffffffu && rstatus[r] == kOk) ? comp_len[r] : 0;
+        slots[r].seg = (const uint4 *)(segs + soff[r]);
+        slots[r].pidx = (const uint16_t *)(segs + soff[n] + poff[r]);
+        slots[r].comp_len = ok ? comp_len[r] : 0;
         slots[r].nseg = 0;
-        segp[r] = (uint2 *)(segs + soff[r]);
+        slots[r].pidx_n = ok ? pidx_blocks(doc_len[r]) : 0;
+        slots[r].pad = 0;
     }
     auto *d_slots = (RecSlot *)heap.alloc((uint64_t)n * sizeof(RecSlot));
-    auto *d_segp = (uint2 **)heap.alloc((uint64_t)n * 8);
     h2d(d_slots, slots.data(), (size_t)n * sizeof(RecSlot));
-    h2d(d_segp, segp.data(), (size_t)n * 8);
     std::vector<uint32_t> tstat(n);
-    hcheck(launch_tokenize(stream, n, d_slots, d_segp, d_nseg, d_status));
+    hcheck(launch_tokenize(stream, n, d_slots, d_nseg, d_status));
     std::vector<uint32_t> nseg(n);
     d2h(nseg.data(), d_nseg, n * 4);
     d2h(tstat.data(), d_status, n * 4);
@@ -787,7 +797,6 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     heap.release(d_gs, gs.size() * sizeof(GstShard));
     heap.release(d_coff, (uint64_t)n * 8);
     heap.release(d_slots, (uint64_t)n * sizeof(RecSlot));
-    heap.release(d_segp, (uint64_t)n * 8);
 
     // ---- register records in their chunks
     std::vector<uint32_t> rgchunk(n, kNone);
@@ -806,7 +815,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             rstatus[r] = kErrCapacity;  // slot order broken: cannot happen
             continue;
         }
-        slots[r].nseg = nseg[r];
+        set_nseg(slots[r], nseg[r]);
         ch.slots.push_back(slots[r]);
         ch.doc_len.push_back(doc_len[r]);
         ch.dead.push_back(0);
@@ -1169,40 +1178,39 @@ int px_last_store(px_ctx *ctx, uint8_t *dst, uint64_t cap, int dst_on_device, ui
 int px_import_chunk(px_ctx *ctx, uint32_t n, const uint8_t *comp, const uint64_t *off, uint32_t *shard_out) {
     if (!ctx || !n || n > (uint32_t)kChunkSlots || !comp || !off) return PX_EINVAL;
     PX_GUARD({
+        // an imported record's source length is unknown up front: index the first
+        // kMaxDoc source bytes (a lane asking past that goes to the serial path)
+        const uint32_t pn = pidx_blocks(kMaxDoc);
         std::vector<uint64_t> coff(n + 1, 0), soff(n + 1, 0);
         for (uint32_t r = 0; r < n; ++r) {
             uint64_t l = off[r + 1] - off[r];
             if (l > (uint64_t)kMaxDoc) return PX_EINVAL;
             coff[r + 1] = coff[r] + round_up(l, 8);
-            soff[r + 1] = soff[r] + (l + 2) * 8;
+            soff[r + 1] = soff[r] + (l + 2) * sizeof(uint4) + round_up((uint64_t)pn * 2, 16);
         }
         auto *store = (uint8_t *)ctx->heap.alloc(coff[n] + 64);
         auto *segs = (uint8_t *)ctx->heap.alloc(soff[n] + 64);
         ctx->store_blocks.emplace_back(store, coff[n] + 64);
         ctx->store_blocks.emplace_back(segs, soff[n] + 64);
         std::vector<RecSlot> slots(n);
-        std::vector<uint2 *> segp(n);
         for (uint32_t r = 0; r < n; ++r) {
             uint64_t l = off[r + 1] - off[r];
             ctx->h2d(store + coff[r], comp + off[r], l);
-            slots[r] = RecSlot{store + coff[r], (const uint2 *)(segs + soff[r]), (uint32_t)l, 0};
-            segp[r] = (uint2 *)(segs + soff[r]);
+            slots[r] = RecSlot{store + coff[r], (const uint4 *)(segs + soff[r]),
+                               (const uint16_t *)(segs + soff[r] + (l + 2) * sizeof(uint4)), (uint32_t)l, 0, pn, 0};
         }
         auto *d_slots = (RecSlot *)ctx->heap.alloc((uint64_t)n * sizeof(RecSlot));
-        auto *d_segp = (uint2 **)ctx->heap.alloc((uint64_t)n * 8);
         auto *d_tmp = (uint32_t *)ctx->heap.alloc((uint64_t)n * 8);
         ctx->h2d(d_slots, slots.data(), (size_t)n * sizeof(RecSlot));
-        ctx->h2d(d_segp, segp.data(), (size_t)n * 8);
-        hcheck(launch_tokenize(ctx->stream, n, d_slots, d_segp, d_tmp, d_tmp + n));
+        hcheck(launch_tokenize(ctx->stream, n, d_slots, d_tmp, d_tmp + n));
         std::vector<uint32_t> nseg(n), tst(n);
         ctx->d2h(nseg.data(), d_tmp, (size_t)n * 4);
         ctx->d2h(tst.data(), d_tmp + n, (size_t)n * 4);
         ctx->sync();
-        std::vector<uint2> sentinel(n);
-        for (uint32_t r = 0; r < n; ++r) ctx->d2h(&sentinel[r], segp[r] + nseg[r], sizeof(uint2));
+        std::vector<uint4> sentinel(n);
+        for (uint32_t r = 0; r < n; ++r) ctx->d2h(&sentinel[r], slots[r].seg + (nseg[r] & ~kNoPidxBit), sizeof(uint4));
         ctx->sync();
         ctx->heap.release(d_slots, (uint64_t)n * sizeof(RecSlot));
-        ctx->heap.release(d_segp, (uint64_t)n * 8);
         ctx->heap.release(d_tmp, (uint64_t)n * 8);
         for (uint32_t r = 0; r < n; ++r)
             if (tst[r] != kOk) return (int)map_status(tst[r]);
@@ -1212,7 +1220,7 @@ int px_import_chunk(px_ctx *ctx, uint32_t n, const uint8_t *comp, const uint64_t
         sh.chunks.push_back(c);
         Chunk &ch = ctx->chunks[c];
         for (uint32_t r = 0; r < n; ++r) {
-            slots[r].nseg = nseg[r];
+            set_nseg(slots[r], nseg[r]);
             ch.slots.push_back(slots[r]);
             ch.doc_len.push_back(std::min<uint32_t>(sentinel[r].x, (uint32_t)kMaxDoc * 4));
             ch.dead.push_back(0);

@@ -6,7 +6,7 @@ import numpy as np
 import pixiu_amd as px
 from pixiu_amd import synth
 NAMES = ["bytes", "ff_calls", "ff_bytes", "pass", "iters", "lookups", "probes", "root", "walk", "link", "canon_lvl",
-         "t_total", "t_ff", "t_derive", "t_walk", "t_split", "t_grow", "t_canon", "t_end", "t_root", "t_enc"]
+         "t_total", "t_ff", "t_derive", "t_walk", "t_split", "t_grow", "t_canon", "t_end", "t_root", "t_enc", "keymiss", "t_key", "t_look"]
 lib = px.load_library()
 lib.px_debug_prof_take.argtypes = [C.c_void_p, C.c_uint32]
 cfg, n, rps = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
@@ -23,4 +23,4 @@ print(f"config {cfg} n {n} rps {rps}: kernel {ms:.1f} ms")
 for name in NAMES:
     x = v[name]
     per = x / b
-    print(f"  {name:10s} {x:16d}  per byte {per:10.3f}" + (f"  ({x / max(v['t_total'],1) * 100:5.1f}% of wave time)" if name.startswith("t_") else ""))
+    print(f"  {name:10s} {x:16d}  per byte {per:10.3f}" + (f"  ({x / max(v['t_total'],1) * 100:5.1f}% of wave time)" if name.startswith("t_") and name != "t_total" or name == "t_total" else ""))
