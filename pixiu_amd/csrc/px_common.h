@@ -68,10 +68,21 @@ struct GstShard {
     uint32_t pad;
 };
 
+// segment index entry (k_tokenize fills it, k_link sets a record token's target)
+struct alignas(16) SegEnt {
+    uint32_t x, ex;  // source range [x, ex) of the segment
+    uint32_t kz;     // comp offset | kind << 30: 0 plain, 1 skip, 2 record, 3 end (sentinel)
+    uint32_t aux;    // record token: idx | from << 16 (its to = from + ex - x)
+    uint64_t ptr;    // plain: address of its first comp byte; record: address of the entry
+                     // of record idx holding source position `from` (0: none)
+    uint64_t pad;
+};
+static_assert(sizeof(SegEnt) == 32, "SegEnt is two 16-byte vectors");
+
 // compressed-record slot: what a chunk table entry points at
 struct alignas(16) RecSlot {
     const uint8_t *comp;    // compressed bytes
-    const uint4 *seg;       // segment index, nseg entries + a sentinel (see k_tokenize)
+    const SegEnt *seg;      // segment index, nseg entries + an end sentinel (see k_tokenize)
     const uint16_t *pidx;   // position index: pidx[b] = segment holding source position 16b
     uint32_t comp_len;
     uint32_t nseg;
@@ -80,6 +91,13 @@ struct alignas(16) RecSlot {
     uint64_t pad2;          // 48 bytes: three 16-byte loads on the device
 };
 static_assert(sizeof(RecSlot) == 48, "RecSlot is loaded as three 16-byte vectors");
+
+// k_link work item: one record whose record tokens get their target entries
+struct LinkJob {
+    SegEnt *seg;
+    const RecSlot *slots;  // the record's chunk table
+    uint32_t nseg, nrec;
+};
 
 // decode query
 struct DecodeQuery {

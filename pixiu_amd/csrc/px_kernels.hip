@@ -76,7 +76,8 @@ PX_DEV uint32_t rd16(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1]
 // debug build only: per-category counters and shader-clock cycles of k_gst_encode
 enum { P_BYTES, P_FF_CALLS, P_FF_BYTES, P_PASS, P_ITERS, P_LOOKUPS, P_PROBES, P_ROOT, P_WALK, P_LINK, P_CANON_LVL,
        P_T_TOTAL, P_T_FF, P_T_DERIVE, P_T_WALK, P_T_SPLIT, P_T_GROW, P_T_CANON, P_T_END, P_T_ROOT, P_T_ENC,
-       P_KEYMISS, P_T_KEY, P_T_LOOK, P_N };
+       P_KEYMISS, P_T_KEY, P_T_LOOK,
+       P_D_BATCH, P_D_LANEIT, P_D_SERIAL, P_D_COMMIT, P_D_FLAGGED, P_D_SHORT, P_D_PUSH, P_D_T_TOTAL, P_D_T_LANE, P_N };
 __device__ unsigned long long g_prof[P_N];
 #define PX_CNT(k, v) (prof[k] += (v))
 #define PX_T0() uint64_t _t0 = __builtin_amdgcn_s_memtime()
@@ -942,24 +943,42 @@ __global__ void __launch_bounds__(256) k_compact(uint32_t n, uint8_t *const *src
     const uint32_t lane = lane_id();
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);
     for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < n; r += waves) {
-        const uint8_t *s = src[r];
-        uint8_t *d = dst + dst_off[r];
+        const PX_GAS uint8_t *s = (const PX_GAS uint8_t *)src[r];
+        PX_GAS uint8_t *d = (PX_GAS uint8_t *)dst + dst_off[r];
         uint32_t l = len[r];
         for (uint32_t o = lane; o < l; o += 64) d[o] = s[o];
     }
 }
 
-// Segment index over the token grammar of PXSGen (PiXiuStr.h:139-192): one 16-byte
-// entry per segment, then a sentinel (src_total, src_total, comp_len, 0):
-//   x = source start          y = source end (= the next segment's start)
-//   z = comp offset | kind << 30   kind 0 plain (literals and 251-pairs, copied
-//       verbatim), 2 record, 1 skip (251 + 3..6: no source bytes)
-//   w = record: idx | from << 16   (to = from + (y - x))
-// pidx[b] = the segment holding source position 16b.  A record whose source
-// positions are not monotone (a record token with to < from) gets no position
-// index (nseg_out bit 31) and is only ever decoded by the serial path.
-constexpr uint32_t kSegRecord = 2u << 30, kSegSkip = 1u << 30, kSegMask = (1u << 30) - 1;
+// 251 bytes per compressed record: bounds its segment count (2 * n + 1, + sentinel)
+__global__ void __launch_bounds__(256) k_count_esc(uint32_t n, uint8_t *const *src, const uint32_t *len,
+                                                   uint32_t *n_esc) {
+    const uint32_t lane = lane_id();
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < n; r += waves) {
+        const PX_GAS uint8_t *s = (const PX_GAS uint8_t *)src[r];
+        const uint32_t l = len[r];
+        uint32_t cnt = 0;
+        for (uint32_t o = lane; o < l; o += 64) cnt += s[o] == kEsc;
+        for (int k = 32; k > 0; k >>= 1) cnt += __shfl_xor(cnt, k);
+        if (lane == 0) n_esc[r] = cnt;
+    }
+}
+
+// Segment index over the token grammar of PXSGen (PiXiuStr.h:139-192): one SegEnt
+// (px_common.h) per segment, then an end sentinel {src_total, src_total, comp_len | 3 << 30}.
+// Kinds: 0 plain (literals and 251-pairs, copied verbatim), 1 skip (251 + 3..6: no
+// source bytes), 2 record, 3 end.  pidx[b] = the segment holding source position 16b.
+// A record whose source positions are not monotone (a record token with to < from)
+// gets no position index (nseg_out bit 31) and is only decoded by the serial path.
+constexpr uint32_t kSegRecord = 2u << 30, kSegSkip = 1u << 30, kSegEnd = 3u << 30, kSegMask = (1u << 30) - 1;
 constexpr uint32_t kNoPidx = 1u << 31;
+
+PX_DEV void put_ent(PX_GAS SegEnt *seg, uint32_t k, u32x4 lo, uint64_t ptr) {
+    PX_GAS u32x4 *e = (PX_GAS u32x4 *)(seg + k);
+    e[0] = lo;
+    e[1] = mk4((uint32_t)ptr, (uint32_t)(ptr >> 32), 0, 0);
+}
 
 __global__ void __launch_bounds__(256) k_tokenize(uint32_t n, const RecSlot *slots_in, uint32_t *nseg_out,
                                                   uint32_t *status) {
@@ -968,8 +987,9 @@ __global__ void __launch_bounds__(256) k_tokenize(uint32_t n, const RecSlot *slo
     for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < n; r += waves) {
         const RecSlot sl = slots_in[r];
         const PX_GAS uint8_t *comp = (const PX_GAS uint8_t *)sl.comp;
+        const uint64_t comp_addr = (uint64_t)sl.comp;
         const uint32_t len = sl.comp_len;
-        PX_GAS u32x4 *seg = (PX_GAS u32x4 *)sl.seg;
+        PX_GAS SegEnt *seg = (PX_GAS SegEnt *)sl.seg;
         PX_GAS uint16_t *pidx = (PX_GAS uint16_t *)sl.pidx;
         const uint32_t pidx_n = sl.pidx_n;
         uint32_t ns = 0, p = 0, wb = 0, err = 0, plain_start = 0;
@@ -979,7 +999,8 @@ __global__ void __launch_bounds__(256) k_tokenize(uint32_t n, const RecSlot *slo
         // the pending segment is written once the next one starts (its end is then known)
         auto emit = [&](int32_t x, uint32_t z, uint32_t w) {
             if (have) {
-                if (lane == 0) seg[ns] = mk4(pend_x, (uint32_t)x, pend_z, pend_w);
+                uint64_t ptr = (pend_z >> 30) == 0 ? comp_addr + (pend_z & kSegMask) : 0;
+                if (lane == 0) put_ent(seg, ns, mk4(pend_x, (uint32_t)x, pend_z, pend_w), ptr);
                 if (x < (int32_t)pend_x) {
                     mono = false;
                 } else if (mono && pidx_n) {
@@ -1049,11 +1070,12 @@ __global__ void __launch_bounds__(256) k_tokenize(uint32_t n, const RecSlot *slo
         }
         if (!err) {
             if (plain_open && plain_start < len) emit(plain_src, plain_start, 0);
-            emit(src, len, 0);  // closes the last segment; the sentinel stays pending
-            if (lane == 0) seg[ns] = mk4((uint32_t)src, (uint32_t)src, len, 0);
+            emit(src, len | kSegEnd, 0);  // closes the last segment; the sentinel stays pending
+            if (lane == 0) put_ent(seg, ns, mk4((uint32_t)src, (uint32_t)src, len | kSegEnd, 0), 0);
             // blocks past the source end: no segment
             if (mono && pidx_n)
-                for (uint32_t k = ((uint32_t)max(src, 0) + 15) / 16 + lane; k < pidx_n; k += 64) pidx[k] = (uint16_t)min(ns, 65535u);
+                for (uint32_t k = ((uint32_t)max(src, 0) + 15) / 16 + lane; k < pidx_n; k += 64)
+                    pidx[k] = (uint16_t)min(ns, 65535u);
         }
         if (lane == 0) {
             nseg_out[r] = err ? 0 : (ns | (mono && pidx_n ? 0u : kNoPidx));
@@ -1061,26 +1083,6 @@ __global__ void __launch_bounds__(256) k_tokenize(uint32_t n, const RecSlot *slo
         }
     }
 }
-
-// ====================================================================== decode
-// One wave per query.  A frame (the reference's PXSGen over one record range) is
-// consumed 64 segments at a time: lane l takes segment f.seg + l, a prefix scan of
-// the requested sizes gives every lane its ret cursor and its output offset, and
-// each lane expands its own record reference depth-first through a small per-lane
-// stack in LDS, writing straight to the output.  A lane whose work leaves the
-// simple case (a periodic self reference, deeper nesting, an output that would
-// reach the consumer's cap or differ from what it asked for, a record without a
-// position index) ends the batch; that one segment then goes through the serial
-// frame machine (a stack of Frames in scratch memory), which is the reference's
-// generator nesting restated.
-constexpr uint32_t kLaneDepth = 8;
-
-struct SlotV {
-    const PX_GAS uint8_t *comp;
-    const PX_GAS u32x4 *seg;
-    const PX_GAS uint16_t *pidx;
-    uint32_t nseg, pidx_n;
-};
 
 // 48-byte records moved as three 16-byte vectors (struct copies cannot cross address spaces)
 template <class T>
@@ -1102,6 +1104,13 @@ PX_DEV void store48(PX_GAS T *p, const T &t) {
     v[2] = w[2];
 }
 
+struct SlotV {
+    const PX_GAS uint8_t *comp;
+    const PX_GAS u32x4 *seg;  // entry k: seg[2k] = {x, ex, kz, aux}, seg[2k + 1] = {ptr lo, ptr hi, 0, 0}
+    const PX_GAS uint16_t *pidx;
+    uint32_t nseg, pidx_n;
+};
+
 PX_DEV SlotV slot_at(const PX_GAS RecSlot *slots, uint32_t r) {
     const RecSlot s = load48(slots + r);
     SlotV v;
@@ -1122,30 +1131,104 @@ PX_DEV SlotV slot_uniform(const PX_GAS RecSlot *slots, uint32_t r) {
     return v;
 }
 
-PX_DEV void wave_copy(PX_GAS uint8_t *dst, const PX_GAS uint8_t *src, uint32_t n) {
+// Resolve every record token of the new records to the entry of its target record
+// that holds the token's `from` (the decoder's lanes then walk entries by address).
+__global__ void __launch_bounds__(256) k_link(uint32_t n, const LinkJob *jobs) {
     const uint32_t lane = lane_id();
-    uint32_t o = 0;
-    for (; o + 256 <= n; o += 256) {  // four loads in flight per lane
-        uint8_t a0 = src[o + lane], a1 = src[o + 64 + lane], a2 = src[o + 128 + lane], a3 = src[o + 192 + lane];
-        dst[o + lane] = a0;
-        dst[o + 64 + lane] = a1;
-        dst[o + 128 + lane] = a2;
-        dst[o + 192 + lane] = a3;
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t j = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); j < n; j += waves) {
+        const LinkJob job = jobs[j];
+        PX_GAS u32x4 *seg = (PX_GAS u32x4 *)job.seg;
+        const PX_GAS RecSlot *slots = (const PX_GAS RecSlot *)job.slots;
+        for (uint32_t k = lane; k < job.nseg; k += 64) {
+            const u32x4 e = seg[2 * k];
+            if ((e.z >> 30) != 2) continue;
+            const uint32_t ridx = e.w & 0xffffu, rfrom = e.w >> 16;
+            uint64_t ptr = 0;
+            if (ridx < job.nrec) {
+                const SlotV t = slot_at(slots, ridx);
+                if (t.pidx_n && (rfrom >> 4) < t.pidx_n) {
+                    uint32_t k2 = min((uint32_t)t.pidx[rfrom >> 4], t.nseg);
+                    while (k2 < t.nseg && t.seg[2 * k2].y <= rfrom) ++k2;
+                    ptr = (uint64_t)(t.seg + 2 * k2);
+                }
+            }
+            seg[2 * k + 1] = mk4((uint32_t)ptr, (uint32_t)(ptr >> 32), 0, 0);
+        }
     }
-    for (uint32_t k = o + lane; k < n; k += 64) dst[k] = src[k];
+}
+
+// ====================================================================== decode
+// One wave per query.  A frame (the reference's PXSGen over one record range) is
+// consumed 64 segments at a time: lane l takes segment f.seg + l, a prefix scan of
+// the requested sizes gives every lane its ret cursor and its output offset, and
+// each lane expands its own record reference depth-first, walking the linked
+// segment entries by address with a small per-lane stack in LDS and writing
+// straight to the output.  A lane whose work leaves the simple case (a periodic
+// self reference, deeper nesting, an output that would reach the consumer's cap or
+// exceed what it asked for, an unlinked token) ends the batch; that one segment
+// then goes through the serial frame machine (a stack of Frames in scratch memory),
+// which is the reference's generator nesting restated.
+constexpr uint32_t kLaneDepth = 8;
+
+// Copies use unaligned 16-byte accesses (gfx950 runs in unaligned access mode; the
+// compiler itself emits them for byte-aligned memcpy).  Sources are compressed
+// bytes, destinations the query output: they never overlap.
+typedef uint32_t u32x4_u __attribute__((ext_vector_type(4), aligned(1)));
+PX_DEV u32x4 ld16(const PX_GAS uint8_t *p) { return *(const PX_GAS u32x4_u *)p; }
+PX_DEV void st16(PX_GAS uint8_t *p, u32x4 v) { *(PX_GAS u32x4_u *)p = v; }
+PX_DEV void copy16(PX_GAS uint8_t *dst, const PX_GAS uint8_t *src) { st16(dst, ld16(src)); }
+
+PX_DEV void wave_copy(PX_GAS uint8_t *dst, const PX_GAS uint8_t *src, uint32_t n) {
+    const uint32_t l16 = lane_id() * 16;
+    uint32_t o = 0;
+    for (; o + 4096 <= n; o += 4096) {  // four 16-byte loads in flight per lane
+        const u32x4 v0 = ld16(src + o + l16), v1 = ld16(src + o + 1024 + l16), v2 = ld16(src + o + 2048 + l16),
+                    v3 = ld16(src + o + 3072 + l16);
+        st16(dst + o + l16, v0);
+        st16(dst + o + 1024 + l16, v1);
+        st16(dst + o + 2048 + l16, v2);
+        st16(dst + o + 3072 + l16, v3);
+    }
+    for (; o + 1024 <= n; o += 1024) copy16(dst + o + l16, src + o + l16);
+    const uint32_t full = (n - o) / 16;
+    if (l16 < full * 16) copy16(dst + o + l16, src + o + l16);
+    const uint32_t t = o + full * 16 + lane_id();
+    if (t < n) dst[t] = src[t];
 }
 
 // one lane copies its own n bytes
 PX_DEV void lane_copy(PX_GAS uint8_t *dst, const PX_GAS uint8_t *src, uint32_t n) {
-    uint32_t i = 0;
-    for (; i + 4 <= n; i += 4) {
-        uint8_t a = src[i], b = src[i + 1], c = src[i + 2], d = src[i + 3];
-        dst[i] = a;
-        dst[i + 1] = b;
-        dst[i + 2] = c;
-        dst[i + 3] = d;
+    if (n >= 16) {
+        uint32_t i = 0;
+        for (; i + 64 <= n; i += 64) {
+            const u32x4 v0 = ld16(src + i), v1 = ld16(src + i + 16), v2 = ld16(src + i + 32), v3 = ld16(src + i + 48);
+            st16(dst + i, v0);
+            st16(dst + i + 16, v1);
+            st16(dst + i + 32, v2);
+            st16(dst + i + 48, v3);
+        }
+        for (; i + 16 <= n; i += 16) copy16(dst + i, src + i);
+        if (i < n) copy16(dst + n - 16, src + n - 16);  // overlapping tail, same bytes
+        return;
     }
-    for (; i < n; ++i) dst[i] = src[i];
+    if (n >= 8) {
+        uint64_t a, b;
+        __builtin_memcpy(&a, (const PX_GAS void *)src, 8);
+        __builtin_memcpy(&b, (const PX_GAS void *)(src + n - 8), 8);
+        __builtin_memcpy((PX_GAS void *)dst, &a, 8);
+        __builtin_memcpy((PX_GAS void *)(dst + n - 8), &b, 8);
+        return;
+    }
+    if (n >= 4) {
+        uint32_t a, b;
+        __builtin_memcpy(&a, (const PX_GAS void *)src, 4);
+        __builtin_memcpy(&b, (const PX_GAS void *)(src + n - 4), 4);
+        __builtin_memcpy((PX_GAS void *)dst, &a, 4);
+        __builtin_memcpy((PX_GAS void *)(dst + n - 4), &b, 4);
+        return;
+    }
+    for (uint32_t i = 0; i < n; ++i) dst[i] = src[i];
 }
 
 PX_DEV int32_t wave_excl_scan(int32_t v) {
@@ -1185,7 +1268,7 @@ PX_DEV uint32_t seg_find(const SlotV &s, int32_t from) {
         lo = min((uint32_t)uni(s.pidx[(uint32_t)from >> 4]), hi);
         for (;;) {  // at most 16 source bytes past a segment start: one probe, almost always
             uint32_t k = lo + lane;
-            uint64_t m = ballot(k < hi && (int32_t)s.seg[k].y > from);
+            uint64_t m = ballot(k < hi && (int32_t)s.seg[2 * k].y > from);
             if (m) return lo + ffs64(m);
             if (hi - lo <= 64) return hi;
             lo += 64;
@@ -1194,7 +1277,7 @@ PX_DEV uint32_t seg_find(const SlotV &s, int32_t from) {
     while (hi - lo > 64) {
         uint32_t step = (hi - lo + 63) / 64;
         uint32_t k = lo + lane * step;
-        bool le = k < hi && (int32_t)s.seg[k].y <= from;  // segment k ends at or before from
+        bool le = k < hi && (int32_t)s.seg[2 * k].y <= from;  // segment k ends at or before from
         uint64_t m = ballot(le);
         uint32_t cnt = (uint32_t)__popcll(m);  // prefix of lanes with le (monotone)
         uint32_t nlo = cnt ? lo + (cnt - 1) * step + 1 : lo;
@@ -1203,24 +1286,13 @@ PX_DEV uint32_t seg_find(const SlotV &s, int32_t from) {
         hi = uni(nhi);
     }
     uint32_t k = lo + lane;
-    bool le = k < hi && (int32_t)s.seg[k].y <= from;
+    bool le = k < hi && (int32_t)s.seg[2 * k].y <= from;
     return uni(lo + (uint32_t)__popcll(ballot(le)));
 }
 
-// per-lane version through the position index; flag when there is none
-PX_DEV uint32_t lane_find(const SlotV &s, int32_t a, bool &flag) {
-    uint32_t b = (uint32_t)a >> 4;
-    if (a < 0 || b >= s.pidx_n) {
-        flag = true;
-        return 0;
-    }
-    uint32_t k = s.pidx[b];
-    while (k < s.nseg && (int32_t)s.seg[k].y <= a) ++k;
-    return k;
-}
-
 struct DecLds {
-    uint32_t stk[kLaneDepth * 5][64];  // per-lane frames: rec, from, len, ret, seg
+    // per-lane frames, 4 words: entry address | rec << 48, from | len << 16, ret
+    uint32_t stk[kLaneDepth * 4][64];
 };
 
 __global__ void __launch_bounds__(64) k_decode(const DecodeQuery *qs, uint32_t nq, const RecSlot *const *chunk_slots,
@@ -1229,6 +1301,10 @@ __global__ void __launch_bounds__(64) k_decode(const DecodeQuery *qs, uint32_t n
     __shared__ DecLds lds;
     const uint32_t lane = lane_id();
     PX_GAS Frame *stk = (PX_GAS Frame *)scratch + (size_t)blockIdx.x * depth_cap;
+#ifdef PX_PROFILE
+    uint64_t prof[P_N] = {};
+    const uint64_t t_kernel0 = __builtin_amdgcn_s_memtime();
+#endif
     for (uint32_t qi = blockIdx.x; qi < nq; qi += gridDim.x) {
         const DecodeQuery q = qs[qi];
         const uint32_t qchunk = uni(q.chunk);
@@ -1271,7 +1347,8 @@ __global__ void __launch_bounds__(64) k_decode(const DecodeQuery *qs, uint32_t n
         auto batch = [&](Frame &f, const SlotV &sv) -> bool {
             const uint32_t k = f.seg + lane;
             const bool valid = k < sv.nseg;
-            const u32x4 E = valid ? sv.seg[k] : mk4(0, 0, 0, 0);
+            const u32x4 E = valid ? sv.seg[2 * k] : mk4(0, 0, 0, 0);
+            const u32x4 EH = valid ? sv.seg[2 * k + 1] : mk4(0, 0, 0, 0);
             const int32_t sx = (int32_t)E.x, ex = (int32_t)E.y;
             const uint32_t kind = E.z >> 30, cs = E.z & kSegMask;
             const uint32_t ridx = E.w & 0xffffu;
@@ -1312,87 +1389,106 @@ __global__ void __launch_bounds__(64) k_decode(const DecodeQuery *qs, uint32_t n
             }
             // record references: each lane expands its own range depth-first
             bool busy = active && !flag && child;
+            PX_CNT(P_D_BATCH, 1);
+#ifdef PX_PROFILE
+            const uint64_t t_lane0 = __builtin_amdgcn_s_memtime();
+#endif
             if (ballot(busy)) {
-                uint32_t rec = ridx, kk = 0, d = 0;
+                const PX_GAS u32x4 *e = (const PX_GAS u32x4 *)((uint64_t)EH.x | (uint64_t)EH.y << 32);
+                uint32_t rec = ridx, d = 0;
                 int32_t from = sub_from, len = reqc, ret = 0;
                 const uint32_t wmax = (uint32_t)reqc;
-                SlotV s{};
-                if (busy) {
-                    s = slot_at(slots, rec);
-                    kk = lane_find(s, from, flag);
-                    busy = !flag;
+                if (busy && !e) {
+                    flag = true;  // token without a linked target
+                    busy = false;
                 }
                 while (ballot(busy)) {
+                    PX_CNT(P_D_LANEIT, 1);
                     if (busy) {
-                        if (ret >= len || kk >= s.nseg) {
+                        const u32x4 F = e[0], FH = e[1];
+                        const int32_t x = (int32_t)F.x, y = (int32_t)F.y;
+                        const uint32_t kd = F.z >> 30;
+                        if (ret >= len || kd == 3) {
                             if (d == 0) {
                                 busy = false;
                             } else {
                                 --d;
-                                rec = lds.stk[d * 5 + 0][lane];
-                                from = (int32_t)lds.stk[d * 5 + 1][lane];
-                                len = (int32_t)lds.stk[d * 5 + 2][lane];
-                                ret = (int32_t)lds.stk[d * 5 + 3][lane];
-                                kk = lds.stk[d * 5 + 4][lane];
-                                s = slot_at(slots, rec);
+                                const uint32_t w0 = lds.stk[d * 4 + 0][lane], w1 = lds.stk[d * 4 + 1][lane];
+                                const uint32_t w2 = lds.stk[d * 4 + 2][lane];
+                                e = (const PX_GAS u32x4 *)((uint64_t)w0 | (uint64_t)(w1 & 0xffffu) << 32);
+                                rec = w1 >> 16;
+                                from = (int32_t)(w2 & 0xffffu);
+                                len = (int32_t)(w2 >> 16);
+                                ret = (int32_t)lds.stk[d * 4 + 3][lane];
                             }
-                        } else {
-                            const u32x4 F = s.seg[kk];
-                            const int32_t x = (int32_t)F.x, y = (int32_t)F.y;
-                            const uint32_t kd = F.z >> 30, c0 = F.z & kSegMask;
-                            if (kd == 0) {
-                                const int32_t q0 = max(x, from);
-                                if (q0 < y) {
-                                    const int32_t avail = y - q0, nd = len - ret;
-                                    int32_t nb = min(avail, nd);
-                                    const uint32_t ci = c0 + (uint32_t)(q0 - x);
-                                    if (avail > nd && compat && (esc_run_lane(s.comp, c0, ci + (uint32_t)nb - 1) & 1)) ++nb;
-                                    if (w + (uint32_t)nb > wmax) {
-                                        flag = true;  // over-yield past the lane's slot
-                                        busy = false;
-                                    } else {
-                                        lane_copy(o + base + w, s.comp + ci, (uint32_t)nb);
-                                        w += (uint32_t)nb;
-                                        ret += nb;
+                        } else if (kd == 0) {
+                            const int32_t q0 = max(x, from);
+                            if (q0 < y) {
+                                const int32_t avail = y - q0, nd = len - ret;
+                                const uint32_t nb = (uint32_t)min(avail, nd);
+                                const PX_GAS uint8_t *seg0 = (const PX_GAS uint8_t *)((uint64_t)FH.x | (uint64_t)FH.y << 32);
+                                const PX_GAS uint8_t *cp = seg0 + (q0 - x);
+                                const bool ov = avail > nd && compat;
+                                const uint32_t last = ov ? cp[nb - 1] : 0u;
+                                if (w + nb > wmax) {
+                                    flag = true;
+                                    busy = false;
+                                } else {
+                                    lane_copy(o + base + w, cp, nb);
+                                    w += nb;
+                                    ret += (int32_t)nb;
+                                    // a range ending inside a 251 pair writes the pair whole
+                                    if (last == kEsc && (esc_run_lane(seg0, 0, (uint32_t)(q0 - x) + nb - 1) & 1)) {
+                                        if (w + 1 > wmax) {
+                                            flag = true;
+                                            busy = false;
+                                        } else {
+                                            o[base + w] = cp[nb];
+                                            ++w;
+                                            ++ret;
+                                        }
                                     }
                                 }
-                                ++kk;
-                            } else if (kd == 2) {
-                                const int32_t sup = y - x;
-                                if (x - 1 + sup >= from) {
-                                    const uint32_t ri = F.w & 0xffffu;
-                                    const int32_t rf = (int32_t)(F.w >> 16), rt = rf + sup;
-                                    const int32_t sf = rf + max(0, from - x);
-                                    const int32_t st = min(rt, sf + (len - ret));
-                                    const int32_t stop = compat ? ret : max(x, from);
-                                    if (ri >= nrec || (ri == rec && sf < stop && stop < st) || d + 1 >= kLaneDepth) {
-                                        flag = true;
-                                        busy = false;
-                                    } else {
-                                        lds.stk[d * 5 + 0][lane] = rec;
-                                        lds.stk[d * 5 + 1][lane] = (uint32_t)from;
-                                        lds.stk[d * 5 + 2][lane] = (uint32_t)len;
-                                        lds.stk[d * 5 + 3][lane] = (uint32_t)(ret + (st - sf));
-                                        lds.stk[d * 5 + 4][lane] = kk + 1;
-                                        ++d;
-                                        rec = ri;
-                                        from = sf;
-                                        len = st - sf;
-                                        ret = 0;
-                                        s = slot_at(slots, rec);
-                                        kk = lane_find(s, from, flag);
-                                        if (flag) busy = false;
-                                    }
+                            }
+                            e += 2;
+                        } else if (kd == 2) {
+                            const int32_t sup = y - x;
+                            if (x - 1 + sup >= from) {
+                                const uint32_t ri = F.w & 0xffffu;
+                                const int32_t rf = (int32_t)(F.w >> 16), rt = rf + sup;
+                                const int32_t sf = rf + max(0, from - x);
+                                const int32_t st = min(rt, sf + (len - ret));
+                                const int32_t stop = compat ? ret : max(x, from);
+                                const PX_GAS u32x4 *t = (const PX_GAS u32x4 *)((uint64_t)FH.x | (uint64_t)FH.y << 32);
+                                const uint64_t nx = (uint64_t)(e + 2);
+                                if (!t || ri >= nrec || (ri == rec && sf < stop && stop < st) || d + 1 >= kLaneDepth ||
+                                    (uint32_t)from > 0xffffu || (uint32_t)len > 0xffffu || (nx >> 48) != 0) {
+                                    flag = true;  // leaves the lane path: serial machine
+                                    busy = false;
                                 } else {
-                                    ++kk;
+                                    lds.stk[d * 4 + 0][lane] = (uint32_t)nx;
+                                    lds.stk[d * 4 + 1][lane] = (uint32_t)(nx >> 32) | rec << 16;
+                                    lds.stk[d * 4 + 2][lane] = (uint32_t)from | (uint32_t)len << 16;
+                                    lds.stk[d * 4 + 3][lane] = (uint32_t)(ret + (st - sf));
+                                    ++d;
+                                    e = t;  // the target's entry holding rf; entries before sf are passed over
+                                    rec = ri;
+                                    from = sf;
+                                    len = st - sf;
+                                    ret = 0;
                                 }
                             } else {
-                                ++kk;
+                                e += 2;
                             }
+                        } else {
+                            e += 2;
                         }
                     }
                 }
             }
+#ifdef PX_PROFILE
+            prof[P_D_T_LANE] += __builtin_amdgcn_s_memtime() - t_lane0;
+#endif
             // commit the lanes before the first flagged one; a lane that produced fewer
             // bytes than it asked for (its record ran out) is committed but ends the batch
             const uint64_t fm = ballot(active && flag);
@@ -1402,6 +1498,9 @@ __global__ void __launch_bounds__(64) k_decode(const DecodeQuery *qs, uint32_t n
             const uint32_t first_flag = fm ? ffs64(fm) : 64u;
             const uint32_t first_short = sm ? ffs64(sm) : 64u;
             const uint32_t C = min(L, min(first_flag, first_short + 1));
+            PX_CNT(P_D_COMMIT, C);
+            PX_CNT(P_D_FLAGGED, first_flag == C && C < L ? 1 : 0);
+            PX_CNT(P_D_SHORT, first_short + 1 == C ? 1 : 0);
             uint64_t lm = ballot(active && !flag && kind == 0 && reqc > 64 && lane < C);
             while (lm) {
                 const uint32_t j = ffs64(lm);
@@ -1472,12 +1571,13 @@ __global__ void __launch_bounds__(64) k_decode(const DecodeQuery *qs, uint32_t n
             bool pushed = false;
             while (!pop && !pushed && !err && f.ret < f.len && f.seg < sv.nseg) {
                 if (!batch(f, sv)) continue;
+                PX_CNT(P_D_SERIAL, 1);
                 // one segment through the serial machine
-                const u32x4 E = sv.seg[f.seg];
+                const u32x4 E = sv.seg[2 * f.seg];
                 const int32_t sx = (int32_t)uni(E.x), ex = (int32_t)uni(E.y);
                 const uint32_t sz = uni(E.z), sw = uni(E.w);
                 const uint32_t cs = sz & kSegMask;
-                if (sz & kSegRecord) {
+                if ((sz >> 30) == 2) {
                     const int32_t ridx = (int32_t)(sw & 0xffffu);
                     const int32_t rfrom = (int32_t)(sw >> 16);
                     const int32_t supply = ex - sx;
@@ -1497,11 +1597,12 @@ __global__ void __launch_bounds__(64) k_decode(const DecodeQuery *qs, uint32_t n
                         uint32_t ccap = periodic ? min(f.cap, outp + (uint32_t)(sub_to - sub_from)) : f.cap;
                         bool ok = periodic ? push(f.rec, sub_from, stop, ccap) : push((uint32_t)ridx, sub_from, sub_to, ccap);
                         if (!ok) break;
+                        PX_CNT(P_D_PUSH, 1);
                         pushed = true;
                         break;
                     }
                     ++f.seg;
-                } else if (sz & kSegSkip) {
+                } else if ((sz >> 30) == 1) {
                     ++f.seg;
                 } else {
                     const int32_t p0 = max(sx, f.from);
@@ -1538,6 +1639,11 @@ __global__ void __launch_bounds__(64) k_decode(const DecodeQuery *qs, uint32_t n
             status[qi] = err ? err : (capped ? (uint32_t)kErrSpace : (uint32_t)kOk);
         }
     }
+#ifdef PX_PROFILE
+    prof[P_D_T_TOTAL] = __builtin_amdgcn_s_memtime() - t_kernel0;
+    if (lane == 0)
+        for (int k = P_D_BATCH; k < P_N; ++k) atomicAdd(&g_prof[k], (unsigned long long)prof[k]);
+#endif
 }
 
 // ====================================================================== migrate
@@ -1601,6 +1707,20 @@ hipError_t launch_compact(hipStream_t s, uint32_t n, uint8_t *const *src, const 
     if (!n) return hipSuccess;
     uint32_t blocks = min((n + 3) / 4, 8192u);
     k_compact<<<blocks, 256, 0, s>>>(n, src, len, dst, dst_off);
+    return hipGetLastError();
+}
+
+hipError_t launch_count_esc(hipStream_t s, uint32_t n, uint8_t *const *src, const uint32_t *len, uint32_t *n_esc) {
+    if (!n) return hipSuccess;
+    uint32_t blocks = min((n + 3) / 4, 8192u);
+    k_count_esc<<<blocks, 256, 0, s>>>(n, src, len, n_esc);
+    return hipGetLastError();
+}
+
+hipError_t launch_link(hipStream_t s, uint32_t n, const LinkJob *jobs) {
+    if (!n) return hipSuccess;
+    uint32_t blocks = min((n + 3) / 4, 8192u);
+    k_link<<<blocks, 256, 0, s>>>(n, jobs);
     return hipGetLastError();
 }
 

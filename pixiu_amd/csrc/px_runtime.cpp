@@ -30,6 +30,8 @@ hipError_t launch_gst_encode(hipStream_t, const GstShard *, uint32_t, const uint
                              uint32_t *, uint32_t *, uint32_t *, uint32_t *);
 hipError_t launch_compact(hipStream_t, uint32_t, uint8_t *const *, const uint32_t *, uint8_t *, const uint64_t *);
 hipError_t launch_tokenize(hipStream_t, uint32_t, const RecSlot *, uint32_t *, uint32_t *);
+hipError_t launch_count_esc(hipStream_t, uint32_t, uint8_t *const *, const uint32_t *, uint32_t *);
+hipError_t launch_link(hipStream_t, uint32_t, const LinkJob *);
 hipError_t launch_decode(hipStream_t, const DecodeQuery *, uint32_t, const RecSlot *const *, uint8_t *,
                          uint32_t *, uint32_t *, Frame *, uint32_t, uint32_t);
 hipError_t launch_rehash(hipStream_t, const uint4 *, uint32_t, uint32_t, uint4 *, uint32_t);
@@ -55,6 +57,9 @@ inline uint64_t round_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
 // position-index blocks for a record of `src_len` source bytes (k_tokenize)
 inline uint32_t pidx_blocks(uint32_t src_len) { return src_len / 16 + 2; }
 constexpr uint32_t kNoPidxBit = 1u << 31;  // k_tokenize: record has no position index
+// segment entries for a compressed record holding `esc` 251 bytes: plain runs and
+// tokens alternate, every token starts with a 251, plus the end sentinel
+inline uint64_t seg_entries(uint32_t esc) { return 2ull * esc + 2; }
 inline void set_nseg(RecSlot &s, uint32_t tok) {
     s.nseg = tok & ~kNoPidxBit;
     if (tok & kNoPidxBit) s.pidx_n = 0;
@@ -201,7 +206,7 @@ struct px_ctx {
     std::vector<std::pair<void *, uint64_t>> store_blocks;  // packed record stores + segment indexes
     uint8_t *last_store = nullptr;  // packed compressed bytes of the last set batch
     uint64_t last_store_bytes = 0;
-    DevBuf scratch_frames, dq_buf, dstat_buf, dlen_buf, in_buf, tmp_buf;
+    DevBuf scratch_frames, dq_buf, dstat_buf, dlen_buf, in_buf, tmp_buf, link_buf;
     px_stats stats{};
     int last_hip = 0;
 
@@ -531,7 +536,7 @@ struct px_ctx {
         st.assign(nq, 0);
         if (!nq) return;
         uint32_t depth = opts.decode_depth ? opts.decode_depth : 4096;
-        uint32_t waves = opts.decode_waves ? opts.decode_waves : 4096;
+        uint32_t waves = opts.decode_waves ? opts.decode_waves : 8192;
         waves = std::min(waves, nq);
         auto *frames = (Frame *)scratch_frames.get((uint64_t)waves * depth * sizeof(Frame));
         auto *dq = (DecodeQuery *)dq_buf.get((uint64_t)nq * sizeof(DecodeQuery));
@@ -552,6 +557,14 @@ struct px_ctx {
             hcheck(hipEventElapsedTime(&ms, ev0, ev1));
             stats.last_decode_kernel_ms = ms;
         }
+    }
+
+    // k_link over `jobs` (device copy staged through a scratch buffer)
+    void link(const std::vector<LinkJob> &jobs) {
+        if (jobs.empty()) return;
+        auto *d = (LinkJob *)link_buf.get(jobs.size() * sizeof(LinkJob));
+        h2d(d, jobs.data(), jobs.size() * sizeof(LinkJob));
+        hcheck(launch_link(stream, (uint32_t)jobs.size(), d));
     }
 
     // drop every record, keep the device memory for reuse
@@ -660,9 +673,9 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     }
 
     // ---- pass 1: escaped doc lengths
-    auto *tmp = (uint32_t *)tmp_buf.get((uint64_t)n * 24 + 64);
+    auto *tmp = (uint32_t *)tmp_buf.get((uint64_t)n * 28 + 64);
     uint32_t *d_doclen = tmp, *d_complen = tmp + n, *d_chunk = tmp + 2 * n, *d_idx = tmp + 3 * n,
-             *d_status = tmp + 4 * n, *d_nseg = tmp + 5 * n;
+             *d_status = tmp + 4 * n, *d_nseg = tmp + 5 * n, *d_nesc = tmp + 6 * n;
     hcheck(launch_doc_len(stream, n, dkeys, dkoff, dvals, dvoff, d_doclen));
     std::vector<uint32_t> doc_len(n);
     d2h(doc_len.data(), d_doclen, n * 4);
@@ -742,7 +755,9 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     hcheck(launch_gst_encode(stream, d_gs, (uint32_t)gs.size(), d_doclen, d_cdst, d_complen, d_chunk, d_idx,
                              d_status));
     hcheck(hipEventRecord(ev1, stream));
-    std::vector<uint32_t> comp_len(n), rchunk(n), ridx(n), rstatus(n);
+    hcheck(launch_count_esc(stream, n, d_cdst, d_complen, d_nesc));
+    std::vector<uint32_t> comp_len(n), rchunk(n), ridx(n), rstatus(n), nesc(n);
+    d2h(nesc.data(), d_nesc, n * 4);
     d2h(comp_len.data(), d_complen, n * 4);
     d2h(rchunk.data(), d_chunk, n * 4);
     d2h(ridx.data(), d_idx, n * 4);
@@ -760,7 +775,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     for (uint32_t r = 0; r < n; ++r) {
         bool ok = doc_len[r] != 0xffffffffu && rstatus[r] == kOk;
         coff[r + 1] = coff[r] + (ok ? round_up(comp_len[r], 8) : 0);
-        soff[r + 1] = soff[r] + (ok ? (uint64_t)(comp_len[r] + 2) * sizeof(uint4) : 0);
+        soff[r + 1] = soff[r] + (ok ? seg_entries(nesc[r]) * sizeof(SegEnt) : 0);
         poff[r + 1] = poff[r] + (ok ? round_up(pidx_blocks(doc_len[r]) * 2, 16) : 0);
     }
     auto *store = (uint8_t *)heap.alloc(coff[n] + 64);
@@ -776,7 +791,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     for (uint32_t r = 0; r < n; ++r) {
         bool ok = doc_len[r] != 0xffffffffu && rstatus[r] == kOk;
         slots[r].comp = store + coff[r];
-        slots[r].seg = (const uint4 *)(segs + soff[r]);
+        slots[r].seg = (const SegEnt *)(segs + soff[r]);
         slots[r].pidx = (const uint16_t *)(segs + soff[n] + poff[r]);
         slots[r].comp_len = ok ? comp_len[r] : 0;
         slots[r].nseg = 0;
@@ -843,6 +858,14 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             h2d(ch.dev + t.second.first, ch.slots.data() + t.second.first,
                 (size_t)(t.second.second - t.second.first) * sizeof(RecSlot));
         }
+        // resolve the new records' tokens to their target entries
+        std::vector<LinkJob> jobs;
+        for (uint32_t r = 0; r < n; ++r) {
+            if (rgchunk[r] == kNone) continue;
+            const Chunk &ch = chunks[rgchunk[r]];
+            jobs.push_back(LinkJob{const_cast<SegEnt *>(slots[r].seg), ch.dev, slots[r].nseg, ch.n});
+        }
+        link(jobs);
     }
 
     // ---- compat key prefixes (GPU decode of each new record's key region)
@@ -1181,12 +1204,15 @@ int px_import_chunk(px_ctx *ctx, uint32_t n, const uint8_t *comp, const uint64_t
         // an imported record's source length is unknown up front: index the first
         // kMaxDoc source bytes (a lane asking past that goes to the serial path)
         const uint32_t pn = pidx_blocks(kMaxDoc);
-        std::vector<uint64_t> coff(n + 1, 0), soff(n + 1, 0);
+        std::vector<uint64_t> coff(n + 1, 0), soff(n + 1, 0), nents(n);
         for (uint32_t r = 0; r < n; ++r) {
             uint64_t l = off[r + 1] - off[r];
             if (l > (uint64_t)kMaxDoc) return PX_EINVAL;
+            uint64_t esc = 0;
+            for (uint64_t i = off[r]; i < off[r + 1]; ++i) esc += comp[i] == kEsc;
+            nents[r] = seg_entries((uint32_t)esc);
             coff[r + 1] = coff[r] + round_up(l, 8);
-            soff[r + 1] = soff[r] + (l + 2) * sizeof(uint4) + round_up((uint64_t)pn * 2, 16);
+            soff[r + 1] = soff[r] + nents[r] * sizeof(SegEnt) + round_up((uint64_t)pn * 2, 16);
         }
         auto *store = (uint8_t *)ctx->heap.alloc(coff[n] + 64);
         auto *segs = (uint8_t *)ctx->heap.alloc(soff[n] + 64);
@@ -1196,8 +1222,8 @@ int px_import_chunk(px_ctx *ctx, uint32_t n, const uint8_t *comp, const uint64_t
         for (uint32_t r = 0; r < n; ++r) {
             uint64_t l = off[r + 1] - off[r];
             ctx->h2d(store + coff[r], comp + off[r], l);
-            slots[r] = RecSlot{store + coff[r], (const uint4 *)(segs + soff[r]),
-                               (const uint16_t *)(segs + soff[r] + (l + 2) * sizeof(uint4)), (uint32_t)l, 0, pn, 0};
+            slots[r] = RecSlot{store + coff[r], (const SegEnt *)(segs + soff[r]),
+                               (const uint16_t *)(segs + soff[r] + nents[r] * sizeof(SegEnt)), (uint32_t)l, 0, pn, 0, 0};
         }
         auto *d_slots = (RecSlot *)ctx->heap.alloc((uint64_t)n * sizeof(RecSlot));
         auto *d_tmp = (uint32_t *)ctx->heap.alloc((uint64_t)n * 8);
@@ -1207,8 +1233,8 @@ int px_import_chunk(px_ctx *ctx, uint32_t n, const uint8_t *comp, const uint64_t
         ctx->d2h(nseg.data(), d_tmp, (size_t)n * 4);
         ctx->d2h(tst.data(), d_tmp + n, (size_t)n * 4);
         ctx->sync();
-        std::vector<uint4> sentinel(n);
-        for (uint32_t r = 0; r < n; ++r) ctx->d2h(&sentinel[r], slots[r].seg + (nseg[r] & ~kNoPidxBit), sizeof(uint4));
+        std::vector<SegEnt> sentinel(n);
+        for (uint32_t r = 0; r < n; ++r) ctx->d2h(&sentinel[r], slots[r].seg + (nseg[r] & ~kNoPidxBit), sizeof(SegEnt));
         ctx->sync();
         ctx->heap.release(d_slots, (uint64_t)n * sizeof(RecSlot));
         ctx->heap.release(d_tmp, (uint64_t)n * 8);
@@ -1230,6 +1256,11 @@ int px_import_chunk(px_ctx *ctx, uint32_t n, const uint8_t *comp, const uint64_t
         ch.n = n;
         ctx->chunk_reserve(c, n);
         ctx->h2d(ctx->chunks[c].dev, ctx->chunks[c].slots.data(), (size_t)n * sizeof(RecSlot));
+        std::vector<LinkJob> jobs(n);
+        for (uint32_t r = 0; r < n; ++r)
+            jobs[r] = LinkJob{const_cast<SegEnt *>(ctx->chunks[c].slots[r].seg), ctx->chunks[c].dev,
+                              ctx->chunks[c].slots[r].nseg, n};
+        ctx->link(jobs);
         ctx->sync();
         if (shard_out) *shard_out = sh.id;
         return PX_OK;
