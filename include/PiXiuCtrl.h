@@ -13,8 +13,7 @@
 //
 // including the CLI's `ctrl.st.cbt_chunk->getitem(ctrl.st.local_chunk.used_num - 1)->len`
 // (main.cpp:67).  Semantics are the reference's single instance (one shard);
-// getitem streams the compat expansion (PXSGen byte-for-byte).  Differences:
-// `iter` returns NULL (prefix iteration is not on the ported path yet) and
+// getitem and iter stream the compat expansion (PXSGen byte-for-byte).  Difference:
 // `reinsert` is a no-op (compaction policy out of scope).
 #ifndef PIXIU_CTRL_FACADE_H
 #define PIXIU_CTRL_FACADE_H
@@ -52,8 +51,18 @@ struct PXSGen {
     char *consume_repr(void);
 };
 
+// PiXiuCtrl::iter's generator (CritBitTree.h:134-157): yields one PXSGen per record,
+// expanded up front on the GPU.
 struct CBTGen {
-    bool operator()(PXSGen *&) { return false; }
+    std::vector<std::vector<uint8_t>> docs;
+    size_t cur = 0;
+
+    bool operator()(PXSGen *&rv) {
+        if (cur >= docs.size()) return false;
+        rv = new PXSGen();
+        rv->buf = std::move(docs[cur++]);
+        return true;
+    }
 };
 
 inline void PXSGen_free(PXSGen *gen) { delete gen; }
@@ -135,7 +144,33 @@ struct PiXiuCtrl {
         return g;
     }
 
-    CBTGen *iter(uint8_t[], int) { return nullptr; }
+    // PiXiuCtrl::iter (PiXiuCtrl.cpp:71-75): NULL for an empty tree
+    CBTGen *iter(uint8_t prefix[], int prefix_len) {
+        uint32_t n = 0;
+        std::vector<px_rec> recs(64);
+        int rc = px_iter(ctx, prefix, (uint64_t)(prefix_len > 0 ? prefix_len : 0), recs.data(), (uint32_t)recs.size(), &n);
+        if (rc == PX_ESPACE) {
+            recs.resize(n);
+            rc = px_iter(ctx, prefix, (uint64_t)(prefix_len > 0 ? prefix_len : 0), recs.data(), n, &n);
+        }
+        if (rc != PX_OK) return nullptr;
+        CBTGen *g = new CBTGen();
+        if (!n) return g;
+        std::vector<uint8_t> out((size_t)n * (4 * PXSG_MAX_TO + 1024));
+        std::vector<uint64_t> off(n);
+        std::vector<uint32_t> len(n), status(n);
+        uint64_t need = 0;
+        rc = px_parse_batch(ctx, n, recs.data(), PX_COMPAT, out.data(), out.size(), 0, off.data(), len.data(),
+                            status.data(), &need);
+        if (rc == PX_ESPACE) {
+            out.resize(need);
+            rc = px_parse_batch(ctx, n, recs.data(), PX_COMPAT, out.data(), out.size(), 0, off.data(), len.data(),
+                                status.data(), &need);
+        }
+        for (uint32_t i = 0; i < n; ++i)
+            g->docs.emplace_back(out.begin() + (long)off[i], out.begin() + (long)(off[i] + (status[i] == PX_OK ? len[i] : 0)));
+        return g;
+    }
 
     int delitem(uint8_t k[], int k_len) {
         uint64_t off[2] = {0, (uint64_t)k_len};

@@ -18,6 +18,7 @@
  *   px_get_batch .............. PiXiuCtrl::getitem + PXSGen drain   (PiXiuCtrl.cpp:59-61, PiXiuStr.h:129-198)
  *   px_contains_batch ......... PiXiuCtrl::contains                 (PiXiuCtrl.cpp:55-57)
  *   px_del_batch .............. PiXiuCtrl::delitem                  (PiXiuCtrl.cpp:63-69)
+ *   px_iter ................... PiXiuCtrl::iter -> CBTGen           (PiXiuCtrl.cpp:71-75, CritBitTree.h:55-157)
  *   px_parse_batch ............ PiXiuStr::parse(from,to,chunk)      (PiXiuStr.cpp:166-176)
  *   px_export ................. cbt_chunk->getitem(idx) bytes       (PiXiuStr.cpp:202-206, main.cpp:67)
  *
@@ -119,6 +120,15 @@ int px_contains_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64
                       uint32_t *result);
 int px_del_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff,
                  uint32_t *result);
+
+/* PiXiuCtrl::iter(prefix) (PiXiuCtrl.cpp:71-75; CBTGen/CBTGHelper, CritBitTree.h:55-157):
+ * the records the reference's generator yields, in yield order (crit-bit order under
+ * the escaped prefix; nothing when the first record reached does not start with it).
+ * Expand them with px_parse_batch over [0, 65535).  Shards are visited in id order
+ * (records_per_shard = 0 is the reference's single tree).  PX_ENOTFOUND: every tree is
+ * empty (the reference returns a NULL generator).  PX_ESPACE: *n_out = records needed. */
+int px_iter(px_ctx *ctx, const uint8_t *prefix, uint64_t prefix_len, px_rec *recs, uint32_t cap,
+            uint32_t *n_out);
 
 /* Compressed bytes of stored records, copied to host CSR (out_off has n+1 entries). */
 int px_export(px_ctx *ctx, uint32_t n, const px_rec *recs, uint8_t *out, uint64_t out_cap,

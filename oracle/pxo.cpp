@@ -809,6 +809,47 @@ struct pxo_shard {
         return 0;
     }
 
+    // PiXiuStr::startswith (PiXiuStr.cpp:145-164): the record's compat stream begins
+    // with `prefix` (escaped, no terminator)
+    bool startswith(const Leaf &l, const Bytes &prefix) {
+        Sink s;
+        s.limit = prefix.size();
+        decode_into(l.chunk, l.idx, 0, kMaxDoc, PXO_COMPAT, s);
+        return s.out.size() == prefix.size() && std::equal(prefix.begin(), prefix.end(), s.out.begin());
+    }
+
+    // CritBitTree::iter / CBTGHelper / CBTGen (CritBitTree.h:55-157, CritBitTree.cpp:271-282):
+    // follow the prefix's crit bits; once a node's diff_at reaches past the prefix the
+    // whole subtree is taken (kid 0 before kid 1).  The first leaf reached is checked
+    // with startswith; if it fails the generator yields NULL and CBTGen stops, else it
+    // and every later leaf are yielded unchecked.  Returns false for an empty tree.
+    bool iter(const Bytes &prefix, std::vector<Leaf> &out) {
+        if (!has_root) return false;
+        bool harvest = false;
+        std::vector<std::pair<CbtRef, bool>> stack{{root, false}};
+        while (!stack.empty()) {
+            auto [ref, include_all] = stack.back();
+            stack.pop_back();
+            if (ref.inner < 0) {
+                if (!harvest && !startswith(ref.leaf, prefix)) break;
+                harvest = true;
+                out.push_back(ref.leaf);
+                continue;
+            }
+            const CbtInner &n = cbt[(size_t)ref.inner];
+            uint8_t crit = prefix.size() > n.diff_at ? prefix[n.diff_at] : 0;
+            int direct = crit_dir(n.mask, crit);
+            if (!include_all && n.diff_at >= prefix.size()) include_all = true;
+            if (include_all) {
+                stack.push_back({n.kid[1], true});
+                stack.push_back({n.kid[0], true});
+            } else {
+                stack.push_back({n.kid[direct], false});
+            }
+        }
+        return true;
+    }
+
     // CritBitTree::getitem + key_eq (CritBitTree.cpp:180-196; PiXiuStr.cpp:129-143)
     bool lookup(const Bytes &q, Leaf *out) {
         if (!has_root) return false;
@@ -905,6 +946,25 @@ int pxo_get(pxo_shard *s, const uint8_t *k, int klen, int mode, uint8_t *out, in
         Sink sk;
         s->decode_into(l.chunk, l.idx, 0, kMaxDoc, mode, sk);
         return copy_out(sk.out, out, cap);
+    } catch (const Fail &f) {
+        return f.code;
+    }
+}
+
+// PiXiuCtrl::iter (PiXiuCtrl.cpp:71-75): the records yielded, in order.  Returns the
+// count (-5 = PXO_NOTFOUND for an empty tree, the reference's NULL generator).
+int pxo_iter(pxo_shard *s, const uint8_t *prefix, int plen, uint32_t *chunk_out, uint32_t *idx_out, int cap) {
+    try {
+        Bytes p;
+        escape_append(prefix, plen, false, p);
+        std::vector<Leaf> got;
+        if (!s->iter(p, got)) return PXO_NOTFOUND;
+        if ((int)got.size() > cap) return PXO_ESPACE;
+        for (size_t i = 0; i < got.size(); ++i) {
+            chunk_out[i] = got[i].chunk;
+            idx_out[i] = got[i].idx;
+        }
+        return (int)got.size();
     } catch (const Fail &f) {
         return f.code;
     }

@@ -52,6 +52,9 @@ int pxo_get(pxo_shard *s, const uint8_t *k, int klen, int mode, uint8_t *out, in
 /* PiXiuCtrl::contains (1/0) and ::delitem (0 deleted, 1 not found) */
 int pxo_contains(pxo_shard *s, const uint8_t *k, int klen);
 int pxo_delete(pxo_shard *s, const uint8_t *k, int klen);
+/* PiXiuCtrl::iter: (chunk, idx) of the yielded records in order; count, PXO_NOTFOUND
+   for an empty tree, PXO_ESPACE if cap is too small. */
+int pxo_iter(pxo_shard *s, const uint8_t *prefix, int plen, uint32_t *chunk_out, uint32_t *idx_out, int cap);
 
 uint32_t pxo_num_chunks(pxo_shard *s);
 uint32_t pxo_chunk_records(pxo_shard *s, uint32_t chunk);

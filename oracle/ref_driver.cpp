@@ -83,6 +83,26 @@ int refx_delitem(const uint8_t *k, int klen) {
     return g_ctrl.delitem((uint8_t *)k, klen);
 }
 
+// PiXiuCtrl::iter: drains every yielded generator into out (CSR offsets in off[]).
+// Returns the record count, -1 for a NULL generator, -2 on overflow.
+int refx_iter(const uint8_t *prefix, int plen, uint8_t *out, int cap, uint64_t *off, int max_recs) {
+    CBTGen *g = g_ctrl.iter((uint8_t *)prefix, plen);
+    if (g == nullptr) return -1;
+    PXSGen *rv = nullptr;
+    int n = 0;
+    uint64_t d = 0;
+    off[0] = 0;
+    while (g->operator()(rv)) {
+        if (n >= max_recs) return -2;
+        int m = drain(rv, out + d, (int)(cap - d));
+        if (m < 0) return -2;
+        d += (uint64_t)m;
+        off[++n] = d;
+    }
+    CBTGen_free(g);
+    return n;
+}
+
 // PiXiuStr::parse(from,to) of record `idx` of the CURRENT chunk (PiXiuStr.cpp:166).
 int refx_parse_current(int idx, int from, int to, uint8_t *out, int cap) {
     PiXiuChunk *c = g_ctrl.st.cbt_chunk;

@@ -72,7 +72,7 @@ REC_DTYPE = np.dtype([("shard", "<u4"), ("chunk", "<u4"), ("idx", "<u4"), ("from
 # every symbol include/pixiu_amd.h declares
 EXPORTS = ["px_open", "px_close", "px_strerror", "px_set_batch", "px_get_batch", "px_parse_batch",
            "px_contains_batch", "px_del_batch", "px_export", "px_stats_get", "px_stream", "px_reset",
-           "px_last_store", "px_import_chunk"]
+           "px_last_store", "px_import_chunk", "px_iter"]
 
 _LIB = None
 
@@ -104,6 +104,7 @@ def load_library() -> C.CDLL:
     lib.px_reset.argtypes = [vp]
     lib.px_last_store.argtypes = [vp, vp, u64, i32, vp]
     lib.px_import_chunk.argtypes = [vp, u32, vp, vp, vp]
+    lib.px_iter.argtypes = [vp, vp, u64, vp, u32, vp]
     _LIB = lib
     return lib
 
@@ -250,6 +251,24 @@ class Store:
         if rc != PX_OK:
             raise PxError(rc, "px_del_batch")
         return r[:n]
+
+    def iter(self, prefix: bytes):
+        """PiXiuCtrl::iter: the yielded records (REC_DTYPE, yield order), or None when every
+        tree is empty (the reference's NULL generator).  Expand with parse_batch."""
+        pb = np.frombuffer(prefix, np.uint8) if prefix else np.zeros(1, np.uint8)
+        n = C.c_uint32(0)
+        cap = 1024
+        while True:
+            recs = np.zeros(cap, REC_DTYPE)
+            rc = self._lib.px_iter(self._h, _ptr(pb), len(prefix), _ptr(recs), cap, C.byref(n))
+            if rc == PX_ESPACE:
+                cap = n.value
+                continue
+            if rc == PX_ENOTFOUND:
+                return None
+            if rc != PX_OK:
+                raise PxError(rc, "px_iter")
+            return recs[:n.value]
 
     def export(self, recs: np.ndarray) -> list:
         recs = np.ascontiguousarray(recs, REC_DTYPE)

@@ -77,7 +77,8 @@ PX_DEV uint32_t rd16(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1]
 enum { P_BYTES, P_FF_CALLS, P_FF_BYTES, P_PASS, P_ITERS, P_LOOKUPS, P_PROBES, P_ROOT, P_WALK, P_LINK, P_CANON_LVL,
        P_T_TOTAL, P_T_FF, P_T_DERIVE, P_T_WALK, P_T_SPLIT, P_T_GROW, P_T_CANON, P_T_END, P_T_ROOT, P_T_ENC,
        P_KEYMISS, P_T_KEY, P_T_LOOK,
-       P_D_BATCH, P_D_LANEIT, P_D_SERIAL, P_D_COMMIT, P_D_FLAGGED, P_D_SHORT, P_D_PUSH, P_D_T_TOTAL, P_D_T_LANE, P_N };
+       P_D_BATCH, P_D_LANEIT, P_D_SERIAL, P_D_COMMIT, P_D_FLAGGED, P_D_SHORT, P_D_PUSH, P_D_T_TOTAL, P_D_T_LANE,
+       P_G_NOSPLIT, P_G_T_LEAF, P_G_T_SPLIT, P_G_T_ADD, P_N };
 __device__ unsigned long long g_prof[P_N];
 #define PX_CNT(k, v) (prof[k] += (v))
 #define PX_T0() uint64_t _t0 = __builtin_amdgcn_s_memtime()
@@ -610,8 +611,18 @@ struct GstWave {
     // the caller (their loads were issued before this function's stores)
     PX_DEV bool grow(Edge &e, uint32_t &last_inner, uint32_t c, bool split, uint32_t key_e) {
         Edge leaf;
+#ifdef PX_PROFILE
+        uint64_t tq = __builtin_amdgcn_s_memtime();
+#endif
         if (!new_leaf(leaf, c)) return false;
         --remainder;
+#ifdef PX_PROFILE
+        {
+            uint64_t t2 = __builtin_amdgcn_s_memtime();
+            prof[P_G_T_LEAF] += t2 - tq;
+            tq = t2;
+        }
+#endif
         if (split) {
             Edge in;
             if (!new_node(in.id)) return false;
@@ -637,7 +648,11 @@ struct GstWave {
                 nrec(in.id)[4] = pk2(leaf);
                 e.slot = kNone;  // e fell out of the tree (replaced under the same byte)
             }
+#ifdef PX_PROFILE
+            prof[P_G_T_SPLIT] += __builtin_amdgcn_s_memtime() - tq;
+#endif
         } else {
+            PX_CNT(P_G_NOSPLIT, 1);
             if (last_inner != kNone) nodes[2 * last_inner].x = e.id;
             last_inner = e.id;
             add_child(e.id, e.cnt, leaf);
@@ -645,6 +660,9 @@ struct GstWave {
                 ++e.cnt;
                 write_entry(e.slot, act_node, e);
             }
+#ifdef PX_PROFILE
+            prof[P_G_T_ADD] += __builtin_amdgcn_s_memtime() - tq;
+#endif
         }
         return true;
     }

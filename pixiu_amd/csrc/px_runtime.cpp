@@ -206,7 +206,7 @@ struct px_ctx {
     std::vector<std::pair<void *, uint64_t>> store_blocks;  // packed record stores + segment indexes
     uint8_t *last_store = nullptr;  // packed compressed bytes of the last set batch
     uint64_t last_store_bytes = 0;
-    DevBuf scratch_frames, dq_buf, dstat_buf, dlen_buf, in_buf, tmp_buf, link_buf;
+    DevBuf scratch_frames, dq_buf, dstat_buf, dlen_buf, in_buf, tmp_buf, link_buf, iter_buf;
     px_stats stats{};
     int last_hip = 0;
 
@@ -507,6 +507,54 @@ struct px_ctx {
             }
         }
         return 1;
+    }
+
+    // PiXiuStr::startswith (PiXiuStr.cpp:145-164) on a stored record: its stored compat
+    // key prefix when that is long enough, else a GPU decode of the first |p| bytes
+    bool rec_startswith(const Leaf &l, const std::string &p) {
+        uint32_t klen;
+        const uint8_t *kp = kp_of(l, &klen);
+        if (p.size() <= klen) return memcmp(kp, p.data(), p.size()) == 0;
+        std::vector<DecodeQuery> q{DecodeQuery{l.chunk, l.idx, 0, kMaxDoc, 0, (uint32_t)p.size(), 0}};
+        auto *d = (uint8_t *)iter_buf.get(round_up(p.size(), 64) + 64);
+        std::vector<uint32_t> len, st;
+        run_decode(q, d, len, st, false);
+        if ((st[0] != kOk && st[0] != kErrSpace) || len[0] < p.size()) return false;
+        std::string got(p.size(), '\0');
+        d2h(&got[0], d, p.size());
+        sync();
+        return got == p;
+    }
+
+    // CritBitTree::iter (CBTGHelper / CBTGen, CritBitTree.h:55-157): follow the
+    // prefix's crit bits; from the first node whose diff_at is past the prefix take
+    // the whole subtree (kid 0 first).  The first leaf reached must start with the
+    // prefix, else the generator yields NULL and stops; later leaves are unchecked.
+    bool cbt_iter(const Shard &s, const std::string &p, std::vector<Leaf> &out) {
+        if (!s.has_root) return false;
+        bool harvest = false;
+        std::vector<std::pair<CbtRef, bool>> stack{{s.root, false}};
+        while (!stack.empty()) {
+            auto [ref, include_all] = stack.back();
+            stack.pop_back();
+            if (ref.inner < 0) {
+                if (!harvest && !rec_startswith(ref.leaf, p)) break;
+                harvest = true;
+                out.push_back(ref.leaf);
+                continue;
+            }
+            const CbtInner &n = s.cbt[(size_t)ref.inner];
+            uint8_t crit = p.size() > n.diff_at ? (uint8_t)p[n.diff_at] : 0;
+            int direct = crit_dir(n.mask, crit);
+            if (!include_all && n.diff_at >= p.size()) include_all = true;
+            if (include_all) {
+                stack.push_back({n.kid[1], true});
+                stack.push_back({n.kid[0], true});
+            } else {
+                stack.push_back({n.kid[direct], false});
+            }
+        }
+        return true;
     }
 
     static std::string esc_key(const uint8_t *k, uint64_t n) {
@@ -1159,6 +1207,32 @@ int px_del_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *k
             Shard *s = ctx->shard_for_key(raw);
             result[i] = s ? (uint32_t)ctx->cbt_delete(*s, px_ctx::esc_key(keys + koff[i], koff[i + 1] - koff[i])) : 1u;
         }
+        return PX_OK;
+    })
+}
+
+int px_iter(px_ctx *ctx, const uint8_t *prefix, uint64_t prefix_len, px_rec *recs, uint32_t cap, uint32_t *n_out) {
+    if (!ctx || !n_out || (prefix_len && !prefix) || (cap && !recs)) return PX_EINVAL;
+    PX_GUARD({
+        std::string p;  // PiXiuStr_init: 251 doubled, no terminator
+        for (uint64_t i = 0; i < prefix_len; ++i) {
+            p.push_back((char)prefix[i]);
+            if (prefix[i] == kEsc) p.push_back((char)kEsc);
+        }
+        std::vector<px_rec> got;
+        bool any_tree = false;
+        for (auto &sp : ctx->shards) {
+            std::vector<Leaf> leaves;
+            if (!ctx->cbt_iter(*sp, p, leaves)) continue;
+            any_tree = true;
+            std::unordered_map<uint32_t, uint32_t> seq;
+            for (uint32_t k = 0; k < sp->chunks.size(); ++k) seq[sp->chunks[k]] = k;
+            for (const Leaf &l : leaves) got.push_back(px_rec{sp->id, seq[l.chunk], l.idx, 0, kMaxDoc});
+        }
+        *n_out = (uint32_t)got.size();
+        if (!any_tree) return PX_ENOTFOUND;
+        if (got.size() > cap) return PX_ESPACE;
+        if (!got.empty()) memcpy(recs, got.data(), got.size() * sizeof(px_rec));
         return PX_OK;
     })
 }

@@ -159,6 +159,18 @@ class _Shard:
     def contains(self, k: bytes) -> int:
         return self.lib.pxo_contains(self.h, k, len(k))
 
+    def iter(self, prefix: bytes):
+        """PiXiuCtrl::iter: [(chunk, idx)] in yield order, None for an empty tree."""
+        cap = 1 << 20
+        ch = (C.c_uint32 * cap)()
+        ix = (C.c_uint32 * cap)()
+        n = self.lib.pxo_iter(self.h, prefix, len(prefix), ch, ix, cap)
+        if n == PXO_NOTFOUND:
+            return None
+        if n < 0:
+            raise RuntimeError(f"pxo_iter: {n}")
+        return [(ch[i], ix[i]) for i in range(n)]
+
     def delete(self, k: bytes) -> int:
         return self.lib.pxo_delete(self.h, k, len(k))
 

@@ -20,3 +20,25 @@ def pytest_configure(config):
 def oracle():
     from _oracle import Oracle
     return Oracle()
+
+
+@pytest.fixture
+def store_factory():
+    """px.Store instances closed at teardown (GPU tests only).  torch probes the device
+    first: once the HIP library has initialised the runtime, a later first call to
+    torch.cuda.is_available() in the same process reports False and would skip the
+    GPU tests that follow."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import pixiu_amd as px
+    made = []
+
+    def make(**kw):
+        st = px.Store(**kw)
+        made.append(st)
+        return st
+
+    yield make
+    for st in made:
+        st.close()

@@ -3,7 +3,9 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
+#include <vector>
 #include <string>
 
 #include "PiXiuCtrl.h"
@@ -77,6 +79,31 @@ int main() {
         CHECK(std::string(r) == kv.first + kv.second);
         free(r);
     }
+    // iter (PiXiuCtrl.cpp:71-75): records under a prefix in crit-bit order, i.e. in the
+    // order of their escaped keys incl. the 251,0 terminator; nothing for an absent prefix
+    const std::string term("\xfb\x00", 2);
+    std::vector<std::string> want;
+    for (auto &kv : ref)
+        if (kv.first[0] == 'A') want.push_back(kv.first);
+    std::sort(want.begin(), want.end(), [&](const std::string &a, const std::string &b) { return a + term < b + term; });
+    CBTGen *it = ctrl.iter((uint8_t *)"A", 1);
+    CHECK(it != NULL);
+    size_t got_n = 0;
+    PXSGen *g = NULL;
+    while (it && (*it)(g)) {
+        char *r = g->consume_repr();
+        CHECK(got_n < want.size() && std::string(r) == want[got_n] + ref[want[got_n]]);
+        free(r);
+        ++got_n;
+    }
+    CHECK(got_n == want.size() && got_n > 0);
+    CBTGen_free(it);
+    it = ctrl.iter((uint8_t *)"F", 1);
+    CHECK(it != NULL && !(*it)(g));
+    CBTGen_free(it);
+    ctrl.free_prop();
+    ctrl.init_prop();
+    CHECK(ctrl.iter((uint8_t *)"A", 1) == NULL);  // empty tree: NULL generator
     ctrl.free_prop();
     printf("facade_test: %s (%zu live keys)\n", fails ? "FAILED" : "ok", ref.size());
     return fails ? 1 : 0;
