@@ -80,6 +80,50 @@ def cpu_baseline(corpus, rps, budget_s):
             "shards": shards, "seconds": t_set + t_get}
 
 
+def cpu_baseline_mt(corpus, rps, set_MBps_1t, budget_s):
+    """The same oracle with N threads = min(#shards, host cores), one independent
+    instance per shard (SURVEY.md §8d second row).  ctypes drops the GIL inside the
+    oracle calls; shards are sized so the set phase takes about budget_s."""
+    import concurrent.futures as cf
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _oracle import Oracle
+    orc = Oracle()
+    rps = rps or corpus.n
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16))  # a GPU box gives one process a 16-core share
+    shard_bytes = corpus.raw_bytes / corpus.n * rps
+    per_thread = max(1, int(set_MBps_1t * 1e6 * budget_s / shard_bytes))
+    nshards = min(corpus.n // rps, cores * per_thread)
+    threads = max(1, min(cores, nshards))
+    starts = [i * rps for i in range(nshards)]
+
+    def do_set(s0):
+        sh = orc.new()
+        ks = [corpus.key(i) for i in range(s0, s0 + rps)]
+        vs = [corpus.val(i) for i in range(s0, s0 + rps)]
+        for k, v in zip(ks, vs):
+            if sh.set(k, v)[0] < 0:
+                raise RuntimeError("oracle setitem failed")
+        return sh, ks, sum(len(k) + len(v) for k, v in zip(ks, vs))
+
+    def do_get(item):
+        sh, ks, _ = item
+        return sum(len(sh.get(k) or b"") for k in ks)
+
+    with cf.ThreadPoolExecutor(threads) as ex:
+        t0 = time.perf_counter()
+        done = list(ex.map(do_set, starts))
+        t1 = time.perf_counter()
+        exp = sum(ex.map(do_get, done))
+        t2 = time.perf_counter()
+    raw = sum(d[2] for d in done)
+    return {"set_MBps": raw / (t1 - t0) / 1e6, "get_MBps": exp / (t2 - t1) / 1e6, "threads": threads,
+            "records": nshards * rps, "raw": raw, "seconds": t2 - t0}
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -239,6 +283,13 @@ def main():
                                           f"corpus, same {a.rps}-record shards, oracle/pxo.cpp single-threaded, "
                                           f"{cb['seconds']:.1f} s"}
         line["parity_sample"] = {"records": tot_c, "compressed_equal": eq_c, "getitem_equal": eq_g}
+        mt = cpu_baseline_mt(corpus, a.rps, cb["set_MBps"], a.cpu_seconds / 2)
+        line["cpu_baseline_mt"] = {"value": round(mt["set_MBps"] + mt["get_MBps"], 4), "unit": "MB/s",
+                                   "set_MBps": round(mt["set_MBps"], 4), "get_MBps": round(mt["get_MBps"], 4),
+                                   "cores": mt["threads"], "kind": "port",
+                                   "sample": f"{mt['records']} records ({mt['raw'] / 1e6:.1f} MB), one oracle "
+                                             f"instance per {a.rps}-record shard, {mt['threads']} threads, "
+                                             f"{mt['seconds']:.1f} s"}
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
