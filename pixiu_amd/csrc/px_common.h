@@ -53,6 +53,8 @@ struct ShardState {
     uint64_t ub_reads;     // out-of-bounds reads the reference would make (UB there)
 };
 
+static_assert(sizeof(ShardState) % 16 == 0, "ShardState is zeroed / copied as 16-byte vectors");
+
 // per-batch shard work descriptor
 struct GstShard {
     uint8_t *text;        // arena text section
@@ -91,6 +93,19 @@ struct alignas(16) RecSlot {
     uint64_t pad2;          // 48 bytes: three 16-byte loads on the device
 };
 static_assert(sizeof(RecSlot) == 48, "RecSlot is loaded as three 16-byte vectors");
+
+// k_shard_init work item: a brand-new shard arena (zeroed child map and state)
+struct ShardInit {
+    uint4 *hash;
+    ShardState *st;
+    uint64_t entries;
+};
+
+// k_scatter_slots work item: one new chunk-table entry
+struct SlotPut {
+    RecSlot *dst;
+    RecSlot val;
+};
 
 // k_link work item: one record whose record tokens get their target entries
 struct LinkJob {

@@ -854,7 +854,7 @@ struct GstWave {
 __global__ void __launch_bounds__(64) k_gst_encode(const GstShard *shards, uint32_t n_shards,
                                                    const uint32_t *doc_len, uint8_t *const *comp_dst,
                                                    uint32_t *comp_len, uint32_t *rec_chunk,
-                                                   uint32_t *rec_idx, uint32_t *rec_status) {
+                                                   uint32_t *rec_idx, uint32_t *rec_status, ShardState *st_out) {
     __shared__ GstLds lds;
     const uint32_t s = blockIdx.x;
     if (s >= n_shards) return;
@@ -951,7 +951,34 @@ __global__ void __launch_bounds__(64) k_gst_encode(const GstShard *shards, uint3
         o.ctext_off = g.ctext_off;
         o.ub_reads = g.ub;
         *sh.st = o;
+        st_out[s] = o;  // compact copy: the host reads every shard's state in one transfer
     }
+}
+
+// ====================================================================== setup
+// Zero the child map and the state of every brand-new shard arena (one launch per
+// batch instead of a memset and a copy per shard).
+__global__ void __launch_bounds__(256) k_shard_init(uint32_t n, const ShardInit *jobs) {
+    const uint32_t lane = lane_id();
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t j = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); j < n; j += waves) {
+        const ShardInit job = jobs[j];
+        PX_GAS u32x4 *h = (PX_GAS u32x4 *)job.hash;
+        for (uint64_t k = lane; k < job.entries; k += 64) h[k] = mk4(0, 0, 0, 0);
+        PX_GAS u32x4 *st = (PX_GAS u32x4 *)job.st;
+        if (lane < sizeof(ShardState) / 16) st[lane] = mk4(0, 0, 0, 0);
+    }
+}
+
+// Write new chunk-table entries (one transfer + one launch per batch).
+__global__ void __launch_bounds__(256) k_scatter_slots(uint32_t n, const SlotPut *puts) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const PX_GAS u32x4 *src = (const PX_GAS u32x4 *)&puts[i].val;
+    PX_GAS u32x4 *dst = (PX_GAS u32x4 *)puts[i].dst;
+    dst[0] = src[0];
+    dst[1] = src[1];
+    dst[2] = src[2];
 }
 
 // ====================================================================== store
@@ -1713,10 +1740,23 @@ hipError_t launch_doc_write(hipStream_t s, uint32_t n, const uint8_t *keys, cons
 
 hipError_t launch_gst_encode(hipStream_t s, const GstShard *shards, uint32_t n_shards, const uint32_t *doc_len,
                              uint8_t *const *comp_dst, uint32_t *comp_len, uint32_t *rec_chunk,
-                             uint32_t *rec_idx, uint32_t *rec_status) {
+                             uint32_t *rec_idx, uint32_t *rec_status, ShardState *st_out) {
     if (!n_shards) return hipSuccess;
     k_gst_encode<<<n_shards, 64, 0, s>>>(shards, n_shards, doc_len, comp_dst, comp_len, rec_chunk, rec_idx,
-                                         rec_status);
+                                         rec_status, st_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_shard_init(hipStream_t s, uint32_t n, const ShardInit *jobs) {
+    if (!n) return hipSuccess;
+    uint32_t blocks = min((n + 3) / 4, 8192u);
+    k_shard_init<<<blocks, 256, 0, s>>>(n, jobs);
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter_slots(hipStream_t s, uint32_t n, const SlotPut *puts) {
+    if (!n) return hipSuccess;
+    k_scatter_slots<<<(n + 255) / 256, 256, 0, s>>>(n, puts);
     return hipGetLastError();
 }
 

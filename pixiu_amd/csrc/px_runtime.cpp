@@ -26,8 +26,10 @@ hipError_t launch_doc_len(hipStream_t, uint32_t, const uint8_t *, const uint64_t
                           const uint64_t *, uint32_t *);
 hipError_t launch_doc_write(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, const uint8_t *,
                             const uint64_t *, uint8_t *const *);
+hipError_t launch_shard_init(hipStream_t, uint32_t, const ShardInit *);
+hipError_t launch_scatter_slots(hipStream_t, uint32_t, const SlotPut *);
 hipError_t launch_gst_encode(hipStream_t, const GstShard *, uint32_t, const uint32_t *, uint8_t *const *,
-                             uint32_t *, uint32_t *, uint32_t *, uint32_t *);
+                             uint32_t *, uint32_t *, uint32_t *, uint32_t *, ShardState *);
 hipError_t launch_compact(hipStream_t, uint32_t, uint8_t *const *, const uint32_t *, uint8_t *, const uint64_t *);
 hipError_t launch_tokenize(hipStream_t, uint32_t, const RecSlot *, uint32_t *, uint32_t *);
 hipError_t launch_count_esc(hipStream_t, uint32_t, uint8_t *const *, const uint32_t *, uint32_t *);
@@ -202,11 +204,14 @@ struct px_ctx {
     std::vector<Chunk> chunks;
     RecSlot **chunk_tab = nullptr;  // device: chunk id -> slot table
     uint32_t chunk_tab_cap = 0;
+    uint32_t tab_lo = ~0u, tab_hi = 0;      // chunk_tab entries not yet uploaded
+    std::vector<ShardInit> pending_init;    // new shard arenas to zero (k_shard_init)
     std::unordered_map<std::string, uint32_t> keymap;  // raw key -> shard (multi-shard only)
     std::vector<std::pair<void *, uint64_t>> store_blocks;  // packed record stores + segment indexes
     uint8_t *last_store = nullptr;  // packed compressed bytes of the last set batch
     uint64_t last_store_bytes = 0;
-    DevBuf scratch_frames, dq_buf, dstat_buf, dlen_buf, in_buf, tmp_buf, link_buf, iter_buf;
+    DevBuf scratch_frames, dq_buf, dstat_buf, dlen_buf, in_buf, tmp_buf, link_buf, iter_buf, init_buf, stout_buf,
+        slotput_buf;
     px_stats stats{};
     int last_hip = 0;
 
@@ -270,7 +275,27 @@ struct px_ctx {
         }
         ch.dev = nt;
         ch.dev_cap = cap;
-        h2d(chunk_tab + c, &ch.dev, sizeof(RecSlot *));
+        tab_lo = std::min(tab_lo, c);
+        tab_hi = std::max(tab_hi, c + 1);
+    }
+
+    // upload the chunk_tab entries changed since the last flush (one transfer)
+    void flush_tab() {
+        if (tab_lo >= tab_hi) return;
+        std::vector<RecSlot *> v(tab_hi - tab_lo);
+        for (uint32_t c = tab_lo; c < tab_hi; ++c) v[c - tab_lo] = chunks[c].dev;
+        h2d(chunk_tab + tab_lo, v.data(), v.size() * sizeof(RecSlot *));
+        tab_lo = ~0u;
+        tab_hi = 0;
+    }
+
+    // zero the new shard arenas of this batch (one transfer + one launch)
+    void flush_shard_init() {
+        if (pending_init.empty()) return;
+        auto *d = (ShardInit *)init_buf.get(pending_init.size() * sizeof(ShardInit));
+        h2d(d, pending_init.data(), pending_init.size() * sizeof(ShardInit));
+        hcheck(launch_shard_init(stream, (uint32_t)pending_init.size(), d));
+        pending_init.clear();
     }
 
     // (re)build a shard's arena so the next batch (B new bytes, D new docs) fits
@@ -310,13 +335,12 @@ struct px_ctx {
         s.doc_cap = (uint32_t)doc_cap - 1;
         s.hash_cap = hash_cap;
         s.text_cap = text_cap;
-        hcheck(hipMemsetAsync(s.hash, 0, hash_cap * 16, stream));
         if (!o.arena) {
-            ShardState z{};
-            h2d(s.st, &z, sizeof z);
+            pending_init.push_back(ShardInit{s.hash, s.st, hash_cap});
             s.text_end = 0;
             return;
         }
+        hcheck(hipMemsetAsync(s.hash, 0, hash_cap * 16, stream));
         // migrate the live chunk: text moves to offset 0, everything else by copy / rehash
         hcheck(hipMemcpyAsync(s.root_tab, o.root_tab, 256 * 16, hipMemcpyDeviceToDevice, stream));
         hcheck(hipMemcpyAsync(s.doc_base, o.doc_base, ((size_t)o.hs.n_docs + 1) * 4, hipMemcpyDeviceToDevice, stream));
@@ -593,6 +617,7 @@ struct px_ctx {
         std::vector<DecodeQuery> qn(q);
         for (auto &d : qn) d.nrec = d.chunk == kNone ? 0 : chunks[d.chunk].n;
         h2d(dq, qn.data(), (size_t)nq * sizeof(DecodeQuery));
+        flush_tab();
         if (timed) hcheck(hipEventRecord(ev0, stream));
         hcheck(launch_decode(stream, dq, nq, (const RecSlot *const *)chunk_tab, out_dev, dl, ds, frames, depth,
                              waves));
@@ -628,6 +653,9 @@ struct px_ctx {
         last_store_bytes = 0;
         shards.clear();
         chunks.clear();
+        tab_lo = ~0u;
+        tab_hi = 0;
+        pending_init.clear();
         keymap.clear();
         uint64_t held = heap.held();
         stats = px_stats{};
@@ -796,12 +824,14 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     h2d(d_dst, dst.data(), (size_t)n * 8);
     h2d(d_cdst, cdst.data(), (size_t)n * 8);
     h2d(d_gs, gs.data(), gs.size() * sizeof(GstShard));
+    flush_shard_init();
     hcheck(launch_doc_write(stream, n, dkeys, dkoff, dvals, dvoff, d_dst));
 
     // ---- the GST walk + encoder
+    auto *d_stout = (ShardState *)stout_buf.get(gs.size() * sizeof(ShardState));
     hcheck(hipEventRecord(ev0, stream));
     hcheck(launch_gst_encode(stream, d_gs, (uint32_t)gs.size(), d_doclen, d_cdst, d_complen, d_chunk, d_idx,
-                             d_status));
+                             d_status, d_stout));
     hcheck(hipEventRecord(ev1, stream));
     hcheck(launch_count_esc(stream, n, d_cdst, d_complen, d_nesc));
     std::vector<uint32_t> comp_len(n), rchunk(n), ridx(n), rstatus(n), nesc(n);
@@ -810,8 +840,10 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     d2h(rchunk.data(), d_chunk, n * 4);
     d2h(ridx.data(), d_idx, n * 4);
     d2h(rstatus.data(), d_status, n * 4);
-    for (auto &w : work) d2h(&w.s->hs, w.s->st, sizeof(ShardState));
+    std::vector<ShardState> stout(gs.size());
+    d2h(stout.data(), d_stout, gs.size() * sizeof(ShardState));
     sync();
+    for (size_t k = 0; k < work.size(); ++k) work[k].s->hs = stout[k];
     {
         float ms = 0;
         hcheck(hipEventElapsedTime(&ms, ev0, ev1));
@@ -900,11 +932,16 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             if (it == touched.end()) touched[rgchunk[r]] = {ridx[r], ridx[r] + 1};
             else it->second.second = ridx[r] + 1;
         }
+        std::vector<SlotPut> puts;
         for (auto &t : touched) {
             chunk_reserve(t.first, chunks[t.first].n);
             Chunk &ch = chunks[t.first];
-            h2d(ch.dev + t.second.first, ch.slots.data() + t.second.first,
-                (size_t)(t.second.second - t.second.first) * sizeof(RecSlot));
+            for (uint32_t i = t.second.first; i < t.second.second; ++i) puts.push_back(SlotPut{ch.dev + i, ch.slots[i]});
+        }
+        if (!puts.empty()) {
+            auto *d = (SlotPut *)slotput_buf.get(puts.size() * sizeof(SlotPut));
+            h2d(d, puts.data(), puts.size() * sizeof(SlotPut));
+            hcheck(launch_scatter_slots(stream, (uint32_t)puts.size(), d));
         }
         // resolve the new records' tokens to their target entries
         std::vector<LinkJob> jobs;

@@ -9,4 +9,6 @@ cfg, n, rps = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
 cp = synth.make(cfg, n)
 with px.Store(records_per_shard=rps) as st:
     st.set_batch((cp.keys, cp.koff.astype(np.uint64)), (cp.vals, cp.voff.astype(np.uint64)))
-    print(f"config {cfg} n {n} rps {rps}: kernel {st.stats()['last_set_kernel_ms']:.1f} ms raw {int(cp.koff[-1] + cp.voff[-1])} B")
+    stt = st.stats()
+    print(f"config {cfg} n {n} rps {rps}: kernel {stt['last_set_kernel_ms']:.1f} ms raw {int(cp.koff[-1] + cp.voff[-1])} B "
+          f"ratio {stt['comp_bytes'] / max(stt['raw_bytes'], 1):.4f}")
