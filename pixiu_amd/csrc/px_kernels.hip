@@ -39,7 +39,7 @@ __device__ int32_t g_trace[kTraceCap];
 __device__ uint32_t g_trace_n;
 #define PX_TRACE_MSG(cmd, pos, val)                                         \
     do {                                                                    \
-        if (blockIdx.x == 0 && lane_id() == 0 && g_trace_n + 3 < kTraceCap) { \
+        if (blockIdx.x == 0 && threadIdx.x == 0 && g_trace_n + 3 < kTraceCap) { \
             g_trace[g_trace_n] = (int32_t)(cmd);                            \
             g_trace[g_trace_n + 1] = (int32_t)(pos);                        \
             g_trace[g_trace_n + 2] = (int32_t)(val);                        \
@@ -326,8 +326,9 @@ struct GstWave {
             slot = kInlineSlot | (ncnt << 26) | n;
             return false;
         }
-        if (ncnt == 2) {
-            slot = kNone;
+        if (ncnt == 2) {  // no hash entries yet: the first free entry of the bucket already read, if any
+            uint64_t me = ballot(lane < kBucket && (v.x >> 26) != epoch);
+            slot = me ? b * kBucket + ffs64(me) : kNone;
             return false;
         }
         const uint32_t want = n | (epoch << 26);
@@ -387,10 +388,12 @@ struct GstWave {
             hash[slot] = mk4(parent | (epoch << 26), pk0(e), pk1(e), pk2(e));
         }
     }
-    // add a child that is known to be absent (charges one map entry)
-    PX_DEV void add_child(uint32_t parent, uint32_t pcnt, const Edge &kid) {
+    // add a child that is known to be absent (charges one map entry).  hint: the free
+    // slot a failed lookup(parent, kid.key) just found (kNone: probe for one)
+    PX_DEV void add_child(uint32_t parent, uint32_t pcnt, const Edge &kid, uint32_t hint) {
         charge(kEdgeBlocks);
-        uint32_t slot = pcnt < 2 ? (kInlineSlot | (pcnt << 26) | parent) : hash_free_slot(parent, kid.key);
+        uint32_t slot = pcnt < 2 ? (kInlineSlot | (pcnt << 26) | parent)
+                                 : (hint != kNone ? hint : hash_free_slot(parent, kid.key));
         write_entry(slot, parent, kid);
         if (parent != kRoot && pcnt < 3) nrec(parent)[1] = pcnt + 1;
     }
@@ -609,7 +612,7 @@ struct GstWave {
 
     // split_grow: `split` and the byte of e at the split point were computed by
     // the caller (their loads were issued before this function's stores)
-    PX_DEV bool grow(Edge &e, uint32_t &last_inner, uint32_t c, bool split, uint32_t key_e) {
+    PX_DEV bool grow(Edge &e, uint32_t &last_inner, uint32_t c, bool split, uint32_t key_e, uint32_t hint) {
         Edge leaf;
 #ifdef PX_PROFILE
         uint64_t tq = __builtin_amdgcn_s_memtime();
@@ -655,7 +658,7 @@ struct GstWave {
             PX_CNT(P_G_NOSPLIT, 1);
             if (last_inner != kNone) nodes[2 * last_inner].x = e.id;
             last_inner = e.id;
-            add_child(e.id, e.cnt, leaf);
+            add_child(e.id, e.cnt, leaf, hint);
             if (e.cnt < 3) {
                 ++e.cnt;
                 write_entry(e.slot, act_node, e);
@@ -734,10 +737,13 @@ struct GstWave {
                 have_e = true;
                 PX_T1(P_T_DERIVE);
             }
+            // free slot for c under e.id found by a failed lookup (valid until the next hash write)
+            uint32_t hint = kNone;
             if (e.from + act_off == e.to) {
                 Edge n;
                 PX_T0();
-                bool wd = e.cnt && lookup(e.id, c, n);
+                uint32_t ncnt;
+                bool wd = e.cnt && lookup(e.id, c, n, hint, ncnt);
                 PX_T1(P_T_WALK);
                 if (wd) {
                     PX_CNT(P_WALK, 1);
@@ -788,7 +794,8 @@ struct GstWave {
                 const bool split = (!e.cnt || e.to - e.from > 1) && e.from + act_off != e.to;
                 uint32_t key_e = 0;
                 if (split) key_e = e_next >= 0 ? (uint32_t)e_next : tbyte(docbase(e.doc) + e.from + act_off);
-                if (!grow(e, last_inner, c, split, key_e)) break;
+                if (!grow(e, last_inner, c, split, key_e, split ? kNone : hint)) break;
+                hint = kNone;
 #ifdef PX_PROFILE
                 prof[P_T_GROW] += __builtin_amdgcn_s_memtime() - tg;
                 tg = __builtin_amdgcn_s_memtime();
@@ -818,7 +825,8 @@ struct GstWave {
                 lraw = act_node != kRoot ? nodes[2 * act_node].x : 0u;
                 if (e.from + act_off == e.to) {
                     Edge n;
-                    if (e.cnt && lookup(e.id, c, n)) {
+                    uint32_t ncnt;
+                    if (e.cnt && lookup(e.id, c, n, hint, ncnt)) {
                         act_node = e.id;
                         set_act_doc(n.doc);
                         act_direct = n.from;
@@ -851,13 +859,19 @@ struct GstWave {
     }
 };
 
-__global__ void __launch_bounds__(64) k_gst_encode(const GstShard *shards, uint32_t n_shards,
+// kGstWaves independent shard waves per block: a CU holds at most 16 blocks, so
+// one-wave blocks would cap residency at 4,096 waves chip-wide
+constexpr uint32_t kGstWaves = 4;
+
+__global__ void __launch_bounds__(64 * kGstWaves) k_gst_encode(const GstShard *shards, uint32_t n_shards,
                                                    const uint32_t *doc_len, uint8_t *const *comp_dst,
                                                    uint32_t *comp_len, uint32_t *rec_chunk,
                                                    uint32_t *rec_idx, uint32_t *rec_status, ShardState *st_out) {
-    __shared__ GstLds lds;
-    const uint32_t s = blockIdx.x;
+    __shared__ GstLds lds_w[kGstWaves];
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    const uint32_t s = blockIdx.x * kGstWaves + wv;
     if (s >= n_shards) return;
+    GstLds &lds = lds_w[wv];
     const uint32_t lane = lane_id();
     const GstShard sh = shards[s];
     ShardState st = *sh.st;
@@ -1340,17 +1354,24 @@ struct DecLds {
     uint32_t stk[kLaneDepth * 4][64];
 };
 
-__global__ void __launch_bounds__(64) k_decode(const DecodeQuery *qs, uint32_t nq, const RecSlot *const *chunk_slots,
-                                               uint8_t *out_, uint32_t *out_len, uint32_t *status,
-                                               Frame *scratch, uint32_t depth_cap) {
-    __shared__ DecLds lds;
+constexpr uint32_t kDecWaves = 4;  // independent query waves per block (see kGstWaves)
+
+__global__ void __launch_bounds__(64 * kDecWaves) k_decode(const DecodeQuery *qs, uint32_t nq,
+                                                         const RecSlot *const *chunk_slots, uint8_t *out_,
+                                                         uint32_t *out_len, uint32_t *status, Frame *scratch,
+                                                         uint32_t depth_cap, uint32_t n_waves) {
+    __shared__ DecLds lds_w[kDecWaves];
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    const uint32_t gw = blockIdx.x * kDecWaves + wv;
+    if (gw >= n_waves) return;
+    DecLds &lds = lds_w[wv];
     const uint32_t lane = lane_id();
-    PX_GAS Frame *stk = (PX_GAS Frame *)scratch + (size_t)blockIdx.x * depth_cap;
+    PX_GAS Frame *stk = (PX_GAS Frame *)scratch + (size_t)gw * depth_cap;
 #ifdef PX_PROFILE
     uint64_t prof[P_N] = {};
     const uint64_t t_kernel0 = __builtin_amdgcn_s_memtime();
 #endif
-    for (uint32_t qi = blockIdx.x; qi < nq; qi += gridDim.x) {
+    for (uint32_t qi = gw; qi < nq; qi += n_waves) {
         const DecodeQuery q = qs[qi];
         const uint32_t qchunk = uni(q.chunk);
         const PX_GAS RecSlot *slots = qchunk == kNone ? nullptr : (const PX_GAS RecSlot *)chunk_slots[qchunk];
@@ -1742,7 +1763,7 @@ hipError_t launch_gst_encode(hipStream_t s, const GstShard *shards, uint32_t n_s
                              uint8_t *const *comp_dst, uint32_t *comp_len, uint32_t *rec_chunk,
                              uint32_t *rec_idx, uint32_t *rec_status, ShardState *st_out) {
     if (!n_shards) return hipSuccess;
-    k_gst_encode<<<n_shards, 64, 0, s>>>(shards, n_shards, doc_len, comp_dst, comp_len, rec_chunk, rec_idx,
+    k_gst_encode<<<(n_shards + kGstWaves - 1) / kGstWaves, 64 * kGstWaves, 0, s>>>(shards, n_shards, doc_len, comp_dst, comp_len, rec_chunk, rec_idx,
                                          rec_status, st_out);
     return hipGetLastError();
 }
@@ -1793,7 +1814,8 @@ hipError_t launch_decode(hipStream_t s, const DecodeQuery *qs, uint32_t nq, cons
                          uint8_t *out, uint32_t *out_len, uint32_t *status, Frame *scratch, uint32_t depth_cap,
                          uint32_t n_waves) {
     if (!nq) return hipSuccess;
-    k_decode<<<n_waves, 64, 0, s>>>(qs, nq, chunk_slots, out, out_len, status, scratch, depth_cap);
+    k_decode<<<(n_waves + kDecWaves - 1) / kDecWaves, 64 * kDecWaves, 0, s>>>(qs, nq, chunk_slots, out, out_len,
+                                                                            status, scratch, depth_cap, n_waves);
     return hipGetLastError();
 }
 
