@@ -13,6 +13,7 @@
 //   k_compact      scratch -> packed compressed store
 //   k_tokenize     segment index over compressed bytes (token grammar of PiXiuStr.h:139-192)
 //   k_decode       PXSGen expansion (compat | exact), one wave per query  (PiXiuStr.h:129-198)
+//   k_decode_keys  the same body for stored-key prefixes (setitem's CritBit inserts, prefix iter)
 //   k_rehash       child-map migration into a larger table
 #include <hip/hip_runtime.h>
 
@@ -164,8 +165,8 @@ __global__ void __launch_bounds__(256) k_doc_write(uint32_t n, const uint8_t *ke
 // probes (one 64-byte line per probe), the current doc's 256-byte byte window,
 // and the encoder's output staging.  Per shard, LDS holds the root's 256 child
 // entries, the first 256 doc starts and the output staging buffer.
-constexpr uint32_t kObuf = 1024;  // per-wave output staging (LDS)
-constexpr uint32_t kFlushAt = kObuf - 64;
+constexpr uint32_t kObuf = 1024;   // per-wave output staging ring (LDS)
+constexpr uint32_t kFlushChunk = 256;  // the ring drains in aligned 256-byte pieces (one dword per lane)
 constexpr uint32_t kDocCache = 256;  // doc starts cached in LDS
 constexpr uint32_t kRootSlot = 0x80000000u;
 constexpr uint32_t kWin = 256;  // current-doc window (4 bytes per lane)
@@ -426,22 +427,31 @@ struct GstWave {
     }
 
     // ---- stream encoder (PiXiuStr_init_stream)
-    PX_DEV void flush_obuf(bool all) {
+    // Output bytes go to an LDS ring; the byte loop drains it in aligned 256-byte
+    // pieces (one dword per lane).  One byte-loop step appends far fewer than
+    // kObuf - kFlushChunk bytes, so draining once per step never overruns the ring.
+    PX_DEV void drain_obuf() {
         const uint32_t lane = lane_id();
-        uint32_t n = out - flushed;
-        if (!all && n < kFlushAt) return;
+        while (out - flushed >= kFlushChunk) {
+            wave_sync();
+            const uint32_t v = *(const PX_LAS uint32_t *)&lds->obuf[(flushed & (kObuf - 1)) + 4 * lane];
+            *(PX_GAS uint32_t *)(out_dst + flushed + 4 * lane) = v;
+            flushed += kFlushChunk;
+        }
+    }
+    PX_DEV void flush_obuf_all() {
+        const uint32_t lane = lane_id();
         wave_sync();
 #pragma unroll 1
-        for (uint32_t o = lane; o < n; o += 64) out_dst[flushed + o] = lds->obuf[o];
+        for (uint32_t o = flushed + lane; o < out; o += 64) out_dst[o] = lds->obuf[o & (kObuf - 1)];
         wave_sync();
         flushed = out;
     }
     // append n (<= 64) bytes; lane k holds byte k
     PX_DEV void put_lanes(uint32_t n, uint32_t b) {
-        if (lane_id() < n) lds->obuf[out - flushed + lane_id()] = (uint8_t)b;
+        if (lane_id() < n) lds->obuf[(out + lane_id()) & (kObuf - 1)] = (uint8_t)b;
         wave_sync();
         out += n;
-        flush_obuf(false);
     }
     PX_DEV void put(uint32_t b) { put_lanes(1, b); }
     PX_DEV void flush_run() {
@@ -713,6 +723,7 @@ struct GstWave {
         uint32_t i = 0;
         while (i < len && status == kOk) {
             if (i - wb >= kWin - 64 && i - wb < 0x80000000u) load_window(i >= 64 ? i - 64 : 0);
+            drain_obuf();
             const uint32_t c = curchar(i);
             PX_TRACE_STATE(0);
             PX_CNT(P_BYTES, 1);
@@ -854,7 +865,7 @@ struct GstWave {
         if (status == kOk) {
             if (held) fail(kErrCorrupt);  // stream ended inside a 251 pair
             flush_run();
-            flush_obuf(true);
+            flush_obuf_all();
         }
     }
 };
@@ -863,7 +874,7 @@ struct GstWave {
 // one-wave blocks would cap residency at 4,096 waves chip-wide
 constexpr uint32_t kGstWaves = 4;
 
-__global__ void __launch_bounds__(64 * kGstWaves) k_gst_encode(const GstShard *shards, uint32_t n_shards,
+__global__ void __launch_bounds__(64 * kGstWaves, 6) k_gst_encode(const GstShard *shards, uint32_t n_shards,
                                                    const uint32_t *doc_len, uint8_t *const *comp_dst,
                                                    uint32_t *comp_len, uint32_t *rec_chunk,
                                                    uint32_t *rec_idx, uint32_t *rec_status, ShardState *st_out) {
@@ -1356,10 +1367,11 @@ struct DecLds {
 
 constexpr uint32_t kDecWaves = 4;  // independent query waves per block (see kGstWaves)
 
-__global__ void __launch_bounds__(64 * kDecWaves) k_decode(const DecodeQuery *qs, uint32_t nq,
-                                                         const RecSlot *const *chunk_slots, uint8_t *out_,
-                                                         uint32_t *out_len, uint32_t *status, Frame *scratch,
-                                                         uint32_t depth_cap, uint32_t n_waves) {
+// the body of k_decode (getitem queries) and k_decode_keys (the stored-key prefixes
+// setitem and prefix iteration decode): one code, two kernel names in the profiles
+PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const *chunk_slots, uint8_t *out_,
+                        uint32_t *out_len, uint32_t *status, Frame *scratch, uint32_t depth_cap,
+                        uint32_t n_waves) {
     __shared__ DecLds lds_w[kDecWaves];
     const uint32_t wv = uni(threadIdx.x >> 6);
     const uint32_t gw = blockIdx.x * kDecWaves + wv;
@@ -1468,12 +1480,24 @@ __global__ void __launch_bounds__(64 * kDecWaves) k_decode(const DecodeQuery *qs
                     flag = true;  // token without a linked target
                     busy = false;
                 }
+                // software-pipelined walk: the entry a lane visits next is known before
+                // its current piece is copied, so its load is issued first and the two
+                // round trips (next entry, piece bytes) overlap
+                u32x4 F = mk4(0, 0, 0, 0), FH = mk4(0, 0, 0, 0);
+                if (busy) {
+                    F = e[0];
+                    FH = e[1];
+                }
                 while (ballot(busy)) {
                     PX_CNT(P_D_LANEIT, 1);
                     if (busy) {
-                        const u32x4 F = e[0], FH = e[1];
                         const int32_t x = (int32_t)F.x, y = (int32_t)F.y;
                         const uint32_t kd = F.z >> 30;
+                        const PX_GAS u32x4 *ne = e + 2;
+                        // the plain piece this step copies (nb == 0: none)
+                        uint32_t nb = 0, poff = 0;
+                        bool ov = false;
+                        const PX_GAS uint8_t *seg0 = (const PX_GAS uint8_t *)((uint64_t)FH.x | (uint64_t)FH.y << 32);
                         if (ret >= len || kd == 3) {
                             if (d == 0) {
                                 busy = false;
@@ -1481,7 +1505,7 @@ __global__ void __launch_bounds__(64 * kDecWaves) k_decode(const DecodeQuery *qs
                                 --d;
                                 const uint32_t w0 = lds.stk[d * 4 + 0][lane], w1 = lds.stk[d * 4 + 1][lane];
                                 const uint32_t w2 = lds.stk[d * 4 + 2][lane];
-                                e = (const PX_GAS u32x4 *)((uint64_t)w0 | (uint64_t)(w1 & 0xffffu) << 32);
+                                ne = (const PX_GAS u32x4 *)((uint64_t)w0 | (uint64_t)(w1 & 0xffffu) << 32);
                                 rec = w1 >> 16;
                                 from = (int32_t)(w2 & 0xffffu);
                                 len = (int32_t)(w2 >> 16);
@@ -1491,32 +1515,16 @@ __global__ void __launch_bounds__(64 * kDecWaves) k_decode(const DecodeQuery *qs
                             const int32_t q0 = max(x, from);
                             if (q0 < y) {
                                 const int32_t avail = y - q0, nd = len - ret;
-                                const uint32_t nb = (uint32_t)min(avail, nd);
-                                const PX_GAS uint8_t *seg0 = (const PX_GAS uint8_t *)((uint64_t)FH.x | (uint64_t)FH.y << 32);
-                                const PX_GAS uint8_t *cp = seg0 + (q0 - x);
-                                const bool ov = avail > nd && compat;
-                                const uint32_t last = ov ? cp[nb - 1] : 0u;
-                                if (w + nb > wmax) {
+                                const uint32_t n = (uint32_t)min(avail, nd);
+                                if (w + n > wmax) {
                                     flag = true;
                                     busy = false;
                                 } else {
-                                    lane_copy(o + base + w, cp, nb);
-                                    w += nb;
-                                    ret += (int32_t)nb;
-                                    // a range ending inside a 251 pair writes the pair whole
-                                    if (last == kEsc && (esc_run_lane(seg0, 0, (uint32_t)(q0 - x) + nb - 1) & 1)) {
-                                        if (w + 1 > wmax) {
-                                            flag = true;
-                                            busy = false;
-                                        } else {
-                                            o[base + w] = cp[nb];
-                                            ++w;
-                                            ++ret;
-                                        }
-                                    }
+                                    nb = n;
+                                    poff = (uint32_t)(q0 - x);
+                                    ov = avail > nd && compat;
                                 }
                             }
-                            e += 2;
                         } else if (kd == 2) {
                             const int32_t sup = y - x;
                             if (x - 1 + sup >= from) {
@@ -1537,18 +1545,42 @@ __global__ void __launch_bounds__(64 * kDecWaves) k_decode(const DecodeQuery *qs
                                     lds.stk[d * 4 + 2][lane] = (uint32_t)from | (uint32_t)len << 16;
                                     lds.stk[d * 4 + 3][lane] = (uint32_t)(ret + (st - sf));
                                     ++d;
-                                    e = t;  // the target's entry holding rf; entries before sf are passed over
+                                    ne = t;  // the target's entry holding rf; entries before sf are passed over
                                     rec = ri;
                                     from = sf;
                                     len = st - sf;
                                     ret = 0;
                                 }
-                            } else {
-                                e += 2;
                             }
-                        } else {
-                            e += 2;
                         }
+                        // next entry first (every entry a lane can reach is in bounds: a
+                        // record's entries end with a sentinel, which pops)
+                        u32x4 NF = F, NFH = FH;
+                        if (busy) {
+                            NF = ne[0];
+                            NFH = ne[1];
+                        }
+                        if (nb) {
+                            const PX_GAS uint8_t *cp = seg0 + poff;
+                            const uint32_t last = ov ? cp[nb - 1] : 0u;
+                            lane_copy(o + base + w, cp, nb);
+                            w += nb;
+                            ret += (int32_t)nb;
+                            // a range ending inside a 251 pair writes the pair whole
+                            if (last == kEsc && (esc_run_lane(seg0, 0, poff + nb - 1) & 1)) {
+                                if (w + 1 > wmax) {
+                                    flag = true;
+                                    busy = false;
+                                } else {
+                                    o[base + w] = cp[nb];
+                                    ++w;
+                                    ++ret;
+                                }
+                            }
+                        }
+                        F = NF;
+                        FH = NFH;
+                        e = ne;
                     }
                 }
             }
@@ -1712,6 +1744,19 @@ __global__ void __launch_bounds__(64 * kDecWaves) k_decode(const DecodeQuery *qs
 #endif
 }
 
+__global__ void __launch_bounds__(64 * kDecWaves) k_decode(const DecodeQuery *qs, uint32_t nq,
+                                                         const RecSlot *const *chunk_slots, uint8_t *out,
+                                                         uint32_t *out_len, uint32_t *status, Frame *scratch,
+                                                         uint32_t depth_cap, uint32_t n_waves) {
+    decode_body(qs, nq, chunk_slots, out, out_len, status, scratch, depth_cap, n_waves);
+}
+__global__ void __launch_bounds__(64 * kDecWaves) k_decode_keys(const DecodeQuery *qs, uint32_t nq,
+                                                              const RecSlot *const *chunk_slots, uint8_t *out,
+                                                              uint32_t *out_len, uint32_t *status, Frame *scratch,
+                                                              uint32_t depth_cap, uint32_t n_waves) {
+    decode_body(qs, nq, chunk_slots, out, out_len, status, scratch, depth_cap, n_waves);
+}
+
 // ====================================================================== migrate
 // Re-insert the live-epoch entries of a child map into a larger (zeroed) table.
 __global__ void __launch_bounds__(256) k_rehash(const uint4 *old_tab, uint32_t old_n, uint32_t epoch,
@@ -1812,10 +1857,15 @@ hipError_t launch_tokenize(hipStream_t s, uint32_t n, const RecSlot *slots, uint
 
 hipError_t launch_decode(hipStream_t s, const DecodeQuery *qs, uint32_t nq, const RecSlot *const *chunk_slots,
                          uint8_t *out, uint32_t *out_len, uint32_t *status, Frame *scratch, uint32_t depth_cap,
-                         uint32_t n_waves) {
+                         uint32_t n_waves, bool keys) {
     if (!nq) return hipSuccess;
-    k_decode<<<(n_waves + kDecWaves - 1) / kDecWaves, 64 * kDecWaves, 0, s>>>(qs, nq, chunk_slots, out, out_len,
-                                                                            status, scratch, depth_cap, n_waves);
+    const uint32_t blocks = (n_waves + kDecWaves - 1) / kDecWaves;
+    if (keys)
+        k_decode_keys<<<blocks, 64 * kDecWaves, 0, s>>>(qs, nq, chunk_slots, out, out_len, status, scratch,
+                                                          depth_cap, n_waves);
+    else
+        k_decode<<<blocks, 64 * kDecWaves, 0, s>>>(qs, nq, chunk_slots, out, out_len, status, scratch, depth_cap,
+                                                     n_waves);
     return hipGetLastError();
 }
 

@@ -35,7 +35,7 @@ hipError_t launch_tokenize(hipStream_t, uint32_t, const RecSlot *, uint32_t *, u
 hipError_t launch_count_esc(hipStream_t, uint32_t, uint8_t *const *, const uint32_t *, uint32_t *);
 hipError_t launch_link(hipStream_t, uint32_t, const LinkJob *);
 hipError_t launch_decode(hipStream_t, const DecodeQuery *, uint32_t, const RecSlot *const *, uint8_t *,
-                         uint32_t *, uint32_t *, Frame *, uint32_t, uint32_t);
+                         uint32_t *, uint32_t *, Frame *, uint32_t, uint32_t, bool);
 hipError_t launch_rehash(hipStream_t, const uint4 *, uint32_t, uint32_t, uint4 *, uint32_t);
 int debug_trace_take(int32_t *, uint32_t);
 int debug_prof_take(unsigned long long *, uint32_t);
@@ -619,8 +619,9 @@ struct px_ctx {
         h2d(dq, qn.data(), (size_t)nq * sizeof(DecodeQuery));
         flush_tab();
         if (timed) hcheck(hipEventRecord(ev0, stream));
+        // timed == a getitem batch (k_decode); otherwise stored-key prefixes (k_decode_keys)
         hcheck(launch_decode(stream, dq, nq, (const RecSlot *const *)chunk_tab, out_dev, dl, ds, frames, depth,
-                             waves));
+                             waves, !timed));
         if (timed) hcheck(hipEventRecord(ev1, stream));
         d2h(len.data(), dl, (size_t)nq * 4);
         d2h(st.data(), ds, (size_t)nq * 4);

@@ -11,19 +11,20 @@ FIRST = 24  # index of P_D_BATCH in the profile enum
 lib = px.load_library()
 lib.px_debug_prof_take.argtypes = [C.c_void_p, C.c_uint32]
 cfg, n, rps = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
+waves = int(sys.argv[4]) if len(sys.argv) > 4 else 0
 cp = synth.make(cfg, n)
 keys_host = (np.ascontiguousarray(cp.keys), cp.koff.astype(np.uint64))
 out_cap = int(2 * cp.raw_bytes + 256 * n + (1 << 20))
 out = torch.empty(out_cap, dtype=torch.uint8, device="cuda")
 buf = (C.c_ulonglong * 64)()
-with px.Store(records_per_shard=rps) as st:
+with px.Store(records_per_shard=rps, decode_waves=waves) as st:
     st.set_batch((cp.keys, cp.koff.astype(np.uint64)), (cp.vals, cp.voff.astype(np.uint64)))
     lib.px_debug_prof_take(buf, 64)
     rc, off, ln, sts, need = st.get_batch_device(keys_host, out.data_ptr(), out_cap, px.COMPAT)
     ms = st.stats()["last_decode_kernel_ms"]
 k = lib.px_debug_prof_take(buf, 64)
 v = dict(zip(NAMES, buf[FIRST:FIRST + len(NAMES)]))
-print(f"config {cfg} n {n} rps {rps}: decode kernel {ms:.2f} ms, expanded {int(np.asarray(ln).sum())} B")
+print(f"config {cfg} n {n} rps {rps} waves {waves}: decode kernel {ms:.2f} ms, expanded {int(np.asarray(ln).sum())} B")
 for name in NAMES:
     print(f"  {name:10s} {v[name]:16d}  per query {v[name] / n:12.1f}")
 print(f"  lane iterations per batch {v['d_laneit'] / max(v['d_batch'], 1):.2f}, committed per batch {v['d_commit'] / max(v['d_batch'], 1):.2f}")
