@@ -79,7 +79,8 @@ enum { P_BYTES, P_FF_CALLS, P_FF_BYTES, P_PASS, P_ITERS, P_LOOKUPS, P_PROBES, P_
        P_T_TOTAL, P_T_FF, P_T_DERIVE, P_T_WALK, P_T_SPLIT, P_T_GROW, P_T_CANON, P_T_END, P_T_ROOT, P_T_ENC,
        P_KEYMISS, P_T_KEY, P_T_LOOK,
        P_D_BATCH, P_D_LANEIT, P_D_SERIAL, P_D_COMMIT, P_D_FLAGGED, P_D_SHORT, P_D_PUSH, P_D_T_TOTAL, P_D_T_LANE,
-       P_G_NOSPLIT, P_G_T_LEAF, P_G_T_SPLIT, P_G_T_ADD, P_N };
+       P_G_NOSPLIT, P_G_T_LEAF, P_G_T_SPLIT, P_G_T_ADD,
+       P_E_LOOK, P_E_OFF1, P_E_OFF2, P_E_OFF3, P_E_OFF4P, P_K_CACHED, P_K_LOAD1, P_K_LOADN, P_N };
 __device__ unsigned long long g_prof[P_N];
 #define PX_CNT(k, v) (prof[k] += (v))
 #define PX_T0() uint64_t _t0 = __builtin_amdgcn_s_memtime()
@@ -805,6 +806,9 @@ struct GstWave {
                 const bool split = (!e.cnt || e.to - e.from > 1) && e.from + act_off != e.to;
                 uint32_t key_e = 0;
                 if (split) key_e = e_next >= 0 ? (uint32_t)e_next : tbyte(docbase(e.doc) + e.from + act_off);
+                PX_CNT(P_K_CACHED, split && e_next >= 0 ? 1 : 0);
+                PX_CNT(P_K_LOAD1, split && e_next < 0 && act_off == 1 ? 1 : 0);
+                PX_CNT(P_K_LOADN, split && e_next < 0 && act_off != 1 ? 1 : 0);
                 if (!grow(e, last_inner, c, split, key_e, split ? kNone : hint)) break;
                 hint = kNone;
 #ifdef PX_PROFILE
@@ -834,6 +838,11 @@ struct GstWave {
 #endif
                 // next iteration's suffix link, issued before this end check's wait
                 lraw = act_node != kRoot ? nodes[2 * act_node].x : 0u;
+                PX_CNT(P_E_LOOK, e.from + act_off == e.to ? 1 : 0);
+                PX_CNT(P_E_OFF1, e.from + act_off < e.to && act_off == 1 ? 1 : 0);
+                PX_CNT(P_E_OFF2, e.from + act_off < e.to && act_off == 2 ? 1 : 0);
+                PX_CNT(P_E_OFF3, e.from + act_off < e.to && act_off == 3 ? 1 : 0);
+                PX_CNT(P_E_OFF4P, e.from + act_off < e.to && act_off >= 4 ? 1 : 0);
                 if (e.from + act_off == e.to) {
                     Edge n;
                     uint32_t ncnt;

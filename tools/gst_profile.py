@@ -6,7 +6,8 @@ import numpy as np
 import pixiu_amd as px
 from pixiu_amd import synth
 NAMES = ["bytes", "ff_calls", "ff_bytes", "pass", "iters", "lookups", "probes", "root", "walk", "link", "canon_lvl",
-         "t_total", "t_ff", "t_derive", "t_walk", "t_split", "t_grow", "t_canon", "t_end", "t_root", "t_enc", "keymiss", "t_key", "t_look", "d_batch", "d_laneit", "d_serial", "d_commit", "d_flagged", "d_short", "d_push", "d_t_total", "d_t_lane", "g_nosplit", "g_t_leaf", "g_t_split", "g_t_add"]
+         "t_total", "t_ff", "t_derive", "t_walk", "t_split", "t_grow", "t_canon", "t_end", "t_root", "t_enc", "keymiss", "t_key", "t_look", "d_batch", "d_laneit", "d_serial", "d_commit", "d_flagged", "d_short", "d_push", "d_t_total", "d_t_lane", "g_nosplit", "g_t_leaf", "g_t_split", "g_t_add",
+         "e_look", "e_off1", "e_off2", "e_off3", "e_off4p", "k_cached", "k_load1", "k_loadn"]
 lib = px.load_library()
 lib.px_debug_prof_take.argtypes = [C.c_void_p, C.c_uint32]
 cfg, n, rps = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
