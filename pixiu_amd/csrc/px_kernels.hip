@@ -80,12 +80,16 @@ enum { P_BYTES, P_FF_CALLS, P_FF_BYTES, P_PASS, P_ITERS, P_LOOKUPS, P_PROBES, P_
        P_KEYMISS, P_T_KEY, P_T_LOOK,
        P_D_BATCH, P_D_LANEIT, P_D_SERIAL, P_D_COMMIT, P_D_FLAGGED, P_D_SHORT, P_D_PUSH, P_D_T_TOTAL, P_D_T_LANE,
        P_G_NOSPLIT, P_G_T_LEAF, P_G_T_SPLIT, P_G_T_ADD,
-       P_E_LOOK, P_E_OFF1, P_E_OFF2, P_E_OFF3, P_E_OFF4P, P_K_CACHED, P_K_LOAD1, P_K_LOADN, P_N };
+       P_E_LOOK, P_E_OFF1, P_E_OFF2, P_E_OFF3, P_E_OFF4P, P_K_CACHED, P_K_LOAD1, P_K_LOADN,
+       P_DF_NONE, P_DF_TOPREF, P_DF_CAP, P_DF_NOLINK, P_DF_OVER, P_DF_LPER, P_DF_DEPTH, P_DF_RANGE, P_DF_BADREC,
+       P_D_TOPB, P_D_SUBB, P_D_TOPC, P_D_MAXIT, P_D_T_ASSIGN, P_D_ROUNDS, P_N };
 __device__ unsigned long long g_prof[P_N];
 #define PX_CNT(k, v) (prof[k] += (v))
 #define PX_T0() uint64_t _t0 = __builtin_amdgcn_s_memtime()
 #define PX_T1(k) (prof[k] += __builtin_amdgcn_s_memtime() - _t0)
+#define PX_FR(r) (freason = freason ? freason : (r))
 #else
+#define PX_FR(r) ((void)0)
 #define PX_CNT(k, v) ((void)0)
 #define PX_T0() ((void)0)
 #define PX_T1(k) ((void)0)
@@ -1249,6 +1253,8 @@ __global__ void __launch_bounds__(256) k_link(uint32_t n, const LinkJob *jobs) {
 // then goes through the serial frame machine (a stack of Frames in scratch memory),
 // which is the reference's generator nesting restated.
 constexpr uint32_t kLaneDepth = 8;
+constexpr uint32_t kLaneCopyMax = 512;  // plain pieces up to this size are copied by one lane
+constexpr uint32_t kAssignMin = 24;      // idle lanes that trigger an assignment round
 
 // Copies use unaligned 16-byte accesses (gfx950 runs in unaligned access mode; the
 // compiler itself emits them for byte-aligned memcpy).  Sources are compressed
@@ -1276,8 +1282,25 @@ PX_DEV void wave_copy(PX_GAS uint8_t *dst, const PX_GAS uint8_t *src, uint32_t n
     if (t < n) dst[t] = src[t];
 }
 
-// one lane copies its own n bytes
+// one lane copies its own n bytes.  Every load is issued before the first store
+// (source and destination never overlap, but the compiler cannot know that), so a
+// piece of up to 64 bytes costs one memory round trip, not one per 16 bytes.
 PX_DEV void lane_copy(PX_GAS uint8_t *dst, const PX_GAS uint8_t *src, uint32_t n) {
+    if (n >= 16 && n <= 32) {
+        const u32x4 v0 = ld16(src), v1 = ld16(src + n - 16);
+        st16(dst, v0);
+        st16(dst + n - 16, v1);
+        return;
+    }
+    if (n > 32 && n <= 64) {
+        const uint32_t o1 = 16u, o2 = min(32u, n - 16), o3 = n - 16;
+        const u32x4 v0 = ld16(src), v1 = ld16(src + o1), v2 = ld16(src + o2), v3 = ld16(src + o3);
+        st16(dst, v0);
+        st16(dst + o1, v1);
+        st16(dst + o2, v2);
+        st16(dst + o3, v3);
+        return;
+    }
     if (n >= 16) {
         uint32_t i = 0;
         for (; i + 64 <= n; i += 64) {
@@ -1307,7 +1330,23 @@ PX_DEV void lane_copy(PX_GAS uint8_t *dst, const PX_GAS uint8_t *src, uint32_t n
         __builtin_memcpy((PX_GAS void *)(dst + n - 4), &b, 4);
         return;
     }
-    for (uint32_t i = 0; i < n; ++i) dst[i] = src[i];
+    if (n) {  // 1..3 bytes: first, middle, last (loads first)
+        const uint8_t a = src[0], b = src[n >> 1], c = src[n - 1];
+        dst[0] = a;
+        dst[n >> 1] = b;
+        dst[n - 1] = c;
+    }
+}
+
+// inclusive wave prefix sum on DPP row shifts and row broadcasts (no LDS round trips)
+PX_DEV int32_t wave_incl_scan_dpp(int32_t x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 into rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 into rows 2, 3
+    return x;
 }
 
 PX_DEV int32_t wave_excl_scan(int32_t v) {
@@ -1429,87 +1468,202 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
             return true;
         };
 
-        // Consume up to 64 segments of frame f in parallel.  Returns true when the
-        // segment at f.seg must go through the serial path next.
-        auto batch = [&](Frame &f, const SlotV &sv) -> bool {
-            const uint32_t k = f.seg + lane;
-            const bool valid = k < sv.nseg;
-            const u32x4 E = valid ? sv.seg[2 * k] : mk4(0, 0, 0, 0);
-            const u32x4 EH = valid ? sv.seg[2 * k + 1] : mk4(0, 0, 0, 0);
-            const int32_t sx = (int32_t)E.x, ex = (int32_t)E.y;
-            const uint32_t kind = E.z >> 30, cs = E.z & kSegMask;
-            const uint32_t ridx = E.w & 0xffffu;
-            const int32_t rfrom = (int32_t)(E.w >> 16), supply = ex - sx, rto = rfrom + supply;
-            const int32_t p0 = max(sx, f.from);
-            const int32_t sub_from = rfrom + max(0, f.from - sx);
-            const bool enter = kind == 2 && sx - 1 + supply >= f.from;
-            int32_t req = 0;  // requested size, unclamped (ret grows by it)
-            if (valid && kind == 0 && p0 < ex) req = ex - p0;
-            if (valid && enter) req = rto - sub_from;
-            const int32_t ret_l = f.ret + wave_excl_scan(req);
-            const bool active = valid && ret_l < f.len;  // a prefix of the lanes
-            const int32_t need = f.len - ret_l;
-            bool flag = false, child = false;
-            int32_t reqc = 0, sub_to = 0;
-            uint32_t csrc = 0;
-            if (active && kind == 0 && p0 < ex) {
-                const int32_t avail = ex - p0;
-                reqc = min(avail, need);
-                csrc = cs + (uint32_t)(p0 - sx);
-                // the range ends here: if its last byte opens a 251 pair, the pair is
-                // written whole (per-token length check, PiXiuStr.h:136,142-147)
-                if (avail > need && compat && (esc_run_lane(sv.comp, cs, csrc + (uint32_t)reqc - 1) & 1)) ++reqc;
-            } else if (active && enter) {
-                sub_to = min(rto, sub_from + need);
-                const int32_t stop = compat ? ret_l : max(sx, f.from);
-                if (ridx >= nrec || (sub_from < stop && stop < sub_to && ridx == f.rec)) flag = true;
-                reqc = sub_to - sub_from;
-                child = true;
+        // Consume frame f's segments with dynamic lane assignment: every idle lane
+        // takes the next unassigned segment (in order), so a lane that finishes a
+        // short expansion picks up new work instead of waiting for the slowest lane
+        // of a fixed 64-segment batch.  Output offsets and ret cursors come from
+        // running prefix sums of the requested sizes (a wave scan per assignment
+        // round).  A segment that leaves the lane path (flag) or produces fewer bytes
+        // than it requested (short) sets `stop`: segments before it are committed,
+        // later ones are abandoned and redone.  Returns true when the segment at
+        // f.seg must go through the serial path next.
+        auto window = [&](Frame &f, const SlotV &sv) -> bool {
+            const uint32_t outp0 = outp;
+            const int32_t ret0 = f.ret;
+            uint32_t next = f.seg;     // next unassigned segment
+            uint32_t end = sv.nseg;    // shrinks to the first inactive segment
+            int32_t run_req = ret0;    // ret cursor at `next`
+            uint32_t run_out = outp0;  // output position at `next`
+            // stop key = 2 * (first segment not committed) + (0: it goes serial, 1: it does not)
+            uint32_t stop_key = 0xffffffffu, stop_out = 0;
+            int32_t stop_ret = 0;
+            // prefetched entries of segments [next, next + 64): lane l holds next + l
+            u32x4 PE = mk4(0, 0, 0, 0), PEH = mk4(0, 0, 0, 0);
+            {
+                const uint32_t kk = next + lane;
+                if (kk < end) {
+                    PE = sv.seg[2 * kk];
+                    PEH = sv.seg[2 * kk + 1];
+                }
             }
-            const uint32_t base = outp + (uint32_t)wave_excl_scan(active ? reqc : 0);
-            if (active && (uint64_t)base + (uint64_t)reqc >= f.cap) flag = true;
-            // short plain pieces: copied by their lane now; long ones cooperatively below
-            uint32_t w = 0;
-            if (active && !flag && kind == 0) {
-                if (reqc <= 64) lane_copy(o + base, sv.comp + csrc, (uint32_t)reqc);
-                w = (uint32_t)reqc;
-            }
-            // record references: each lane expands its own range depth-first
-            bool busy = active && !flag && child;
+            // per-lane segment state
+            uint32_t k = kNone, base = 0, w = 0, wmax = 0;
+            int32_t kret = 0;
+            bool busy = false, flag = false, pmode = false, fresh = false;
+            const PX_GAS uint8_t *psrc = nullptr;
+#ifdef PX_PROFILE
+            uint32_t freason = 0, freason_first = 0;
+            uint32_t lane_it = 0;
+#endif
+            // walk state
+            const PX_GAS u32x4 *e = nullptr;
+            u32x4 F = mk4(0, 0, 0, 0), FH = mk4(0, 0, 0, 0);
+            uint32_t rec = 0, d = 0;
+            int32_t from = 0, len = 0, ret = 0;
             PX_CNT(P_D_BATCH, 1);
 #ifdef PX_PROFILE
             const uint64_t t_lane0 = __builtin_amdgcn_s_memtime();
 #endif
-            if (ballot(busy)) {
-                const PX_GAS u32x4 *e = (const PX_GAS u32x4 *)((uint64_t)EH.x | (uint64_t)EH.y << 32);
-                uint32_t rec = ridx, d = 0;
-                int32_t from = sub_from, len = reqc, ret = 0;
-                const uint32_t wmax = (uint32_t)reqc;
-                if (busy && !e) {
-                    flag = true;  // token without a linked target
-                    busy = false;
+            for (;;) {
+                const uint32_t lim = min(end, stop_key >> 1);
+                const uint64_t im = ballot(k == kNone);
+                // an assignment round once enough lanes are idle (or none is working)
+                if (next < lim && im && (__popcll(im) >= kAssignMin || !ballot(busy))) {
+#ifdef PX_PROFILE
+                    const uint64_t t_as0 = __builtin_amdgcn_s_memtime();
+#endif
+                    // ---- assignment round: idle lane of rank r takes segment next + r
+                    const uint32_t rank =
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0));
+                    const bool take = k == kNone && next + rank < lim;
+                    const int src_l = (int)(rank & 63u);
+                    const u32x4 E = mk4(__shfl(PE.x, src_l), __shfl(PE.y, src_l), __shfl(PE.z, src_l),
+                                        __shfl(PE.w, src_l));
+                    const uint32_t ehx = __shfl(PEH.x, src_l), ehy = __shfl(PEH.y, src_l);
+                    const int32_t sx = (int32_t)E.x, ex = (int32_t)E.y;
+                    const uint32_t kind = E.z >> 30, cs = E.z & kSegMask;
+                    const uint32_t ridx = E.w & 0xffffu;
+                    const int32_t rfrom = (int32_t)(E.w >> 16), supply = ex - sx, rto = rfrom + supply;
+                    const int32_t p0 = max(sx, f.from);
+                    const int32_t sub_from = rfrom + max(0, f.from - sx);
+                    const bool enter = kind == 2 && sx - 1 + supply >= f.from;
+                    int32_t req = 0;
+                    if (take && kind == 0 && p0 < ex) req = ex - p0;
+                    if (take && enter) req = rto - sub_from;
+                    const int32_t ret_l = run_req + wave_incl_scan_dpp(req) - req;
+                    const bool active = take && ret_l < f.len;  // a prefix of the takers
+                    const int32_t need = f.len - ret_l;
+                    int32_t reqc = 0, sub_to = 0;
+                    uint32_t csrc = 0;
+                    bool child = false, fl = false;
+                    if (active && kind == 0 && p0 < ex) {
+                        const int32_t avail = ex - p0;
+                        reqc = min(avail, need);
+                        csrc = cs + (uint32_t)(p0 - sx);
+                        // the range ends here: if its last byte opens a 251 pair, the pair
+                        // is written whole (per-token length check, PiXiuStr.h:136,142-147)
+                        if (avail > need && compat && (esc_run_lane(sv.comp, cs, csrc + (uint32_t)reqc - 1) & 1))
+                            ++reqc;
+                    } else if (active && enter) {
+                        sub_to = min(rto, sub_from + need);
+                        const int32_t stp = compat ? ret_l : max(sx, f.from);
+                        if (ridx >= nrec || (sub_from < stp && stp < sub_to && ridx == f.rec)) {
+                            fl = true;
+                            PX_FR(1);
+                        }
+                        reqc = sub_to - sub_from;
+                        child = true;
+                    }
+                    // every active segment before the last one asks for exactly req bytes, so
+                    // the output offset follows the same scan
+                    const uint32_t b = run_out + (uint32_t)(ret_l - run_req);
+                    if (active && (uint64_t)b + (uint64_t)reqc >= f.cap) {
+                        fl = true;
+                        PX_FR(2);
+                    }
+                    const uint64_t am = ballot(active);
+                    const uint32_t na = (uint32_t)__popcll(am), nt = (uint32_t)__popcll(ballot(take));
+                    if (na) {
+                        const uint32_t hl = 63u - (uint32_t)__clzll((long long)am);  // highest active lane
+                        run_req = unii(readlane((uint32_t)(ret_l + req), hl));
+                        run_out = uni(readlane(b + (uint32_t)reqc, hl));
+                    }
+                    if (na < nt) end = next + na;  // the frame's range ends inside this round
+                    next += na;
+                    if (active) {
+                        k = next - na + rank;
+                        base = b;
+                        kret = ret_l;
+                        wmax = (uint32_t)reqc;
+                        w = 0;
+                        flag = fl;
+                    }
+                    // long plain pieces: copied by the whole wave now; shorter ones by their
+                    // lane, 64 bytes per walk step
+                    uint64_t lm = ballot(active && !fl && kind == 0 && reqc > (int32_t)kLaneCopyMax);
+                    while (lm) {
+                        const uint32_t j = ffs64(lm);
+                        lm &= lm - 1;
+                        wave_copy(o + readlane(b, j), sv.comp + readlane(csrc, j), readlane((uint32_t)reqc, j));
+                    }
+                    if (active && !fl && kind == 0 && reqc > 0 && reqc <= (int32_t)kLaneCopyMax) {
+                        // a shorter plain piece: copied by its lane in the walk steps below,
+                        // where its loads overlap the walking lanes' loads
+                        busy = true;
+                        pmode = true;
+                        psrc = sv.comp + csrc;
+                    } else if (active && !fl && !child) {
+                        w = (uint32_t)reqc;
+                        k = kNone;  // done (a plain or empty segment is never short)
+                    }
+                    if (active && !fl && child) {
+                        e = (const PX_GAS u32x4 *)((uint64_t)ehx | (uint64_t)ehy << 32);
+                        if (!e) {
+                            PX_FR(3);
+                            flag = true;  // token without a linked target
+                        } else {
+                            // the first entry is loaded by the lane's first walk step
+                            busy = true;
+                            fresh = true;
+                            rec = ridx;
+                            d = 0;
+                            from = sub_from;
+                            len = reqc;
+                            ret = 0;
+                        }
+                    }
+                    // refill the prefetch buffer from the new `next`
+                    {
+                        const uint32_t kk = next + lane;
+                        if (kk < end) {
+                            PE = sv.seg[2 * kk];
+                            PEH = sv.seg[2 * kk + 1];
+                        }
+                    }
+#ifdef PX_PROFILE
+                    prof[P_D_T_ASSIGN] += __builtin_amdgcn_s_memtime() - t_as0;
+                    prof[P_D_ROUNDS] += 1;
+#endif
                 }
-                // software-pipelined walk: the entry a lane visits next is known before
-                // its current piece is copied, so its load is issued first and the two
-                // round trips (next entry, piece bytes) overlap
-                u32x4 F = mk4(0, 0, 0, 0), FH = mk4(0, 0, 0, 0);
-                if (busy) {
-                    F = e[0];
-                    FH = e[1];
-                }
-                while (ballot(busy)) {
+                // ---- one walk step for every busy lane
+                bool done = false;
+                if (ballot(busy)) {
                     PX_CNT(P_D_LANEIT, 1);
+#ifdef PX_PROFILE
+                    lane_it += 1;
+#endif
                     if (busy) {
                         const int32_t x = (int32_t)F.x, y = (int32_t)F.y;
                         const uint32_t kd = F.z >> 30;
-                        const PX_GAS u32x4 *ne = e + 2;
-                        // the plain piece this step copies (nb == 0: none)
+                        const PX_GAS u32x4 *ne = fresh ? e : e + 2;
                         uint32_t nb = 0, poff = 0;
                         bool ov = false;
                         const PX_GAS uint8_t *seg0 = (const PX_GAS uint8_t *)((uint64_t)FH.x | (uint64_t)FH.y << 32);
-                        if (ret >= len || kd == 3) {
+                        if (pmode) {
+                            seg0 = psrc;
+                            nb = min(wmax - w, 64u);
+                            psrc += nb;
+                            if (w + nb == wmax) {
+                                pmode = false;
+                                busy = false;
+                                done = true;
+                            }
+                        } else if (fresh) {
+                            fresh = false;  // this step only loads the first entry
+                        } else if (ret >= len || kd == 3) {
                             if (d == 0) {
                                 busy = false;
+                                done = true;
                             } else {
                                 --d;
                                 const uint32_t w0 = lds.stk[d * 4 + 0][lane], w1 = lds.stk[d * 4 + 1][lane];
@@ -1526,6 +1680,7 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                                 const int32_t avail = y - q0, nd = len - ret;
                                 const uint32_t n = (uint32_t)min(avail, nd);
                                 if (w + n > wmax) {
+                                    PX_FR(4);
                                     flag = true;
                                     busy = false;
                                 } else {
@@ -1541,11 +1696,12 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                                 const int32_t rf = (int32_t)(F.w >> 16), rt = rf + sup;
                                 const int32_t sf = rf + max(0, from - x);
                                 const int32_t st = min(rt, sf + (len - ret));
-                                const int32_t stop = compat ? ret : max(x, from);
+                                const int32_t stp = compat ? ret : max(x, from);
                                 const PX_GAS u32x4 *t = (const PX_GAS u32x4 *)((uint64_t)FH.x | (uint64_t)FH.y << 32);
                                 const uint64_t nx = (uint64_t)(e + 2);
-                                if (!t || ri >= nrec || (ri == rec && sf < stop && stop < st) || d + 1 >= kLaneDepth ||
+                                if (!t || ri >= nrec || (ri == rec && sf < stp && stp < st) || d + 1 >= kLaneDepth ||
                                     (uint32_t)from > 0xffffu || (uint32_t)len > 0xffffu || (nx >> 48) != 0) {
+                                    PX_FR(!t ? 3 : ri >= nrec ? 8 : (ri == rec && sf < stp && stp < st) ? 5 : d + 1 >= kLaneDepth ? 6 : 7);
                                     flag = true;  // leaves the lane path: serial machine
                                     busy = false;
                                 } else {
@@ -1565,7 +1721,7 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                         // next entry first (every entry a lane can reach is in bounds: a
                         // record's entries end with a sentinel, which pops)
                         u32x4 NF = F, NFH = FH;
-                        if (busy) {
+                        if (busy && !pmode) {
                             NF = ne[0];
                             NFH = ne[1];
                         }
@@ -1578,6 +1734,7 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                             // a range ending inside a 251 pair writes the pair whole
                             if (last == kEsc && (esc_run_lane(seg0, 0, poff + nb - 1) & 1)) {
                                 if (w + 1 > wmax) {
+                                    PX_FR(4);
                                     flag = true;
                                     busy = false;
                                 } else {
@@ -1592,36 +1749,69 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                         e = ne;
                     }
                 }
+                // ---- events: a flagged segment (goes serial) or a short one (committed,
+                // but later offsets are wrong) moves `stop` down
+                const bool fl_ev = k != kNone && flag;
+                const bool sh_ev = k != kNone && done && w != wmax;
+                if (ballot(fl_ev || sh_ev)) {
+                    uint32_t key = fl_ev ? 2u * k : sh_ev ? 2u * (k + 1u) + 1u : 0xffffffffu;
+                    uint32_t mn = key;
+                    for (int ofs = 32; ofs >= 1; ofs >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, ofs));
+                    mn = uni(mn);
+                    if (mn < stop_key) {
+                        const uint32_t hl = ffs64(ballot((fl_ev || sh_ev) && key == mn));
+                        stop_key = mn;
+                        if (mn & 1u) {  // short: committed through it
+                            stop_out = uni(readlane(base + w, hl));
+                            stop_ret = unii(readlane((uint32_t)kret + wmax, hl));
+                        } else {
+#ifdef PX_PROFILE
+                            freason_first = readlane(freason, hl);
+#endif
+                            stop_out = uni(readlane(base, hl));
+                            stop_ret = unii(readlane((uint32_t)kret, hl));
+                        }
+                    }
+                }
+                if (done) k = kNone;
+                // abandon flagged lanes and everything at or past stop
+                if (k != kNone && (flag || k >= (stop_key >> 1))) {
+                    k = kNone;
+                    busy = false;
+                    pmode = false;
+                    fresh = false;
+                }
+                flag = flag && k != kNone;
+#ifdef PX_PROFILE
+                if (k == kNone) freason = 0;
+#endif
+                if (!ballot(k != kNone) && next >= min(end, stop_key >> 1)) break;
             }
 #ifdef PX_PROFILE
             prof[P_D_T_LANE] += __builtin_amdgcn_s_memtime() - t_lane0;
+            {
+                uint32_t mx = lane_it;
+                prof[P_D_MAXIT] += uni(mx);
+            }
 #endif
-            // commit the lanes before the first flagged one; a lane that produced fewer
-            // bytes than it asked for (its record ran out) is committed but ends the batch
-            const uint64_t fm = ballot(active && flag);
-            const uint64_t sm = ballot(active && !flag && w != (uint32_t)reqc);
-            const uint64_t am = ballot(active);
-            const uint32_t L = (uint32_t)__popcll(am);
-            const uint32_t first_flag = fm ? ffs64(fm) : 64u;
-            const uint32_t first_short = sm ? ffs64(sm) : 64u;
-            const uint32_t C = min(L, min(first_flag, first_short + 1));
-            PX_CNT(P_D_COMMIT, C);
-            PX_CNT(P_D_FLAGGED, first_flag == C && C < L ? 1 : 0);
-            PX_CNT(P_D_SHORT, first_short + 1 == C ? 1 : 0);
-            uint64_t lm = ballot(active && !flag && kind == 0 && reqc > 64 && lane < C);
-            while (lm) {
-                const uint32_t j = ffs64(lm);
-                lm &= lm - 1;
-                wave_copy(o + readlane(base, j), sv.comp + readlane(csrc, j), readlane((uint32_t)reqc, j));
+            if (stop_key != 0xffffffffu && (stop_key >> 1) <= next) {
+                PX_CNT(P_D_COMMIT, (stop_key >> 1) - f.seg);
+                f.seg = stop_key >> 1;
+                outp = stop_out;
+                f.ret = stop_ret;
+                const bool serial = (stop_key & 1u) == 0;
+#ifdef PX_PROFILE
+                if (serial) prof[P_DF_NONE + freason_first] += 1;
+                PX_CNT(P_D_FLAGGED, serial ? 1 : 0);
+                PX_CNT(P_D_SHORT, serial ? 0 : 1);
+#endif
+                return serial;
             }
-            const int32_t rsum = wave_excl_scan(lane < C ? reqc : 0) + (lane < C ? reqc : 0);
-            const int32_t wsum = wave_excl_scan(lane < C ? (int32_t)w : 0) + (lane < C ? (int32_t)w : 0);
-            if (C) {
-                f.ret += unii(readlane((uint32_t)rsum, C - 1));
-                outp += (uint32_t)uni(readlane((uint32_t)wsum, C - 1));
-                f.seg += C;
-            }
-            return first_flag == C && C < L;
+            PX_CNT(P_D_COMMIT, next - f.seg);
+            f.seg = next;
+            f.ret = ret0 + (int32_t)(run_out - outp0);
+            outp = run_out;
+            return false;
         };
 
         if (qchunk == kNone || !push(uni(q.idx), unii(q.from), unii(q.to), qcap)) {
@@ -1677,7 +1867,7 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
             }
             bool pushed = false;
             while (!pop && !pushed && !err && f.ret < f.len && f.seg < sv.nseg) {
-                if (!batch(f, sv)) continue;
+                if (!window(f, sv)) continue;
                 PX_CNT(P_D_SERIAL, 1);
                 // one segment through the serial machine
                 const u32x4 E = sv.seg[2 * f.seg];

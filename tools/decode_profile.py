@@ -6,8 +6,13 @@ import numpy as np
 import torch
 import pixiu_amd as px
 from pixiu_amd import synth
-NAMES = ["d_batch", "d_laneit", "d_serial", "d_commit", "d_flagged", "d_short", "d_push", "d_t_total", "d_t_lane"]
-FIRST = 24  # index of P_D_BATCH in the profile enum
+import re
+_src = open(os.path.join(os.path.dirname(__file__), "..", "pixiu_amd", "csrc", "px_kernels.hip")).read()
+_enum = re.search(r"enum \{ (P_BYTES.*?) P_N \};", _src, re.S).group(1)
+IDX = {n.strip()[2:].lower(): i for i, n in enumerate(_enum.replace("\n", " ").split(",")) if n.strip()}
+NAMES = ["d_batch", "d_laneit", "d_serial", "d_commit", "d_flagged", "d_short", "d_push", "d_t_total", "d_t_lane",
+         "df_none", "df_topref", "df_cap", "df_nolink", "df_over", "df_lper", "df_depth", "df_range", "df_badrec",
+         "d_topb", "d_subb", "d_topc", "d_maxit", "d_t_assign", "d_rounds"]
 lib = px.load_library()
 lib.px_debug_prof_take.argtypes = [C.c_void_p, C.c_uint32]
 cfg, n, rps = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
@@ -16,14 +21,14 @@ cp = synth.make(cfg, n)
 keys_host = (np.ascontiguousarray(cp.keys), cp.koff.astype(np.uint64))
 out_cap = int(2 * cp.raw_bytes + 256 * n + (1 << 20))
 out = torch.empty(out_cap, dtype=torch.uint8, device="cuda")
-buf = (C.c_ulonglong * 64)()
+buf = (C.c_ulonglong * 128)()
 with px.Store(records_per_shard=rps, decode_waves=waves) as st:
     st.set_batch((cp.keys, cp.koff.astype(np.uint64)), (cp.vals, cp.voff.astype(np.uint64)))
-    lib.px_debug_prof_take(buf, 64)
+    lib.px_debug_prof_take(buf, 128)
     rc, off, ln, sts, need = st.get_batch_device(keys_host, out.data_ptr(), out_cap, px.COMPAT)
     ms = st.stats()["last_decode_kernel_ms"]
-k = lib.px_debug_prof_take(buf, 64)
-v = dict(zip(NAMES, buf[FIRST:FIRST + len(NAMES)]))
+k = lib.px_debug_prof_take(buf, 128)
+v = {name: buf[IDX[name]] for name in NAMES}
 print(f"config {cfg} n {n} rps {rps} waves {waves}: decode kernel {ms:.2f} ms, expanded {int(np.asarray(ln).sum())} B")
 for name in NAMES:
     print(f"  {name:10s} {v[name]:16d}  per query {v[name] / n:12.1f}")
