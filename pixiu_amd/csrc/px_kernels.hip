@@ -49,7 +49,7 @@ __device__ uint32_t g_trace_n;
     } while (0)
 #define PX_TRACE_STATE(k)                                                                     \
     do {                                                                                        \
-        PX_TRACE_MSG(-100 - (int32_t)(counter + (k)), act_node, act_doc);                       \
+        PX_TRACE_MSG(-100 - (int32_t)(i + (k)), act_node, act_doc);                       \
         PX_TRACE_MSG(act_direct, act_off + (k), remainder + (int32_t)(k));                      \
         PX_TRACE_MSG(n_nodes, pools, used);                                                     \
     } while (0)
@@ -192,8 +192,26 @@ PX_DEV uint32_t hslot(uint32_t parent, uint32_t c) {
 // an edge = the child's entry in its parent's map.  cnt = the child's own child
 // count, saturated at 3; slot = where the entry lives (root table, one of the
 // parent's two inline slots, or a hash slot).
+// Kept in its packed entry form (the three words a map entry stores), so loads and
+// stores move it without repacking and it occupies four scalar registers, not seven.
 struct Edge {
-    uint32_t id, doc, from, to, cnt, slot, key;
+    uint32_t w0;    // child id | child count (saturated at 3) << 26
+    uint32_t w1;    // label doc | from << 16
+    uint32_t w2;    // label to | key (first byte) << 16
+    uint32_t slot;
+    PX_DEV uint32_t id() const { return w0 & kNodeMask; }
+    PX_DEV uint32_t cnt() const { return (w0 >> 26) & 3u; }
+    PX_DEV uint32_t doc() const { return w1 & 0xffffu; }
+    PX_DEV uint32_t from() const { return w1 >> 16; }
+    PX_DEV uint32_t to() const { return w2 & 0xffffu; }
+    PX_DEV uint32_t key() const { return (w2 >> 16) & 0xffu; }
+    PX_DEV void set(uint32_t id, uint32_t cnt, uint32_t doc, uint32_t from, uint32_t to, uint32_t key) {
+        w0 = id | cnt << 26;
+        w1 = doc | from << 16;
+        w2 = to | key << 16;
+    }
+    PX_DEV void set_from(uint32_t f) { w1 = (w1 & 0xffffu) | f << 16; }
+    PX_DEV void set_key(uint32_t k) { w2 = (w2 & 0xffffu) | k << 16; }
 };
 constexpr uint32_t kInlineSlot = 0x40000000u;  // | which << 26 | parent
 
@@ -214,11 +232,13 @@ struct GstWave {
     // persistent counters
     uint32_t n_nodes, n_docs, chunk_seq, epoch, status;
     int32_t pools, used, pool_open;
-    uint64_t ctext_off, ub;
+    uint64_t ctext_off;
+    uint32_t ub;  // this launch's UB reads (added to the shard's 64-bit total at the end)
     // current doc + its byte window (lane l holds bytes [wb + 4l, wb + 4l + 4))
     uint32_t cur, cur_base, cur_len, wb, win;
     // active point (SuffixTree.h:33-40); act_base/act_len: text extent of act_doc
-    uint32_t act_node, act_doc, act_direct, act_off, counter, act_base, act_len;
+    // i: the doc byte being inserted (the reference's `counter`)
+    uint32_t act_node, act_doc, act_direct, act_off, i, act_base, act_len;
     int32_t remainder;
     // encoder (the reference keeps these as statics, PiXiuStr.cpp:17-26)
     uint32_t out, flushed, run, run_idx, run_to, applied, held, h_c, h_idx, h_pos;
@@ -234,17 +254,17 @@ struct GstWave {
     }
 
     // MemPool::p_malloc block accounting (MemPool.cpp:7-37)
+    // The pool is always open while docs are encoded (clear_tree's root node opens
+    // it), so the hot path is the branch-free "next pool when the request does not fit".
     PX_DEV void charge(int32_t blocks) {
-        if (!pool_open) {
-            pool_open = 1;
-            ++pools;
-            used = 0;
-        }
-        if (blocks > kPoolBlocks - used) {
-            ++pools;
-            used = 0;
-        }
-        used += blocks;
+        const bool next = blocks > kPoolBlocks - used;
+        pools += next ? 1 : 0;
+        used = (next ? 0 : used) + blocks;
+    }
+    PX_DEV void charge_first(int32_t blocks) {  // MemPool's first p_malloc opens pool 1
+        pool_open = 1;
+        pools = 1;
+        used = blocks;
     }
 
     // ---- doc extents: LDS cache for the first kDocCache docs
@@ -287,16 +307,13 @@ struct GstWave {
 
     // ---- child map
     PX_DEV static void unpack(uint32_t w0, uint32_t w1, uint32_t w2, Edge &e) {
-        e.id = w0 & kNodeMask;
-        e.cnt = (w0 >> 26) & 3u;
-        e.doc = w1 & 0xffffu;
-        e.from = w1 >> 16;
-        e.to = w2 & 0xffffu;
-        e.key = (w2 >> 16) & 0xffu;
+        e.w0 = w0;
+        e.w1 = w1;
+        e.w2 = w2;
     }
-    PX_DEV static uint32_t pk0(const Edge &e) { return e.id | (min(e.cnt, 3u) << 26); }
-    PX_DEV static uint32_t pk1(const Edge &e) { return e.doc | (e.from << 16); }
-    PX_DEV static uint32_t pk2(const Edge &e) { return e.to | (e.key << 16); }
+    PX_DEV static uint32_t pk0(const Edge &e) { return e.w0; }
+    PX_DEV static uint32_t pk1(const Edge &e) { return e.w1; }
+    PX_DEV static uint32_t pk2(const Edge &e) { return e.w2; }
 
     // child of n keyed by byte c.  found: fills e.  not found: slot = where a new
     // child goes (kNone: a hash slot must still be probed) and ncnt = n's count.
@@ -399,16 +416,14 @@ struct GstWave {
     PX_DEV void add_child(uint32_t parent, uint32_t pcnt, const Edge &kid, uint32_t hint) {
         charge(kEdgeBlocks);
         uint32_t slot = pcnt < 2 ? (kInlineSlot | (pcnt << 26) | parent)
-                                 : (hint != kNone ? hint : hash_free_slot(parent, kid.key));
+                                 : (hint != kNone ? hint : hash_free_slot(parent, kid.key()));
         write_entry(slot, parent, kid);
         if (parent != kRoot && pcnt < 3) nrec(parent)[1] = pcnt + 1;
     }
 
+    // capacity: encode_doc checks once per doc that 2 * len more nodes fit (a doc adds
+    // at most one leaf per suffix and one inner node per leaf)
     PX_DEV bool new_node(uint32_t &id) {
-        if (n_nodes >= node_cap || n_nodes >= kMaxNodes) {
-            fail(kErrCapacity);
-            return false;
-        }
         charge(kNodeBlocks);
         id = n_nodes++;
         return true;
@@ -427,8 +442,8 @@ struct GstWave {
             epoch = 1;
         }
         wave_sync();
-        uint32_t root;
-        if (new_node(root)) nodes[2 * root] = mk4(kRoot, 0, 0, 0);
+        charge_first(kNodeBlocks);  // the root (SuffixTree::init_prop)
+        nodes[2 * n_nodes++] = mk4(kRoot, 0, 0, 0);
     }
 
     // ---- stream encoder (PiXiuStr_init_stream)
@@ -563,13 +578,10 @@ struct GstWave {
 
     // ---- Ukkonen step pieces (SuffixTree.cpp:144-289)
     PX_DEV bool new_leaf(Edge &leaf, uint32_t c) {
-        if (!new_node(leaf.id)) return false;
-        nodes[2 * leaf.id] = mk4(kRoot, 0, 0, 0);  // link, child count
-        leaf.doc = cur;
-        leaf.from = counter;
-        leaf.to = cur_len;
-        leaf.cnt = 0;
-        leaf.key = c;
+        uint32_t id;
+        if (!new_node(id)) return false;
+        nodes[2 * id] = mk4(kRoot, 0, 0, 0);  // link, child count
+        leaf.set(id, 0, cur, i, cur_len, c);
         return true;
     }
 
@@ -585,10 +597,10 @@ struct GstWave {
             if (send) feed(false, 0, 0, c);
             return false;
         }
-        set_act_doc(e.doc);
-        act_direct = e.from;
+        set_act_doc(e.doc());
+        act_direct = e.from();
         act_off = (act_off + 1) & 0xffffu;
-        if (send) feed(true, e.doc, e.from, c);
+        if (send) feed(true, e.doc(), e.from(), c);
         return true;
     }
 
@@ -604,22 +616,22 @@ struct GstWave {
     PX_DEV bool canonise(Edge &e) {
 #ifdef PX_PROFILE
         uint64_t tk = __builtin_amdgcn_s_memtime();
-        if ((counter - act_off) - wb >= kWin) PX_CNT(P_KEYMISS, 1);
-        uint32_t key0 = curchar(counter - act_off);
+        if ((i - act_off) - wb >= kWin) PX_CNT(P_KEYMISS, 1);
+        uint32_t key0 = curchar(i - act_off);
         uint64_t tl = __builtin_amdgcn_s_memtime();
         prof[P_T_KEY] += tl - tk;
         bool ok0 = must_lookup(act_node, key0, e);
         prof[P_T_LOOK] += __builtin_amdgcn_s_memtime() - tl;
         if (!ok0) return false;
 #else
-        if (!must_lookup(act_node, curchar(counter - act_off), e)) return false;
+        if (!must_lookup(act_node, curchar(i - act_off), e)) return false;
 #endif
         uint32_t supply;
-        while (act_off > (supply = e.to - e.from)) {
-            act_node = e.id;
+        while (act_off > (supply = e.to() - e.from())) {
+            act_node = e.id();
             act_off = (act_off - supply) & 0xffffu;
-            if (!must_lookup(act_node, curchar(counter - act_off), e)) return false;
-            act_direct = e.from;
+            if (!must_lookup(act_node, curchar(i - act_off), e)) return false;
+            act_direct = e.from();
             PX_CNT(P_CANON_LVL, 1);
         }
         return true;
@@ -643,27 +655,25 @@ struct GstWave {
 #endif
         if (split) {
             Edge in;
-            if (!new_node(in.id)) return false;
-            if (last_inner != kNone) nodes[2 * last_inner].x = in.id;
-            last_inner = in.id;
-            in.doc = e.doc;
-            in.from = e.from;
-            in.to = (e.from + act_off) & 0xffffu;
-            in.key = e.key;
-            in.cnt = key_e != c ? 2 : 1;
+            uint32_t in_id;
+            if (!new_node(in_id)) return false;
+            if (last_inner != kNone) nodes[2 * last_inner].x = in_id;
+            last_inner = in_id;
+            const uint32_t in_to = (e.from() + act_off) & 0xffffu;
+            in.set(in_id, key_e != c ? 2 : 1, e.doc(), e.from(), in_to, e.key());
             write_entry(e.slot, act_node, in);  // replaces e under its first byte: no charge
-            e.from = in.to;
-            e.key = key_e;
+            e.set_from(in_to);
+            e.set_key(key_e);
             // inner->set_sub(edge); inner->set_sub(leaf): an equal key replaces
             charge(kEdgeBlocks);
             if (key_e != c) {
                 charge(kEdgeBlocks);
-                nodes[2 * in.id] = mk4(kRoot, 2, pk0(e), pk1(e));
-                nodes[2 * in.id + 1] = mk4(pk2(e), pk0(leaf), pk1(leaf), pk2(leaf));
-                e.slot = kInlineSlot | in.id;
+                nodes[2 * in_id] = mk4(kRoot, 2, pk0(e), pk1(e));
+                nodes[2 * in_id + 1] = mk4(pk2(e), pk0(leaf), pk1(leaf), pk2(leaf));
+                e.slot = kInlineSlot | in_id;
             } else {
-                nodes[2 * in.id] = mk4(kRoot, 1, pk0(leaf), pk1(leaf));
-                nrec(in.id)[4] = pk2(leaf);
+                nodes[2 * in_id] = mk4(kRoot, 1, pk0(leaf), pk1(leaf));
+                nrec(in_id)[4] = pk2(leaf);
                 e.slot = kNone;  // e fell out of the tree (replaced under the same byte)
             }
 #ifdef PX_PROFILE
@@ -671,11 +681,11 @@ struct GstWave {
 #endif
         } else {
             PX_CNT(P_G_NOSPLIT, 1);
-            if (last_inner != kNone) nodes[2 * last_inner].x = e.id;
-            last_inner = e.id;
-            add_child(e.id, e.cnt, leaf, hint);
-            if (e.cnt < 3) {
-                ++e.cnt;
+            if (last_inner != kNone) nodes[2 * last_inner].x = e.id();
+            last_inner = e.id();
+            add_child(e.id(), e.cnt(), leaf, hint);
+            if (e.cnt() < 3) {
+                e.w0 += 1u << 26;
                 write_entry(e.slot, act_node, e);
             }
 #ifdef PX_PROFILE
@@ -690,11 +700,11 @@ struct GstWave {
     // matching prefix as COMPRESS messages in bulk.  Returns matched length.
     PX_DEV uint32_t fast_forward(const Edge &e, uint32_t i) {
         const uint32_t lane = lane_id();
-        uint32_t limit = min(e.to - e.from - act_off, cur_len - i);
+        uint32_t limit = min(e.to() - e.from() - act_off, cur_len - i);
         uint32_t m = 0;
         while (m < limit) {
             uint32_t w = min(64u, limit - m);
-            uint32_t t = e.from + act_off + m + lane;  // position in the active doc
+            uint32_t t = e.from() + act_off + m + lane;  // position in the active doc
             bool live = lane < w;
             uint32_t a = live ? text[cur_base + i + m + lane] : 0;
             bool oob = live && t >= act_len;
@@ -702,7 +712,7 @@ struct GstWave {
             uint64_t mism = ballot(live && (oob || a != b));
             uint64_t m251 = ballot(live && a == kEsc);
             uint32_t got = mism ? ffs64(mism) : w;
-            if (got) feed_bulk(e.doc, e.from + act_off + m, got, m251);
+            if (got) feed_bulk(e.doc(), e.from() + act_off + m, got, m251);
             m += got;
             if (mism) {
                 if (readlane((uint32_t)oob, got)) ++ub;
@@ -716,7 +726,7 @@ struct GstWave {
     PX_DEV void encode_doc(uint32_t len) {
         cur_len = len;
         remainder = 0;
-        counter = 0;
+        i = 0;
         act_node = kRoot;
         act_doc = act_direct = act_off = 0;
         act_base = docbase(0);
@@ -725,7 +735,7 @@ struct GstWave {
         load_window(0);
         bool have_e = false;
         Edge e;
-        uint32_t i = 0;
+        if (n_nodes + 2 * len + 1 > min(node_cap, kMaxNodes)) fail(kErrCapacity);
         while (i < len && status == kOk) {
             if (i - wb >= kWin - 64 && i - wb < 0x80000000u) load_window(i >= 64 ? i - 64 : 0);
             drain_obuf();
@@ -736,7 +746,6 @@ struct GstWave {
                 PX_T0();
                 ++remainder;
                 have_e = at_root(c, true, e);
-                ++counter;
                 ++i;
                 PX_CNT(P_ROOT, 1);
                 PX_T1(P_T_ROOT);
@@ -755,26 +764,25 @@ struct GstWave {
             }
             // free slot for c under e.id found by a failed lookup (valid until the next hash write)
             uint32_t hint = kNone;
-            if (e.from + act_off == e.to) {
+            if (e.from() + act_off == e.to()) {
                 Edge n;
                 PX_T0();
                 uint32_t ncnt;
-                bool wd = e.cnt && lookup(e.id, c, n, hint, ncnt);
+                bool wd = e.cnt() && lookup(e.id(), c, n, hint, ncnt);
                 PX_T1(P_T_WALK);
                 if (wd) {
                     PX_CNT(P_WALK, 1);
                     ++remainder;
-                    act_node = e.id;
-                    set_act_doc(n.doc);
-                    act_direct = n.from;
+                    act_node = e.id();
+                    set_act_doc(n.doc());
+                    act_direct = n.from();
                     act_off = 1;
-                    feed(true, n.doc, n.from, c);
+                    feed(true, n.doc(), n.from(), c);
                     e = n;  // child(act_node, text[act_doc][act_direct]) == n
-                    ++counter;
                     ++i;
                     continue;
                 }
-            } else if (e.from + act_off < e.to) {
+            } else if (e.from() + act_off < e.to()) {
                 PX_T0();
                 uint32_t m = fast_forward(e, i);
                 PX_T1(P_T_FF);
@@ -786,7 +794,6 @@ struct GstWave {
                 if (m) {
                     remainder += (int32_t)m;
                     act_off = (act_off + m) & 0xffffu;
-                    counter += m;
                     i += m;
                     continue;
                 }
@@ -807,9 +814,9 @@ struct GstWave {
 #ifdef PX_PROFILE
                 uint64_t tg = __builtin_amdgcn_s_memtime();
 #endif
-                const bool split = (!e.cnt || e.to - e.from > 1) && e.from + act_off != e.to;
+                const bool split = (!e.cnt() || e.to() - e.from() > 1) && e.from() + act_off != e.to();
                 uint32_t key_e = 0;
-                if (split) key_e = e_next >= 0 ? (uint32_t)e_next : tbyte(docbase(e.doc) + e.from + act_off);
+                if (split) key_e = e_next >= 0 ? (uint32_t)e_next : tbyte(docbase(e.doc()) + e.from() + act_off);
                 PX_CNT(P_K_CACHED, split && e_next >= 0 ? 1 : 0);
                 PX_CNT(P_K_LOAD1, split && e_next < 0 && act_off == 1 ? 1 : 0);
                 PX_CNT(P_K_LOADN, split && e_next < 0 && act_off != 1 ? 1 : 0);
@@ -842,24 +849,24 @@ struct GstWave {
 #endif
                 // next iteration's suffix link, issued before this end check's wait
                 lraw = act_node != kRoot ? nodes[2 * act_node].x : 0u;
-                PX_CNT(P_E_LOOK, e.from + act_off == e.to ? 1 : 0);
-                PX_CNT(P_E_OFF1, e.from + act_off < e.to && act_off == 1 ? 1 : 0);
-                PX_CNT(P_E_OFF2, e.from + act_off < e.to && act_off == 2 ? 1 : 0);
-                PX_CNT(P_E_OFF3, e.from + act_off < e.to && act_off == 3 ? 1 : 0);
-                PX_CNT(P_E_OFF4P, e.from + act_off < e.to && act_off >= 4 ? 1 : 0);
-                if (e.from + act_off == e.to) {
+                PX_CNT(P_E_LOOK, e.from() + act_off == e.to() ? 1 : 0);
+                PX_CNT(P_E_OFF1, e.from() + act_off < e.to() && act_off == 1 ? 1 : 0);
+                PX_CNT(P_E_OFF2, e.from() + act_off < e.to() && act_off == 2 ? 1 : 0);
+                PX_CNT(P_E_OFF3, e.from() + act_off < e.to() && act_off == 3 ? 1 : 0);
+                PX_CNT(P_E_OFF4P, e.from() + act_off < e.to() && act_off >= 4 ? 1 : 0);
+                if (e.from() + act_off == e.to()) {
                     Edge n;
                     uint32_t ncnt;
-                    if (e.cnt && lookup(e.id, c, n, hint, ncnt)) {
-                        act_node = e.id;
-                        set_act_doc(n.doc);
-                        act_direct = n.from;
+                    if (e.cnt() && lookup(e.id(), c, n, hint, ncnt)) {
+                        act_node = e.id();
+                        set_act_doc(n.doc());
+                        act_direct = n.from();
                         act_off = 1;
                         if (last_inner != kNone) nodes[2 * last_inner].x = act_node;
                         break;
                     }
-                } else if (e.from + act_off < e.to) {
-                    uint32_t ch = tbyte(docbase(e.doc) + e.from + act_off);
+                } else if (e.from() + act_off < e.to()) {
+                    uint32_t ch = tbyte(docbase(e.doc()) + e.from() + act_off);
                     if (c == ch) {
                         act_off = (act_off + 1) & 0xffffu;
                         break;
@@ -872,7 +879,6 @@ struct GstWave {
             }
             PX_T1(P_T_SPLIT);
             have_e = false;
-            ++counter;
             ++i;
         }
         if (status == kOk) {
@@ -916,7 +922,7 @@ __global__ void __launch_bounds__(64 * kGstWaves, 6) k_gst_encode(const GstShard
     g.used = unii(st.used_blocks);
     g.pool_open = unii(st.pool_open);
     g.ctext_off = uni64(st.ctext_off);
-    g.ub = uni64(st.ub_reads);
+    g.ub = 0;
     g.text = (PX_GAS uint8_t *)sh.text + g.ctext_off;
 #ifdef PX_PROFILE
     for (int k = 0; k < P_N; ++k) g.prof[k] = 0;
@@ -987,7 +993,7 @@ __global__ void __launch_bounds__(64 * kGstWaves, 6) k_gst_encode(const GstShard
         o.epoch = g.epoch;
         o.status = g.status;
         o.ctext_off = g.ctext_off;
-        o.ub_reads = g.ub;
+        o.ub_reads = sh.st->ub_reads + g.ub;
         *sh.st = o;
         st_out[s] = o;  // compact copy: the host reads every shard's state in one transfer
     }
