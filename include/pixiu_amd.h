@@ -84,8 +84,10 @@ typedef struct px_stats {
     uint64_t raw_bytes, doc_bytes, comp_bytes;
     uint64_t ub_reads;        /* reads the reference makes out of bounds (UB there) */
     uint64_t device_bytes;    /* device memory held */
-    double last_set_kernel_ms;    /* k_gst_encode time of the last px_set_batch */
+    double last_set_kernel_ms;    /* k_gst_encode + k_gst_emit time of the last px_set_batch */
     double last_decode_kernel_ms; /* k_decode time of the last get/parse batch */
+    double last_walk_kernel_ms;   /* k_gst_encode (suffix-tree walk -> encoder messages) alone */
+    double last_emit_kernel_ms;   /* k_gst_emit (stream encoder -> compressed bytes) alone */
 } px_stats;
 
 px_ctx *px_open(const px_opts *opts);

@@ -62,7 +62,8 @@ class PxStats(C.Structure):
     _fields_ = [("records", C.c_uint64), ("shards", C.c_uint64), ("chunks", C.c_uint64),
                 ("raw_bytes", C.c_uint64), ("doc_bytes", C.c_uint64), ("comp_bytes", C.c_uint64),
                 ("ub_reads", C.c_uint64), ("device_bytes", C.c_uint64),
-                ("last_set_kernel_ms", C.c_double), ("last_decode_kernel_ms", C.c_double)]
+                ("last_set_kernel_ms", C.c_double), ("last_decode_kernel_ms", C.c_double),
+                ("last_walk_kernel_ms", C.c_double), ("last_emit_kernel_ms", C.c_double)]
 
 
 SET_RESULT_DTYPE = np.dtype([("status", "<u4"), ("replaced", "<u4"), ("shard", "<u4"), ("chunk", "<u4"),

@@ -73,6 +73,17 @@ PX_DEV uint32_t ffs64(uint64_t m) { return (uint32_t)__ffsll((unsigned long long
 PX_DEV uint32_t readlane(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
 PX_DEV uint32_t rd16(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
 
+// inclusive wave prefix sum on DPP row shifts and row broadcasts (no LDS round trips)
+PX_DEV int32_t wave_incl_scan_dpp(int32_t x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 into rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 into rows 2, 3
+    return x;
+}
+
 #ifdef PX_PROFILE
 // debug build only: per-category counters and shader-clock cycles of k_gst_encode
 enum { P_BYTES, P_FF_CALLS, P_FF_BYTES, P_PASS, P_ITERS, P_LOOKUPS, P_PROBES, P_ROOT, P_WALK, P_LINK, P_CANON_LVL,
@@ -170,8 +181,7 @@ __global__ void __launch_bounds__(256) k_doc_write(uint32_t n, const uint8_t *ke
 // probes (one 64-byte line per probe), the current doc's 256-byte byte window,
 // and the encoder's output staging.  Per shard, LDS holds the root's 256 child
 // entries, the first 256 doc starts and the output staging buffer.
-constexpr uint32_t kObuf = 1024;   // per-wave output staging ring (LDS)
-constexpr uint32_t kFlushChunk = 256;  // the ring drains in aligned 256-byte pieces (one dword per lane)
+constexpr uint32_t kPassMsg = 0xffffffffu;  // NO_COMPRESS (a COMPRESS idx is at most 65,534)
 constexpr uint32_t kDocCache = 256;  // doc starts cached in LDS
 constexpr uint32_t kRootSlot = 0x80000000u;
 constexpr uint32_t kWin = 256;  // current-doc window (4 bytes per lane)
@@ -218,7 +228,6 @@ constexpr uint32_t kInlineSlot = 0x40000000u;  // | which << 26 | parent
 struct GstLds {
     u32x4 root[256];
     uint32_t doc_base[kDocCache + 1];
-    uint8_t obuf[kObuf];
 };
 
 struct GstWave {
@@ -240,9 +249,7 @@ struct GstWave {
     // i: the doc byte being inserted (the reference's `counter`)
     uint32_t act_node, act_doc, act_direct, act_off, i, act_base, act_len;
     int32_t remainder;
-    // encoder (the reference keeps these as statics, PiXiuStr.cpp:17-26)
-    uint32_t out, flushed, run, run_idx, run_to, applied, held, h_c, h_idx, h_pos;
-    PX_GAS uint8_t *out_dst;
+    PX_GAS uint32_t *msg;  // the current doc's encoder messages
 #ifdef PX_PROFILE
     uint64_t prof[P_N];
 #endif
@@ -446,134 +453,21 @@ struct GstWave {
         nodes[2 * n_nodes++] = mk4(kRoot, 0, 0, 0);
     }
 
-    // ---- stream encoder (PiXiuStr_init_stream)
-    // Output bytes go to an LDS ring; the byte loop drains it in aligned 256-byte
-    // pieces (one dword per lane).  One byte-loop step appends far fewer than
-    // kObuf - kFlushChunk bytes, so draining once per step never overruns the ring.
-    PX_DEV void drain_obuf() {
-        const uint32_t lane = lane_id();
-        while (out - flushed >= kFlushChunk) {
-            wave_sync();
-            const uint32_t v = *(const PX_LAS uint32_t *)&lds->obuf[(flushed & (kObuf - 1)) + 4 * lane];
-            *(PX_GAS uint32_t *)(out_dst + flushed + 4 * lane) = v;
-            flushed += kFlushChunk;
-        }
-    }
-    PX_DEV void flush_obuf_all() {
-        const uint32_t lane = lane_id();
-        wave_sync();
-#pragma unroll 1
-        for (uint32_t o = flushed + lane; o < out; o += 64) out_dst[o] = lds->obuf[o & (kObuf - 1)];
-        wave_sync();
-        flushed = out;
-    }
-    // append n (<= 64) bytes; lane k holds byte k
-    PX_DEV void put_lanes(uint32_t n, uint32_t b) {
-        if (lane_id() < n) lds->obuf[(out + lane_id()) & (kObuf - 1)] = (uint8_t)b;
-        wave_sync();
-        out += n;
-    }
-    PX_DEV void put(uint32_t b) { put_lanes(1, b); }
-    PX_DEV void flush_run() {
-        if (run == 0) return;
-        const uint32_t lane = lane_id();
-        uint32_t n, b;
-        if (run > 6) {
-            // [251, run, idx:2, to:2] or, past 255, [251, 1, idx:2, to:2, from:2];
-            // run == 251 aliases the escape (PiXiuStr.cpp:72): kept
-            uint32_t w0, w1;
-            if (run > 255) {
-                uint32_t from = (run_to - run) & 0xffffu;
-                w0 = kEsc | (uint32_t)kBigSign << 8 | (run_idx & 0xffffu) << 16;
-                w1 = (run_to & 0xffffu) | from << 16;
-                n = 8;
-            } else {
-                w0 = kEsc | run << 8 | (run_idx & 0xffffu) << 16;
-                w1 = run_to & 0xffffu;
-                n = 6;
-            }
-            b = ((lane < 4 ? w0 : w1) >> ((lane & 3) * 8)) & 0xffu;
-        } else {
-            // the run's bytes were appended literally: they are the doc bytes just consumed
-            uint32_t p = applied - run + lane;
-            uint32_t d = p - wb;
-            uint32_t wv = __shfl(win, (int)((d >> 2) & 63u));
-            b = (wv >> ((d & 3) * 8)) & 0xffu;
-            if (lane < run && d >= kWin) b = text[cur_base + p];
-            n = run;
-        }
-        put_lanes(n, b);
-        run = 0;
-    }
-    PX_DEV void apply_c(uint32_t idx, uint32_t pos) {
-        run_idx = idx;
-        run_to = pos + 1;
-        ++run;
-        ++applied;
-    }
-    PX_DEV void apply_p() {
-        flush_run();
-        put(curchar(applied));
-        ++applied;
-    }
-    // one message for doc byte `b` (2-message 251 look-ahead, PiXiuStr.cpp:33-54)
+    // ---- encoder messages (the PXSMsg stream SuffixTree::setitem hands to
+    // PiXiuStr_init_stream, PiXiuStr.h:55-59, SuffixTree.cpp:291-304): one u32 per doc
+    // byte, idx << 16 | pos for COMPRESS, kPassMsg for NO_COMPRESS.  The stream
+    // encoder itself runs lane-parallel afterwards (k_gst_emit), so the walk carries
+    // none of its state.  All lanes store the same word (no exec-mask juggling).
     PX_DEV void feed(bool is_c, uint32_t idx, uint32_t pos, uint32_t b) {
         PX_TRACE_MSG(is_c ? (int32_t)idx : -3, is_c ? pos : 0, b);
-        feed_nt(is_c, idx, pos, b);
+        msg[i] = is_c ? (idx << 16 | pos) : kPassMsg;
     }
-    PX_DEV void feed_nt(bool is_c, uint32_t idx, uint32_t pos, uint32_t b) {
-        if (held) {
-            held = 0;
-            if (h_c && is_c) {
-                apply_c(h_idx, h_pos);
-                apply_c(idx, pos);
-            } else {
-#pragma unroll 1
-                for (int k = 0; k < 2; ++k) apply_p();
-            }
-        } else if (b == kEsc) {
-            held = 1;
-            h_c = is_c;
-            h_idx = idx;
-            h_pos = pos;
-        } else if (is_c) {
-            apply_c(idx, pos);
-        } else {
-            apply_p();
-        }
-    }
-    // m (<= 64) consecutive COMPRESS messages (idx, pos0 + k); m251 = bit k set iff byte k is 251
-    PX_DEV void feed_bulk(uint32_t idx, uint32_t pos0, uint32_t m, uint64_t m251) {
+    // m (<= 64) consecutive COMPRESS messages (idx, pos0 + k) for doc bytes at + k
+    PX_DEV void feed_bulk(uint32_t at, uint32_t idx, uint32_t pos0, uint32_t m, uint64_t m251) {
 #ifdef PX_TRACE
         for (uint32_t t = 0; t < m; ++t) PX_TRACE_MSG(idx, pos0 + t, ((m251 >> t) & 1) ? 251 : -1);
 #endif
-        uint32_t k = 0;
-        if (held) {
-            feed_nt(true, idx, pos0, (m251 & 1) ? kEsc : 0);
-            k = 1;
-        }
-        if (k >= m) return;
-        bool last_held = false;
-        if ((m251 >> (m - 1)) & 1) {
-            uint64_t span = (m == 64 ? ~0ull : ((1ull << m) - 1)) & ~((1ull << k) - 1);
-            uint64_t non = ~m251 & span;  // non-251 bytes in [k, m)
-            uint32_t hz = non ? 63u - (uint32_t)__clzll((long long)non) : k - 1;  // highest non-251
-            uint32_t L = (m - 1) - hz;  // trailing 251 run length
-            last_held = (L & 1) != 0;
-        }
-        uint32_t cnt = m - k - (last_held ? 1 : 0);
-        if (cnt) {
-            run += cnt;
-            run_idx = idx;
-            run_to = pos0 + k + cnt;
-            applied += cnt;
-        }
-        if (last_held) {
-            held = 1;
-            h_c = 1;
-            h_idx = idx;
-            h_pos = pos0 + m - 1;
-        }
+        if (lane_id() < m) msg[at + lane_id()] = (idx << 16) | (pos0 + lane_id());
     }
 
     // ---- Ukkonen step pieces (SuffixTree.cpp:144-289)
@@ -712,7 +606,7 @@ struct GstWave {
             uint64_t mism = ballot(live && (oob || a != b));
             uint64_t m251 = ballot(live && a == kEsc);
             uint32_t got = mism ? ffs64(mism) : w;
-            if (got) feed_bulk(e.doc(), e.from() + act_off + m, got, m251);
+            if (got) feed_bulk(i + m, e.doc(), e.from() + act_off + m, got, m251);
             m += got;
             if (mism) {
                 if (readlane((uint32_t)oob, got)) ++ub;
@@ -731,14 +625,12 @@ struct GstWave {
         act_doc = act_direct = act_off = 0;
         act_base = docbase(0);
         act_len = docbase(1) - act_base;
-        out = flushed = run = applied = held = 0;
         load_window(0);
         bool have_e = false;
         Edge e;
         if (n_nodes + 2 * len + 1 > min(node_cap, kMaxNodes)) fail(kErrCapacity);
         while (i < len && status == kOk) {
             if (i - wb >= kWin - 64 && i - wb < 0x80000000u) load_window(i >= 64 ? i - 64 : 0);
-            drain_obuf();
             const uint32_t c = curchar(i);
             PX_TRACE_STATE(0);
             PX_CNT(P_BYTES, 1);
@@ -881,11 +773,6 @@ struct GstWave {
             have_e = false;
             ++i;
         }
-        if (status == kOk) {
-            if (held) fail(kErrCorrupt);  // stream ended inside a 251 pair
-            flush_run();
-            flush_obuf_all();
-        }
     }
 };
 
@@ -895,7 +782,7 @@ constexpr uint32_t kGstWaves = 4;
 
 __global__ void __launch_bounds__(64 * kGstWaves, 6) k_gst_encode(const GstShard *shards, uint32_t n_shards,
                                                    const uint32_t *doc_len, uint8_t *const *comp_dst,
-                                                   uint32_t *comp_len, uint32_t *rec_chunk,
+                                                   const uint8_t *comp_base, uint32_t *msgs, uint32_t *rec_chunk,
                                                    uint32_t *rec_idx, uint32_t *rec_status, ShardState *st_out) {
     __shared__ GstLds lds_w[kGstWaves];
     const uint32_t wv = uni(threadIdx.x >> 6);
@@ -942,7 +829,6 @@ __global__ void __launch_bounds__(64 * kGstWaves, 6) k_gst_encode(const GstShard
         if (g.status != kOk || len == 0xffffffffu) {
             if (lane == 0) {
                 rec_status[r] = g.status != kOk ? g.status : (uint32_t)kErrInval;
-                comp_len[r] = 0;
             }
             continue;
         }
@@ -965,11 +851,10 @@ __global__ void __launch_bounds__(64 * kGstWaves, 6) k_gst_encode(const GstShard
         g.cur_base = g.docbase(g.cur);
         g.set_docbase(g.cur + 1, g.cur_base + len);
         wave_sync();
-        g.out_dst = (PX_GAS uint8_t *)comp_dst[r];
+        g.msg = (PX_GAS uint32_t *)msgs + (comp_dst[r] - comp_base);
         g.encode_doc(len);
         ++g.n_docs;
         if (lane == 0) {
-            comp_len[r] = g.out;
             rec_chunk[r] = g.chunk_seq;
             rec_idx[r] = g.cur;
             rec_status[r] = g.status;
@@ -996,6 +881,113 @@ __global__ void __launch_bounds__(64 * kGstWaves, 6) k_gst_encode(const GstShard
         o.ub_reads = sh.st->ub_reads + g.ub;
         *sh.st = o;
         st_out[s] = o;  // compact copy: the host reads every shard's state in one transfer
+    }
+}
+
+// ====================================================================== stream encoder
+// PiXiuStr_init_stream (PiXiuStr.cpp:16-118) over one doc's message stream, one wave
+// per record, 64 messages per step.  The sequential encoder is restated as
+// per-position rules that lanes evaluate independently:
+//   * 251 look-ahead (:33-54): a doc byte 251 that is not itself the second byte of
+//     a pair starts a pair with its successor (in an escaped doc these are the escape
+//     pairs); both messages of a pair are COMPRESS only if both were, else both PASS.
+//   * a run = maximal sequence of (effective) COMPRESS messages; it ends at its last
+//     message, whose idx and pos + 1 are the token's idx and `to` (:84-88, :112-115).
+//   * try_explode (:56-82): a run of len > 6 becomes [251, len, idx:2, to:2] (len <= 255;
+//     len 251 aliases the escape, kept) or [251, 1, idx:2, to:2, from:2]; shorter runs
+//     and PASS messages are their doc bytes, literally.
+// Output offsets come from a wave prefix sum of the per-position output sizes; the
+// open run, the pair parity and the output cursor carry between steps.
+__global__ void __launch_bounds__(256) k_gst_emit(uint32_t n, const uint8_t *const *doc_ptr, const uint32_t *doc_len,
+                                                  uint8_t *const *comp_dst, const uint8_t *comp_base,
+                                                  const uint32_t *msgs, uint32_t *rec_status, uint32_t *comp_len) {
+    const uint32_t lane = lane_id();
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    const uint64_t below = (1ull << lane) - 1;
+    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < n; r += waves) {
+        const uint32_t len = uni(doc_len[r]);
+        if (len == 0xffffffffu || uni(rec_status[r]) != kOk) {
+            if (lane == 0) comp_len[r] = 0;
+            continue;
+        }
+        const PX_GAS uint8_t *doc = (const PX_GAS uint8_t *)doc_ptr[r];
+        PX_GAS uint8_t *out = (PX_GAS uint8_t *)comp_dst[r];
+        const PX_GAS uint32_t *msg = (const PX_GAS uint32_t *)msgs + (comp_dst[r] - comp_base);
+        uint32_t outp = 0;
+        bool second_in = false;  // position ws is the second byte of a pair
+        bool prevc_in = false;   // raw COMPRESS-ness of position ws - 1
+        uint32_t open_start = 0; // first position of the run open at ws (== ws: none)
+        uint32_t open_msg = 0;   // message at ws - 1 (the open run's last so far)
+        bool corrupt = false;
+        // a run's output at o: a token, or its doc bytes when it is 6 or shorter
+        auto run_out = [&](uint32_t o, uint32_t rl, uint32_t m, uint32_t start) {
+            if (rl > 6) {
+                const uint32_t idx = m >> 16, to = ((m & 0xffffu) + 1u) & 0xffffu;
+                out[o] = kEsc;
+                out[o + 1] = rl > 255 ? kBigSign : (uint8_t)rl;
+                out[o + 2] = (uint8_t)idx;
+                out[o + 3] = (uint8_t)(idx >> 8);
+                out[o + 4] = (uint8_t)to;
+                out[o + 5] = (uint8_t)(to >> 8);
+                if (rl > 255) {
+                    const uint32_t from = (to - rl) & 0xffffu;
+                    out[o + 6] = (uint8_t)from;
+                    out[o + 7] = (uint8_t)(from >> 8);
+                }
+            } else {
+                for (uint32_t j = 0; j < rl; ++j) out[o + j] = doc[start + j];
+            }
+        };
+        auto run_size = [](uint32_t rl) -> uint32_t { return rl > 6 ? (rl > 255 ? 8u : 6u) : rl; };
+        for (uint32_t ws = 0; ws < len; ws += 64) {
+            const uint32_t k = ws + lane;
+            const bool live = k < len;
+            const uint32_t b = live ? doc[k] : 0u;
+            const uint32_t m = live ? msg[k] : kPassMsg;
+            const bool isc = m != kPassMsg;
+            const uint64_t cm = ballot(isc);
+            const bool nextc_63 = ws + 64 < len && uni(msg[ws + 64]) != kPassMsg;
+            const bool isc_next = lane < 63 ? ((cm >> (lane + 1)) & 1) != 0 : nextc_63;
+            const bool isc_prev = lane > 0 ? ((cm >> (lane - 1)) & 1) != 0 : prevc_in;
+            // pair starts: within a run of 251 bytes they alternate from the run's start
+            const uint64_t non251 = ~ballot(live && b == kEsc);
+            const uint64_t nb = non251 & below;
+            const uint32_t rlen = nb ? lane - (64u - (uint32_t)__clzll((long long)nb)) : lane + (second_in ? 1u : 0u);
+            const bool ps = live && b == kEsc && (rlen & 1u) == 0;
+            const uint64_t psm = ballot(ps);
+            const bool sec = lane > 0 ? ((psm >> (lane - 1)) & 1) != 0 : second_in;
+            if (ballot(ps && k + 1 >= len)) corrupt = true;  // stream ends inside a pair
+            const bool effc = isc && (ps ? isc_next : sec ? isc_prev : true);
+            const uint64_t em = ballot(live && effc);
+            // a run ending at lane 63 is only known to end with the doc; otherwise it
+            // stays open and the next step's lane 0 emits it if that lane breaks it
+            const bool end = effc && (lane < 63 ? ((em >> (lane + 1)) & 1) == 0 : k + 1 >= len);
+            const bool flush_prev = lane == 0 && open_start < ws && !effc;
+            const uint64_t nc = ~em & below;
+            const uint32_t start = nc ? ws + (64u - (uint32_t)__clzll((long long)nc)) : open_start;
+            const uint32_t rl = k + 1 - start;
+            const uint32_t pre = flush_prev ? run_size(ws - open_start) : 0u;
+            uint32_t size = pre;
+            if (live && !effc) size += 1;
+            if (end) size += run_size(rl);
+            const int32_t incl = wave_incl_scan_dpp((int32_t)size);
+            uint32_t o = outp + (uint32_t)incl - size;
+            if (flush_prev) {
+                run_out(o, ws - open_start, open_msg, open_start);
+                o += pre;
+            }
+            if (live && !effc) out[o] = (uint8_t)b;
+            if (end) run_out(o, rl, m, start);
+            outp += uni(readlane((uint32_t)incl, 63));
+            second_in = (psm >> 63) & 1;
+            prevc_in = (cm >> 63) & 1;
+            open_start = ((em >> 63) & 1) ? uni(readlane(start, 63)) : ws + 64;
+            open_msg = uni(readlane(m, 63));
+        }
+        if (lane == 0) {
+            comp_len[r] = outp;
+            if (corrupt) rec_status[r] = kErrCorrupt;
+        }
     }
 }
 
@@ -1342,17 +1334,6 @@ PX_DEV void lane_copy(PX_GAS uint8_t *dst, const PX_GAS uint8_t *src, uint32_t n
         dst[n >> 1] = b;
         dst[n - 1] = c;
     }
-}
-
-// inclusive wave prefix sum on DPP row shifts and row broadcasts (no LDS round trips)
-PX_DEV int32_t wave_incl_scan_dpp(int32_t x) {
-    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);  // row_shr:1
-    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);  // row_shr:2
-    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);  // row_shr:4
-    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);  // row_shr:8
-    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 into rows 1, 3
-    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 into rows 2, 3
-    return x;
 }
 
 PX_DEV int32_t wave_excl_scan(int32_t v) {
@@ -2010,11 +1991,20 @@ hipError_t launch_doc_write(hipStream_t s, uint32_t n, const uint8_t *keys, cons
 }
 
 hipError_t launch_gst_encode(hipStream_t s, const GstShard *shards, uint32_t n_shards, const uint32_t *doc_len,
-                             uint8_t *const *comp_dst, uint32_t *comp_len, uint32_t *rec_chunk,
-                             uint32_t *rec_idx, uint32_t *rec_status, ShardState *st_out) {
+                             uint8_t *const *comp_dst, const uint8_t *comp_base, uint32_t *msgs,
+                             uint32_t *rec_chunk, uint32_t *rec_idx, uint32_t *rec_status, ShardState *st_out) {
     if (!n_shards) return hipSuccess;
-    k_gst_encode<<<(n_shards + kGstWaves - 1) / kGstWaves, 64 * kGstWaves, 0, s>>>(shards, n_shards, doc_len, comp_dst, comp_len, rec_chunk, rec_idx,
-                                         rec_status, st_out);
+    k_gst_encode<<<(n_shards + kGstWaves - 1) / kGstWaves, 64 * kGstWaves, 0, s>>>(
+        shards, n_shards, doc_len, comp_dst, comp_base, msgs, rec_chunk, rec_idx, rec_status, st_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_gst_emit(hipStream_t s, uint32_t n, const uint8_t *const *doc_ptr, const uint32_t *doc_len,
+                           uint8_t *const *comp_dst, const uint8_t *comp_base, const uint32_t *msgs,
+                           uint32_t *rec_status, uint32_t *comp_len) {
+    if (!n) return hipSuccess;
+    const uint32_t blocks = min((n + 3) / 4, 8192u);
+    k_gst_emit<<<blocks, 256, 0, s>>>(n, doc_ptr, doc_len, comp_dst, comp_base, msgs, rec_status, comp_len);
     return hipGetLastError();
 }
 

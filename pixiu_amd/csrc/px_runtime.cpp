@@ -29,7 +29,9 @@ hipError_t launch_doc_write(hipStream_t, uint32_t, const uint8_t *, const uint64
 hipError_t launch_shard_init(hipStream_t, uint32_t, const ShardInit *);
 hipError_t launch_scatter_slots(hipStream_t, uint32_t, const SlotPut *);
 hipError_t launch_gst_encode(hipStream_t, const GstShard *, uint32_t, const uint32_t *, uint8_t *const *,
-                             uint32_t *, uint32_t *, uint32_t *, uint32_t *, ShardState *);
+                             const uint8_t *, uint32_t *, uint32_t *, uint32_t *, uint32_t *, ShardState *);
+hipError_t launch_gst_emit(hipStream_t, uint32_t, const uint8_t *const *, const uint32_t *, uint8_t *const *,
+                           const uint8_t *, const uint32_t *, uint32_t *, uint32_t *);
 hipError_t launch_compact(hipStream_t, uint32_t, uint8_t *const *, const uint32_t *, uint8_t *, const uint64_t *);
 hipError_t launch_tokenize(hipStream_t, uint32_t, const RecSlot *, uint32_t *, uint32_t *);
 hipError_t launch_count_esc(hipStream_t, uint32_t, uint8_t *const *, const uint32_t *, uint32_t *);
@@ -198,7 +200,7 @@ struct Shard {
 struct px_ctx {
     px_opts opts{};
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_mid = nullptr;
     DevHeap heap;
     std::vector<std::unique_ptr<Shard>> shards;
     std::vector<Chunk> chunks;
@@ -791,6 +793,8 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     for (uint32_t r = 0; r < n; ++r)
         if (doc_len[r] != 0xffffffffu) scratch_bytes += round_up(doc_len[r], 16);
     auto *comp_scratch = (uint8_t *)heap.alloc(scratch_bytes + 256);
+    // encoder messages: one u32 per doc byte, at 4x the record's comp scratch offset
+    auto *msgs = (uint32_t *)heap.alloc(scratch_bytes * 4 + 256);
     uint64_t so = 0;
     std::vector<GstShard> gs;
     gs.reserve(work.size());
@@ -828,11 +832,13 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     flush_shard_init();
     hcheck(launch_doc_write(stream, n, dkeys, dkoff, dvals, dvoff, d_dst));
 
-    // ---- the GST walk + encoder
+    // ---- the GST walk (encoder messages), then the stream encoder
     auto *d_stout = (ShardState *)stout_buf.get(gs.size() * sizeof(ShardState));
     hcheck(hipEventRecord(ev0, stream));
-    hcheck(launch_gst_encode(stream, d_gs, (uint32_t)gs.size(), d_doclen, d_cdst, d_complen, d_chunk, d_idx,
-                             d_status, d_stout));
+    hcheck(launch_gst_encode(stream, d_gs, (uint32_t)gs.size(), d_doclen, d_cdst, comp_scratch, msgs, d_chunk,
+                             d_idx, d_status, d_stout));
+    hcheck(hipEventRecord(ev_mid, stream));
+    hcheck(launch_gst_emit(stream, n, d_dst, d_doclen, d_cdst, comp_scratch, msgs, d_status, d_complen));
     hcheck(hipEventRecord(ev1, stream));
     hcheck(launch_count_esc(stream, n, d_cdst, d_complen, d_nesc));
     std::vector<uint32_t> comp_len(n), rchunk(n), ridx(n), rstatus(n), nesc(n);
@@ -849,6 +855,10 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         float ms = 0;
         hcheck(hipEventElapsedTime(&ms, ev0, ev1));
         stats.last_set_kernel_ms = ms;
+        hcheck(hipEventElapsedTime(&ms, ev0, ev_mid));
+        stats.last_walk_kernel_ms = ms;
+        hcheck(hipEventElapsedTime(&ms, ev_mid, ev1));
+        stats.last_emit_kernel_ms = ms;
     }
 
     // ---- packed store + segment index
@@ -888,6 +898,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     d2h(tstat.data(), d_status, n * 4);
     sync();
     heap.release(comp_scratch, scratch_bytes + 256);
+    heap.release(msgs, scratch_bytes * 4 + 256);
     heap.release(d_dst, (uint64_t)n * 8);
     heap.release(d_cdst, (uint64_t)n * 8);
     heap.release(d_gs, gs.size() * sizeof(GstShard));
@@ -1115,6 +1126,7 @@ px_ctx *px_open(const px_opts *opts) {
         hcheck(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         hcheck(hipEventCreate(&c->ev0));
         hcheck(hipEventCreate(&c->ev1));
+        hcheck(hipEventCreate(&c->ev_mid));
         return c;
     } catch (...) {
         return nullptr;
@@ -1126,6 +1138,7 @@ void px_close(px_ctx *ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->ev_mid) (void)hipEventDestroy(ctx->ev_mid);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
