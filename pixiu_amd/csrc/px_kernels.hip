@@ -71,6 +71,11 @@ PX_DEV uint64_t uni64(uint64_t v) {
 PX_DEV uint64_t ballot(bool p) { return __ballot(p); }
 PX_DEV uint32_t ffs64(uint64_t m) { return (uint32_t)__ffsll((unsigned long long)m) - 1u; }
 PX_DEV uint32_t readlane(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
+// a value the compiler must keep in a VGPR (it cannot prove it wave-uniform)
+PX_DEV uint32_t vreg(uint32_t x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
 PX_DEV uint32_t rd16(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
 
 // inclusive wave prefix sum on DPP row shifts and row broadcasts (no LDS round trips)
@@ -232,10 +237,13 @@ struct GstLds {
 
 struct GstWave {
     // shard arena
-    PX_GAS uint8_t *text;  // live chunk text base
-    PX_GAS uint32_t *doc_base;
-    PX_GAS u32x4 *nodes;   // 2 x uint4 per node: {link, cnt, e0.w0, e0.w1}, {e0.w2, e1.w0, e1.w1, e1.w2}
-    PX_GAS u32x4 *hash;
+    // The shard arena is reached through buffer resources: a wave-uniform byte offset
+    // rides in the instruction's scalar offset (one s_lshl per access instead of
+    // 64-bit address arithmetic) and the section offsets sit in VGPRs (vreg).
+    //   nodes: 2 x uint4 per node: {link, cnt, e0.w0, e0.w1}, {e0.w2, e1.w0, e1.w1, e1.w2}
+    __amdgpu_buffer_rsrc_t ar;  // shard arena: doc starts, nodes, child-map hash
+    __amdgpu_buffer_rsrc_t tr;  // live chunk text
+    uint32_t v_doc, v_nodes, v_hash, v_hash4, v_zero, v_lane, v_lane4;  // VGPRs
     uint32_t node_cap, hash_mask, doc_cap;
     PX_LAS GstLds *lds;
     // persistent counters
@@ -254,7 +262,35 @@ struct GstWave {
     uint64_t prof[P_N];
 #endif
 
-    PX_DEV uint32_t tbyte(uint32_t rel) const { return uni(text[rel]); }
+    PX_DEV uint32_t ldt(uint32_t vo, uint32_t rel) const {  // text byte at vo + rel
+        return __builtin_amdgcn_raw_buffer_load_b8(tr, (int)vo, (int)rel, 0);
+    }
+    PX_DEV uint32_t tbyte(uint32_t rel) const { return uni(ldt(v_zero, rel)); }
+    PX_DEV u32x4 nld(uint32_t n, uint32_t h) const {  // half h of node n's record
+        return __builtin_amdgcn_raw_buffer_load_b128(ar, (int)v_nodes, (int)(n * 32u + h * 16u), 0);
+    }
+    PX_DEV uint32_t nlink(uint32_t n) const {
+        return __builtin_amdgcn_raw_buffer_load_b32(ar, (int)v_nodes, (int)(n * 32u), 0);
+    }
+    PX_DEV void nst(uint32_t n, uint32_t h, u32x4 v) {
+        __builtin_amdgcn_raw_buffer_store_b128(v, ar, (int)v_nodes, (int)(n * 32u + h * 16u), 0);
+    }
+    PX_DEV void nstw(uint32_t n, uint32_t w, uint32_t v) {  // word w of node n's record
+        __builtin_amdgcn_raw_buffer_store_b32(v, ar, (int)v_nodes, (int)(n * 32u + w * 4u), 0);
+    }
+    PX_DEV u32x4 hld(uint32_t b) const {  // bucket b: lane l holds entry 4b + (l & 3)
+        return __builtin_amdgcn_raw_buffer_load_b128(ar, (int)v_hash4, (int)(b * 64u), 0);
+    }
+    PX_DEV void hst(uint32_t slot, u32x4 v) {
+        __builtin_amdgcn_raw_buffer_store_b128(v, ar, (int)v_hash, (int)(slot * 16u), 0);
+    }
+    PX_DEV uint32_t dld(uint32_t d) const {
+        return __builtin_amdgcn_raw_buffer_load_b32(ar, (int)v_doc, (int)(d * 4u), 0);
+    }
+    PX_DEV void dst(uint32_t d, uint32_t v) { __builtin_amdgcn_raw_buffer_store_b32(v, ar, (int)v_doc, (int)(d * 4u), 0); }
+    PX_DEV void set_text(PX_GAS uint8_t *p) {
+        tr = __builtin_amdgcn_make_buffer_rsrc((void *)p, 0, 0x7fffffff, 0x00020000);
+    }
 
     PX_DEV void fail(uint32_t code) {
         if (status == kOk) status = code;
@@ -276,10 +312,10 @@ struct GstWave {
 
     // ---- doc extents: LDS cache for the first kDocCache docs
     PX_DEV uint32_t docbase(uint32_t d) const {
-        return d <= kDocCache ? uni(lds->doc_base[d]) : uni(doc_base[d]);
+        return d <= kDocCache ? uni(lds->doc_base[d]) : uni(dld(d));
     }
     PX_DEV void set_docbase(uint32_t d, uint32_t v) {
-        doc_base[d] = v;
+        dst(d, v);
         if (d <= kDocCache) lds->doc_base[d] = v;
     }
     PX_DEV void set_act_doc(uint32_t d) {
@@ -292,7 +328,7 @@ struct GstWave {
     PX_DEV void load_window(uint32_t at) {
         uint32_t abs0 = (cur_base + at) & ~3u;  // 4-byte aligned window start
         wb = abs0 - cur_base;                    // may wrap below 0 (unsigned): range tests cope
-        win = *(const PX_GAS uint32_t *)(text + abs0 + 4 * lane_id());
+        win = __builtin_amdgcn_raw_buffer_load_b32(tr, (int)v_lane4, (int)abs0, 0);
     }
     PX_DEV uint32_t curchar(uint32_t p) {  // byte p of the current doc
         uint32_t d = p - wb;
@@ -310,7 +346,6 @@ struct GstWave {
         return (int32_t)tbyte(act_base + pos);
     }
 
-    PX_DEV PX_GAS uint32_t *nrec(uint32_t n) const { return (PX_GAS uint32_t *)&nodes[2 * n]; }
 
     // ---- child map
     PX_DEV static void unpack(uint32_t w0, uint32_t w1, uint32_t w2, Edge &e) {
@@ -339,8 +374,8 @@ struct GstWave {
         const uint32_t nb = (hash_mask >> 2);
         uint32_t b = hslot(n, c) & nb;
         // the node record and the first hash bucket, issued together
-        u32x4 r0 = nodes[2 * n], r1 = nodes[2 * n + 1];
-        u32x4 v = lane < kBucket ? hash[b * kBucket + lane] : mk4(0, 0, 0, 0);
+        u32x4 r0 = nld(n, 0), r1 = nld(n, 1);
+        u32x4 v = hld(b);
         ncnt = uni(r0.y);
         if (ncnt >= 1 && ((uni(r1.x) >> 16) & 0xffu) == c) {
             unpack(uni(r0.z), uni(r0.w), uni(r1.x), e);
@@ -379,7 +414,7 @@ struct GstWave {
                 return false;
             }
             b = (b + 1) & nb;
-            v = lane < kBucket ? hash[b * kBucket + lane] : mk4(0, 0, 0, 0);
+            v = hld(b);
         }
         fail(kErrCapacity);
         slot = kNone;
@@ -396,7 +431,7 @@ struct GstWave {
         uint32_t b = hslot(n, c) & nb;
         for (uint32_t guard = 0; guard <= nb; ++guard) {
             PX_CNT(P_PROBES, 1);
-            u32x4 v = lane < kBucket ? hash[b * kBucket + lane] : mk4(0, 0, 0, 0);
+            u32x4 v = hld(b);
             uint64_t me = ballot(lane < kBucket && (v.x >> 26) != epoch);
             if (me) return b * kBucket + ffs64(me);
             b = (b + 1) & nb;
@@ -409,13 +444,12 @@ struct GstWave {
             lds->root[slot & 0xffu] = mk4(0, pk0(e), pk1(e), pk2(e));
         } else if (slot & kInlineSlot) {
             uint32_t n = slot & kNodeMask;
-            PX_GAS uint32_t *rec = nrec(n);
-            uint32_t o = (slot >> 26) & 1u ? 5 : 2;  // e1 at words 5..7, e0 at words 2..4
-            rec[o] = pk0(e);
-            rec[o + 1] = pk1(e);
-            rec[o + 2] = pk2(e);
+            const uint32_t o = (slot >> 26) & 1u ? 5 : 2;  // e1 at words 5..7, e0 at words 2..4
+            typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+            __builtin_amdgcn_raw_buffer_store_b96(u32x3{pk0(e), pk1(e), pk2(e)}, ar, (int)v_nodes,
+                                                  (int)(n * 32u + o * 4u), 0);
         } else if (slot != kNone) {
-            hash[slot] = mk4(parent | (epoch << 26), pk0(e), pk1(e), pk2(e));
+            hst(slot, mk4(parent | (epoch << 26), pk0(e), pk1(e), pk2(e)));
         }
     }
     // add a child that is known to be absent (charges one map entry).  hint: the free
@@ -425,7 +459,7 @@ struct GstWave {
         uint32_t slot = pcnt < 2 ? (kInlineSlot | (pcnt << 26) | parent)
                                  : (hint != kNone ? hint : hash_free_slot(parent, kid.key()));
         write_entry(slot, parent, kid);
-        if (parent != kRoot && pcnt < 3) nrec(parent)[1] = pcnt + 1;
+        if (parent != kRoot && pcnt < 3) nstw(parent, 1, pcnt + 1);
     }
 
     // capacity: encode_doc checks once per doc that 2 * len more nodes fit (a doc adds
@@ -445,12 +479,13 @@ struct GstWave {
         pool_open = 0;
         for (uint32_t c = lane; c < 256; c += 64) lds->root[c] = mk4(0, kNone, 0, 0);
         if (++epoch > (uint32_t)kMaxEpoch) {  // epochs exhausted: really clear
-            for (uint32_t s = lane; s <= hash_mask; s += 64) hash[s] = mk4(0, 0, 0, 0);
+            for (uint32_t s = 0; s <= hash_mask; s += 64)
+                if (s + lane <= hash_mask) hst(s + lane, mk4(0, 0, 0, 0));
             epoch = 1;
         }
         wave_sync();
         charge_first(kNodeBlocks);  // the root (SuffixTree::init_prop)
-        nodes[2 * n_nodes++] = mk4(kRoot, 0, 0, 0);
+        nst(n_nodes++, 0, mk4(kRoot, 0, 0, 0));
     }
 
     // ---- encoder messages (the PXSMsg stream SuffixTree::setitem hands to
@@ -474,7 +509,7 @@ struct GstWave {
     PX_DEV bool new_leaf(Edge &leaf, uint32_t c) {
         uint32_t id;
         if (!new_node(id)) return false;
-        nodes[2 * id] = mk4(kRoot, 0, 0, 0);  // link, child count
+        nst(id, 0, mk4(kRoot, 0, 0, 0));  // link, child count
         leaf.set(id, 0, cur, i, cur_len, c);
         return true;
     }
@@ -551,7 +586,7 @@ struct GstWave {
             Edge in;
             uint32_t in_id;
             if (!new_node(in_id)) return false;
-            if (last_inner != kNone) nodes[2 * last_inner].x = in_id;
+            if (last_inner != kNone) nstw(last_inner, 0, in_id);
             last_inner = in_id;
             const uint32_t in_to = (e.from() + act_off) & 0xffffu;
             in.set(in_id, key_e != c ? 2 : 1, e.doc(), e.from(), in_to, e.key());
@@ -562,12 +597,12 @@ struct GstWave {
             charge(kEdgeBlocks);
             if (key_e != c) {
                 charge(kEdgeBlocks);
-                nodes[2 * in_id] = mk4(kRoot, 2, pk0(e), pk1(e));
-                nodes[2 * in_id + 1] = mk4(pk2(e), pk0(leaf), pk1(leaf), pk2(leaf));
+                nst(in_id, 0, mk4(kRoot, 2, pk0(e), pk1(e)));
+                nst(in_id, 1, mk4(pk2(e), pk0(leaf), pk1(leaf), pk2(leaf)));
                 e.slot = kInlineSlot | in_id;
             } else {
-                nodes[2 * in_id] = mk4(kRoot, 1, pk0(leaf), pk1(leaf));
-                nrec(in_id)[4] = pk2(leaf);
+                nst(in_id, 0, mk4(kRoot, 1, pk0(leaf), pk1(leaf)));
+                nstw(in_id, 4, pk2(leaf));
                 e.slot = kNone;  // e fell out of the tree (replaced under the same byte)
             }
 #ifdef PX_PROFILE
@@ -575,7 +610,7 @@ struct GstWave {
 #endif
         } else {
             PX_CNT(P_G_NOSPLIT, 1);
-            if (last_inner != kNone) nodes[2 * last_inner].x = e.id();
+            if (last_inner != kNone) nstw(last_inner, 0, e.id());
             last_inner = e.id();
             add_child(e.id(), e.cnt(), leaf, hint);
             if (e.cnt() < 3) {
@@ -600,9 +635,9 @@ struct GstWave {
             uint32_t w = min(64u, limit - m);
             uint32_t t = e.from() + act_off + m + lane;  // position in the active doc
             bool live = lane < w;
-            uint32_t a = live ? text[cur_base + i + m + lane] : 0;
+            uint32_t a = live ? ldt(v_lane, cur_base + i + m) : 0;
             bool oob = live && t >= act_len;
-            uint32_t b = (live && !oob) ? text[act_base + t] : 0x100u;
+            uint32_t b = (live && !oob) ? ldt(v_lane, act_base + e.from() + act_off + m) : 0x100u;
             uint64_t mism = ballot(live && (oob || a != b));
             uint64_t m251 = ballot(live && a == kEsc);
             uint32_t got = mism ? ffs64(mism) : w;
@@ -700,7 +735,7 @@ struct GstWave {
             int32_t e_next = -1;
             // the suffix link of act_node is loaded one iteration ahead (next to the
             // previous end check), so an iteration costs two dependent round trips
-            uint32_t lraw = act_node != kRoot ? nodes[2 * act_node].x : 0u;
+            uint32_t lraw = act_node != kRoot ? nlink(act_node) : 0u;
             while (remainder > 0 && status == kOk) {
                 PX_CNT(P_ITERS, 1);
 #ifdef PX_PROFILE
@@ -740,7 +775,7 @@ struct GstWave {
                 tg = __builtin_amdgcn_s_memtime();
 #endif
                 // next iteration's suffix link, issued before this end check's wait
-                lraw = act_node != kRoot ? nodes[2 * act_node].x : 0u;
+                lraw = act_node != kRoot ? nlink(act_node) : 0u;
                 PX_CNT(P_E_LOOK, e.from() + act_off == e.to() ? 1 : 0);
                 PX_CNT(P_E_OFF1, e.from() + act_off < e.to() && act_off == 1 ? 1 : 0);
                 PX_CNT(P_E_OFF2, e.from() + act_off < e.to() && act_off == 2 ? 1 : 0);
@@ -754,7 +789,7 @@ struct GstWave {
                         set_act_doc(n.doc());
                         act_direct = n.from();
                         act_off = 1;
-                        if (last_inner != kNone) nodes[2 * last_inner].x = act_node;
+                        if (last_inner != kNone) nstw(last_inner, 0, act_node);
                         break;
                     }
                 } else if (e.from() + act_off < e.to()) {
@@ -793,9 +828,17 @@ __global__ void __launch_bounds__(64 * kGstWaves, 6) k_gst_encode(const GstShard
     const GstShard sh = shards[s];
     ShardState st = *sh.st;
     GstWave g;
-    g.doc_base = (PX_GAS uint32_t *)sh.doc_base;
-    g.nodes = (PX_GAS u32x4 *)sh.nodes;
-    g.hash = (PX_GAS u32x4 *)sh.hash;
+    {
+        const uint8_t *arena = (const uint8_t *)sh.st;  // the arena starts with the shard state
+        g.ar = __builtin_amdgcn_make_buffer_rsrc((void *)arena, 0, 0x7fffffff, 0x00020000);
+        g.v_doc = vreg((uint32_t)((const uint8_t *)sh.doc_base - arena));
+        g.v_nodes = vreg((uint32_t)((const uint8_t *)sh.nodes - arena));
+        g.v_hash = vreg((uint32_t)((const uint8_t *)sh.hash - arena));
+        g.v_hash4 = g.v_hash + (lane & 3u) * 16u;
+        g.v_zero = vreg(0);
+        g.v_lane = lane;
+        g.v_lane4 = lane * 4u;
+    }
     g.node_cap = sh.node_cap;
     g.hash_mask = sh.hash_mask;
     g.doc_cap = sh.doc_cap;
@@ -810,7 +853,7 @@ __global__ void __launch_bounds__(64 * kGstWaves, 6) k_gst_encode(const GstShard
     g.pool_open = unii(st.pool_open);
     g.ctext_off = uni64(st.ctext_off);
     g.ub = 0;
-    g.text = (PX_GAS uint8_t *)sh.text + g.ctext_off;
+    g.set_text((PX_GAS uint8_t *)sh.text + g.ctext_off);
 #ifdef PX_PROFILE
     for (int k = 0; k < P_N; ++k) g.prof[k] = 0;
     uint64_t t_kernel0 = __builtin_amdgcn_s_memtime();
@@ -836,7 +879,7 @@ __global__ void __launch_bounds__(64 * kGstWaves, 6) k_gst_encode(const GstShard
         if (g.pools >= kRotatePools || g.n_docs == (uint32_t)kChunkSlots) {
             uint32_t shift = g.docbase(g.n_docs);
             g.ctext_off += shift;
-            g.text = (PX_GAS uint8_t *)sh.text + g.ctext_off;
+            g.set_text((PX_GAS uint8_t *)sh.text + g.ctext_off);
             g.n_docs = 0;
             g.set_docbase(0, 0);
             ++g.chunk_seq;
