@@ -244,6 +244,9 @@ struct GstWave {
     __amdgpu_buffer_rsrc_t ar;  // shard arena: doc starts, nodes, child-map hash
     __amdgpu_buffer_rsrc_t tr;  // live chunk text
     uint32_t v_doc, v_nodes, v_hash, v_hash4, v_zero, v_lane, v_lane4;  // VGPRs
+    // lookup candidates: the child count lane l's candidate needs (lane 0/1: inline
+    // child 0/1, lanes 4..7: bucket entries, others never) and whether it is inline
+    uint32_t v_need, v_inl;
     uint32_t node_cap, hash_mask, doc_cap;
     PX_LAS GstLds *lds;
     // persistent counters
@@ -372,32 +375,49 @@ struct GstWave {
         PX_CNT(P_LOOKUPS, 1);
         const uint32_t lane = lane_id();
         const uint32_t nb = (hash_mask >> 2);
-        uint32_t b = hslot(n, c) & nb;
+        // the bucket index is hashed on the vector unit (n forced into a VGPR), so the
+        // scalar unit, which the walk saturates, only sees the result's uses
+        const uint32_t vb = hslot(vreg(n), c) & nb;
         // the node record and the first hash bucket, issued together
         u32x4 r0 = nld(n, 0), r1 = nld(n, 1);
-        u32x4 v = hld(b);
+        u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(ar, (int)(v_hash4 + vb * 64u), 0, 0);
         ncnt = uni(r0.y);
-        if (ncnt >= 1 && ((uni(r1.x) >> 16) & 0xffu) == c) {
-            unpack(uni(r0.z), uni(r0.w), uni(r1.x), e);
-            e.slot = slot = kInlineSlot | n;
-            return true;
-        }
-        if (ncnt >= 2 && ((uni(r1.w) >> 16) & 0xffu) == c) {
-            unpack(uni(r1.y), uni(r1.z), uni(r1.w), e);
-            e.slot = slot = kInlineSlot | (1u << 26) | n;
-            return true;
+        const uint32_t want = n | (epoch << 26);
+        {
+            // one candidate per lane: lane 0 / 1 = inline child 0 / 1, lanes 4..7 = the
+            // bucket's entries 0..3; a single ballot finds the child keyed c
+            // (branch-free: every term is a per-lane vector value)
+            const bool in0 = lane == 0, in1 = lane == 1;
+            const uint32_t w0 = in0 ? r0.z : in1 ? r1.y : v.y;
+            const uint32_t w1 = in0 ? r0.w : in1 ? r1.z : v.z;
+            const uint32_t w2 = in0 ? r1.x : in1 ? r1.w : v.w;
+            const uint32_t ok = (uint32_t)(ncnt >= v_need) & ((uint32_t)(v.x == want) | v_inl) &
+                                (uint32_t)(((w2 >> 16) & 0xffu) == c);
+            const uint64_t mm = ballot(ok != 0);
+            if (mm) {
+                const uint32_t l = ffs64(mm);
+                unpack(readlane(w0, l), readlane(w1, l), readlane(w2, l), e);
+                e.slot = slot = l < 2 ? (kInlineSlot | (l << 26) | n) : uni(vb) * kBucket + (l - 4);
+                return true;
+            }
         }
         if (ncnt < 2) {
             slot = kInlineSlot | (ncnt << 26) | n;
             return false;
         }
-        if (ncnt == 2) {  // no hash entries yet: the first free entry of the bucket already read, if any
-            uint64_t me = ballot(lane < kBucket && (v.x >> 26) != epoch);
-            slot = me ? b * kBucket + ffs64(me) : kNone;
-            return false;
+        uint32_t b = uni(vb);
+        {
+            // the bucket's first free entry, if any (for ncnt == 2 there are no hash entries yet)
+            const uint64_t me = ballot(lane - 4u < 4u && (v.x >> 26) != epoch);
+            if (me || ncnt == 2) {
+                slot = me ? b * kBucket + (ffs64(me) - 4) : kNone;
+                return false;
+            }
         }
-        const uint32_t want = n | (epoch << 26);
-        for (uint32_t guard = 0; guard <= nb; ++guard) {
+        // the first bucket is full of other parents' entries: probe on
+        b = (b + 1) & nb;
+        v = hld(b);
+        for (uint32_t guard = 0; guard < nb; ++guard) {
             PX_CNT(P_PROBES, 1);
             bool valid = (v.x >> 26) == epoch;
             bool match = lane < kBucket && v.x == want && ((v.w >> 16) & 0xffu) == c;
@@ -838,6 +858,8 @@ __global__ void __launch_bounds__(64 * kGstWaves, 6) k_gst_encode(const GstShard
         g.v_zero = vreg(0);
         g.v_lane = lane;
         g.v_lane4 = lane * 4u;
+        g.v_need = lane == 0 ? 1u : lane == 1 ? 2u : lane - 4u < 4u ? 3u : 4u;
+        g.v_inl = lane < 2 ? 1u : 0u;
     }
     g.node_cap = sh.node_cap;
     g.hash_mask = sh.hash_mask;
