@@ -500,7 +500,8 @@ struct GstWave {
         for (uint32_t c = lane; c < 256; c += 64) lds->root[c] = mk4(0, kNone, 0, 0);
         if (++epoch > (uint32_t)kMaxEpoch) {  // epochs exhausted: really clear
             for (uint32_t s = 0; s <= hash_mask; s += 64)
-                if (s + lane <= hash_mask) hst(s + lane, mk4(0, 0, 0, 0));
+                if (s + lane <= hash_mask)
+                    __builtin_amdgcn_raw_buffer_store_b128(mk4(0, 0, 0, 0), ar, (int)(v_hash + lane * 16u), (int)(s * 16u), 0);
             epoch = 1;
         }
         wave_sync();
@@ -607,7 +608,7 @@ struct GstWave {
             uint32_t in_id;
             if (!new_node(in_id)) return false;
             if (last_inner != kNone) nstw(last_inner, 0, in_id);
-            last_inner = in_id;
+            last_inner = uni(in_id);
             const uint32_t in_to = (e.from() + act_off) & 0xffffu;
             in.set(in_id, key_e != c ? 2 : 1, e.doc(), e.from(), in_to, e.key());
             write_entry(e.slot, act_node, in);  // replaces e under its first byte: no charge
@@ -631,7 +632,7 @@ struct GstWave {
         } else {
             PX_CNT(P_G_NOSPLIT, 1);
             if (last_inner != kNone) nstw(last_inner, 0, e.id());
-            last_inner = e.id();
+            last_inner = uni(e.id());
             add_child(e.id(), e.cnt(), leaf, hint);
             if (e.cnt() < 3) {
                 e.w0 += 1u << 26;
