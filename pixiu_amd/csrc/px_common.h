@@ -81,6 +81,23 @@ struct alignas(16) SegEnt {
 };
 static_assert(sizeof(SegEnt) == 32, "SegEnt is two 16-byte vectors");
 
+// lane-walk entry (k_decode's lanes), parallel to SegEnt k of the same record: one
+// 16-byte load per step.  Only records whose source coordinates fit 16 bits (every
+// record the encoder produces) have them; the serial path and the position lookups
+// keep using SegEnt.
+//   xe  = x | ex << 16
+//   kz  = comp offset | kind << 30 (as SegEnt)
+//   aux = record token: idx | from << 16
+//   rel = plain: (the record's comp base - this entry's address) / 8 (same allocation);
+//         record token: (target entry - this entry) / 16, kRelNone when unlinked or
+//         too far away (the token then goes to the serial path)
+struct alignas(16) LaneEnt {
+    uint32_t xe, kz, aux;
+    int32_t rel;
+};
+static_assert(sizeof(LaneEnt) == 16, "LaneEnt is one 16-byte vector");
+constexpr int32_t kRelNone = (int32_t)0x80000000;
+
 // compressed-record slot: what a chunk table entry points at
 struct alignas(16) RecSlot {
     const uint8_t *comp;    // compressed bytes
@@ -90,7 +107,7 @@ struct alignas(16) RecSlot {
     uint32_t nseg;
     uint32_t pidx_n;        // blocks in pidx (0: no position index, serial decode only)
     uint32_t pad;
-    uint64_t pad2;          // 48 bytes: three 16-byte loads on the device
+    const LaneEnt *lane;    // lane-walk entries (null: serial decode only); 48 bytes in all
 };
 static_assert(sizeof(RecSlot) == 48, "RecSlot is loaded as three 16-byte vectors");
 
@@ -110,6 +127,7 @@ struct SlotPut {
 // k_link work item: one record whose record tokens get their target entries
 struct LinkJob {
     SegEnt *seg;
+    LaneEnt *lane;         // the record's lane entries (null: none)
     const RecSlot *slots;  // the record's chunk table
     uint32_t nseg, nrec;
 };

@@ -1138,6 +1138,7 @@ __global__ void __launch_bounds__(256) k_tokenize(uint32_t n, const RecSlot *slo
         const uint32_t len = sl.comp_len;
         PX_GAS SegEnt *seg = (PX_GAS SegEnt *)sl.seg;
         PX_GAS uint16_t *pidx = (PX_GAS uint16_t *)sl.pidx;
+        PX_GAS LaneEnt *lanes = (PX_GAS LaneEnt *)sl.lane;
         const uint32_t pidx_n = sl.pidx_n;
         uint32_t ns = 0, p = 0, wb = 0, err = 0, plain_start = 0;
         int32_t src = 0, plain_src = 0;
@@ -1147,8 +1148,15 @@ __global__ void __launch_bounds__(256) k_tokenize(uint32_t n, const RecSlot *slo
         auto emit = [&](int32_t x, uint32_t z, uint32_t w) {
             if (have) {
                 uint64_t ptr = (pend_z >> 30) == 0 ? comp_addr + (pend_z & kSegMask) : 0;
-                if (lane == 0) put_ent(seg, ns, mk4(pend_x, (uint32_t)x, pend_z, pend_w), ptr);
-                if (x < (int32_t)pend_x) {
+                if (lane == 0) {
+                    put_ent(seg, ns, mk4(pend_x, (uint32_t)x, pend_z, pend_w), ptr);
+                    if (lanes) {
+                        const int64_t d = (int64_t)comp_addr - (int64_t)(uint64_t)(lanes + ns);
+                        const int32_t rel = (pend_z >> 30) == 0 ? (int32_t)(d >> 3) : kRelNone;
+                        *(PX_GAS u32x4 *)(lanes + ns) = mk4(pend_x | (uint32_t)x << 16, pend_z, pend_w, (uint32_t)rel);
+                    }
+                }
+                if (x < (int32_t)pend_x || x > 0xffff) {  // lane entries need 16-bit coordinates
                     mono = false;
                 } else if (mono && pidx_n) {
                     uint32_t b0 = (pend_x + 15) >> 4, b1 = min(((uint32_t)x + 15) >> 4, pidx_n);
@@ -1218,7 +1226,10 @@ __global__ void __launch_bounds__(256) k_tokenize(uint32_t n, const RecSlot *slo
         if (!err) {
             if (plain_open && plain_start < len) emit(plain_src, plain_start, 0);
             emit(src, len | kSegEnd, 0);  // closes the last segment; the sentinel stays pending
-            if (lane == 0) put_ent(seg, ns, mk4((uint32_t)src, (uint32_t)src, len | kSegEnd, 0), 0);
+            if (lane == 0) {
+                put_ent(seg, ns, mk4((uint32_t)src, (uint32_t)src, len | kSegEnd, 0), 0);
+                if (lanes) *(PX_GAS u32x4 *)(lanes + ns) = mk4((uint32_t)src | (uint32_t)src << 16, len | kSegEnd, 0, 0);
+            }
             // blocks past the source end: no segment
             if (mono && pidx_n)
                 for (uint32_t k = ((uint32_t)max(src, 0) + 15) / 16 + lane; k < pidx_n; k += 64)
@@ -1255,6 +1266,7 @@ struct SlotV {
     const PX_GAS uint8_t *comp;
     const PX_GAS u32x4 *seg;  // entry k: seg[2k] = {x, ex, kz, aux}, seg[2k + 1] = {ptr lo, ptr hi, 0, 0}
     const PX_GAS uint16_t *pidx;
+    const PX_GAS u32x4 *lane;  // LaneEnt k = lane[k] (null: serial decode only)
     uint32_t nseg, pidx_n;
 };
 
@@ -1264,6 +1276,7 @@ PX_DEV SlotV slot_at(const PX_GAS RecSlot *slots, uint32_t r) {
     v.comp = (const PX_GAS uint8_t *)s.comp;
     v.seg = (const PX_GAS u32x4 *)s.seg;
     v.pidx = (const PX_GAS uint16_t *)s.pidx;
+    v.lane = (const PX_GAS u32x4 *)s.lane;
     v.nseg = s.nseg;
     v.pidx_n = s.pidx_n;
     return v;
@@ -1273,6 +1286,7 @@ PX_DEV SlotV slot_uniform(const PX_GAS RecSlot *slots, uint32_t r) {
     v.comp = (const PX_GAS uint8_t *)uni64((uint64_t)v.comp);
     v.seg = (const PX_GAS u32x4 *)uni64((uint64_t)v.seg);
     v.pidx = (const PX_GAS uint16_t *)uni64((uint64_t)v.pidx);
+    v.lane = (const PX_GAS u32x4 *)uni64((uint64_t)v.lane);
     v.nseg = uni(v.nseg);
     v.pidx_n = uni(v.pidx_n);
     return v;
@@ -1286,21 +1300,28 @@ __global__ void __launch_bounds__(256) k_link(uint32_t n, const LinkJob *jobs) {
     for (uint32_t j = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); j < n; j += waves) {
         const LinkJob job = jobs[j];
         PX_GAS u32x4 *seg = (PX_GAS u32x4 *)job.seg;
+        PX_GAS u32x4 *lanes = (PX_GAS u32x4 *)job.lane;
         const PX_GAS RecSlot *slots = (const PX_GAS RecSlot *)job.slots;
         for (uint32_t k = lane; k < job.nseg; k += 64) {
             const u32x4 e = seg[2 * k];
             if ((e.z >> 30) != 2) continue;
             const uint32_t ridx = e.w & 0xffffu, rfrom = e.w >> 16;
             uint64_t ptr = 0;
+            int32_t rel = kRelNone;
             if (ridx < job.nrec) {
                 const SlotV t = slot_at(slots, ridx);
                 if (t.pidx_n && (rfrom >> 4) < t.pidx_n) {
                     uint32_t k2 = min((uint32_t)t.pidx[rfrom >> 4], t.nseg);
                     while (k2 < t.nseg && t.seg[2 * k2].y <= rfrom) ++k2;
                     ptr = (uint64_t)(t.seg + 2 * k2);
+                    if (lanes && t.lane) {
+                        const int64_t d = ((int64_t)(uint64_t)(t.lane + k2) - (int64_t)(uint64_t)(lanes + k)) / 16;
+                        if (d > INT32_MIN && d <= INT32_MAX) rel = (int32_t)d;
+                    }
                 }
             }
             seg[2 * k + 1] = mk4((uint32_t)ptr, (uint32_t)(ptr >> 32), 0, 0);
+            if (lanes) lanes[k].w = (uint32_t)rel;
         }
     }
 }
@@ -1531,6 +1552,7 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
         // later ones are abandoned and redone.  Returns true when the segment at
         // f.seg must go through the serial path next.
         auto window = [&](Frame &f, const SlotV &sv) -> bool {
+            if (!sv.lane) return true;  // no lane entries: the serial path takes every segment
             const uint32_t outp0 = outp;
             const int32_t ret0 = f.ret;
             uint32_t next = f.seg;     // next unassigned segment
@@ -1540,14 +1562,11 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
             // stop key = 2 * (first segment not committed) + (0: it goes serial, 1: it does not)
             uint32_t stop_key = 0xffffffffu, stop_out = 0;
             int32_t stop_ret = 0;
-            // prefetched entries of segments [next, next + 64): lane l holds next + l
-            u32x4 PE = mk4(0, 0, 0, 0), PEH = mk4(0, 0, 0, 0);
+            // prefetched lane entries of segments [next, next + 64): lane l holds next + l
+            u32x4 PE = mk4(0, 0, 0, 0);
             {
                 const uint32_t kk = next + lane;
-                if (kk < end) {
-                    PE = sv.seg[2 * kk];
-                    PEH = sv.seg[2 * kk + 1];
-                }
+                if (kk < end) PE = sv.lane[kk];
             }
             // per-lane segment state
             uint32_t k = kNone, base = 0, w = 0, wmax = 0;
@@ -1559,8 +1578,8 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
             uint32_t lane_it = 0;
 #endif
             // walk state
-            const PX_GAS u32x4 *e = nullptr;
-            u32x4 F = mk4(0, 0, 0, 0), FH = mk4(0, 0, 0, 0);
+            const PX_GAS u32x4 *e = nullptr;  // the lane entry F was loaded from
+            u32x4 F = mk4(0, 0, 0, 0);
             uint32_t rec = 0, d = 0;
             int32_t from = 0, len = 0, ret = 0;
             PX_CNT(P_D_BATCH, 1);
@@ -1582,11 +1601,10 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                     const int src_l = (int)(rank & 63u);
                     const u32x4 E = mk4(__shfl(PE.x, src_l), __shfl(PE.y, src_l), __shfl(PE.z, src_l),
                                         __shfl(PE.w, src_l));
-                    const uint32_t ehx = __shfl(PEH.x, src_l), ehy = __shfl(PEH.y, src_l);
-                    const int32_t sx = (int32_t)E.x, ex = (int32_t)E.y;
-                    const uint32_t kind = E.z >> 30, cs = E.z & kSegMask;
-                    const uint32_t ridx = E.w & 0xffffu;
-                    const int32_t rfrom = (int32_t)(E.w >> 16), supply = ex - sx, rto = rfrom + supply;
+                    const int32_t sx = (int32_t)(E.x & 0xffffu), ex = (int32_t)(E.x >> 16);
+                    const uint32_t kind = E.y >> 30, cs = E.y & kSegMask;
+                    const uint32_t ridx = E.z & 0xffffu;
+                    const int32_t rfrom = (int32_t)(E.z >> 16), supply = ex - sx, rto = rfrom + supply;
                     const int32_t p0 = max(sx, f.from);
                     const int32_t sub_from = rfrom + max(0, f.from - sx);
                     const bool enter = kind == 2 && sx - 1 + supply >= f.from;
@@ -1660,7 +1678,7 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                         k = kNone;  // done (a plain or empty segment is never short)
                     }
                     if (active && !fl && child) {
-                        e = (const PX_GAS u32x4 *)((uint64_t)ehx | (uint64_t)ehy << 32);
+                        e = (int32_t)E.w == kRelNone ? nullptr : sv.lane + (next - na + rank) + (int32_t)E.w;
                         if (!e) {
                             PX_FR(3);
                             flag = true;  // token without a linked target
@@ -1678,10 +1696,7 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                     // refill the prefetch buffer from the new `next`
                     {
                         const uint32_t kk = next + lane;
-                        if (kk < end) {
-                            PE = sv.seg[2 * kk];
-                            PEH = sv.seg[2 * kk + 1];
-                        }
+                        if (kk < end) PE = sv.lane[kk];
                     }
 #ifdef PX_PROFILE
                     prof[P_D_T_ASSIGN] += __builtin_amdgcn_s_memtime() - t_as0;
@@ -1696,12 +1711,15 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                     lane_it += 1;
 #endif
                     if (busy) {
-                        const int32_t x = (int32_t)F.x, y = (int32_t)F.y;
-                        const uint32_t kd = F.z >> 30;
-                        const PX_GAS u32x4 *ne = fresh ? e : e + 2;
+                        const int32_t x = (int32_t)(F.x & 0xffffu), y = (int32_t)(F.x >> 16);
+                        const uint32_t kd = F.y >> 30;
+                        const PX_GAS u32x4 *ne = fresh ? e : e + 1;
                         uint32_t nb = 0, poff = 0;
                         bool ov = false;
-                        const PX_GAS uint8_t *seg0 = (const PX_GAS uint8_t *)((uint64_t)FH.x | (uint64_t)FH.y << 32);
+                        // a plain entry's first comp byte: the record's comp base (rel, in 8-byte
+                        // units from the entry) + the segment's comp offset
+                        const PX_GAS uint8_t *seg0 =
+                            (const PX_GAS uint8_t *)e + (int64_t)(int32_t)F.w * 8 + (F.y & kSegMask);
                         if (pmode) {
                             seg0 = psrc;
                             nb = min(wmax - w, 64u);
@@ -1745,13 +1763,13 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                         } else if (kd == 2) {
                             const int32_t sup = y - x;
                             if (x - 1 + sup >= from) {
-                                const uint32_t ri = F.w & 0xffffu;
-                                const int32_t rf = (int32_t)(F.w >> 16), rt = rf + sup;
+                                const uint32_t ri = F.z & 0xffffu;
+                                const int32_t rf = (int32_t)(F.z >> 16), rt = rf + sup;
                                 const int32_t sf = rf + max(0, from - x);
                                 const int32_t st = min(rt, sf + (len - ret));
                                 const int32_t stp = compat ? ret : max(x, from);
-                                const PX_GAS u32x4 *t = (const PX_GAS u32x4 *)((uint64_t)FH.x | (uint64_t)FH.y << 32);
-                                const uint64_t nx = (uint64_t)(e + 2);
+                                const PX_GAS u32x4 *t = (int32_t)F.w == kRelNone ? nullptr : e + (int32_t)F.w;
+                                const uint64_t nx = (uint64_t)(e + 1);
                                 if (!t || ri >= nrec || (ri == rec && sf < stp && stp < st) || d + 1 >= kLaneDepth ||
                                     (uint32_t)from > 0xffffu || (uint32_t)len > 0xffffu || (nx >> 48) != 0) {
                                     PX_FR(!t ? 3 : ri >= nrec ? 8 : (ri == rec && sf < stp && stp < st) ? 5 : d + 1 >= kLaneDepth ? 6 : 7);
@@ -1773,11 +1791,8 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                         }
                         // next entry first (every entry a lane can reach is in bounds: a
                         // record's entries end with a sentinel, which pops)
-                        u32x4 NF = F, NFH = FH;
-                        if (busy && !pmode) {
-                            NF = ne[0];
-                            NFH = ne[1];
-                        }
+                        u32x4 NF = F;
+                        if (busy && !pmode) NF = ne[0];
                         if (nb) {
                             const PX_GAS uint8_t *cp = seg0 + poff;
                             const uint32_t last = ov ? cp[nb - 1] : 0u;
@@ -1798,7 +1813,6 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                             }
                         }
                         F = NF;
-                        FH = NFH;
                         e = ne;
                     }
                 }

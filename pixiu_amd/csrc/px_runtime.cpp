@@ -66,7 +66,10 @@ constexpr uint32_t kNoPidxBit = 1u << 31;  // k_tokenize: record has no position
 inline uint64_t seg_entries(uint32_t esc) { return 2ull * esc + 2; }
 inline void set_nseg(RecSlot &s, uint32_t tok) {
     s.nseg = tok & ~kNoPidxBit;
-    if (tok & kNoPidxBit) s.pidx_n = 0;
+    if (tok & kNoPidxBit) {
+        s.pidx_n = 0;
+        s.lane = nullptr;  // lane entries need monotone 16-bit source coordinates
+    }
 }
 inline uint64_t pow2_at_least(uint64_t v) {
     uint64_t p = 1024;
@@ -866,12 +869,17 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     for (uint32_t r = 0; r < n; ++r) {
         bool ok = doc_len[r] != 0xffffffffu && rstatus[r] == kOk;
         coff[r + 1] = coff[r] + (ok ? round_up(comp_len[r], 8) : 0);
-        soff[r + 1] = soff[r] + (ok ? seg_entries(nesc[r]) * sizeof(SegEnt) : 0);
+        // a failed record still gets one entry: k_tokenize writes its end sentinel
+        soff[r + 1] = soff[r] + (ok ? seg_entries(nesc[r]) : 1) * sizeof(SegEnt);
         poff[r + 1] = poff[r] + (ok ? round_up(pidx_blocks(doc_len[r]) * 2, 16) : 0);
     }
-    auto *store = (uint8_t *)heap.alloc(coff[n] + 64);
+    // compressed bytes and the lane entries share one allocation: a plain lane entry
+    // reaches its record's bytes by a 32-bit relative offset (LaneEnt::rel)
+    const uint64_t lane_at = round_up(coff[n] + 64, 16);
+    const uint64_t store_bytes = lane_at + soff[n] / 2 + 64;  // LaneEnt is half a SegEnt
+    auto *store = (uint8_t *)heap.alloc(store_bytes);
     auto *segs = (uint8_t *)heap.alloc(soff[n] + poff[n] + 64);
-    store_blocks.emplace_back(store, coff[n] + 64);
+    store_blocks.emplace_back(store, store_bytes);
     last_store = store;
     last_store_bytes = coff[n];
     store_blocks.emplace_back(segs, soff[n] + poff[n] + 64);
@@ -888,6 +896,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         slots[r].nseg = 0;
         slots[r].pidx_n = ok ? pidx_blocks(doc_len[r]) : 0;
         slots[r].pad = 0;
+        slots[r].lane = (const LaneEnt *)(store + lane_at + soff[r] / 2);
     }
     auto *d_slots = (RecSlot *)heap.alloc((uint64_t)n * sizeof(RecSlot));
     h2d(d_slots, slots.data(), (size_t)n * sizeof(RecSlot));
@@ -960,7 +969,8 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         for (uint32_t r = 0; r < n; ++r) {
             if (rgchunk[r] == kNone) continue;
             const Chunk &ch = chunks[rgchunk[r]];
-            jobs.push_back(LinkJob{const_cast<SegEnt *>(slots[r].seg), ch.dev, slots[r].nseg, ch.n});
+            jobs.push_back(LinkJob{const_cast<SegEnt *>(slots[r].seg), const_cast<LaneEnt *>(slots[r].lane), ch.dev,
+                                   slots[r].nseg, ch.n});
         }
         link(jobs);
     }
@@ -1339,16 +1349,20 @@ int px_import_chunk(px_ctx *ctx, uint32_t n, const uint8_t *comp, const uint64_t
             coff[r + 1] = coff[r] + round_up(l, 8);
             soff[r + 1] = soff[r] + nents[r] * sizeof(SegEnt) + round_up((uint64_t)pn * 2, 16);
         }
-        auto *store = (uint8_t *)ctx->heap.alloc(coff[n] + 64);
+        std::vector<uint64_t> loff(n + 1, 0);
+        for (uint32_t r = 0; r < n; ++r) loff[r + 1] = loff[r] + nents[r] * sizeof(LaneEnt);
+        const uint64_t lane_at = round_up(coff[n] + 64, 16), store_bytes = lane_at + loff[n] + 64;
+        auto *store = (uint8_t *)ctx->heap.alloc(store_bytes);
         auto *segs = (uint8_t *)ctx->heap.alloc(soff[n] + 64);
-        ctx->store_blocks.emplace_back(store, coff[n] + 64);
+        ctx->store_blocks.emplace_back(store, store_bytes);
         ctx->store_blocks.emplace_back(segs, soff[n] + 64);
         std::vector<RecSlot> slots(n);
         for (uint32_t r = 0; r < n; ++r) {
             uint64_t l = off[r + 1] - off[r];
             ctx->h2d(store + coff[r], comp + off[r], l);
             slots[r] = RecSlot{store + coff[r], (const SegEnt *)(segs + soff[r]),
-                               (const uint16_t *)(segs + soff[r] + nents[r] * sizeof(SegEnt)), (uint32_t)l, 0, pn, 0, 0};
+                               (const uint16_t *)(segs + soff[r] + nents[r] * sizeof(SegEnt)), (uint32_t)l, 0, pn, 0,
+                               (const LaneEnt *)(store + lane_at + loff[r])};
         }
         auto *d_slots = (RecSlot *)ctx->heap.alloc((uint64_t)n * sizeof(RecSlot));
         auto *d_tmp = (uint32_t *)ctx->heap.alloc((uint64_t)n * 8);
@@ -1383,7 +1397,8 @@ int px_import_chunk(px_ctx *ctx, uint32_t n, const uint8_t *comp, const uint64_t
         ctx->h2d(ctx->chunks[c].dev, ctx->chunks[c].slots.data(), (size_t)n * sizeof(RecSlot));
         std::vector<LinkJob> jobs(n);
         for (uint32_t r = 0; r < n; ++r)
-            jobs[r] = LinkJob{const_cast<SegEnt *>(ctx->chunks[c].slots[r].seg), ctx->chunks[c].dev,
+            jobs[r] = LinkJob{const_cast<SegEnt *>(ctx->chunks[c].slots[r].seg),
+                              const_cast<LaneEnt *>(ctx->chunks[c].slots[r].lane), ctx->chunks[c].dev,
                               ctx->chunks[c].slots[r].nseg, n};
         ctx->link(jobs);
         ctx->sync();
