@@ -853,6 +853,21 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     std::vector<ShardState> stout(gs.size());
     d2h(stout.data(), d_stout, gs.size() * sizeof(ShardState));
     sync();
+    // Invariant: a walked record has a non-empty compressed form (a doc is >= 3 bytes).
+    // A violation was seen once in the GPU suite and never reproduced (4,969-batch
+    // stress, tools/fuzz_stress.py); re-read the record's length and status, say so
+    // on stderr, and fail the record rather than store it empty.
+    for (uint32_t r = 0; r < n; ++r) {
+        if (doc_len[r] == 0xffffffffu || rstatus[r] != kOk || comp_len[r] != 0) continue;
+        uint32_t cl = 0, rs = 0;
+        d2h(&cl, d_complen + r, 4);
+        d2h(&rs, d_status + r, 4);
+        sync();
+        fprintf(stderr, "pixiu_amd: record %u of a %u-record batch: status 0 with comp_len 0 (doc %u B); "
+                        "re-read comp_len %u status %u\n", r, n, doc_len[r], cl, rs);
+        comp_len[r] = cl;
+        rstatus[r] = rs != kOk ? rs : (cl ? (uint32_t)kOk : (uint32_t)kErrCapacity);
+    }
     for (size_t k = 0; k < work.size(); ++k) work[k].s->hs = stout[k];
     {
         float ms = 0;
