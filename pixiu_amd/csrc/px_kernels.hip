@@ -266,31 +266,33 @@ struct GstWave {
 #endif
 
     PX_DEV uint32_t ldt(uint32_t vo, uint32_t rel) const {  // text byte at vo + rel
-        return __builtin_amdgcn_raw_buffer_load_b8(tr, (int)vo, (int)rel, 0);
+        return __builtin_amdgcn_raw_buffer_load_b8(tr, (int)(vo + rel), 0, 0);
     }
     PX_DEV uint32_t tbyte(uint32_t rel) const { return uni(ldt(v_zero, rel)); }
+    // offsets are formed on the vector unit (v_lshl_add into the voffset operand): the
+    // scalar unit, which the walk saturates, only supplies the node id
     PX_DEV u32x4 nld(uint32_t n, uint32_t h) const {  // half h of node n's record
-        return __builtin_amdgcn_raw_buffer_load_b128(ar, (int)v_nodes, (int)(n * 32u + h * 16u), 0);
+        return __builtin_amdgcn_raw_buffer_load_b128(ar, (int)(v_nodes + n * 32u + h * 16u), 0, 0);
     }
     PX_DEV uint32_t nlink(uint32_t n) const {
-        return __builtin_amdgcn_raw_buffer_load_b32(ar, (int)v_nodes, (int)(n * 32u), 0);
+        return __builtin_amdgcn_raw_buffer_load_b32(ar, (int)(v_nodes + n * 32u), 0, 0);
     }
     PX_DEV void nst(uint32_t n, uint32_t h, u32x4 v) {
-        __builtin_amdgcn_raw_buffer_store_b128(v, ar, (int)v_nodes, (int)(n * 32u + h * 16u), 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, ar, (int)(v_nodes + n * 32u + h * 16u), 0, 0);
     }
     PX_DEV void nstw(uint32_t n, uint32_t w, uint32_t v) {  // word w of node n's record
-        __builtin_amdgcn_raw_buffer_store_b32(v, ar, (int)v_nodes, (int)(n * 32u + w * 4u), 0);
+        __builtin_amdgcn_raw_buffer_store_b32(v, ar, (int)(v_nodes + n * 32u + w * 4u), 0, 0);
     }
     PX_DEV u32x4 hld(uint32_t b) const {  // bucket b: lane l holds entry 4b + (l & 3)
-        return __builtin_amdgcn_raw_buffer_load_b128(ar, (int)v_hash4, (int)(b * 64u), 0);
+        return __builtin_amdgcn_raw_buffer_load_b128(ar, (int)(v_hash4 + b * 64u), 0, 0);
     }
     PX_DEV void hst(uint32_t slot, u32x4 v) {
-        __builtin_amdgcn_raw_buffer_store_b128(v, ar, (int)v_hash, (int)(slot * 16u), 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, ar, (int)(v_hash + slot * 16u), 0, 0);
     }
     PX_DEV uint32_t dld(uint32_t d) const {
-        return __builtin_amdgcn_raw_buffer_load_b32(ar, (int)v_doc, (int)(d * 4u), 0);
+        return __builtin_amdgcn_raw_buffer_load_b32(ar, (int)(v_doc + d * 4u), 0, 0);
     }
-    PX_DEV void dst(uint32_t d, uint32_t v) { __builtin_amdgcn_raw_buffer_store_b32(v, ar, (int)v_doc, (int)(d * 4u), 0); }
+    PX_DEV void dst(uint32_t d, uint32_t v) { __builtin_amdgcn_raw_buffer_store_b32(v, ar, (int)(v_doc + d * 4u), 0, 0); }
     PX_DEV void set_text(PX_GAS uint8_t *p) {
         tr = __builtin_amdgcn_make_buffer_rsrc((void *)p, 0, 0x7fffffff, 0x00020000);
     }
