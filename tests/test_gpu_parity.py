@@ -193,3 +193,33 @@ def test_device_resident_inputs(oracle):
         vals = [cp.val(i) for i in range(cp.n)]
         for s in (0, 3):
             assert _check_shard(st, res, keys, vals, oracle, [s, s + 1, s + 2]) == "eq"
+
+
+def _edge_docs(rng):
+    """Records whose encoder runs end on, just before and just after the 64-message
+    steps of k_gst_emit (the open-run carry), runs of exactly 6/7/255/256 bytes (the
+    literal / small / big token limits) and 251 pairs split across a step boundary."""
+    base = bytes(rng.choice(b"abcdefghijklmnopqrstuvwxyz") for _ in range(3000))
+    keys, vals = [b"base"], [base]
+    # copies of base slices: the key plus the 2-byte separator shifts them by len(key)+2
+    for n, (lo, ln) in enumerate([(0, 6), (0, 7), (10, 255), (10, 256), (5, 57), (5, 58), (5, 59),
+                                  (100, 121), (100, 122), (100, 123), (7, 1000), (200, 2047)]):
+        keys.append(b"c%02d" % n)
+        vals.append(base[lo:lo + ln] + b"#" + base[lo + 1:lo + ln] + b"!")
+    # 251 pairs (escaped 251 = 251,251) straddling positions 63/64 and 127/128
+    for n, at in enumerate([57, 58, 59, 60, 121, 122, 123]):
+        v = bytearray(base[:400])
+        v[at] = 251
+        v[at + 1] = 251
+        keys.append(b"e%02d" % n)
+        vals.append(bytes(v))
+        keys.append(b"f%02d" % n)
+        vals.append(bytes(v[:at + 1]) + b"\xfb" + base[500:700])
+    return keys, vals
+
+
+def test_encoder_step_boundaries(oracle):
+    keys, vals = _edge_docs(random.Random(64))
+    with _store(records_per_shard=0) as st:
+        res = st.set_batch(keys, vals)
+        assert _check_shard(st, res, keys, vals, oracle, list(range(len(keys)))) == "eq"
