@@ -1339,7 +1339,7 @@ __global__ void __launch_bounds__(256) k_link(uint32_t n, const LinkJob *jobs) {
 // exceed what it asked for, an unlinked token) ends the batch; that one segment
 // then goes through the serial frame machine (a stack of Frames in scratch memory),
 // which is the reference's generator nesting restated.
-constexpr uint32_t kLaneDepth = 8;
+constexpr uint32_t kLaneDepth = 10;  // 10 KB of LDS per wave: 4 blocks (16 waves) per CU
 constexpr uint32_t kLaneCopyMax = 512;  // plain pieces up to this size are copied by one lane
 constexpr uint32_t kAssignMin = 24;      // idle lanes that trigger an assignment round
 
