@@ -613,7 +613,9 @@ struct px_ctx {
         st.assign(nq, 0);
         if (!nq) return;
         uint32_t depth = opts.decode_depth ? opts.decode_depth : 4096;
-        uint32_t waves = opts.decode_waves ? opts.decode_waves : 8192;
+        // auto: one wave per query up to 16,384 (measured on config 3: 10k queries take
+        // 6.27 ms on 8,192 waves, 5.96 ms on one wave each)
+        uint32_t waves = opts.decode_waves ? opts.decode_waves : 16384;
         waves = std::min(waves, nq);
         auto *frames = (Frame *)scratch_frames.get((uint64_t)waves * depth * sizeof(Frame));
         auto *dq = (DecodeQuery *)dq_buf.get((uint64_t)nq * sizeof(DecodeQuery));
