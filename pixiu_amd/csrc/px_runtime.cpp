@@ -142,6 +142,46 @@ struct DevBuf {
     }
 };
 
+// pinned host staging buffer (grown on demand): small per-batch transfers without the
+// runtime's pageable-copy path
+struct HostBuf {
+    void *p = nullptr;
+    uint64_t cap = 0;
+    void *get(uint64_t n) {
+        if (n > cap) {
+            if (p) (void)hipHostFree(p);
+            cap = std::max<uint64_t>(round_up(n, 1 << 16), cap * 2);
+            p = nullptr;
+            if (hipHostMalloc(&p, cap, hipHostMallocDefault) != hipSuccess) {
+                cap = 0;
+                throw PxFail{PX_ENOMEM};
+            }
+        }
+        return p;
+    }
+    ~HostBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+};
+
+// fn(lo, hi) over [0, n) on up to `threads` host threads (inline for small n)
+template <class F>
+void parallel_ranges(uint32_t n, uint32_t threads, F fn) {
+    if (threads <= 1 || n < 4096) {
+        fn(0u, n);
+        return;
+    }
+    threads = std::min<uint32_t>(threads, n / 1024);
+    std::vector<std::thread> pool;
+    const uint32_t per = (n + threads - 1) / threads;
+    for (uint32_t t = 1; t < threads; ++t) {
+        const uint32_t lo = t * per, hi = std::min(n, lo + per);
+        if (lo < hi) pool.emplace_back([=] { fn(lo, hi); });
+    }
+    fn(0u, std::min(n, per));
+    for (auto &th : pool) th.join();
+}
+
 // ---------------------------------------------------------------- crit-bit index
 // Restates CritBitTree.cpp:13-269 over the COMPAT-decoded key prefix of each stored
 // record (computed on the GPU at setitem time).  Walk bytes past a key's end read 0
@@ -217,6 +257,11 @@ struct px_ctx {
     uint64_t last_store_bytes = 0;
     DevBuf scratch_frames, dq_buf, dstat_buf, dlen_buf, in_buf, tmp_buf, link_buf, iter_buf, init_buf, stout_buf,
         slotput_buf;
+    HostBuf hq_buf, hres_buf;  // pinned: decode queries up, lengths + statuses down
+    uint32_t host_threads() const {
+        const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
+        return opts.host_threads ? opts.host_threads : std::min(16u, hw);
+    }
     px_stats stats{};
     int last_hip = 0;
 
@@ -621,18 +666,23 @@ struct px_ctx {
         auto *dq = (DecodeQuery *)dq_buf.get((uint64_t)nq * sizeof(DecodeQuery));
         auto *dl = (uint32_t *)dlen_buf.get((uint64_t)nq * 8);
         uint32_t *ds = dl + nq;
-        std::vector<DecodeQuery> qn(q);
-        for (auto &d : qn) d.nrec = d.chunk == kNone ? 0 : chunks[d.chunk].n;
-        h2d(dq, qn.data(), (size_t)nq * sizeof(DecodeQuery));
+        auto *qn = (DecodeQuery *)hq_buf.get((uint64_t)nq * sizeof(DecodeQuery));
+        for (uint32_t i = 0; i < nq; ++i) {
+            qn[i] = q[i];
+            qn[i].nrec = q[i].chunk == kNone ? 0 : chunks[q[i].chunk].n;
+        }
+        hcheck(hipMemcpyAsync(dq, qn, (size_t)nq * sizeof(DecodeQuery), hipMemcpyHostToDevice, stream));
         flush_tab();
         if (timed) hcheck(hipEventRecord(ev0, stream));
         // timed == a getitem batch (k_decode); otherwise stored-key prefixes (k_decode_keys)
         hcheck(launch_decode(stream, dq, nq, (const RecSlot *const *)chunk_tab, out_dev, dl, ds, frames, depth,
                              waves, !timed));
         if (timed) hcheck(hipEventRecord(ev1, stream));
-        d2h(len.data(), dl, (size_t)nq * 4);
-        d2h(st.data(), ds, (size_t)nq * 4);
+        auto *hr = (uint32_t *)hres_buf.get((uint64_t)nq * 8);
+        hcheck(hipMemcpyAsync(hr, dl, (size_t)nq * 8, hipMemcpyDeviceToHost, stream));  // lengths, then statuses
         sync();
+        std::memcpy(len.data(), hr, (size_t)nq * 4);
+        std::memcpy(st.data(), hr + nq, (size_t)nq * 4);
         if (timed) {
             float ms = 0;
             hcheck(hipEventElapsedTime(&ms, ev0, ev1));
@@ -1212,20 +1262,23 @@ int px_get_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *k
     PX_GUARD({
         std::vector<DecodeQuery> q(n);
         std::vector<uint32_t> pre(n, PX_OK);
-        for (uint32_t i = 0; i < n; ++i) {
-            std::string raw(reinterpret_cast<const char *>(keys + koff[i]), koff[i + 1] - koff[i]);
-            std::string ek = px_ctx::esc_key(keys + koff[i], koff[i + 1] - koff[i]);
-            Shard *s = ctx->shard_for_key(raw);
-            Leaf l;
-            q[i] = DecodeQuery{kNone, 0, 0, kMaxDoc, 0, 0, (uint32_t)mode};
-            if (!s || !ctx->cbt_lookup(*s, ek, &l)) {
-                pre[i] = PX_ENOTFOUND;
-                continue;
+        // key -> record lookups are read-only: host threads over key ranges
+        parallel_ranges(n, ctx->host_threads(), [&](uint32_t lo, uint32_t hi) {
+            for (uint32_t i = lo; i < hi; ++i) {
+                std::string raw(reinterpret_cast<const char *>(keys + koff[i]), koff[i + 1] - koff[i]);
+                std::string ek = px_ctx::esc_key(keys + koff[i], koff[i + 1] - koff[i]);
+                Shard *s = ctx->shard_for_key(raw);
+                Leaf l;
+                q[i] = DecodeQuery{kNone, 0, 0, kMaxDoc, 0, 0, (uint32_t)mode};
+                if (!s || !ctx->cbt_lookup(*s, ek, &l)) {
+                    pre[i] = PX_ENOTFOUND;
+                    continue;
+                }
+                q[i].chunk = l.chunk;
+                q[i].idx = l.idx;
+                q[i].out_cap = (uint32_t)round_up(ctx->chunks[l.chunk].doc_len[l.idx] + 64, 16);
             }
-            q[i].chunk = l.chunk;
-            q[i].idx = l.idx;
-            q[i].out_cap = (uint32_t)round_up(ctx->chunks[l.chunk].doc_len[l.idx] + 64, 16);
-        }
+        });
         int rc = ctx->expand(q, out, out_cap, out_on_device, out_off, out_len, status, needed, pre);
         if (rc == PX_OK)
             for (uint32_t i = 0; i < n; ++i)
