@@ -55,8 +55,8 @@ typedef struct px_opts {
     int device;                 /* HIP device ordinal */
     uint32_t records_per_shard; /* 0 = single shard (reference semantics) */
     uint32_t decode_depth;      /* frames per decode stack; 0 = 4096 */
-    uint32_t decode_waves;      /* concurrent decode wavefronts; 0 = auto */
-    uint32_t host_threads;      /* host CritBit worker threads; 0 = auto */
+    uint32_t decode_waves;      /* concurrent decode wavefronts; 0 = one per query, up to 16,384 */
+    uint32_t host_threads;      /* host threads for batch key lookups; 0 = min(16, cores) */
 } px_opts;
 
 typedef struct px_ctx px_ctx;
