@@ -1158,7 +1158,10 @@ __global__ void __launch_bounds__(256) k_tokenize(uint32_t n, const RecSlot *slo
                         *(PX_GAS u32x4 *)(lanes + ns) = mk4(pend_x | (uint32_t)x << 16, pend_z, pend_w, (uint32_t)rel);
                     }
                 }
-                if (x < (int32_t)pend_x || x > 0xffff) {  // lane entries need 16-bit coordinates
+                // lane entries need 16-bit coordinates and a comp base within +-16 GiB
+                const int64_t dz = (int64_t)comp_addr - (int64_t)(uint64_t)(lanes + ns);
+                if (lanes && (dz >> 3) != (int64_t)(int32_t)(dz >> 3)) mono = false;
+                if (x < (int32_t)pend_x || x > 0xffff) {
                     mono = false;
                 } else if (mono && pidx_n) {
                     uint32_t b0 = (pend_x + 15) >> 4, b1 = min(((uint32_t)x + 15) >> 4, pidx_n);
