@@ -247,6 +247,7 @@ struct GstWave {
     // lookup candidates: the child count lane l's candidate needs (lane 0/1: inline
     // child 0/1, lanes 4..7: bucket entries, others never) and whether it is inline
     uint32_t v_need, v_inl;
+    uint32_t kc_off, kc_key;  // canonise's cached first key (valid within one split loop)
     uint32_t node_cap, hash_mask, doc_cap;
     PX_LAS GstLds *lds;
     // persistent counters
@@ -305,9 +306,10 @@ struct GstWave {
     // The pool is always open while docs are encoded (clear_tree's root node opens
     // it), so the hot path is the branch-free "next pool when the request does not fit".
     PX_DEV void charge(int32_t blocks) {
-        const bool next = blocks > kPoolBlocks - used;
-        pools += next ? 1 : 0;
-        used = (next ? 0 : used) + blocks;
+        const int32_t t = used + blocks;
+        const bool next = t > kPoolBlocks;
+        pools += (int32_t)next;
+        used = next ? blocks : t;
     }
     PX_DEV void charge_first(int32_t blocks) {  // MemPool's first p_malloc opens pool 1
         pool_open = 1;
@@ -576,7 +578,13 @@ struct GstWave {
         prof[P_T_LOOK] += __builtin_amdgcn_s_memtime() - tl;
         if (!ok0) return false;
 #else
-        if (!must_lookup(act_node, curchar(i - act_off), e)) return false;
+        // the first key is text[i - act_off]: act_off rarely changes between the
+        // iterations of one split loop, so the byte is kept (kc_off = its act_off)
+        if (act_off != kc_off) {
+            kc_key = curchar(i - act_off);
+            kc_off = act_off;
+        }
+        if (!must_lookup(act_node, kc_key, e)) return false;
 #endif
         uint32_t supply;
         while (act_off > (supply = e.to() - e.from())) {
@@ -759,7 +767,8 @@ struct GstWave {
             // the suffix link of act_node is loaded one iteration ahead (next to the
             // previous end check), so an iteration costs two dependent round trips
             uint32_t lraw = act_node != kRoot ? nlink(act_node) : 0u;
-            while (remainder > 0 && status == kOk) {
+            kc_off = kNone;
+            while (remainder > 0) {
                 PX_CNT(P_ITERS, 1);
 #ifdef PX_PROFILE
                 uint64_t tg = __builtin_amdgcn_s_memtime();
