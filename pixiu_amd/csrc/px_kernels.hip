@@ -1183,11 +1183,21 @@ __global__ void __launch_bounds__(256) k_tokenize(uint32_t n, const RecSlot *slo
             pend_w = w;
             have = true;
         };
+        // two aligned 64-byte windows, [wb, wb + 64) in b and the next one in bn: a token
+        // starting in the first is wholly inside the pair, and the next window's load is
+        // issued a whole window ahead (its wait does not drain this window's stores)
         uint32_t b = lane < len ? comp[lane] : 0;
+        uint32_t bn = 64 + lane < len ? comp[64 + lane] : 0;
+        auto byte_at = [&](uint32_t q) -> uint32_t {  // q < wb + 128
+            const uint32_t d = q - wb;
+            const uint32_t r0 = readlane(b, d & 63u), r1 = readlane(bn, d & 63u);
+            return d < 64 ? r0 : r1;
+        };
         while (p < len) {
-            if (p >= wb + 64 || (p + 8 > wb + 64 && wb + 64 < len)) {
-                wb = p;
-                b = wb + lane < len ? comp[wb + lane] : 0;
+            while (p >= wb + 64) {
+                wb += 64;
+                b = bn;
+                bn = wb + 64 + lane < len ? comp[wb + 64 + lane] : 0;
             }
             if (!plain_open) {
                 plain_open = true;
@@ -1205,12 +1215,11 @@ __global__ void __launch_bounds__(256) k_tokenize(uint32_t n, const RecSlot *slo
             uint32_t q = wb + ffs64(m);
             src += (int32_t)(q - p);
             p = q;
-            if (p + 8 > wb + 64 && wb + 64 < len) continue;  // refill so the token is in the window
             if (p + 1 >= len) {
                 err = kErrCorrupt;
                 break;
             }
-            uint32_t nx = readlane(b, p + 1 - wb);
+            uint32_t nx = byte_at(p + 1);
             if (nx == kKeyEnd || nx == kEsc || nx == kValEnd) {
                 p += 2;
                 src += 2;
@@ -1224,10 +1233,9 @@ __global__ void __launch_bounds__(256) k_tokenize(uint32_t n, const RecSlot *slo
                     err = kErrCorrupt;
                     break;
                 }
-                uint32_t idx = readlane(b, p + 2 - wb) | (readlane(b, p + 3 - wb) << 8);
-                uint32_t to = readlane(b, p + 4 - wb) | (readlane(b, p + 5 - wb) << 8);
-                uint32_t from = nx == kBigSign ? (readlane(b, p + 6 - wb) | (readlane(b, p + 7 - wb) << 8))
-                                               : ((to - nx) & 0xffffu);
+                uint32_t idx = byte_at(p + 2) | (byte_at(p + 3) << 8);
+                uint32_t to = byte_at(p + 4) | (byte_at(p + 5) << 8);
+                uint32_t from = nx == kBigSign ? (byte_at(p + 6) | (byte_at(p + 7) << 8)) : ((to - nx) & 0xffffu);
                 emit(src, p | kSegRecord, idx | from << 16);
                 src += (int32_t)to - (int32_t)from;
                 p += size;
