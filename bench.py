@@ -164,7 +164,8 @@ def main():
         set_kms, walk_kms, emit_kms = sst["last_set_kernel_ms"], sst["last_walk_kernel_ms"], sst["last_emit_kernel_ms"]
         rc, off, ln, sts, need = st.get_batch_device(keys_host, out.data_ptr(), out_cap, px.COMPAT)
         t2 = time.perf_counter()
-        dec_kms = st.stats()["last_decode_kernel_ms"]
+        gst = st.stats()
+        dec_kms, look_ms, call_ms = gst["last_decode_kernel_ms"], gst["last_get_lookup_ms"], gst["last_get_call_ms"]
         g_ms = 0.0
         if world > 1:  # gather every rank's compressed blob to rank 0 (RCCL over xGMI)
             nonlocal gather_buf
@@ -182,7 +183,7 @@ def main():
         # setitem's one exchange (the compressed-blob gather to rank 0) counts as setitem time
         return {"set_s": t1 - t0 + g_ms * 1e-3, "get_s": t2 - t1, "set_kms": set_kms, "walk_kms": walk_kms,
                 "emit_kms": emit_kms,
-                "dec_kms": dec_kms, "gather_ms": g_ms,
+                "dec_kms": dec_kms, "gather_ms": g_ms, "look_ms": look_ms, "call_ms": call_ms,
                 "comp": int(res["comp_len"].sum()), "exp": int(ln.sum()), "res": res}
 
     for _ in range(a.warmup):
@@ -213,6 +214,11 @@ def main():
     walk_kms = float(np.mean([r["walk_kms"] for r in runs]))
     emit_kms = float(np.mean([r["emit_kms"] for r in runs]))
     dec_kms = float(np.mean([r["dec_kms"] for r in runs]))
+    # getitem wall time split: host key lookups, the rest of the C call (query upload,
+    # k_decode, length/status download), and the Python binding around it
+    get_split = {"lookup_ms": float(np.mean([r["look_ms"] for r in runs])),
+                 "call_ms": float(np.mean([r["call_ms"] for r in runs])),
+                 "wall_ms": float(np.mean([r["get_s"] for r in runs])) * 1e3}
     stats = st.stats()
 
     if rank != 0:
@@ -265,6 +271,7 @@ def main():
         "getitem_MBps": round(get_MBps, 3),
         "compression_ratio": round(job_comp / job_raw, 4),
         "kernel_ms": {"k_gst_encode": round(walk_kms, 3), "k_gst_emit": round(emit_kms, 3), "k_decode": round(dec_kms, 3)},
+        "getitem_split_ms": {k: round(v, 3) for k, v in get_split.items()},
         "gather_ms": round(float(np.mean([r["gather_ms"] for r in runs])), 3),
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 3), "peak": PEAK_HBM_GBPS,
                      "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBPS, 6), "traffic": tr},

@@ -88,6 +88,8 @@ typedef struct px_stats {
     double last_decode_kernel_ms; /* k_decode time of the last get/parse batch */
     double last_walk_kernel_ms;   /* k_gst_encode (suffix-tree walk -> encoder messages) alone */
     double last_emit_kernel_ms;   /* k_gst_emit (stream encoder -> compressed bytes) alone */
+    double last_get_lookup_ms;    /* host key -> record lookups of the last px_get_batch */
+    double last_get_call_ms;      /* wall time inside the last px_get_batch call */
 } px_stats;
 
 px_ctx *px_open(const px_opts *opts);

@@ -63,7 +63,8 @@ class PxStats(C.Structure):
                 ("raw_bytes", C.c_uint64), ("doc_bytes", C.c_uint64), ("comp_bytes", C.c_uint64),
                 ("ub_reads", C.c_uint64), ("device_bytes", C.c_uint64),
                 ("last_set_kernel_ms", C.c_double), ("last_decode_kernel_ms", C.c_double),
-                ("last_walk_kernel_ms", C.c_double), ("last_emit_kernel_ms", C.c_double)]
+                ("last_walk_kernel_ms", C.c_double), ("last_emit_kernel_ms", C.c_double),
+                ("last_get_lookup_ms", C.c_double), ("last_get_call_ms", C.c_double)]
 
 
 SET_RESULT_DTYPE = np.dtype([("status", "<u4"), ("replaced", "<u4"), ("shard", "<u4"), ("chunk", "<u4"),
@@ -130,9 +131,9 @@ class Store:
     i.e. exactly the reference's single PiXiuCtrl instance."""
 
     def __init__(self, records_per_shard: int = 0, device: int = 0, decode_depth: int = 0,
-                 decode_waves: int = 0):
+                 decode_waves: int = 0, host_threads: int = 0):
         self._lib = load_library()
-        opts = PxOpts(device, records_per_shard, decode_depth, decode_waves, 0)
+        opts = PxOpts(device, records_per_shard, decode_depth, decode_waves, host_threads)
         h = self._lib.px_open(C.byref(opts))
         if not h:
             raise PxError(9, "px_open (no usable HIP device?)")

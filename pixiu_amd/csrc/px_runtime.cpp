@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -164,6 +165,83 @@ struct HostBuf {
     }
 };
 
+// raw key -> shard for multi-shard stores.  Open addressing over 64-bit key hashes
+// with the key bytes in one arena: a lookup touches one slot and the key's bytes,
+// with no per-key heap node and no std::string built for the probe.
+class KeyMap {
+    struct Slot {
+        uint64_t h, off;
+        uint32_t len, shard;  // len == kFree: empty
+    };
+    static constexpr uint32_t kFree = ~0u;
+    std::vector<Slot> tab_;
+    std::vector<uint8_t> bytes_;
+    size_t n_ = 0;
+
+    static uint64_t mix(uint64_t h) {
+        h ^= h >> 32;
+        h *= 0xD6E8FEB86659FD93ull;
+        h ^= h >> 32;
+        return h;
+    }
+    size_t probe(uint64_t h, const uint8_t *k, size_t n) const {  // slot of k, or the free slot it goes in
+        const size_t m = tab_.size() - 1;
+        for (size_t i = h & m;; i = (i + 1) & m) {
+            const Slot &e = tab_[i];
+            if (e.len == kFree) return i;
+            if (e.h == h && e.len == n && (n == 0 || std::memcmp(bytes_.data() + e.off, k, n) == 0)) return i;
+        }
+    }
+    void grow() {
+        std::vector<Slot> old(std::max<size_t>(tab_.size() * 2, 1024), Slot{0, 0, kFree, 0});
+        old.swap(tab_);
+        const size_t m = tab_.size() - 1;
+        for (const Slot &e : old)
+            if (e.len != kFree) {
+                size_t i = e.h & m;
+                while (tab_[i].len != kFree) i = (i + 1) & m;
+                tab_[i] = e;
+            }
+    }
+
+  public:
+    static uint64_t hash(const uint8_t *k, size_t n) {
+        uint64_t h = 0x9E3779B97F4A7C15ull ^ n;
+        size_t i = 0;
+        for (; i + 8 <= n; i += 8) {
+            uint64_t w;
+            std::memcpy(&w, k + i, 8);
+            h = mix(h ^ w) * 0x9E3779B97F4A7C15ull;
+        }
+        uint64_t w = 0;
+        std::memcpy(&w, k + i, n - i);
+        return mix(mix(h ^ w) + n);
+    }
+    // shard of k, or -1
+    int64_t find(const uint8_t *k, size_t n) const {
+        if (tab_.empty()) return -1;
+        const Slot &e = tab_[probe(hash(k, n), k, n)];
+        return e.len == kFree ? -1 : (int64_t)e.shard;
+    }
+    void put(const uint8_t *k, size_t n, uint32_t shard) {
+        if ((n_ + 1) * 2 > tab_.size()) grow();
+        const uint64_t h = hash(k, n);
+        Slot &e = tab_[probe(h, k, n)];
+        if (e.len == kFree) {
+            e = Slot{h, bytes_.size(), (uint32_t)n, shard};
+            bytes_.insert(bytes_.end(), k, k + n);
+            ++n_;
+        } else {
+            e.shard = shard;
+        }
+    }
+    void clear() {
+        tab_.clear();
+        bytes_.clear();
+        n_ = 0;
+    }
+};
+
 // fn(lo, hi) over [0, n) on up to `threads` host threads (inline for small n)
 template <class F>
 void parallel_ranges(uint32_t n, uint32_t threads, F fn) {
@@ -240,10 +318,16 @@ struct Shard {
 
 }  // namespace
 
+namespace {
+px_status map_status(uint32_t s);  // device status -> px_status (defined below)
+}  // namespace
+
 struct px_ctx {
     px_opts opts{};
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_mid = nullptr;
+    hipStream_t stream2 = nullptr;  // getitem's second decode launch (get_overlapped)
+    hipEvent_t ev_join = nullptr;
     DevHeap heap;
     std::vector<std::unique_ptr<Shard>> shards;
     std::vector<Chunk> chunks;
@@ -251,7 +335,7 @@ struct px_ctx {
     uint32_t chunk_tab_cap = 0;
     uint32_t tab_lo = ~0u, tab_hi = 0;      // chunk_tab entries not yet uploaded
     std::vector<ShardInit> pending_init;    // new shard arenas to zero (k_shard_init)
-    std::unordered_map<std::string, uint32_t> keymap;  // raw key -> shard (multi-shard only)
+    KeyMap keymap;  // raw key -> shard (multi-shard only)
     std::vector<std::pair<void *, uint64_t>> store_blocks;  // packed record stores + segment indexes
     uint8_t *last_store = nullptr;  // packed compressed bytes of the last set batch
     uint64_t last_store_bytes = 0;
@@ -631,22 +715,33 @@ struct px_ctx {
         return true;
     }
 
-    static std::string esc_key(const uint8_t *k, uint64_t n) {
-        std::string q;
-        q.reserve(n + 2);
-        for (uint64_t i = 0; i < n; ++i) {
-            q.push_back((char)k[i]);
-            if (k[i] == kEsc) q.push_back((char)kEsc);
+    // the escaped key the CritBit stores (raw bytes, 251 doubled, then 251,0), built
+    // into q (reused buffers keep lookups off the allocator)
+    static void esc_key_into(std::string &q, const uint8_t *k, uint64_t n) {
+        q.clear();
+        const uint8_t *e = (const uint8_t *)std::memchr(k, kEsc, n);
+        if (!e) {
+            q.append(reinterpret_cast<const char *>(k), n);
+        } else {
+            q.reserve(n + 8);
+            for (uint64_t i = 0; i < n; ++i) {
+                q.push_back((char)k[i]);
+                if (k[i] == kEsc) q.push_back((char)kEsc);
+            }
         }
         q.push_back((char)kEsc);
         q.push_back((char)kKeyEnd);
+    }
+    static std::string esc_key(const uint8_t *k, uint64_t n) {
+        std::string q;
+        esc_key_into(q, k, n);
         return q;
     }
 
-    Shard *shard_for_key(const std::string &raw) {
+    Shard *shard_for_key(const uint8_t *k, uint64_t n) const {
         if (opts.records_per_shard == 0) return shards.empty() ? nullptr : shards[0].get();
-        auto it = keymap.find(raw);
-        return it == keymap.end() ? nullptr : shards[it->second].get();
+        const int64_t s = keymap.find(k, n);
+        return s < 0 ? nullptr : shards[(size_t)s].get();
     }
 
     // ------------------------------------------------------------ decode
@@ -688,6 +783,121 @@ struct px_ctx {
             hcheck(hipEventElapsedTime(&ms, ev0, ev1));
             stats.last_decode_kernel_ms = ms;
         }
+    }
+
+    // key -> decode query (CritBit lookup, CritBitTree.cpp:13-40); pre = PX_ENOTFOUND when absent
+    void resolve_key(const uint8_t *k, uint64_t kn, int mode, std::string &ek, DecodeQuery &q, uint32_t &pre) const {
+        esc_key_into(ek, k, kn);
+        const Shard *s = shard_for_key(k, kn);
+        Leaf l;
+        q = DecodeQuery{kNone, 0, 0, kMaxDoc, 0, 0, (uint32_t)mode};
+        pre = PX_OK;
+        if (!s || !cbt_lookup(*s, ek, &l)) {
+            pre = PX_ENOTFOUND;
+            return;
+        }
+        q.chunk = l.chunk;
+        q.idx = l.idx;
+        q.out_cap = (uint32_t)round_up(chunks[l.chunk].doc_len[l.idx] + 64, 16);
+    }
+
+    // share of a get batch (in 64ths) resolved before the first decode launch
+    static uint32_t opts_head_frac() {
+        static const uint32_t f = [] {
+            const char *e = std::getenv("PX_GET_HEAD64");
+            const int v = e ? std::atoi(e) : 0;
+            return v > 0 && v < 64 ? (uint32_t)v : 24u;
+        }();
+        return f;
+    }
+
+    // getitem into a device buffer with the host key lookups overlapped with k_decode:
+    // the first `head` keys are resolved and their decode launched at once; the rest
+    // are resolved on host threads while the GPU expands the head, then launched on a
+    // second stream, so the two launches share the GPU (the head alone does not fill
+    // it).  Same results as resolving everything first and calling expand().
+    int get_overlapped(uint32_t n, const uint8_t *keys, const uint64_t *koff, int mode, uint8_t *out,
+                       uint64_t out_cap, uint64_t *out_off, uint32_t *out_len, uint32_t *status, uint64_t *needed,
+                       double &lookup_ms) {
+        using clk = std::chrono::steady_clock;
+        std::vector<DecodeQuery> q(n);
+        std::vector<uint32_t> pre(n, PX_OK);
+        auto resolve = [&](uint32_t lo, uint32_t hi) {
+            std::string ek;
+            for (uint32_t i = lo; i < hi; ++i) resolve_key(keys + koff[i], koff[i + 1] - koff[i], mode, ek, q[i], pre[i]);
+        };
+        uint64_t total = 0;
+        auto place = [&](uint32_t lo, uint32_t hi) {  // output offsets, in key order
+            for (uint32_t i = lo; i < hi; ++i) {
+                out_off[i] = total;
+                q[i].out_off = total;
+                q[i].nrec = q[i].chunk == kNone ? 0 : chunks[q[i].chunk].n;
+                if (q[i].chunk != kNone) total += q[i].out_cap;
+            }
+        };
+        const uint32_t head = std::max<uint32_t>(1024, (uint32_t)((uint64_t)n * opts_head_frac() / 64));
+        auto t0 = clk::now();
+        resolve(0, head);
+        place(0, head);
+        double head_ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+        if (total > out_cap) {  // cannot launch the head: plain path (reports PX_ESPACE)
+            parallel_ranges(n - head, host_threads(), [&](uint32_t lo, uint32_t hi) { resolve(head + lo, head + hi); });
+            lookup_ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+            return expand(q, out, out_cap, 1, out_off, out_len, status, needed, pre);
+        }
+        const uint32_t depth = opts.decode_depth ? opts.decode_depth : 4096;
+        const uint32_t w1 = std::min<uint32_t>(16384, head), w2 = std::min<uint32_t>(16384, n - head);
+        auto *frames = (Frame *)scratch_frames.get((uint64_t)(w1 + w2) * depth * sizeof(Frame));
+        auto *dq = (DecodeQuery *)dq_buf.get((uint64_t)n * sizeof(DecodeQuery));
+        auto *dl = (uint32_t *)dlen_buf.get((uint64_t)n * 8);
+        uint32_t *ds = dl + n;
+        auto *qn = (DecodeQuery *)hq_buf.get((uint64_t)n * sizeof(DecodeQuery));
+        auto *hr = (uint32_t *)hres_buf.get((uint64_t)n * 8);
+        std::memcpy(qn, q.data(), (size_t)head * sizeof(DecodeQuery));
+        hcheck(hipMemcpyAsync(dq, qn, (size_t)head * sizeof(DecodeQuery), hipMemcpyHostToDevice, stream));
+        flush_tab();
+        hcheck(hipEventRecord(ev0, stream));
+        hcheck(launch_decode(stream, dq, head, (const RecSlot *const *)chunk_tab, out, dl, ds, frames, depth, w1,
+                             false));
+        // the tail: resolved while the head decodes
+        auto t1 = clk::now();
+        parallel_ranges(n - head, host_threads(), [&](uint32_t lo, uint32_t hi) { resolve(head + lo, head + hi); });
+        place(head, n);
+        lookup_ms = head_ms + std::chrono::duration<double, std::milli>(clk::now() - t1).count();
+        if (needed) *needed = total;
+        if (total > out_cap) {
+            sync();
+            return PX_ESPACE;
+        }
+        std::memcpy(qn + head, q.data() + head, (size_t)(n - head) * sizeof(DecodeQuery));
+        hcheck(hipStreamWaitEvent(stream2, ev0, 0));  // chunk table and head queries uploaded
+        hcheck(hipMemcpyAsync(dq + head, qn + head, (size_t)(n - head) * sizeof(DecodeQuery), hipMemcpyHostToDevice,
+                              stream2));
+        hcheck(launch_decode(stream2, dq + head, n - head, (const RecSlot *const *)chunk_tab, out, dl + head,
+                             ds + head, frames + (uint64_t)w1 * depth, depth, w2, false));
+        hcheck(hipEventRecord(ev_join, stream2));
+        hcheck(hipStreamWaitEvent(stream, ev_join, 0));
+        hcheck(hipEventRecord(ev1, stream));
+        hcheck(hipMemcpyAsync(hr, dl, (size_t)n * 8, hipMemcpyDeviceToHost, stream));  // lengths, then statuses
+        sync();
+        float ms = 0;
+        hcheck(hipEventElapsedTime(&ms, ev0, ev1));
+        stats.last_decode_kernel_ms = ms;
+        for (uint32_t i = 0; i < n; ++i)  // an overrun slot: the plain path re-runs with room (rare)
+            if (q[i].chunk != kNone && hr[n + i] == kErrSpace)
+                return expand(q, out, out_cap, 1, out_off, out_len, status, needed, pre);
+        int rc = PX_OK;
+        for (uint32_t i = 0; i < n; ++i) {
+            if (q[i].chunk == kNone) {
+                out_len[i] = 0;
+                status[i] = pre[i];
+            } else {
+                out_len[i] = hr[i];
+                status[i] = map_status(hr[n + i]);
+            }
+            if (status[i] != PX_OK && rc == PX_OK) rc = (int)status[i];
+        }
+        return rc;
     }
 
     // k_link over `jobs` (device copy staged through a scratch buffer)
@@ -1103,13 +1313,12 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         uint64_t klen = hkoff[r + 1] - hkoff[r];
         std::string q = esc_key(kp, klen);
         if (opts.records_per_shard != 0) {
-            std::string raw(reinterpret_cast<const char *>(kp), klen);
-            auto it = keymap.find(raw);
-            if (it != keymap.end() && it->second != s.id) {
-                cbt_delete(*shards[it->second], q);  // cross-shard replace
+            const int64_t prev = keymap.find(kp, klen);
+            if (prev >= 0 && (uint32_t)prev != s.id) {
+                cbt_delete(*shards[(size_t)prev], q);  // cross-shard replace
                 replaced[r] = 1;
             }
-            keymap[raw] = s.id;
+            keymap.put(kp, klen, s.id);
         }
         replaced[r] |= (uint32_t)cbt_insert(s, q, Leaf{rgchunk[r], ridx[r]});
     }
@@ -1201,6 +1410,8 @@ px_ctx *px_open(const px_opts *opts) {
         if (opts) c->opts = *opts;
         hcheck(hipSetDevice(c->opts.device));
         hcheck(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        hcheck(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+        hcheck(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
         hcheck(hipEventCreate(&c->ev0));
         hcheck(hipEventCreate(&c->ev1));
         hcheck(hipEventCreate(&c->ev_mid));
@@ -1216,6 +1427,11 @@ void px_close(px_ctx *ctx) {
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->ev_mid) (void)hipEventDestroy(ctx->ev_mid);
+    if (ctx->stream2) {
+        (void)hipStreamSynchronize(ctx->stream2);
+        (void)hipStreamDestroy(ctx->stream2);
+    }
+    if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -1260,32 +1476,32 @@ int px_get_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *k
                  uint64_t *needed) {
     if (!ctx || (n && (!keys || !koff || !out_off || !out_len || !status))) return PX_EINVAL;
     PX_GUARD({
-        std::vector<DecodeQuery> q(n);
-        std::vector<uint32_t> pre(n, PX_OK);
-        // key -> record lookups are read-only: host threads over key ranges
-        parallel_ranges(n, ctx->host_threads(), [&](uint32_t lo, uint32_t hi) {
-            for (uint32_t i = lo; i < hi; ++i) {
-                std::string raw(reinterpret_cast<const char *>(keys + koff[i]), koff[i + 1] - koff[i]);
-                std::string ek = px_ctx::esc_key(keys + koff[i], koff[i + 1] - koff[i]);
-                Shard *s = ctx->shard_for_key(raw);
-                Leaf l;
-                q[i] = DecodeQuery{kNone, 0, 0, kMaxDoc, 0, 0, (uint32_t)mode};
-                if (!s || !ctx->cbt_lookup(*s, ek, &l)) {
-                    pre[i] = PX_ENOTFOUND;
-                    continue;
-                }
-                q[i].chunk = l.chunk;
-                q[i].idx = l.idx;
-                q[i].out_cap = (uint32_t)round_up(ctx->chunks[l.chunk].doc_len[l.idx] + 64, 16);
-            }
-        });
-        int rc = ctx->expand(q, out, out_cap, out_on_device, out_off, out_len, status, needed, pre);
+        const auto t0 = std::chrono::steady_clock::now();
+        int rc;
+        double lookup_ms = 0;
+        if (out_on_device && n >= 4096 && ctx->opts.decode_waves == 0) {
+            rc = ctx->get_overlapped(n, keys, koff, mode, out, out_cap, out_off, out_len, status, needed, lookup_ms);
+        } else {
+            std::vector<DecodeQuery> q(n);
+            std::vector<uint32_t> pre(n, PX_OK);
+            // key -> record lookups are read-only: host threads over key ranges
+            parallel_ranges(n, ctx->host_threads(), [&](uint32_t lo, uint32_t hi) {
+                std::string ek;
+                for (uint32_t i = lo; i < hi; ++i)
+                    ctx->resolve_key(keys + koff[i], koff[i + 1] - koff[i], mode, ek, q[i], pre[i]);
+            });
+            lookup_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            rc = ctx->expand(q, out, out_cap, out_on_device, out_off, out_len, status, needed, pre);
+        }
         if (rc == PX_OK)
             for (uint32_t i = 0; i < n; ++i)
                 if (status[i] != PX_OK) {
                     rc = (int)status[i];
                     break;
                 }
+        ctx->stats.last_get_lookup_ms = lookup_ms;
+        ctx->stats.last_get_call_ms =
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         return rc;
     })
 }
@@ -1322,8 +1538,7 @@ int px_contains_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64
     if (!ctx || (n && (!keys || !koff || !result))) return PX_EINVAL;
     PX_GUARD({
         for (uint32_t i = 0; i < n; ++i) {
-            std::string raw(reinterpret_cast<const char *>(keys + koff[i]), koff[i + 1] - koff[i]);
-            Shard *s = ctx->shard_for_key(raw);
+            Shard *s = ctx->shard_for_key(keys + koff[i], koff[i + 1] - koff[i]);
             result[i] = s && ctx->cbt_contains(*s, px_ctx::esc_key(keys + koff[i], koff[i + 1] - koff[i]));
         }
         return PX_OK;
@@ -1334,8 +1549,7 @@ int px_del_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *k
     if (!ctx || (n && (!keys || !koff || !result))) return PX_EINVAL;
     PX_GUARD({
         for (uint32_t i = 0; i < n; ++i) {
-            std::string raw(reinterpret_cast<const char *>(keys + koff[i]), koff[i + 1] - koff[i]);
-            Shard *s = ctx->shard_for_key(raw);
+            Shard *s = ctx->shard_for_key(keys + koff[i], koff[i + 1] - koff[i]);
             result[i] = s ? (uint32_t)ctx->cbt_delete(*s, px_ctx::esc_key(keys + koff[i], koff[i + 1] - koff[i])) : 1u;
         }
         return PX_OK;
