@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--rps", type=int, default=2, help="records per shard (independent GST); DESIGN.md §6 has the ratio curve")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r01g.json"))
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r01h.json"))
     return ap.parse_args()
 
 
