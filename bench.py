@@ -39,6 +39,7 @@ def parse():
     ap.add_argument("--records", type=int, default=None, help="records per rank (default: full config)")
     ap.add_argument("--rps", type=int, default=2, help="records per shard (independent GST); DESIGN.md §6 has the ratio curve")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r01h.json"))
     return ap.parse_args()
@@ -122,6 +123,28 @@ def cpu_baseline_mt(corpus, rps, set_MBps_1t, budget_s):
     raw = sum(d[2] for d in done)
     return {"set_MBps": raw / (t1 - t0) / 1e6, "get_MBps": exp / (t2 - t1) / 1e6, "threads": threads,
             "records": nshards * rps, "raw": raw, "seconds": t2 - t0}
+
+
+def pcie_leg(st, px, corpus, keys_host, out_cap):
+    """The same batch through host buffers, as the PiXiuCtrl facade hands them over:
+    setitem uploads the raw records, getitem downloads the expanded bytes into host
+    memory. Reported beside `value` (never as it); the second of two passes is kept
+    (the first touches the host pages)."""
+    vals_host = (np.ascontiguousarray(corpus.vals), corpus.voff.astype(np.uint64))
+    out_h = np.empty(out_cap, np.uint8)
+    for _ in range(2):
+        st.reset()
+        t0 = time.perf_counter()
+        res = st.set_batch(keys_host, vals_host)
+        t1 = time.perf_counter()
+        rc, off, ln, sts, need = st.get_batch_host(keys_host, out_h, px.COMPAT)
+        t2 = time.perf_counter()
+        if rc != px.PX_OK or int(res["status"].max()) != 0 or int(sts.max()) != 0:
+            raise SystemExit(f"host-buffer leg: rc={rc}")
+    return {"set_MBps": round(corpus.raw_bytes / (t1 - t0) / 1e6, 3),
+            "get_MBps": round(int(ln.sum()) / (t2 - t1) / 1e6, 3),
+            "set_ms": round((t1 - t0) * 1e3, 3), "get_ms": round((t2 - t1) * 1e3, 3),
+            "note": "host (pageable) inputs and output buffer, PCIe transfers inside the timed calls"}
 
 
 def main():
@@ -309,6 +332,8 @@ def main():
                                    "sample": f"{mt['records']} records ({mt['raw'] / 1e6:.1f} MB), one oracle "
                                              f"instance per {a.rps}-record shard, {mt['threads']} threads, "
                                              f"{mt['seconds']:.1f} s"}
+    if not a.no_pcie and world == 1:
+        line["pcie_inclusive"] = pcie_leg(st, px, corpus, keys_host, out_cap)
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -226,6 +226,19 @@ class Store:
                                                 out_ptr, out_cap)
         return rc, off, ln, st, need
 
+    def get_batch_host(self, keys, out: np.ndarray, mode: int = COMPAT):
+        """Expand into a caller-owned host buffer (one call, no retry); returns
+        (rc, offsets, lengths, statuses, needed) like get_batch_device."""
+        kb, ko = keys if isinstance(keys, tuple) else csr(keys)
+        n = len(ko) - 1
+        off = np.zeros(max(n, 1), np.uint64)
+        ln = np.zeros(max(n, 1), np.uint32)
+        st = np.zeros(max(n, 1), np.uint32)
+        need = np.zeros(1, np.uint64)
+        rc = self._lib.px_get_batch(self._h, n, _ptr(kb), _ptr(ko), mode, _ptr(out), out.nbytes, 0,
+                                    _ptr(off), _ptr(ln), _ptr(st), _ptr(need))
+        return rc, off[:n], ln[:n], st[:n], int(need[0])
+
     def parse_batch(self, recs: np.ndarray, mode: int = COMPAT, out_ptr: int | None = None, out_cap: int = 0):
         """PiXiuStr::parse(from, to) of stored records (REC_DTYPE array)."""
         recs = np.ascontiguousarray(recs, REC_DTYPE)
