@@ -28,6 +28,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
+# records per shard (independent GST instances) benchmarked for each BASELINE config;
+# DESIGN.md §6 has the compression-vs-shard-size curve
+DEFAULT_RPS = {1: 0, 2: 500, 3: 2, 4: 2000, 5: 16}
 
 
 def parse():
@@ -35,13 +38,18 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--config", type=int, default=3, help="the headline config (BASELINE.json metric: 3)")
     ap.add_argument("--records", type=int, default=None, help="records per rank (default: full config)")
-    ap.add_argument("--rps", type=int, default=2, help="records per shard (independent GST); DESIGN.md §6 has the ratio curve")
+    ap.add_argument("--rps", type=int, default=None, help="records per shard (default: DEFAULT_RPS[config])")
+    ap.add_argument("--configs", default="2,4,5",
+                    help="further BASELINE configs reported under per_config ('' for none)")
+    ap.add_argument("--extra-steps", type=int, default=2, help="timed steps of each further config")
+    ap.add_argument("--no-checks", action="store_true", help="skip the compat/exact/original parity counts")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r01h.json"))
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r02.json"),
+                    help="per-kernel PMC summary (tools/pmc_summary.py); used only if its workload matches")
     return ap.parse_args()
 
 
@@ -147,22 +155,83 @@ def pcie_leg(st, px, corpus, keys_host, out_cap):
             "note": "host (pageable) inputs and output buffer, PCIe transfers inside the timed calls"}
 
 
-def main():
-    a = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+def _docs_np(corpus):
+    """Every record's escaped doc (PiXiuCtrl.cpp:31-44) as one host buffer + offsets."""
+    if not (corpus.keys == 251).any() and not (corpus.vals == 251).any():
+        n = corpus.n
+        kl, vl = np.diff(corpus.koff), np.diff(corpus.voff)
+        dl = kl + 2 + np.where(vl > 0, vl + 2, 0)
+        off = np.zeros(n + 1, np.int64)
+        np.cumsum(dl, out=off[1:])
+        buf = np.empty(int(off[-1]), np.uint8)
+        for i in range(n):  # vectorising this buys little next to the decode
+            o = int(off[i])
+            k = corpus.keys[corpus.koff[i]:corpus.koff[i + 1]]
+            buf[o:o + len(k)] = k
+            buf[o + len(k):o + len(k) + 2] = (251, 0)
+            if vl[i]:
+                v = corpus.vals[corpus.voff[i]:corpus.voff[i + 1]]
+                p = o + len(k) + 2
+                buf[p:p + len(v)] = v
+                buf[p + len(v):p + len(v) + 2] = (251, 2)
+        return buf, off
+    parts = []
+    for i in range(corpus.n):
+        k, v = corpus.key(i), corpus.val(i)
+        d = k.replace(b"\xfb", b"\xfb\xfb") + b"\xfb\x00"
+        if v:
+            d += v.replace(b"\xfb", b"\xfb\xfb") + b"\xfb\x02"
+        parts.append(d)
+    off = np.zeros(corpus.n + 1, np.int64)
+    np.cumsum([len(x) for x in parts], out=off[1:])
+    return np.frombuffer(b"".join(parts), np.uint8), off
+
+
+def _count_ne(a, a_off, a_len, b, b_off, b_len, dev, piece=1 << 26):
+    """Records whose byte ranges differ: a[a_off[i]:+a_len[i]] vs b[b_off[i]:+b_len[i]]
+    (device buffers; compared on the GPU in pieces of about `piece` bytes)."""
+    import torch
+    a_off = np.asarray(a_off, np.int64)
+    b_off = np.asarray(b_off, np.int64)
+    a_len = np.asarray(a_len, np.int64)
+    b_len = np.asarray(b_len, np.int64)
+    n = len(a_len)
+    bad = int((a_len != b_len).sum())
+    same = np.nonzero(a_len == b_len)[0]
+    lens = a_len[same]
+    i = 0
+    while i < len(same):
+        j = i
+        tot = 0
+        while j < len(same) and (tot == 0 or tot + lens[j] <= piece):
+            tot += int(lens[j])
+            j += 1
+        sel = same[i:j]
+        ln = torch.from_numpy(lens[i:j]).to(dev)
+        seg = torch.repeat_interleave(torch.arange(j - i, device=dev), ln)
+        start = torch.cumsum(ln, 0) - ln
+        within = torch.arange(int(ln.sum()), device=dev) - torch.repeat_interleave(start, ln)
+        ia = torch.from_numpy(a_off[sel]).to(dev)[seg] + within
+        ib = torch.from_numpy(b_off[sel]).to(dev)[seg] + within
+        neq = (a[ia] != b[ib]).to(torch.int32)
+        per = torch.zeros(j - i, dtype=torch.int32, device=dev).index_add_(0, seg, neq)
+        bad += int((per > 0).sum())
+        i = j
+    assert n >= bad
+    return bad
+
+
+def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, checks=True):
+    """One BASELINE config on this rank: warmup + `steps` timed steps of batch setitem
+    (+ the blob gather when world > 1) and compat getitem, then (untimed) an exact-mode
+    getitem and the compat / exact / original parity counts over every record."""
     import torch
     import torch.distributed as dist
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
     import pixiu_amd as px
     from pixiu_amd import synth
     from pixiu_amd.dist import gather_blobs
 
-    corpus = synth.make(a.config, a.records, part=rank) if a.config == 3 else synth.make(a.config, a.records)
+    corpus = synth.make(cfg, records, part=rank)  # weak scaling: an independent part per rank
     n = corpus.n
     dev = torch.device("cuda", local)
     kb = torch.from_numpy(corpus.keys).to(dev)
@@ -174,9 +243,8 @@ def main():
     # every doc is <= 2*raw + 4 escaped bytes; the decoder gets doc_len + 64 per record
     out_cap = int(2 * raw_bytes + 256 * n + (1 << 20))
     out = torch.empty(out_cap, dtype=torch.uint8, device=dev)
-    gather_buf = None
-
-    st = px.Store(records_per_shard=a.rps, device=local)
+    gather_buf = [None]
+    st = px.Store(records_per_shard=rps, device=local)
 
     def step():
         st.reset()
@@ -190,123 +258,188 @@ def main():
         gst = st.stats()
         dec_kms, look_ms, call_ms = gst["last_decode_kernel_ms"], gst["last_get_lookup_ms"], gst["last_get_call_ms"]
         g_ms = 0.0
-        if world > 1:  # gather every rank's compressed blob to rank 0 (RCCL over xGMI)
-            nonlocal gather_buf
+        if world > 1:  # every rank's chunk blob (pixiu_amd/blob.py) to rank 0, RCCL over xGMI
             tg = time.perf_counter()
-            nb = st.last_store_bytes()
-            if gather_buf is None or gather_buf.numel() < nb:
-                gather_buf = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
-            st.copy_last_store(gather_buf.data_ptr(), gather_buf.numel(), True)
-            gather_blobs(gather_buf[:nb], dst=0)
+            nb = st.save_device(0, 0)
+            if gather_buf[0] is None or gather_buf[0].numel() < nb:
+                gather_buf[0] = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
+            st.save_device(gather_buf[0].data_ptr(), nb)
+            gather_blobs(gather_buf[0][:nb], dst=0)
             torch.cuda.synchronize()
             g_ms = (time.perf_counter() - tg) * 1e3
         if rc != px.PX_OK or int(res["status"].max()) != 0:
             bad = int((res["status"] != 0).sum())
-            raise SystemExit(f"rank {rank}: setitem failures={bad} getitem rc={rc}")
+            raise SystemExit(f"rank {rank} config {cfg}: setitem failures={bad} getitem rc={rc}")
         # setitem's one exchange (the compressed-blob gather to rank 0) counts as setitem time
         return {"set_s": t1 - t0 + g_ms * 1e-3, "get_s": t2 - t1, "set_kms": set_kms, "walk_kms": walk_kms,
-                "emit_kms": emit_kms,
-                "dec_kms": dec_kms, "gather_ms": g_ms, "look_ms": look_ms, "call_ms": call_ms,
-                "comp": int(res["comp_len"].sum()), "exp": int(ln.sum()), "res": res}
+                "emit_kms": emit_kms, "dec_kms": dec_kms, "gather_ms": g_ms, "look_ms": look_ms,
+                "call_ms": call_ms, "comp": int(res["comp_len"].sum()), "exp": int(ln.sum()), "res": res,
+                "off": off, "len": ln}
 
-    for _ in range(a.warmup):
+    for _ in range(warmup):
         step()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     T0 = time.perf_counter()
-    runs = [step() for _ in range(a.steps)]
+    runs = [step() for _ in range(steps)]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     T1 = time.perf_counter()
+    r = {"corpus": corpus, "st": st, "runs": runs, "elapsed": T1 - T0, "n": n, "raw": raw_bytes,
+         "out": out, "out_cap": out_cap, "keys_host": keys_host}
+    # exact-mode getitem (one timed call, outside the step loop) and parity counts
+    last = runs[-1]
+    out2 = torch.empty(out_cap, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    te = time.perf_counter()
+    rc, eoff, eln, ests, _ = st.get_batch_device(keys_host, out2.data_ptr(), out_cap, px.EXACT)
+    r["exact_s"] = time.perf_counter() - te
+    r["exact_dec_kms"] = st.stats()["last_decode_kernel_ms"]
+    r["exact_exp"] = int(eln.sum())
+    if rc != px.PX_OK:
+        raise SystemExit(f"config {cfg}: exact getitem rc={rc}")
+    if checks:
+        docs, doff = _docs_np(corpus)
+        dbuf = torch.from_numpy(docs).to(dev)
+        ne_ce = _count_ne(out, last["off"], last["len"], out2, eoff, eln, dev)
+        ne_eo = _count_ne(out2, eoff, eln, dbuf, doff[:-1], np.diff(doff), dev)
+        r["parity_counts"] = {"records": n, "compat_ne_exact": ne_ce, "exact_ne_original": ne_eo}
+        del dbuf
+    del out2
+    return r
 
-    elapsed = T1 - T0
-    set_s = sum(r["set_s"] for r in runs)
-    get_s = sum(r["get_s"] for r in runs)
-    tot = torch.tensor([elapsed, set_s, get_s], dtype=torch.float64, device=dev)
-    vol = torch.tensor([raw_bytes, runs[-1]["comp"], runs[-1]["exp"]], dtype=torch.float64, device=dev)
+
+def summarize(cfg, r, rps, world, a, pmc_path):
+    """Aggregate one config's runs (whole-job volumes over ranks) into its report."""
+    import torch
+    import torch.distributed as dist
+    runs = r["runs"]
+    steps = len(runs)
+    dev = r["out"].device
+    set_s = sum(x["set_s"] for x in runs)
+    get_s = sum(x["get_s"] for x in runs)
+    tot = torch.tensor([r["elapsed"], set_s, get_s, r["exact_s"]], dtype=torch.float64, device=dev)
+    vol = torch.tensor([r["raw"], runs[-1]["comp"], runs[-1]["exp"], r["exact_exp"]], dtype=torch.float64, device=dev)
     if world > 1:  # slowest rank's clock, every rank's bytes
         dist.all_reduce(tot, op=dist.ReduceOp.MAX)
         dist.all_reduce(vol, op=dist.ReduceOp.SUM)
-    elapsed, set_s, get_s = (float(x) for x in tot.tolist())
-    job_raw, job_comp, job_exp = (float(x) for x in vol.tolist())
-    comp = runs[-1]["comp"]
-    exp = runs[-1]["exp"]
-    set_kms = float(np.mean([r["set_kms"] for r in runs]))
-    walk_kms = float(np.mean([r["walk_kms"] for r in runs]))
-    emit_kms = float(np.mean([r["emit_kms"] for r in runs]))
-    dec_kms = float(np.mean([r["dec_kms"] for r in runs]))
-    # getitem wall time split: host key lookups, the rest of the C call (query upload,
-    # k_decode, length/status download), and the Python binding around it
-    get_split = {"lookup_ms": float(np.mean([r["look_ms"] for r in runs])),
-                 "call_ms": float(np.mean([r["call_ms"] for r in runs])),
-                 "wall_ms": float(np.mean([r["get_s"] for r in runs])) * 1e3}
-    stats = st.stats()
+    elapsed, set_s, get_s, exact_s = (float(x) for x in tot.tolist())
+    job_raw, job_comp, job_exp, job_exact = (float(x) for x in vol.tolist())
+    set_MBps = job_raw * steps / set_s / 1e6
+    get_MBps = job_exp * steps / get_s / 1e6
+    comp, exp, raw = runs[-1]["comp"], runs[-1]["exp"], r["raw"]
+    walk_kms = float(np.mean([x["walk_kms"] for x in runs]))
+    emit_kms = float(np.mean([x["emit_kms"] for x in runs]))
+    dec_kms = float(np.mean([x["dec_kms"] for x in runs]))
+    # roofline: algorithmic bytes per launch (SURVEY.md §8d) / avg launch time, HIP events
+    # on the context's stream (px_stats)
+    set_gbps = (raw + comp) / (walk_kms * 1e-3) / 1e9   # k_gst_encode: raw in + compressed out
+    emit_gbps = (raw * 5 + comp) / (emit_kms * 1e-3) / 1e9
+    dec_gbps = (comp + exp) / (dec_kms * 1e-3) / 1e9     # k_decode: compressed in + expanded out
+    dominant = "k_gst_encode" if walk_kms >= dec_kms else "k_decode"
+    ach = set_gbps if dominant == "k_gst_encode" else dec_gbps
+    traffic, tsrc = None, None
+    if pmc_path and os.path.exists(pmc_path):
+        try:
+            pmc = json.load(open(pmc_path))
+            w = pmc.get("workload", {})
+            # only a profile of this exact workload counts (config, shard size, records)
+            if w.get("config") == cfg and w.get("rps") == rps and w.get("records") == r["n"]:
+                traffic = pmc.get(dominant, {}).get("hbm_bytes_per_launch")
+                tsrc = f"{os.path.relpath(pmc_path, ROOT)} ({pmc.get('source', '')})"
+        except Exception:
+            traffic = None
+    out = {
+        "records_per_gpu": r["n"], "raw_bytes_per_gpu": raw, "records_per_shard": rps,
+        "shards_per_gpu": int(r["st"].stats()["shards"]), "steps": steps,
+        "value": round(set_MBps + get_MBps, 3), "unit": "MB/s",
+        "ms_per_step": round(elapsed / steps * 1e3, 3),
+        "setitem_MBps": round(set_MBps, 3), "getitem_MBps": round(get_MBps, 3),
+        "getitem_exact_MBps": round(job_exact / exact_s / 1e6, 3),
+        "compression_ratio": round(job_comp / job_raw, 4),
+        "kernel_ms": {"k_gst_encode": round(walk_kms, 3), "k_gst_emit": round(emit_kms, 3),
+                      "k_decode": round(dec_kms, 3), "k_decode_exact": round(r["exact_dec_kms"], 3)},
+        "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 3), "peak": PEAK_HBM_GBPS,
+                     "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBPS, 6), "traffic": traffic,
+                     "traffic_source": tsrc},
+        "roofline_kernels_GBps": {"k_gst_encode": round(set_gbps, 3), "k_gst_emit": round(emit_gbps, 3),
+                                  "k_decode": round(dec_gbps, 3)},
+        "gather_ms": round(float(np.mean([x["gather_ms"] for x in runs])), 3),
+    }
+    if "parity_counts" in r:
+        out["parity_counts"] = r["parity_counts"]
+    return out
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import pixiu_amd as px
+
+    rps = a.rps if a.rps is not None else DEFAULT_RPS[a.config]
+    r = run_config(a.config, a, rank, world, local, a.steps, a.warmup, rps, a.records, checks=not a.no_checks)
+    main_sum = summarize(a.config, r, rps, world, a, a.pmc)
+    per_config = {}
+    extra = [int(c) for c in a.configs.split(",") if c.strip()] if a.configs else []
+    for cfg in extra:
+        if cfg == a.config:
+            continue
+        rc_ = run_config(cfg, a, rank, world, local, a.extra_steps, 1, DEFAULT_RPS[cfg], None,
+                         checks=not a.no_checks)
+        per_config[str(cfg)] = summarize(cfg, rc_, DEFAULT_RPS[cfg], world, a, a.pmc)
+        rc_["st"].close()
+        del rc_
+        torch.cuda.empty_cache()
 
     if rank != 0:
+        r["st"].close()
         if world > 1:
             dist.destroy_process_group()
         return
 
-    K = a.steps
-    set_MBps = job_raw * K / set_s / 1e6
-    get_MBps = job_exp * K / get_s / 1e6
-    # roofline: algorithmic bytes per launch / avg launch time
-    set_alg = raw_bytes + comp                  # raw in + compressed out
-    dec_alg = comp + exp                        # compressed in + expanded out
-    # the setitem path is two launches: k_gst_encode (suffix-tree walk -> encoder
-    # messages) and k_gst_emit (lane-parallel stream encoder); the walk bounds it
-    set_gbps = set_alg / (walk_kms * 1e-3) / 1e9
-    emit_alg = raw_bytes * 5 + comp             # doc bytes + 4-byte messages in, compressed out
-    emit_gbps = emit_alg / (emit_kms * 1e-3) / 1e9
-    dec_gbps = dec_alg / (dec_kms * 1e-3) / 1e9
-    pmc = {}
-    if os.path.exists(a.pmc):
-        try:
-            pmc = json.load(open(a.pmc))
-        except Exception:
-            pmc = {}
-    dominant = "k_gst_encode" if walk_kms >= dec_kms else "k_decode"
-    if dominant == "k_gst_encode":
-        ach, tr = set_gbps, pmc.get("k_gst_encode", {}).get("hbm_bytes_per_launch")
-    else:
-        ach, tr = dec_gbps, pmc.get("k_decode", {}).get("hbm_bytes_per_launch")
+    st, corpus, runs = r["st"], r["corpus"], r["runs"]
+    n, raw_bytes = r["n"], r["raw"]
+    get_split = {"lookup_ms": float(np.mean([x["look_ms"] for x in runs])),
+                 "call_ms": float(np.mean([x["call_ms"] for x in runs])),
+                 "wall_ms": float(np.mean([x["get_s"] for x in runs])) * 1e3}
     line = {
         "metric": "MB/s ingested (setitem) + MB/s expanded (getitem), 10k×60KB corpus, 1/2/4/8 GPU",
-        "value": round(set_MBps + get_MBps, 3),
+        "value": main_sum["value"],
         "unit": "MB/s",
         "n_gpus": world,
-        "steps": K,
+        "steps": a.steps,
         "warmup": a.warmup,
-        "ms_per_step": round(elapsed / K * 1e3, 3),
+        "ms_per_step": main_sum["ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (pixiu_amd/synth.py, splitmix64 seed 0x5049585500+config)",
-        "config": {"workload": f"config{a.config}: {n} records x {raw_bytes // max(n, 1)} B per GPU "
-                               f"(HTML-shape pages)" if a.config == 3 else f"config{a.config}: {n} records per GPU",
-                   "records_per_gpu": n, "raw_bytes_per_gpu": raw_bytes, "records_per_shard": a.rps,
-                   "shards_per_gpu": int(stats["shards"]), "decode_mode": "compat",
+        "data": "synthetic (pixiu_amd/synth.py, splitmix64 seed 0x5049585500+config, one part per rank)",
+        "config": {"workload": (f"config{a.config}: {n} records x {raw_bytes // max(n, 1)} B per GPU "
+                                f"(HTML-shape pages)") if a.config == 3 else f"config{a.config}: {n} records per GPU",
+                   "records_per_gpu": n, "raw_bytes_per_gpu": raw_bytes, "records_per_shard": rps,
+                   "shards_per_gpu": main_sum["shards_per_gpu"], "decode_mode": "compat",
                    "parallelism": f"dp{world} (record-range shards, no cross-GPU refs)"},
-        "setitem_MBps": round(set_MBps, 3),
-        "getitem_MBps": round(get_MBps, 3),
-        "compression_ratio": round(job_comp / job_raw, 4),
-        "kernel_ms": {"k_gst_encode": round(walk_kms, 3), "k_gst_emit": round(emit_kms, 3), "k_decode": round(dec_kms, 3)},
-        "getitem_split_ms": {k: round(v, 3) for k, v in get_split.items()},
-        "gather_ms": round(float(np.mean([r["gather_ms"] for r in runs])), 3),
-        "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 3), "peak": PEAK_HBM_GBPS,
-                     "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBPS, 6), "traffic": tr},
-        "roofline_other": {"kernel": "k_decode" if dominant == "k_gst_encode" else "k_gst_encode",
-                           "achieved": round(dec_gbps if dominant == "k_gst_encode" else set_gbps, 3),
-                           "unit": "GB/s"},
-        "roofline_emit": {"kernel": "k_gst_emit", "achieved": round(emit_gbps, 3), "unit": "GB/s",
-                          "frac": round(emit_gbps / PEAK_HBM_GBPS, 6)},
-        "ub_reads": int(stats["ub_reads"]),
     }
+    for k in ("setitem_MBps", "getitem_MBps", "getitem_exact_MBps", "compression_ratio", "kernel_ms",
+              "roofline", "roofline_kernels_GBps", "gather_ms", "parity_counts"):
+        if k in main_sum:
+            line[k] = main_sum[k]
+    line["getitem_split_ms"] = {k: round(v, 3) for k, v in get_split.items()}
+    line["ub_reads"] = int(st.stats()["ub_reads"])
+    if per_config:
+        line["per_config"] = per_config
     if not a.no_cpu and world == 1:
-        cb = cpu_baseline(corpus, a.rps, a.cpu_seconds)
+        cb = cpu_baseline(corpus, rps, a.cpu_seconds)
         # parity spot-check: the sampled shards' compressed bytes and compat getitems
         res = runs[-1]["res"]
         eq_c = eq_g = tot_c = 0
@@ -322,19 +455,20 @@ def main():
                                 "set_MBps": round(cb["set_MBps"], 4), "get_MBps": round(cb["get_MBps"], 4),
                                 "cores": 1, "kind": "port",
                                 "sample": f"first {cb['records']} records ({cb['raw'] / 1e6:.1f} MB) of the same "
-                                          f"corpus, same {a.rps}-record shards, oracle/pxo.cpp single-threaded, "
+                                          f"corpus, same {rps}-record shards, oracle/pxo.cpp single-threaded, "
                                           f"{cb['seconds']:.1f} s"}
         line["parity_sample"] = {"records": tot_c, "compressed_equal": eq_c, "getitem_equal": eq_g}
-        mt = cpu_baseline_mt(corpus, a.rps, cb["set_MBps"], a.cpu_seconds / 2)
+        mt = cpu_baseline_mt(corpus, rps, cb["set_MBps"], a.cpu_seconds / 2)
         line["cpu_baseline_mt"] = {"value": round(mt["set_MBps"] + mt["get_MBps"], 4), "unit": "MB/s",
                                    "set_MBps": round(mt["set_MBps"], 4), "get_MBps": round(mt["get_MBps"], 4),
                                    "cores": mt["threads"], "kind": "port",
                                    "sample": f"{mt['records']} records ({mt['raw'] / 1e6:.1f} MB), one oracle "
-                                             f"instance per {a.rps}-record shard, {mt['threads']} threads, "
+                                             f"instance per {rps}-record shard, {mt['threads']} threads, "
                                              f"{mt['seconds']:.1f} s"}
     if not a.no_pcie and world == 1:
-        line["pcie_inclusive"] = pcie_leg(st, px, corpus, keys_host, out_cap)
+        line["pcie_inclusive"] = pcie_leg(st, px, corpus, r["keys_host"], r["out_cap"])
     print(json.dumps(line), flush=True)
+    st.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -21,6 +21,7 @@
  *   px_iter ................... PiXiuCtrl::iter -> CBTGen           (PiXiuCtrl.cpp:71-75, CritBitTree.h:55-157)
  *   px_parse_batch ............ PiXiuStr::parse(from,to,chunk)      (PiXiuStr.cpp:166-176)
  *   px_export ................. cbt_chunk->getitem(idx) bytes       (PiXiuStr.cpp:202-206, main.cpp:67)
+ *   px_save / px_load ......... (none: the reference has no persistence; chunk blob v1)
  *
  * All calls are synchronous on the context's HIP stream.  A context is not
  * thread-safe; distinct contexts are fully independent (no globals).
@@ -149,6 +150,27 @@ int px_last_store(px_ctx *ctx, uint8_t *dst, uint64_t cap, int dst_on_device, ui
  * new read-only shard (chunk 0, slots 0..n-1), e.g. records exported by px_export.
  * They can then be expanded with px_parse_batch. */
 int px_import_chunk(px_ctx *ctx, uint32_t n, const uint8_t *comp, const uint64_t *off, uint32_t *shard);
+
+/* Chunk blob: the wire / on-disk format of stored records (v1; SURVEY.md §8f row 3 --
+ * the reference keeps everything in memory and has no such format).  Little-endian:
+ *   header  64 B : u32 magic "PXCB" (0x42435850), u32 version (1), u32 n_chunks,
+ *                  u32 n_records, u64 data_off, u64 data_bytes, u32 flags, 28 B zero
+ *   chunks  16 B : u32 shard (source shard id), u32 chunk (sequence in that shard),
+ *                  u32 first (index of its first record), u32 n (records, <= 65,535)
+ *   records 16 B : u64 off (into data), u32 comp_len, u32 doc_len | 1 << 31 (dead)
+ *   data         : every record's compressed bytes (8-byte aligned), at data_off
+ * Record i of a chunk is the chunk-local slot `idx` that references point at, so a
+ * chunk's records decode on their own (no cross-chunk references).
+ *
+ * px_save writes every chunk of the context (dst NULL: *bytes = size needed;
+ * PX_ESPACE if cap is short).  px_load adds a blob's chunks as read-only chunks and
+ * indexes their live records (CritBit over the decoded key prefixes): getitem,
+ * contains, iter and delitem then work on them.  Each source shard becomes a new
+ * shard (*first_shard = the first one); a records_per_shard = 0 context must be
+ * empty and takes every chunk into its single shard.  Records set after a load start
+ * a fresh chunk (the suffix tree of a loaded chunk is not rebuilt). */
+int px_save(px_ctx *ctx, uint8_t *dst, uint64_t cap, int dst_on_device, uint64_t *bytes);
+int px_load(px_ctx *ctx, const uint8_t *src, uint64_t len, int src_on_device, uint32_t *first_shard);
 
 /* Drop every stored record (PiXiuCtrl::free_prop + init_prop, PiXiuCtrl.cpp:77-86) while
  * keeping the context's device memory for reuse. */

@@ -74,7 +74,7 @@ REC_DTYPE = np.dtype([("shard", "<u4"), ("chunk", "<u4"), ("idx", "<u4"), ("from
 # every symbol include/pixiu_amd.h declares
 EXPORTS = ["px_open", "px_close", "px_strerror", "px_set_batch", "px_get_batch", "px_parse_batch",
            "px_contains_batch", "px_del_batch", "px_export", "px_stats_get", "px_stream", "px_reset",
-           "px_last_store", "px_import_chunk", "px_iter"]
+           "px_last_store", "px_import_chunk", "px_iter", "px_save", "px_load"]
 
 _LIB = None
 
@@ -107,6 +107,8 @@ def load_library() -> C.CDLL:
     lib.px_last_store.argtypes = [vp, vp, u64, i32, vp]
     lib.px_import_chunk.argtypes = [vp, u32, vp, vp, vp]
     lib.px_iter.argtypes = [vp, vp, u64, vp, u32, vp]
+    lib.px_save.argtypes = [vp, vp, u64, i32, vp]
+    lib.px_load.argtypes = [vp, vp, u64, i32, vp]
     _LIB = lib
     return lib
 
@@ -303,6 +305,40 @@ class Store:
         rc = self._lib.px_import_chunk(self._h, len(recs), _ptr(buf), _ptr(off), _ptr(sid))
         if rc != PX_OK:
             raise PxError(rc, "px_import_chunk")
+        return int(sid[0])
+
+    # ------------------------------------------------------------ chunk blob (v1)
+    def save(self) -> bytes:
+        """Every stored chunk as one blob (include/pixiu_amd.h; pixiu_amd/blob.py reads it)."""
+        b = np.zeros(1, np.uint64)
+        rc = self._lib.px_save(self._h, None, 0, 0, _ptr(b))
+        if rc != PX_OK:
+            raise PxError(rc, "px_save")
+        out = np.zeros(max(int(b[0]), 1), np.uint8)
+        rc = self._lib.px_save(self._h, _ptr(out), out.nbytes, 0, _ptr(b))
+        if rc != PX_OK:
+            raise PxError(rc, "px_save")
+        return out[:int(b[0])].tobytes()
+
+    def save_device(self, dst_ptr: int, cap: int) -> int:
+        """Write the blob into a device buffer; returns its size (cap 0: size only)."""
+        b = np.zeros(1, np.uint64)
+        rc = self._lib.px_save(self._h, dst_ptr if cap else None, cap, 1, _ptr(b))
+        if rc != PX_OK:
+            raise PxError(rc, "px_save")
+        return int(b[0])
+
+    def load(self, blob, on_device: bool = False, length: int = 0) -> int:
+        """Add a blob's chunks (host bytes, or a device pointer + length); returns the
+        first new shard id."""
+        sid = np.zeros(1, np.uint32)
+        if on_device:
+            rc = self._lib.px_load(self._h, blob, length, 1, _ptr(sid))
+        else:
+            buf = np.frombuffer(blob, np.uint8)
+            rc = self._lib.px_load(self._h, _ptr(buf), buf.nbytes, 0, _ptr(sid))
+        if rc != PX_OK:
+            raise PxError(rc, "px_load")
         return int(sid[0])
 
     def reset(self):

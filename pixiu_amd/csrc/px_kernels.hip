@@ -113,9 +113,12 @@ __device__ unsigned long long g_prof[P_N];
 
 // ====================================================================== escape
 // One wave per record (grid-stride).  doc_len = esc(k)+2 (+ esc(v)+2 when vlen>0).
+// It also defines every per-record result word of the batch (status OK / EINVAL,
+// comp_len, chunk and slot all-ones) so no value can survive from an earlier batch
+// that used the same scratch: each later kernel overwrites them, never relies on them.
 __global__ void __launch_bounds__(256) k_doc_len(uint32_t n, const uint8_t *keys, const uint64_t *koff,
                                                  const uint8_t *vals, const uint64_t *voff,
-                                                 uint32_t *doc_len) {
+                                                 uint32_t *doc_len, uint32_t *rec_init) {
     const uint32_t lane = lane_id();
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);
     for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < n; r += waves) {
@@ -127,7 +130,14 @@ __global__ void __launch_bounds__(256) k_doc_len(uint32_t n, const uint8_t *keys
         if (lane == 0) {
             uint64_t kl = kb - ka, vl = vb - va;
             uint64_t len = kl + 2 + (vl ? vl + 2 : 0) + cnt;
-            doc_len[r] = (kl == 0 || len > (uint64_t)kMaxDoc) ? 0xffffffffu : (uint32_t)len;
+            const bool bad = kl == 0 || len > (uint64_t)kMaxDoc;
+            doc_len[r] = bad ? 0xffffffffu : (uint32_t)len;
+            if (rec_init) {  // [comp_len | chunk | idx | status] x n, after doc_len
+                rec_init[r] = 0xffffffffu;
+                rec_init[n + r] = 0xffffffffu;
+                rec_init[2 * n + r] = 0xffffffffu;
+                rec_init[3 * n + r] = bad ? (uint32_t)kErrInval : (uint32_t)kOk;
+            }
         }
     }
 }
@@ -2077,10 +2087,10 @@ __global__ void __launch_bounds__(256) k_rehash(const uint4 *old_tab, uint32_t o
 namespace px {
 
 hipError_t launch_doc_len(hipStream_t s, uint32_t n, const uint8_t *keys, const uint64_t *koff,
-                          const uint8_t *vals, const uint64_t *voff, uint32_t *doc_len) {
+                          const uint8_t *vals, const uint64_t *voff, uint32_t *doc_len, uint32_t *rec_init) {
     if (!n) return hipSuccess;
     uint32_t blocks = min((n + 3) / 4, 8192u);
-    k_doc_len<<<blocks, 256, 0, s>>>(n, keys, koff, vals, voff, doc_len);
+    k_doc_len<<<blocks, 256, 0, s>>>(n, keys, koff, vals, voff, doc_len, rec_init);
     return hipGetLastError();
 }
 

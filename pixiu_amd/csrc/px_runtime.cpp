@@ -24,7 +24,7 @@
 
 namespace px {
 hipError_t launch_doc_len(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, const uint8_t *,
-                          const uint64_t *, uint32_t *);
+                          const uint64_t *, uint32_t *, uint32_t *);
 hipError_t launch_doc_write(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, const uint8_t *,
                             const uint64_t *, uint8_t *const *);
 hipError_t launch_shard_init(hipStream_t, uint32_t, const ShardInit *);
@@ -72,6 +72,18 @@ inline void set_nseg(RecSlot &s, uint32_t tok) {
         s.lane = nullptr;  // lane entries need monotone 16-bit source coordinates
     }
 }
+// set batches with more raw bytes than this (when one shard may take them all) are
+// processed in pieces; a shard's live chunk text plus its batch must stay below
+// kMaxShardText (32-bit text offsets through a 2^31-byte buffer resource)
+constexpr uint64_t kMaxBatchRaw = 512ull << 20;
+constexpr uint64_t kMaxShardText = (2ull << 30) - (64ull << 20);
+// nodes a live chunk can hold: rotation happens before a doc once MemPool has opened
+// 2,048 pools (PiXiuCtrl.cpp:13), so a doc starts with <= 2,047 x 65,535 blocks in use
+// (a node costs 5 of them, MemPool.cpp:7-37) and adds at most 2 nodes per byte.
+// Sizing node and hash sections from this bound (not from the batch bytes) keeps every
+// arena offset below 2^31 (nodes 863 MB + hash 512 MB).
+constexpr uint64_t kChunkNodeCap = (uint64_t)(kRotatePools - 1) * kPoolBlocks / kNodeBlocks + 2ull * kMaxDoc + 64;
+static_assert(kChunkNodeCap <= kMaxNodes, "node ids are 26 bits");
 inline uint64_t pow2_at_least(uint64_t v) {
     uint64_t p = 1024;
     while (p < v) p <<= 1;
@@ -320,6 +332,7 @@ struct Shard {
 
 namespace {
 px_status map_status(uint32_t s);  // device status -> px_status (defined below)
+uint32_t key_end(const uint8_t *p, uint32_t n);  // (defined below)
 }  // namespace
 
 struct px_ctx {
@@ -335,6 +348,7 @@ struct px_ctx {
     uint32_t chunk_tab_cap = 0;
     uint32_t tab_lo = ~0u, tab_hi = 0;      // chunk_tab entries not yet uploaded
     std::vector<ShardInit> pending_init;    // new shard arenas to zero (k_shard_init)
+    std::vector<std::pair<ShardState *, ShardState>> pending_state;  // states set after the zeroing (loaded shards)
     KeyMap keymap;  // raw key -> shard (multi-shard only)
     std::vector<std::pair<void *, uint64_t>> store_blocks;  // packed record stores + segment indexes
     uint8_t *last_store = nullptr;  // packed compressed bytes of the last set batch
@@ -353,8 +367,44 @@ struct px_ctx {
     // Host->device copies are staged in buffers owned until the next sync(), so the
     // caller's (pageable, possibly short-lived) source may go away immediately.
     std::vector<std::vector<uint8_t>> staged;
+    // Device->host copies never DMA into pageable memory: a small copy lands in pinned
+    // staging (pre-filled with 0xff, so a copy that did not land reads as all-ones, not
+    // as a plausible zero) and sync() moves it to its destination after the stream has
+    // drained; a large one goes through a pinned bounce buffer synchronously.  Round 1
+    // read result vectors filled by back-to-back pageable hipMemcpyAsync calls: once, a
+    // record read status 0 / comp_len 0 -- the zero-initialised vector values, i.e. a
+    // copy that had not landed.
+    struct PendingD2H {
+        void *dst;
+        const void *src;
+        size_t n;
+    };
+    std::vector<PendingD2H> pending_d2h;
+    std::vector<std::pair<uint8_t *, size_t>> pin_blocks;  // pinned staging blocks (kept)
+    size_t pin_blk = 0, pin_used = 0;
+    static constexpr size_t kPinBlock = 4u << 20;
+    uint8_t *pin_alloc(size_t n) {
+        n = round_up(n, 64);
+        while (pin_blk < pin_blocks.size() && pin_used + n > pin_blocks[pin_blk].second) {
+            ++pin_blk;
+            pin_used = 0;
+        }
+        if (pin_blk == pin_blocks.size()) {
+            void *p = nullptr;
+            const size_t sz = std::max(n, kPinBlock);
+            if (hipHostMalloc(&p, sz, hipHostMallocDefault) != hipSuccess) throw PxFail{PX_ENOMEM};
+            pin_blocks.emplace_back(static_cast<uint8_t *>(p), sz);
+            pin_used = 0;
+        }
+        uint8_t *p = pin_blocks[pin_blk].first + pin_used;
+        pin_used += n;
+        return p;
+    }
     void sync() {
         hcheck(hipStreamSynchronize(stream));
+        for (const PendingD2H &c : pending_d2h) std::memcpy(c.dst, c.src, c.n);
+        pending_d2h.clear();
+        pin_blk = pin_used = 0;
         staged.clear();
     }
     void h2d(void *d, const void *h, size_t n) {
@@ -389,7 +439,26 @@ struct px_ctx {
         }
     }
     void d2h(void *h, const void *d, size_t n) {
-        if (n) hcheck(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, stream));
+        if (!n) return;
+        if (n <= kPinBlock / 4) {
+            uint8_t *p = pin_alloc(n);
+            std::memset(p, 0xff, n);
+            hcheck(hipMemcpyAsync(p, d, n, hipMemcpyDeviceToHost, stream));
+            pending_d2h.push_back(PendingD2H{h, p, n});
+            return;
+        }
+        // large: through one pinned bounce block, piece by piece (synchronous)
+        sync();
+        uint8_t *bounce = pin_alloc(kPinBlock);
+        auto *dst = static_cast<uint8_t *>(h);
+        const auto *src = static_cast<const uint8_t *>(d);
+        for (size_t o = 0; o < n; o += kPinBlock) {
+            const size_t m = std::min(kPinBlock, n - o);
+            hcheck(hipMemcpyAsync(bounce, src + o, m, hipMemcpyDeviceToHost, stream));
+            hcheck(hipStreamSynchronize(stream));
+            std::memcpy(dst + o, bounce, m);
+        }
+        pin_blk = pin_used = 0;
     }
 
     Shard &new_shard() {
@@ -455,21 +524,22 @@ struct px_ctx {
         h2d(d, pending_init.data(), pending_init.size() * sizeof(ShardInit));
         hcheck(launch_shard_init(stream, (uint32_t)pending_init.size(), d));
         pending_init.clear();
+        for (auto &ps : pending_state) h2d(ps.first, &ps.second, sizeof(ShardState));
+        pending_state.clear();
     }
 
     // (re)build a shard's arena so the next batch (B new bytes, D new docs) fits
     void shard_reserve(Shard &s, uint64_t B, uint32_t D) {
-        uint64_t need_nodes = (uint64_t)s.hs.n_nodes + 2 * B + 4;
+        uint64_t need_nodes = std::min<uint64_t>((uint64_t)s.hs.n_nodes + 2 * B + 4, kChunkNodeCap);
         uint64_t need_docs = std::min<uint64_t>((uint64_t)s.hs.n_docs + D, kChunkSlots) + 1;
         uint64_t need_text = s.text_end + B;
         uint64_t need_hash = pow2_at_least(need_nodes);  // only 3rd+ children live in the hash
-        if (need_nodes > kMaxNodes) need_nodes = kMaxNodes;
         bool fits = s.arena && need_nodes <= s.node_cap && need_docs <= s.doc_cap && need_text <= s.text_cap &&
                     need_hash <= s.hash_cap;
         if (fits) return;
         // new capacities (grow geometrically when the shard already exists)
         uint64_t g = s.arena ? 2 : 1;
-        uint64_t node_cap = std::min<uint64_t>(std::max(need_nodes, (uint64_t)s.node_cap * g), kMaxNodes);
+        uint64_t node_cap = std::min<uint64_t>(std::max(need_nodes, (uint64_t)s.node_cap * g), kChunkNodeCap);
         uint64_t doc_cap = std::min<uint64_t>(std::max(need_docs, (uint64_t)s.doc_cap * g), kChunkSlots + 1);
         uint64_t live_text = s.text_end - s.hs.ctext_off;
         uint64_t text_cap = std::max(live_text + B, s.arena ? (live_text + B) * 3 / 2 : live_text + B);
@@ -496,6 +566,8 @@ struct px_ctx {
         s.text_cap = text_cap;
         if (!o.arena) {
             pending_init.push_back(ShardInit{s.hash, s.st, hash_cap});
+            // a shard holding loaded chunks starts its GST in a fresh chunk after them
+            if (s.hs.chunk_seq) pending_state.emplace_back(s.st, s.hs);
             s.text_end = 0;
             return;
         }
@@ -949,6 +1021,7 @@ struct px_ctx {
         tab_lo = ~0u;
         tab_hi = 0;
         pending_init.clear();
+        pending_state.clear();
         keymap.clear();
         uint64_t held = heap.held();
         stats = px_stats{};
@@ -957,6 +1030,74 @@ struct px_ctx {
 
     int set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, const uint8_t *vals,
                   const uint64_t *voff, int on_device, px_set_result *res);
+    // stored records whose compat key prefix the CritBit needs (CritBitTree.cpp:27-28)
+    struct KpJob {
+        uint32_t chunk, idx, doc_len, cap;  // cap: first decode's output cap
+    };
+    // GPU-decode each record's key prefix (up to the spec-aware 251,0) into its chunk's
+    // kp table; a prefix that overran `cap` is decoded again with the whole doc's room.
+    // st[i] = kOk or the decode's failure status.
+    void decode_key_prefixes(const std::vector<KpJob> &jobs, std::vector<uint32_t> &st) {
+        st.assign(jobs.size(), kOk);
+        std::vector<DecodeQuery> q;
+        std::vector<uint32_t> qj;
+        uint64_t qo = 0;
+        for (size_t i = 0; i < jobs.size(); ++i) {
+            q.push_back(DecodeQuery{jobs[i].chunk, jobs[i].idx, 0, kMaxDoc, qo, jobs[i].cap, 0});
+            qj.push_back((uint32_t)i);
+            qo += round_up(jobs[i].cap, 16);
+        }
+        for (int pass = 0; pass < 2 && !q.empty(); ++pass) {
+            auto *kbuf = (uint8_t *)heap.alloc(qo + 64);
+            std::vector<uint32_t> ql, qs;
+            run_decode(q, kbuf, ql, qs, false);
+            std::vector<uint8_t> hk(qo);
+            d2h(hk.data(), kbuf, qo);
+            sync();
+            heap.release(kbuf, qo + 64);
+            std::vector<DecodeQuery> again;
+            std::vector<uint32_t> again_j;
+            uint64_t ao = 0;
+            for (size_t i = 0; i < q.size(); ++i) {
+                const KpJob &j = jobs[qj[i]];
+                const uint8_t *p = hk.data() + q[i].out_off;
+                uint32_t ke = key_end(p, ql[i]);
+                if (qs[i] != kOk && qs[i] != kErrSpace) {
+                    st[qj[i]] = qs[i];
+                    continue;
+                }
+                if (ke == 0 && qs[i] == kErrSpace && pass == 0) {  // decoded key ran past the cap
+                    DecodeQuery d = q[i];
+                    d.out_off = ao;
+                    d.out_cap = j.doc_len + 256;
+                    ao += round_up(d.out_cap, 16);
+                    again.push_back(d);
+                    again_j.push_back(qj[i]);
+                    continue;
+                }
+                uint32_t keep = ke ? ke : ql[i];
+                Chunk &ch = chunks[j.chunk];
+                ch.kp_off[j.idx] = ch.kp.size();
+                ch.kp_len[j.idx] = keep;
+                ch.kp.append(reinterpret_cast<const char *>(p), keep);
+            }
+            q.swap(again);
+            qj.swap(again_j);
+            qo = ao;
+        }
+    }
+    // chunk blob (include/pixiu_amd.h: px_save / px_load)
+    int save(uint8_t *dst, uint64_t cap, int dst_on_device, uint64_t *bytes);
+    int load(const uint8_t *src, uint64_t len, int src_on_device, uint32_t *first_shard);
+    // PX_DEBUG_POISON=1: fill the batch scratch with garbage before each set batch (tests
+    // that no per-record result depends on what an earlier batch left there)
+    static bool debug_poison() {
+        const char *e = std::getenv("PX_DEBUG_POISON");
+        return e && *e && *e != '0';
+    }
+    ~px_ctx() {
+        for (auto &b : pin_blocks) (void)hipHostFree(b.first);
+    }
     int expand(const std::vector<DecodeQuery> &q0, uint8_t *out, uint64_t out_cap, int out_on_device,
                uint64_t *out_off, uint32_t *out_len, uint32_t *status, uint64_t *needed,
                const std::vector<uint32_t> &pre_status);
@@ -995,6 +1136,32 @@ uint32_t key_end(const uint8_t *p, uint32_t n) {
 int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, const uint8_t *vals,
                       const uint64_t *voff, int on_device, px_set_result *res) {
     if (n == 0) return PX_OK;
+    // A shard's text is addressed with 32-bit offsets from its live chunk (buffer
+    // resources of 2^31 bytes): a batch that could put more than kMaxBatchRaw raw
+    // bytes (<= 2x that escaped) into one shard is processed in pieces, in order --
+    // the same records in the same order, so the same result.
+    if (n > 1 && (opts.records_per_shard == 0 || opts.records_per_shard > 4096)) {
+        std::vector<uint64_t> ko(n + 1), vo(n + 1);
+        if (on_device) {
+            d2h(ko.data(), koff, (size_t)(n + 1) * 8);
+            d2h(vo.data(), voff, (size_t)(n + 1) * 8);
+            sync();
+        } else {
+            std::memcpy(ko.data(), koff, (size_t)(n + 1) * 8);
+            std::memcpy(vo.data(), voff, (size_t)(n + 1) * 8);
+        }
+        if ((ko[n] - ko[0]) + (vo[n] - vo[0]) > kMaxBatchRaw) {
+            int rc = PX_OK;
+            for (uint32_t a = 0; a < n;) {
+                uint32_t b = a + 1;
+                while (b < n && (ko[b + 1] - ko[a]) + (vo[b + 1] - vo[a]) <= kMaxBatchRaw) ++b;
+                const int r2 = set_batch(b - a, keys, koff + a, vals, voff + a, on_device, res ? res + a : nullptr);
+                if (rc == PX_OK) rc = r2;
+                a = b;
+            }
+            return rc;
+        }
+    }
     // ---- inputs on device; raw keys also on host (the CritBit needs them)
     std::vector<uint64_t> hkoff(n + 1), hvoff(n + 1);
     const uint8_t *dkeys, *dvals;
@@ -1045,7 +1212,8 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     auto *tmp = (uint32_t *)tmp_buf.get((uint64_t)n * 28 + 64);
     uint32_t *d_doclen = tmp, *d_complen = tmp + n, *d_chunk = tmp + 2 * n, *d_idx = tmp + 3 * n,
              *d_status = tmp + 4 * n, *d_nseg = tmp + 5 * n, *d_nesc = tmp + 6 * n;
-    hcheck(launch_doc_len(stream, n, dkeys, dkoff, dvals, dvoff, d_doclen));
+    if (debug_poison()) hcheck(hipMemsetAsync(tmp, 0xa5, (size_t)n * 28 + 64, stream));  // stale-scratch test
+    hcheck(launch_doc_len(stream, n, dkeys, dkoff, dvals, dvoff, d_doclen, d_complen));
     std::vector<uint32_t> doc_len(n);
     d2h(doc_len.data(), d_doclen, n * 4);
     sync();
@@ -1076,6 +1244,11 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             work.back().docs++;
         }
     }
+    for (const Work &w : work)  // a live chunk + batch beyond 32-bit text offsets (pathological)
+        if (w.s->text_end - w.s->hs.ctext_off + w.bytes > kMaxShardText) {
+            for (const Work &u : work) u.s->records -= u.r1 - u.r0;
+            return PX_ECAPACITY;
+        }
 
     // ---- arenas, doc destinations, comp scratch
     std::vector<uint8_t *> dst(n, nullptr), cdst(n, nullptr);
@@ -1140,20 +1313,29 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     std::vector<ShardState> stout(gs.size());
     d2h(stout.data(), d_stout, gs.size() * sizeof(ShardState));
     sync();
-    // Invariant: a walked record has a non-empty compressed form (a doc is >= 3 bytes).
-    // A violation was seen once in the GPU suite and never reproduced (4,969-batch
-    // stress, tools/fuzz_stress.py); re-read the record's length and status, say so
-    // on stderr, and fail the record rather than store it empty.
+    // Invariants of the walk + encoder: a record the walk placed (chunk/slot written)
+    // has a compressed form of 1..2*doc_len+8 bytes; a record it did not place has a
+    // non-OK status.  Every word was defined by k_doc_len for this batch, so a
+    // violation is a kernel or transfer bug: fail loudly, never repair.
+    int corrupt = 0;
     for (uint32_t r = 0; r < n; ++r) {
-        if (doc_len[r] == 0xffffffffu || rstatus[r] != kOk || comp_len[r] != 0) continue;
-        uint32_t cl = 0, rs = 0;
-        d2h(&cl, d_complen + r, 4);
-        d2h(&rs, d_status + r, 4);
-        sync();
-        fprintf(stderr, "pixiu_amd: record %u of a %u-record batch: status 0 with comp_len 0 (doc %u B); "
-                        "re-read comp_len %u status %u\n", r, n, doc_len[r], cl, rs);
-        comp_len[r] = cl;
-        rstatus[r] = rs != kOk ? rs : (cl ? (uint32_t)kOk : (uint32_t)kErrCapacity);
+        const bool valid = doc_len[r] != 0xffffffffu;
+        const bool placed = rchunk[r] != 0xffffffffu && ridx[r] != 0xffffffffu;
+        bool bad = false;
+        if (placed) bad = !valid || comp_len[r] == 0 || comp_len[r] > 2 * doc_len[r] + 8 || rstatus[r] > kErrSpace;
+        else bad = rstatus[r] == kOk || (valid && rstatus[r] > kErrSpace);
+        if (bad) {
+            fprintf(stderr, "pixiu_amd: internal error: record %u of a %u-record batch: doc %u B, placed %d "
+                            "(chunk %u slot %u), status %u, comp_len %u\n",
+                    r, n, doc_len[r], (int)placed, rchunk[r], ridx[r], rstatus[r], comp_len[r]);
+            if (!placed) rstatus[r] = kErrCorrupt;
+            else if (rstatus[r] == kOk) rstatus[r] = kErrCorrupt;
+            corrupt = PX_ECORRUPT;
+        }
+    }
+    if (const char *e = std::getenv("PX_DEBUG_FAIL_REC")) {  // test hook: fail one placed record
+        const uint32_t r = (uint32_t)std::atoi(e);
+        if (r < n && rstatus[r] == kOk) rstatus[r] = kErrCorrupt;
     }
     for (size_t k = 0; k < work.size(); ++k) work[k].s->hs = stout[k];
     {
@@ -1167,9 +1349,17 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     }
 
     // ---- packed store + segment index
+    // Every record the walk placed gets its bytes stored and its slot registered, even
+    // if it failed later (emit / tokenize / the check above): later records of its
+    // chunk may reference it, and the chunk's slot numbering must stay in step with
+    // the device's.  A failed record is registered dead (not indexed).
+    std::vector<uint8_t> placed(n);
+    for (uint32_t r = 0; r < n; ++r)
+        placed[r] = rchunk[r] != 0xffffffffu && ridx[r] != 0xffffffffu && doc_len[r] != 0xffffffffu &&
+                    comp_len[r] <= 2 * doc_len[r] + 8;
     std::vector<uint64_t> coff(n + 1, 0), soff(n + 1, 0), poff(n + 1, 0);
     for (uint32_t r = 0; r < n; ++r) {
-        bool ok = doc_len[r] != 0xffffffffu && rstatus[r] == kOk;
+        bool ok = placed[r];
         coff[r + 1] = coff[r] + (ok ? round_up(comp_len[r], 8) : 0);
         // a failed record still gets one entry: k_tokenize writes its end sentinel
         soff[r + 1] = soff[r] + (ok ? seg_entries(nesc[r]) : 1) * sizeof(SegEnt);
@@ -1190,7 +1380,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     hcheck(launch_compact(stream, n, d_cdst, d_complen, store, d_coff));
     std::vector<RecSlot> slots(n);
     for (uint32_t r = 0; r < n; ++r) {
-        bool ok = doc_len[r] != 0xffffffffu && rstatus[r] == kOk;
+        bool ok = placed[r];
         slots[r].comp = store + coff[r];
         slots[r].seg = (const SegEnt *)(segs + soff[r]);
         slots[r].pidx = (const uint16_t *)(segs + soff[n] + poff[r]);
@@ -1217,30 +1407,34 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     heap.release(d_slots, (uint64_t)n * sizeof(RecSlot));
 
     // ---- register records in their chunks
-    std::vector<uint32_t> rgchunk(n, kNone);
+    std::vector<uint32_t> rgchunk(n, kNone);  // chunk of every placed record
+    std::vector<uint8_t> live(n, 0);          // placed, OK and indexed
     for (uint32_t r = 0; r < n; ++r) {
         if (doc_len[r] == 0xffffffffu) rstatus[r] = kErrInval;
-        if (rstatus[r] != kOk) continue;
-        if (tstat[r] != kOk) {
-            rstatus[r] = tstat[r];
-            continue;
-        }
+        if (!placed[r]) continue;
+        if (rstatus[r] == kOk && tstat[r] != kOk) rstatus[r] = tstat[r];
         Shard &s = *shards[rec_shard[r]];
         while (s.chunks.size() <= rchunk[r]) s.chunks.push_back(new_chunk(s.id));
         uint32_t c = s.chunks[rchunk[r]];
         Chunk &ch = chunks[c];
-        if (ridx[r] != ch.n) {
-            rstatus[r] = kErrCapacity;  // slot order broken: cannot happen
+        if (ridx[r] != ch.n) {  // the device numbered slots differently: fail loudly
+            fprintf(stderr, "pixiu_amd: internal error: record %u placed at slot %u of chunk %u holding %u\n", r,
+                    ridx[r], rchunk[r], ch.n);
+            rstatus[r] = kErrCorrupt;
+            corrupt = PX_ECORRUPT;
             continue;
         }
+        const bool ok = rstatus[r] == kOk;
         set_nseg(slots[r], nseg[r]);
         ch.slots.push_back(slots[r]);
         ch.doc_len.push_back(doc_len[r]);
-        ch.dead.push_back(0);
+        ch.dead.push_back(ok ? 0 : 1);
         ch.kp_off.push_back(0);
         ch.kp_len.push_back(0);
         ch.n++;
         rgchunk[r] = c;
+        live[r] = ok;
+        if (!ok) continue;
         stats.records++;
         stats.raw_bytes += (hkoff[r + 1] - hkoff[r]) + (hvoff[r + 1] - hvoff[r]);
         stats.doc_bytes += doc_len[r];
@@ -1278,61 +1472,31 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     }
 
     // ---- compat key prefixes (GPU decode of each new record's key region)
-    std::vector<DecodeQuery> q;
-    std::vector<uint32_t> qrec;
-    uint64_t qo = 0;
-    for (uint32_t r = 0; r < n; ++r) {
-        if (rgchunk[r] == kNone) continue;
-        uint64_t klen = hkoff[r + 1] - hkoff[r];
-        uint32_t cap = (uint32_t)std::min<uint64_t>(doc_len[r] + 64, 2 * klen + 2 + 64);
-        DecodeQuery d{rgchunk[r], ridx[r], 0, kMaxDoc, qo, cap, 0};
-        q.push_back(d);
-        qrec.push_back(r);
-        qo += round_up(cap, 16);
-    }
-    for (int pass = 0; pass < 2 && !q.empty(); ++pass) {
-        auto *kbuf = (uint8_t *)heap.alloc(qo + 64);
-        std::vector<uint32_t> ql, qs;
-        run_decode(q, kbuf, ql, qs, false);
-        std::vector<uint8_t> hk(qo);
-        d2h(hk.data(), kbuf, qo);
-        sync();
-        heap.release(kbuf, qo + 64);
-        std::vector<DecodeQuery> again;
-        std::vector<uint32_t> again_rec;
-        uint64_t ao = 0;
-        for (size_t i = 0; i < q.size(); ++i) {
-            uint32_t r = qrec[i];
-            const uint8_t *p = hk.data() + q[i].out_off;
-            uint32_t ke = key_end(p, ql[i]);
-            if (qs[i] != kOk && qs[i] != kErrSpace) {
-                rstatus[r] = qs[i];
-                continue;
-            }
-            if (ke == 0 && qs[i] == kErrSpace && pass == 0) {  // decoded key ran past the cap
-                DecodeQuery d = q[i];
-                d.out_off = ao;
-                d.out_cap = doc_len[r] + 256;
-                ao += round_up(d.out_cap, 16);
-                again.push_back(d);
-                again_rec.push_back(r);
-                continue;
-            }
-            uint32_t keep = ke ? ke : ql[i];
-            Chunk &ch = chunks[rgchunk[r]];
-            ch.kp_off[ridx[r]] = ch.kp.size();
-            ch.kp_len[ridx[r]] = keep;
-            ch.kp.append(reinterpret_cast<const char *>(p), keep);
+    {
+        std::vector<KpJob> jobs;
+        std::vector<uint32_t> jrec;
+        for (uint32_t r = 0; r < n; ++r) {
+            if (!live[r]) continue;
+            uint64_t klen = hkoff[r + 1] - hkoff[r];
+            jobs.push_back(KpJob{rgchunk[r], ridx[r], doc_len[r],
+                                 (uint32_t)std::min<uint64_t>(doc_len[r] + 64, 2 * klen + 2 + 64)});
+            jrec.push_back(r);
         }
-        q.swap(again);
-        qrec.swap(again_rec);
-        qo = ao;
+        std::vector<uint32_t> kst;
+        decode_key_prefixes(jobs, kst);
+        for (size_t i = 0; i < jobs.size(); ++i)
+            if (kst[i] != kOk) {
+                const uint32_t r = jrec[i];
+                rstatus[r] = kst[i];
+                chunks[rgchunk[r]].dead[ridx[r]] = 1;
+                live[r] = 0;
+            }
     }
 
     // ---- CritBit inserts (per shard, in arrival order)
     std::vector<uint32_t> replaced(n, 0);
     for (uint32_t r = 0; r < n; ++r) {
-        if (rgchunk[r] == kNone || rstatus[r] != kOk) continue;
+        if (!live[r]) continue;
         Shard &s = *shards[rec_shard[r]];
         const uint8_t *kp = hkeys.data() + hkoff[r];
         uint64_t klen = hkoff[r + 1] - hkoff[r];
@@ -1349,7 +1513,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     }
 
     // ---- results
-    int rc = PX_OK;
+    int rc = corrupt;
     uint64_t ub = 0;
     for (auto &sp : shards) ub += sp->hs.ub_reads;
     stats.ub_reads = ub;
@@ -1423,6 +1587,290 @@ int px_ctx::expand(const std::vector<DecodeQuery> &q0, uint8_t *out, uint64_t ou
         d2h(out, dout, total);
         sync();
     }
+    return rc;
+}
+
+// ====================================================================== chunk blob
+// Wire / on-disk format v1 of stored records (include/pixiu_amd.h px_save; SURVEY.md
+// §8f row 3 -- the reference has no persistence).  Little-endian:
+//   BlobHeader (64 B) | BlobChunk x n_chunks | BlobRec x n_records | data
+// data holds every record's compressed bytes, each 8-byte aligned, in chunk order.
+namespace {
+constexpr uint32_t kBlobMagic = 0x42435850u;  // "PXCB"
+constexpr uint32_t kBlobVersion = 1;
+constexpr uint32_t kBlobDead = 1u << 31;  // BlobRec::doc_len flag: deleted / failed record
+struct BlobHeader {
+    uint32_t magic, version, n_chunks, n_records;
+    uint64_t data_off, data_bytes;
+    uint32_t flags, pad[7];
+};
+struct BlobChunk {
+    uint32_t shard, seq, first, n;  // source shard, chunk sequence in it, first record, records
+};
+struct BlobRec {
+    uint64_t off;  // into data
+    uint32_t comp_len, doc_len;  // doc_len | kBlobDead
+};
+static_assert(sizeof(BlobHeader) == 64 && sizeof(BlobChunk) == 16 && sizeof(BlobRec) == 16, "blob layout");
+}  // namespace
+
+int px_ctx::save(uint8_t *dst, uint64_t cap, int dst_on_device, uint64_t *bytes) {
+    std::vector<BlobChunk> bc;
+    std::vector<BlobRec> br;
+    std::vector<const uint8_t *> src;
+    uint64_t data = 0;
+    for (auto &sp : shards)
+        for (uint32_t seq = 0; seq < sp->chunks.size(); ++seq) {
+            const Chunk &ch = chunks[sp->chunks[seq]];
+            if (!ch.n) continue;
+            bc.push_back(BlobChunk{sp->id, seq, (uint32_t)br.size(), ch.n});
+            for (uint32_t i = 0; i < ch.n; ++i) {
+                const RecSlot &sl = ch.slots[i];
+                br.push_back(BlobRec{data, sl.comp_len, ch.doc_len[i] | (ch.dead[i] ? kBlobDead : 0u)});
+                src.push_back(sl.comp);
+                data += round_up(sl.comp_len, 8);
+            }
+        }
+    BlobHeader h{};
+    h.magic = kBlobMagic;
+    h.version = kBlobVersion;
+    h.n_chunks = (uint32_t)bc.size();
+    h.n_records = (uint32_t)br.size();
+    h.data_off = round_up(sizeof(BlobHeader) + bc.size() * sizeof(BlobChunk) + br.size() * sizeof(BlobRec), 64);
+    h.data_bytes = data;
+    const uint64_t total = h.data_off + data;
+    if (bytes) *bytes = total;
+    if (!dst) return PX_OK;
+    if (cap < total) return PX_ESPACE;
+    std::vector<uint8_t> head(h.data_off, 0);
+    std::memcpy(head.data(), &h, sizeof h);
+    std::memcpy(head.data() + sizeof h, bc.data(), bc.size() * sizeof(BlobChunk));
+    std::memcpy(head.data() + sizeof h + bc.size() * sizeof(BlobChunk), br.data(), br.size() * sizeof(BlobRec));
+    // pack the records' bytes on the device (k_compact), then place the blob
+    uint8_t *pack = dst_on_device ? dst : (uint8_t *)heap.alloc(total + 64);
+    const uint32_t n = h.n_records;
+    if (n) {
+        auto *d_src = (uint8_t **)heap.alloc((uint64_t)n * 8);
+        auto *d_len = (uint32_t *)heap.alloc((uint64_t)n * 4);
+        auto *d_off = (uint64_t *)heap.alloc((uint64_t)n * 8);
+        std::vector<uint32_t> len(n);
+        std::vector<uint64_t> off(n);
+        for (uint32_t i = 0; i < n; ++i) {
+            len[i] = br[i].comp_len;
+            off[i] = br[i].off;
+        }
+        h2d(d_src, src.data(), (size_t)n * 8);
+        h2d(d_len, len.data(), (size_t)n * 4);
+        h2d(d_off, off.data(), (size_t)n * 8);
+        hcheck(launch_compact(stream, n, d_src, d_len, pack + h.data_off, d_off));
+        sync();
+        heap.release(d_src, (uint64_t)n * 8);
+        heap.release(d_len, (uint64_t)n * 4);
+        heap.release(d_off, (uint64_t)n * 8);
+    }
+    if (dst_on_device) {
+        h2d(dst, head.data(), head.size());
+        sync();
+    } else {
+        std::memcpy(dst, head.data(), head.size());
+        d2h(dst + h.data_off, pack + h.data_off, data);
+        sync();
+        heap.release(pack, total + 64);
+    }
+    return PX_OK;
+}
+
+int px_ctx::load(const uint8_t *src, uint64_t len, int src_on_device, uint32_t *first_shard) {
+    if (len < sizeof(BlobHeader)) return PX_EINVAL;
+    BlobHeader h;
+    if (src_on_device) {
+        d2h(&h, src, sizeof h);
+        sync();
+    } else {
+        std::memcpy(&h, src, sizeof h);
+    }
+    const uint64_t tables = sizeof(BlobHeader) + (uint64_t)h.n_chunks * sizeof(BlobChunk) +
+                            (uint64_t)h.n_records * sizeof(BlobRec);
+    if (h.magic != kBlobMagic || h.version != kBlobVersion || h.data_off < tables || h.data_off > len ||
+        h.data_bytes > len - h.data_off)
+        return PX_EINVAL;
+    std::vector<uint8_t> tab(tables);
+    if (src_on_device) {
+        d2h(tab.data(), src, tables);
+        sync();
+    } else {
+        std::memcpy(tab.data(), src, tables);
+    }
+    std::vector<BlobChunk> bc(h.n_chunks);
+    std::vector<BlobRec> br(h.n_records);
+    std::memcpy(bc.data(), tab.data() + sizeof h, bc.size() * sizeof(BlobChunk));
+    std::memcpy(br.data(), tab.data() + sizeof h + bc.size() * sizeof(BlobChunk), br.size() * sizeof(BlobRec));
+    // validate: chunks tile the records in order, each shard's chunks are 0..k-1
+    uint64_t next = 0;
+    std::map<uint32_t, uint32_t> seqs;  // source shard -> chunks seen
+    for (const BlobChunk &c : bc) {
+        if (c.first != next || c.n == 0 || c.n > (uint32_t)kChunkSlots || c.seq != seqs[c.shard]) return PX_EINVAL;
+        seqs[c.shard]++;
+        next += c.n;
+    }
+    if (next != h.n_records) return PX_EINVAL;
+    for (const BlobRec &r : br)
+        if ((r.doc_len & ~kBlobDead) > (uint32_t)kMaxDoc || r.comp_len > (uint32_t)kMaxDoc ||
+            r.off + r.comp_len > h.data_bytes || (r.off & 7))
+            return PX_EINVAL;
+    // single-shard stores take the blob's chunks into shard 0, which must be empty
+    if (opts.records_per_shard == 0 && !shards.empty() && shards[0]->records) return PX_EINVAL;
+    const uint32_t n = h.n_records;
+    if (!n) {
+        if (first_shard) *first_shard = (uint32_t)shards.size();
+        return PX_OK;
+    }
+    // ---- bytes to the device (one store allocation: data, then lane entries)
+    auto *d_src = (uint8_t **)heap.alloc((uint64_t)n * 8);
+    auto *d_len = (uint32_t *)heap.alloc((uint64_t)n * 8);
+    uint32_t *d_nesc = d_len + n;
+    const uint64_t data_cap = round_up(h.data_bytes + 64, 16);
+    // lane entries need the 251 counts: stage the data first, count, then size the rest
+    auto *data = (uint8_t *)heap.alloc(data_cap);
+    if (src_on_device)
+        hcheck(hipMemcpyAsync(data, src + h.data_off, h.data_bytes, hipMemcpyDeviceToDevice, stream));
+    else
+        h2d_bulk(data, src + h.data_off, h.data_bytes);
+    std::vector<uint8_t *> sp(n);
+    std::vector<uint32_t> cl(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        sp[i] = data + br[i].off;
+        cl[i] = br[i].comp_len;
+    }
+    h2d(d_src, sp.data(), (size_t)n * 8);
+    h2d(d_len, cl.data(), (size_t)n * 4);
+    hcheck(launch_count_esc(stream, n, d_src, d_len, d_nesc));
+    std::vector<uint32_t> nesc(n);
+    d2h(nesc.data(), d_nesc, (size_t)n * 4);
+    sync();
+    heap.release(d_src, (uint64_t)n * 8);
+    heap.release(d_len, (uint64_t)n * 8);
+    std::vector<uint64_t> soff(n + 1, 0), poff(n + 1, 0);
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t dl = br[i].doc_len & ~kBlobDead;
+        soff[i + 1] = soff[i] + seg_entries(nesc[i]) * sizeof(SegEnt);
+        poff[i + 1] = poff[i] + round_up(pidx_blocks(dl) * 2, 16);
+    }
+    // the store keeps data and lane entries in one allocation (LaneEnt::rel is relative)
+    const uint64_t lane_at = data_cap, store_bytes = lane_at + soff[n] / 2 + 64;
+    auto *store = (uint8_t *)heap.alloc(store_bytes);
+    hcheck(hipMemcpyAsync(store, data, h.data_bytes, hipMemcpyDeviceToDevice, stream));
+    auto *segs = (uint8_t *)heap.alloc(soff[n] + poff[n] + 64);
+    store_blocks.emplace_back(store, store_bytes);
+    store_blocks.emplace_back(segs, soff[n] + poff[n] + 64);
+    std::vector<RecSlot> slots(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t dl = br[i].doc_len & ~kBlobDead;
+        slots[i] = RecSlot{store + br[i].off, (const SegEnt *)(segs + soff[i]),
+                           (const uint16_t *)(segs + soff[n] + poff[i]), br[i].comp_len, 0, pidx_blocks(dl), 0,
+                           (const LaneEnt *)(store + lane_at + soff[i] / 2)};
+    }
+    auto *d_slots = (RecSlot *)heap.alloc((uint64_t)n * sizeof(RecSlot));
+    auto *d_tmp = (uint32_t *)heap.alloc((uint64_t)n * 8);
+    h2d(d_slots, slots.data(), (size_t)n * sizeof(RecSlot));
+    hcheck(launch_tokenize(stream, n, d_slots, d_tmp, d_tmp + n));
+    std::vector<uint32_t> nseg(n), tst(n);
+    d2h(nseg.data(), d_tmp, (size_t)n * 4);
+    d2h(tst.data(), d_tmp + n, (size_t)n * 4);
+    sync();
+    heap.release(data, data_cap);
+    heap.release(d_slots, (uint64_t)n * sizeof(RecSlot));
+    heap.release(d_tmp, (uint64_t)n * 8);
+    // ---- shards and chunks
+    const uint32_t first = (uint32_t)shards.size();
+    std::map<uint32_t, Shard *> target;  // source shard -> shard here
+    std::vector<uint32_t> rchunk(n);
+    std::vector<Shard *> rshard(n);
+    for (const BlobChunk &c : bc) {
+        Shard *s;
+        if (opts.records_per_shard == 0) {
+            s = shards.empty() ? &new_shard() : shards[0].get();
+        } else {
+            auto it = target.find(c.shard);
+            s = it != target.end() ? it->second : (target[c.shard] = &new_shard());
+        }
+        const uint32_t g = new_chunk(s->id);
+        s->chunks.push_back(g);
+        Chunk &ch = chunks[g];
+        for (uint32_t i = c.first; i < c.first + c.n; ++i) {
+            set_nseg(slots[i], nseg[i]);
+            ch.slots.push_back(slots[i]);
+            ch.doc_len.push_back(br[i].doc_len & ~kBlobDead);
+            ch.dead.push_back((br[i].doc_len & kBlobDead) || tst[i] != kOk ? 1 : 0);
+            ch.kp_off.push_back(0);
+            ch.kp_len.push_back(0);
+            rchunk[i] = g;
+            rshard[i] = s;
+        }
+        ch.n = c.n;
+        s->records += c.n;
+        // the next set batch starts this shard's GST in a fresh chunk after the loaded ones
+        s->hs.chunk_seq = (uint32_t)s->chunks.size();
+        chunk_reserve(g, c.n);
+        h2d(ch.dev, ch.slots.data(), (size_t)c.n * sizeof(RecSlot));
+    }
+    if (opts.records_per_shard != 0)  // new records go to new shards, never into a loaded one
+        for (auto &t : target) t.second->records = std::max(t.second->records, opts.records_per_shard);
+    {
+        std::vector<LinkJob> jobs;
+        for (const BlobChunk &c : bc) {
+            const uint32_t g = rchunk[c.first];
+            for (uint32_t i = 0; i < c.n; ++i) {
+                const RecSlot &sl = chunks[g].slots[i];
+                jobs.push_back(LinkJob{const_cast<SegEnt *>(sl.seg), const_cast<LaneEnt *>(sl.lane), chunks[g].dev,
+                                       sl.nseg, c.n});
+            }
+        }
+        link(jobs);
+    }
+    // ---- index the live records: compat key prefixes, then CritBit (and the key map)
+    std::vector<KpJob> jobs;
+    std::vector<uint32_t> jrec;
+    for (const BlobChunk &c : bc)
+        for (uint32_t k = 0; k < c.n; ++k) {
+            const uint32_t i = c.first + k;
+            if (chunks[rchunk[i]].dead[k]) continue;
+            const uint32_t dl = br[i].doc_len & ~kBlobDead;
+            jobs.push_back(KpJob{rchunk[i], k, dl, std::min<uint32_t>(dl + 64, 576)});
+            jrec.push_back(i);
+        }
+    std::vector<uint32_t> kst;
+    decode_key_prefixes(jobs, kst);
+    int rc = PX_OK;
+    for (size_t j = 0; j < jobs.size(); ++j) {
+        Chunk &ch = chunks[jobs[j].chunk];
+        const uint32_t k = jobs[j].idx;
+        uint32_t kl = 0;
+        const uint8_t *kp = kp_of(Leaf{jobs[j].chunk, k}, &kl);
+        if (kst[j] != kOk || kl < 2 || kp[kl - 2] != kEsc || kp[kl - 1] != kKeyEnd) {
+            ch.dead[k] = 1;  // no decodable key: not indexed
+            if (rc == PX_OK) rc = kst[j] != kOk ? (int)map_status(kst[j]) : PX_ECORRUPT;
+            continue;
+        }
+        Shard &s = *rshard[jrec[j]];
+        std::string q(reinterpret_cast<const char *>(kp), kl);
+        if (opts.records_per_shard != 0) {
+            std::string raw;  // the raw key: the escaped prefix without 251,0, 251 pairs undoubled
+            for (uint32_t b = 0; b + 2 < kl + 0u; ++b) {
+                raw.push_back((char)kp[b]);
+                if (kp[b] == kEsc) ++b;
+            }
+            const auto *rk = reinterpret_cast<const uint8_t *>(raw.data());
+            const int64_t prev = keymap.find(rk, raw.size());
+            if (prev >= 0 && (uint32_t)prev != s.id) cbt_delete(*shards[(size_t)prev], q);
+            keymap.put(rk, raw.size(), s.id);
+        }
+        if (cbt_insert(s, q, Leaf{jobs[j].chunk, k})) {
+            // a duplicate key inside the blob: the later record replaced the earlier
+        }
+    }
+    stats.chunks = chunks.size();
+    if (first_shard) *first_shard = first;
     return rc;
 }
 
@@ -1634,9 +2082,10 @@ int px_last_store(px_ctx *ctx, uint8_t *dst, uint64_t cap, int dst_on_device, ui
         if (bytes) *bytes = ctx->last_store_bytes;
         if (!dst) return PX_OK;
         if (cap < ctx->last_store_bytes) return PX_ESPACE;
-        if (ctx->last_store_bytes)
-            hcheck(hipMemcpyAsync(dst, ctx->last_store, ctx->last_store_bytes,
-                                  dst_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, ctx->stream));
+        if (ctx->last_store_bytes && dst_on_device)
+            hcheck(hipMemcpyAsync(dst, ctx->last_store, ctx->last_store_bytes, hipMemcpyDeviceToDevice, ctx->stream));
+        else
+            ctx->d2h(dst, ctx->last_store, ctx->last_store_bytes);
         ctx->sync();
         return PX_OK;
     })
@@ -1716,6 +2165,16 @@ int px_import_chunk(px_ctx *ctx, uint32_t n, const uint8_t *comp, const uint64_t
         if (shard_out) *shard_out = sh.id;
         return PX_OK;
     })
+}
+
+int px_save(px_ctx *ctx, uint8_t *dst, uint64_t cap, int dst_on_device, uint64_t *bytes) {
+    if (!ctx) return PX_EINVAL;
+    PX_GUARD(return ctx->save(dst, cap, dst_on_device, bytes);)
+}
+
+int px_load(px_ctx *ctx, const uint8_t *src, uint64_t len, int src_on_device, uint32_t *first_shard) {
+    if (!ctx || (len && !src)) return PX_EINVAL;
+    PX_GUARD(return ctx->load(src, len, src_on_device, first_shard);)
 }
 
 int px_reset(px_ctx *ctx) {

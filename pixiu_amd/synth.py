@@ -160,10 +160,10 @@ def _soup(st: Stream, nbytes: int, num_hi: int, num_frac: float) -> np.ndarray:
     return np.concatenate(out)[:nbytes]
 
 
-def config1(n: int = 1000) -> Corpus:
-    st = Stream(1, 0)
+def config1(n: int = 1000, part: int = 0) -> Corpus:
+    st = Stream(1, part * 1_000_000)
     ids = st.randint(0, 100_000_000, n)
-    keys = [b"http://www.zhihu.com/question/%08d_%d" % (int(ids[i]), i) for i in range(n)]
+    keys = [b"http://www.zhihu.com/question/%08d_%d" % (int(ids[i]), i + part * n) for i in range(n)]
     lens = st.randint(60, 80, n)
     vals = []
     for i in range(n):
@@ -174,9 +174,9 @@ def config1(n: int = 1000) -> Corpus:
     return Corpus(1, kb, ko, vb, vo)
 
 
-def config2(n: int = 100_000) -> Corpus:
-    st = Stream(2, 0)
-    keys = [b"rec/%08d" % i for i in range(n)]
+def config2(n: int = 100_000, part: int = 0) -> Corpus:
+    st = Stream(2, part * 1_000_000)
+    keys = [b"rec/%08d" % (i + part * n) for i in range(n)]
     soup = _soup(st, 1000 * n, 1000, 0.2)
     kb, ko = _csr(keys)
     vo = np.arange(n + 1, dtype=np.int64) * 1000
@@ -227,9 +227,9 @@ def config3(n: int = 10_000, value_len: int = 60_000, workers: int = 0, part: in
     return Corpus(3, kb, ko, vals, vo)
 
 
-def config4(n: int = 1_000_000, rec_len: int = 256) -> Corpus:
-    st = Stream(4, 0)
-    keys = [b"k%07d" % i for i in range(n)]
+def config4(n: int = 1_000_000, rec_len: int = 256, part: int = 0) -> Corpus:
+    st = Stream(4, part * 1_000_000)
+    keys = [b"k%07d" % (i + part * n) for i in range(n)]
     kb, ko = _csr(keys)
     vlen = rec_len - 8
     u = st.uniform(n * vlen)
@@ -239,10 +239,10 @@ def config4(n: int = 1_000_000, rec_len: int = 256) -> Corpus:
     return Corpus(4, kb, ko, vals, vo)
 
 
-def config5(n: int = 10_000, total: int = 65_531) -> Corpus:
+def config5(n: int = 10_000, total: int = 65_531, part: int = 0) -> Corpus:
     """Max-size binary records (no byte 251) with planted repeats of earlier records."""
-    st = Stream(5, 0)
-    keys = [b"bin%07d" % i for i in range(n)]
+    st = Stream(5, part * 1_000_000)
+    keys = [b"bin%07d" % (i + part * n) for i in range(n)]
     kb, ko = _csr(keys)
     vlen = total - 10
     vals = np.empty(n * vlen, np.uint8)
@@ -279,10 +279,7 @@ FULL_SIZES = {1: 1000, 2: 100_000, 3: 10_000, 4: 1_000_000, 5: 10_000}
 
 
 def make(config: int, n: int | None = None, part: int = 0) -> Corpus:
-    """Corpus of `config`; `part` selects an independent, same-shaped corpus (per rank)."""
+    """Corpus of `config`; `part` selects an independent, same-shaped corpus with
+    disjoint keys (one per rank in weak-scaling runs).  part 0 is the canonical corpus."""
     n = FULL_SIZES[config] if n is None else n
-    if config == 3:
-        return config3(n, part=part)
-    if part:
-        raise ValueError("part is only implemented for config 3")
-    return GENERATORS[config](n)
+    return GENERATORS[config](n, part=part)

@@ -102,6 +102,16 @@ class Oracle(_Runner):
             raise RuntimeError(f"pxo_encode_docs failed: {rc}")
         return [comp[coff[i]:coff[i + 1]].tobytes() for i in range(n)], ch[:n].tolist(), ix[:n].tolist()
 
+    def decode_chunk(self, recs, idx, frm=0, to=65535, mode=COMPAT) -> bytes:
+        """PiXiuStr::parse(frm, to) of record idx of a chunk given as compressed bytes."""
+        buf, off = _csr(list(recs))
+        out = C.create_string_buffer(1 << 20)
+        r = self.lib.pxo_decode_chunk(C.c_int(len(recs)), _p(buf), _p(off), C.c_int(idx), C.c_int(frm),
+                                      C.c_int(to), C.c_int(mode), out, C.c_int(len(out)))
+        if r < 0:
+            raise RuntimeError(f"pxo_decode_chunk: {r}")
+        return out.raw[:r]
+
     def escape(self, src: bytes, is_key: bool) -> bytes:
         out = C.create_string_buffer(2 * len(src) + 4)
         n = self.lib.pxo_escape(src, len(src), int(is_key), out, len(out))
@@ -195,7 +205,13 @@ class Reference(_Runner):
 
 
 def have_reference() -> bool:
-    return os.path.exists(REF_SO) and os.path.isdir("/root/reference/src")
+    """The reference build, made on demand from /root/reference/src (build container
+    only: the GPU box has no reference, and oracle/_ref never travels there)."""
+    if not os.path.isdir("/root/reference/src"):
+        return False
+    if not os.path.exists(REF_SO):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "ref"], check=False)
+    return os.path.exists(REF_SO)
 
 
 def assemble(k: bytes, v: bytes) -> bytes:

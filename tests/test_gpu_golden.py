@@ -110,7 +110,7 @@ def test_config_corpora(cfg):
         assert st.get_batch((cp.keys, cp.koff.astype(np.uint64))) == [g[go[i]:go[i + 1]].tobytes() for i in range(n)]
 
 
-@pytest.mark.parametrize("name", ["slots_tiny", "pools_c2"])
+@pytest.mark.parametrize("name", ["slots_tiny", "pools_c2", "pools_c4"])
 def test_rotation(name):
     from pixiu_amd import synth
     rot = json.load(open(os.path.join(GOLD, "rotation.json")))[name]

@@ -1,10 +1,14 @@
 """Fold rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE counter CSVs (separate passes) into the
 per-kernel JSON bench.py reads for roofline.traffic.  Usage:
-  python tools/pmc_summary.py FETCH.csv WRITE.csv OUT.json "source description"
+  python tools/pmc_summary.py FETCH.csv WRITE.csv OUT.json "source description" [CONFIG RPS RECORDS]
+bench.py uses the file only when CONFIG / RPS / RECORDS match the run it reports.
 """
 import collections, csv, json, re, sys
 
 fetch_csv, write_csv, out, source = sys.argv[1:5]
+workload = None
+if len(sys.argv) >= 8:
+    workload = {"config": int(sys.argv[5]), "rps": int(sys.argv[6]), "records": int(sys.argv[7])}
 
 
 def per_kernel(path, counter):
@@ -21,7 +25,7 @@ def per_kernel(path, counter):
 
 f = per_kernel(fetch_csv, "FETCH_SIZE")
 w = per_kernel(write_csv, "WRITE_SIZE")
-res = {"source": source,
+res = {"source": source, "workload": workload,
        "formula": "hbm_bytes = (FETCH_SIZE + WRITE_SIZE) * 1024 (KB counters, separate passes); no gfx950 "
                   "wide-stream correction applied: these kernels issue scattered narrow accesses"}
 for k in sorted(set(f) | set(w)):
