@@ -1662,6 +1662,7 @@ int px_ctx::save(uint8_t *dst, uint64_t cap, int dst_on_device, uint64_t *bytes)
         h2d(d_src, src.data(), (size_t)n * 8);
         h2d(d_len, len.data(), (size_t)n * 4);
         h2d(d_off, off.data(), (size_t)n * 8);
+        hcheck(hipMemsetAsync(pack + h.data_off, 0, data, stream));  // alignment padding is zero
         hcheck(launch_compact(stream, n, d_src, d_len, pack + h.data_off, d_off));
         sync();
         heap.release(d_src, (uint64_t)n * 8);
