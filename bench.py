@@ -253,6 +253,7 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
         t1 = time.perf_counter()
         sst = st.stats()
         set_kms, walk_kms, emit_kms = sst["last_set_kernel_ms"], sst["last_walk_kernel_ms"], sst["last_emit_kernel_ms"]
+        psa = (sst["last_psa_ms"], int(sst["last_psa_shards"]), int(sst["last_walk_shards"]))
         rc, off, ln, sts, need = st.get_batch_device(keys_host, out.data_ptr(), out_cap, px.COMPAT)
         t2 = time.perf_counter()
         gst = st.stats()
@@ -274,7 +275,7 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
         return {"set_s": t1 - t0 + g_ms * 1e-3, "get_s": t2 - t1, "set_kms": set_kms, "walk_kms": walk_kms,
                 "emit_kms": emit_kms, "dec_kms": dec_kms, "gather_ms": g_ms, "look_ms": look_ms,
                 "call_ms": call_ms, "comp": int(res["comp_len"].sum()), "exp": int(ln.sum()), "res": res,
-                "off": off, "len": ln}
+                "off": off, "len": ln, "psa": psa}
 
     for _ in range(warmup):
         step()
@@ -334,12 +335,18 @@ def summarize(cfg, r, rps, world, a, pmc_path):
     emit_kms = float(np.mean([x["emit_kms"] for x in runs]))
     dec_kms = float(np.mean([x["dec_kms"] for x in runs]))
     # roofline: algorithmic bytes per launch / avg launch time, HIP events
-    # on the context's stream (px_stats)
-    set_gbps = (raw + comp) / (walk_kms * 1e-3) / 1e9   # k_gst_encode: raw in + compressed out
+    # on the context's stream (px_stats).  The setitem encode stage is the suffix-array
+    # pipeline (px_psa.hip: rocPRIM sorts + k_psa_*) for PSA shards and k_gst_encode for
+    # walked ones; its span is timed as one stage.
+    psa_shards = int(np.mean([x["psa"][1] for x in runs]))
+    walk_shards = int(np.mean([x["psa"][2] for x in runs]))
+    enc_name = ("k_psa (suffix-array pipeline)" if walk_shards == 0 else "k_psa + k_gst_encode") if psa_shards \
+        else "k_gst_encode"
+    set_gbps = (raw + comp) / (walk_kms * 1e-3) / 1e9   # encode stage: raw in + compressed out
     emit_gbps = (raw * 5 + comp) / (emit_kms * 1e-3) / 1e9
     dec_gbps = (comp + exp) / (dec_kms * 1e-3) / 1e9     # k_decode: compressed in + expanded out
-    dominant = "k_gst_encode" if walk_kms >= dec_kms else "k_decode"
-    ach = set_gbps if dominant == "k_gst_encode" else dec_gbps
+    dominant = enc_name if walk_kms >= dec_kms else "k_decode"
+    ach = set_gbps if dominant == enc_name else dec_gbps
     traffic, tsrc = None, None
     if pmc_path and os.path.exists(pmc_path):
         try:
@@ -347,7 +354,14 @@ def summarize(cfg, r, rps, world, a, pmc_path):
             w = pmc.get("workload", {})
             # only a profile of this exact workload counts (config, shard size, records)
             if w.get("config") == cfg and w.get("rps") == rps and w.get("records") == r["n"]:
-                traffic = pmc.get(dominant, {}).get("hbm_bytes_per_launch")
+                if dominant == "k_decode":
+                    traffic = pmc.get("k_decode", {}).get("hbm_bytes_per_launch")
+                else:  # every kernel of the encode stage, summed over its launches
+                    tot_b = 0.0
+                    for k, v in pmc.items():
+                        if isinstance(v, dict) and (k.startswith("k_psa") or "rocprim" in k or k == "k_gst_encode"):
+                            tot_b += v["hbm_bytes_per_launch"] * v["dispatches"]
+                    traffic = tot_b or None
                 tsrc = f"{os.path.relpath(pmc_path, ROOT)} ({pmc.get('source', '')})"
         except Exception:
             traffic = None
@@ -359,12 +373,14 @@ def summarize(cfg, r, rps, world, a, pmc_path):
         "setitem_MBps": round(set_MBps, 3), "getitem_MBps": round(get_MBps, 3),
         "getitem_exact_MBps": round(job_exact / exact_s / 1e6, 3),
         "compression_ratio": round(job_comp / job_raw, 4),
-        "kernel_ms": {"k_gst_encode": round(walk_kms, 3), "k_gst_emit": round(emit_kms, 3),
+        "kernel_ms": {"encode_stage": round(walk_kms, 3), "k_gst_emit": round(emit_kms, 3),
                       "k_decode": round(dec_kms, 3), "k_decode_exact": round(r["exact_dec_kms"], 3)},
+        "encode_stage": {"kernels": enc_name, "psa_shards": psa_shards, "walked_shards": walk_shards,
+                         "psa_host_ms": round(float(np.mean([x["psa"][0] for x in runs])), 3)},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 3), "peak": PEAK_HBM_GBPS,
                      "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBPS, 6), "traffic": traffic,
                      "traffic_source": tsrc},
-        "roofline_kernels_GBps": {"k_gst_encode": round(set_gbps, 3), "k_gst_emit": round(emit_gbps, 3),
+        "roofline_kernels_GBps": {"encode_stage": round(set_gbps, 3), "k_gst_emit": round(emit_gbps, 3),
                                   "k_decode": round(dec_gbps, 3)},
         "gather_ms": round(float(np.mean([x["gather_ms"] for x in runs])), 3),
     }
@@ -431,7 +447,7 @@ def main():
                    "parallelism": f"dp{world} (record-range shards, no cross-GPU refs)"},
     }
     for k in ("setitem_MBps", "getitem_MBps", "getitem_exact_MBps", "compression_ratio", "kernel_ms",
-              "roofline", "roofline_kernels_GBps", "gather_ms", "parity_counts"):
+              "encode_stage", "roofline", "roofline_kernels_GBps", "gather_ms", "parity_counts"):
         if k in main_sum:
             line[k] = main_sum[k]
     line["getitem_split_ms"] = {k: round(v, 3) for k, v in get_split.items()}

@@ -91,6 +91,9 @@ typedef struct px_stats {
     double last_emit_kernel_ms;   /* k_gst_emit (stream encoder -> compressed bytes) alone */
     double last_get_lookup_ms;    /* host key -> record lookups of the last px_get_batch */
     double last_get_call_ms;      /* wall time inside the last px_get_batch call */
+    double last_psa_ms;           /* the suffix-array pass of the last px_set_batch (host wall) */
+    uint64_t last_psa_shards;     /* shards the last px_set_batch encoded by the suffix-array pass */
+    uint64_t last_walk_shards;    /* shards it walked with k_gst_encode */
 } px_stats;
 
 px_ctx *px_open(const px_opts *opts);

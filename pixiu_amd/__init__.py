@@ -64,7 +64,8 @@ class PxStats(C.Structure):
                 ("ub_reads", C.c_uint64), ("device_bytes", C.c_uint64),
                 ("last_set_kernel_ms", C.c_double), ("last_decode_kernel_ms", C.c_double),
                 ("last_walk_kernel_ms", C.c_double), ("last_emit_kernel_ms", C.c_double),
-                ("last_get_lookup_ms", C.c_double), ("last_get_call_ms", C.c_double)]
+                ("last_get_lookup_ms", C.c_double), ("last_get_call_ms", C.c_double),
+                ("last_psa_ms", C.c_double), ("last_psa_shards", C.c_uint64), ("last_walk_shards", C.c_uint64)]
 
 
 SET_RESULT_DTYPE = np.dtype([("status", "<u4"), ("replaced", "<u4"), ("shard", "<u4"), ("chunk", "<u4"),

@@ -67,8 +67,44 @@ struct GstShard {
     uint32_t hash_mask;   // entries - 1 (a multiple of kBucket minus 1)
     uint32_t doc_cap;
     uint32_t r0, r1;      // batch records [r0, r1) belong to this shard, in order
+    uint32_t replay;      // docs of the live chunk to re-walk first (tree not materialised)
+};
+
+// ---- PSA: the parallel suffix-array formulation of the GST walk (px_psa.hip,
+// DESIGN.md §9).  A PSA shard's live chunk (earlier docs + this batch's) is one text
+// in a global position space; every doc of it is listed, earlier docs with msg null.
+struct PsaDoc {
+    const uint8_t *src;  // escaped doc (in its shard's arena text)
+    uint32_t *msg;       // its encoder messages, one u32 per byte (null: an earlier doc)
+    uint32_t start;      // global position of its first byte
+    uint32_t len;
+    uint32_t shard;      // PSA shard index
+    uint32_t slot;       // chunk-local idx (what reference tokens carry)
+    uint32_t rec;        // batch record index (earlier docs: unused)
     uint32_t pad;
 };
+static_assert(sizeof(PsaDoc) == 40, "PsaDoc layout");
+struct PsaShard {
+    uint32_t base, len;  // global positions [base, base + len): also its suffix-array range
+    uint32_t chunk;      // chunk sequence number of the live chunk
+    uint32_t pad;
+};
+// device scratch for px_psa.hip, borrowed from the runtime's heap
+struct PsaAlloc {
+    void *(*alloc)(void *self, uint64_t n);
+    void (*release)(void *self, void *p, uint64_t n);
+    void *self;
+};
+struct PsaStats {
+    uint32_t iterations;  // prefix-doubling steps after the first sort
+    uint32_t active[24];  // unsorted suffixes entering each doubling step
+    float ms_sort, ms_lcp, ms_msg;
+};
+// a live chunk of at most this many doc bytes cannot rotate by pool count: MemPool charges
+// <= 16 blocks per inserted leaf (leaf 5 + entry 3, split node 5 + entry 3) and at most one
+// leaf per byte, a closed pool holds >= 65,531 blocks, and rotation needs 2,048 pools
+// (PiXiuCtrl.cpp:13; MemPool.cpp:7-37): (2047 * 65531 - 5) / 16
+constexpr uint32_t kPsaMaxText = (uint32_t)((2047ull * 65531ull - 5ull) / 16ull);
 
 // segment index entry (k_tokenize fills it, k_link sets a record token's target)
 struct alignas(16) SegEnt {

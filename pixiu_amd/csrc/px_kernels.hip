@@ -860,7 +860,8 @@ constexpr uint32_t kGstWaves = 4;
 __global__ void __launch_bounds__(64 * kGstWaves, 6) k_gst_encode(const GstShard *shards, uint32_t n_shards,
                                                    const uint32_t *doc_len, uint8_t *const *comp_dst,
                                                    const uint8_t *comp_base, uint32_t *msgs, uint32_t *rec_chunk,
-                                                   uint32_t *rec_idx, uint32_t *rec_status, ShardState *st_out) {
+                                                   uint32_t *rec_idx, uint32_t *rec_status, ShardState *st_out,
+                                                   uint32_t *sink) {
     __shared__ GstLds lds_w[kGstWaves];
     const uint32_t wv = uni(threadIdx.x >> 6);
     const uint32_t s = blockIdx.x * kGstWaves + wv;
@@ -904,12 +905,23 @@ __global__ void __launch_bounds__(64 * kGstWaves, 6) k_gst_encode(const GstShard
 #endif
     // stage the persistent root entries and doc starts into LDS
     for (uint32_t c = lane; c < 256; c += 64) lds.root[c] = ((const PX_GAS u32x4 *)sh.root)[c];
-    for (uint32_t d = lane; d <= kDocCache; d += 64) lds.doc_base[d] = d <= g.n_docs ? sh.doc_base[d] : 0;
+    for (uint32_t d = lane; d <= kDocCache; d += 64)
+        lds.doc_base[d] = d <= max(g.n_docs, sh.replay) ? sh.doc_base[d] : 0;
     wave_sync();
     if (g.epoch == 0) {  // brand-new shard
         g.clear_tree();
         g.set_docbase(0, 0);
         g.n_docs = 0;
+    }
+    // a live chunk whose docs were encoded by the suffix-array path (px_psa.hip) has no
+    // tree: re-walk its docs first (their messages go to a sink), then continue
+    for (uint32_t d = 0; d < sh.replay && g.status == kOk; ++d) {
+        g.cur = d;
+        g.cur_base = g.docbase(d);
+        const uint32_t len = g.docbase(d + 1) - g.cur_base;
+        g.msg = (PX_GAS uint32_t *)sink;
+        g.encode_doc(len);
+        ++g.n_docs;
     }
     for (uint32_t r = sh.r0; r < sh.r1; ++r) {
         const uint32_t len = uni(doc_len[r]);
@@ -2104,10 +2116,11 @@ hipError_t launch_doc_write(hipStream_t s, uint32_t n, const uint8_t *keys, cons
 
 hipError_t launch_gst_encode(hipStream_t s, const GstShard *shards, uint32_t n_shards, const uint32_t *doc_len,
                              uint8_t *const *comp_dst, const uint8_t *comp_base, uint32_t *msgs,
-                             uint32_t *rec_chunk, uint32_t *rec_idx, uint32_t *rec_status, ShardState *st_out) {
+                             uint32_t *rec_chunk, uint32_t *rec_idx, uint32_t *rec_status, ShardState *st_out,
+                             uint32_t *sink) {
     if (!n_shards) return hipSuccess;
     k_gst_encode<<<(n_shards + kGstWaves - 1) / kGstWaves, 64 * kGstWaves, 0, s>>>(
-        shards, n_shards, doc_len, comp_dst, comp_base, msgs, rec_chunk, rec_idx, rec_status, st_out);
+        shards, n_shards, doc_len, comp_dst, comp_base, msgs, rec_chunk, rec_idx, rec_status, st_out, sink);
     return hipGetLastError();
 }
 

@@ -1,0 +1,514 @@
+// px_psa.hip — the GST walk of setitem restated as suffix-array work.
+//
+// The reference inserts every doc byte into an online generalized suffix tree
+// (SuffixTree.cpp:144-289) and hands the stream encoder one message per byte
+// (SuffixTree.cpp:136-142, 183, 186).  Its active point after byte i of doc `cur` is the
+// longest suffix of cur[0..i] that occurs earlier in the live chunk, and the edge label
+// it reports is the first leaf created under that point, i.e. the earliest occurrence
+// (leaves are created in (doc, start) order, splits keep the upper label:
+// SuffixTree.cpp:154-157, 196-222).  With lpf(j) = the longest prefix of T[j..doc end)
+// occurring at an earlier start of the shard text T (the Longest Previous Factor):
+//   * byte i is COMPRESS iff lpf(i) >= 1, except at i = j-1 + lpf(j-1) for every j
+//     whose lpf(j) >= lpf(j-1) (there the active point restarts: a PASS);
+//   * the COMPRESS run started by j has lpf(j) - lpf(j-1) bytes and ends at
+//     b = j + lpf(j) - 1 with message (doc, pos) = the earliest occurrence E of
+//     T[j .. j+lpf(j)): pos = E + lpf(j) - 1 (and one byte shorter at b-1 when T[b] is a
+//     251 that the encoder's pair rule can cut, PiXiuStr.cpp:33-54).
+// Only runs of >= 7 bytes become reference tokens (PiXiuStr.cpp:56-82), so only those
+// ends need E.  The stream is the textbook Ukkonen walk's; the reference differs from it
+// only when its stale (act_chunk_idx, act_direct) pair is read (SuffixTree.cpp:171,184 vs
+// the canonisation at 232-249), which needs a PASS step whose split loop stops inside an
+// edge -- possible only when the restarted factor's earliest occurrence ends at a doc
+// end.  Such shards are flagged and walked by k_gst_encode instead.
+//
+// Pipeline over all PSA shards of a batch (one global position space, shard-major):
+//   k_psa_gather   docs -> global text G + doc id per position
+//   k_psa_key0     5-symbol keys (shard in the top bits) -> radix sort (rocPRIM)
+//   prefix doubling: keys (group, rank[p+h]) of unsorted suffixes only, stable radix
+//                  sort, group heads by max-scans, ranks and SA written back
+//   k_psa_minlvl / k_psa_ansv   nearest smaller position left/right in SA order
+//                  (a 64-ary min tree; one wave per 64 ranks, ballot descents)
+//   k_psa_lce      lcp with those two neighbours, Kasai-style in text order
+//                  (lcp(p) >= lcp(p-1) - 1 for both neighbours)
+//   k_psa_msg0 / k_psa_runs   messages, earliest occurrences (neighbour chains), the
+//                  stale-pair check; k_psa_place   chunk / slot / status per record
+#include <cstring>
+
+#include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_select.hpp>
+
+#include "px_common.h"
+
+namespace px {
+
+namespace {
+
+constexpr uint32_t kNoPos = 0xffffffffu;
+constexpr uint32_t kPass = 0xffffffffu;
+#define PSA_DEV __device__ __forceinline__
+#define PX_GAS __attribute__((address_space(1)))
+
+PSA_DEV uint32_t lane_id() { return threadIdx.x & 63u; }
+
+// ---------------------------------------------------------------- text
+__global__ void __launch_bounds__(256) k_psa_gather(uint32_t ndocs, const PsaDoc *docs, uint8_t *G, uint32_t *pdoc) {
+    const uint32_t lane = lane_id();
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t g = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); g < ndocs; g += waves) {
+        const PsaDoc d = docs[g];
+        const PX_GAS uint8_t *src = (const PX_GAS uint8_t *)d.src;
+        for (uint32_t o = lane; o < d.len; o += 64) {
+            G[d.start + o] = src[o];
+            pdoc[d.start + o] = g;
+        }
+    }
+}
+
+// doc end (exclusive, global) of position p
+PSA_DEV uint32_t doc_end(const PsaDoc *docs, const uint32_t *pdoc, uint32_t p) {
+    const uint32_t g = pdoc[p];
+    return docs[g].start + docs[g].len;
+}
+
+// initial keys: shard (top 19 bits) | 5 symbols of 9 bits (byte + 1; 0 past the doc end)
+constexpr int kSym0 = 5;
+__global__ void __launch_bounds__(256) k_psa_key0(uint32_t N, const uint8_t *G, const uint32_t *pdoc,
+                                                  const PsaDoc *docs, uint64_t *keys, uint32_t *vals) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= N) return;
+    const uint32_t g = pdoc[p];
+    const uint32_t end = docs[g].start + docs[g].len;
+    uint64_t k = (uint64_t)docs[g].shard << 45;
+#pragma unroll
+    for (int s = 0; s < kSym0; ++s) {
+        const uint32_t q = p + s;
+        const uint64_t sym = q < end ? (uint64_t)G[q] + 1 : 0;
+        k |= sym << (36 - 9 * s);
+    }
+    keys[p] = k;
+    vals[p] = p;
+}
+
+// group heads of the first sort: a new group at a key change, and every suffix shorter
+// than 5 symbols (its key holds its whole string: equal ones are equal strings, kept
+// in position order by the stable sort and resolved as they are)
+__global__ void __launch_bounds__(256) k_psa_head0(uint32_t N, const uint64_t *keys, const uint32_t *sa,
+                                                   const uint32_t *pdoc, const PsaDoc *docs, uint32_t *hflag) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= N) return;
+    const uint32_t p = sa[r];
+    const bool complete = doc_end(docs, pdoc, p) - p < (uint32_t)kSym0;
+    hflag[r] = (r == 0 || keys[r] != keys[r - 1] || complete) ? r : 0u;
+}
+
+// rank = group head index; active = not a singleton group
+__global__ void __launch_bounds__(256) k_psa_rank0(uint32_t N, const uint32_t *sa, const uint32_t *head,
+                                                   uint32_t *rank, uint8_t *active) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= N) return;
+    rank[sa[r]] = head[r];
+    const bool h = head[r] == r;
+    const bool hn = r + 1 == N || head[r + 1] == r + 1;
+    active[r] = (h && hn) ? 0 : 1;
+}
+
+// doubling step h: key (group, rank of the suffix h further, 0 past the doc end)
+__global__ void __launch_bounds__(256) k_psa_key2(uint32_t m, const uint32_t *act, const uint32_t *rank,
+                                                  const uint32_t *pdoc, const PsaDoc *docs, uint32_t h,
+                                                  uint64_t *keys, uint32_t *vals) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= m) return;
+    const uint32_t p = act[t];
+    const uint32_t end = doc_end(docs, pdoc, p);
+    const uint64_t hi = rank[p];
+    const uint64_t lo = p + h < end ? (uint64_t)rank[p + h] + 1 : 0;
+    keys[t] = hi << 32 | lo;
+    vals[t] = p;
+}
+
+__global__ void __launch_bounds__(256) k_psa_head2(uint32_t m, const uint64_t *keys, uint32_t *gflag, uint32_t *sflag) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= m) return;
+    const uint64_t k = keys[t];
+    const bool first = t == 0;
+    gflag[t] = (first || (k >> 32) != (keys[t - 1] >> 32)) ? t : 0u;
+    // a suffix whose string ended (lo == 0) is complete: its own group
+    sflag[t] = (first || k != keys[t - 1] || (uint32_t)k == 0) ? t : 0u;
+}
+
+__global__ void __launch_bounds__(256) k_psa_rank2(uint32_t m, const uint64_t *keys, const uint32_t *pos,
+                                                   const uint32_t *gfirst, const uint32_t *sfirst, uint32_t *sa,
+                                                   uint32_t *rank, uint8_t *active) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= m) return;
+    const uint64_t k = keys[t];
+    const uint32_t g = (uint32_t)(k >> 32);
+    const uint32_t p = pos[t];
+    sa[g + (t - gfirst[t])] = p;
+    rank[p] = g + (sfirst[t] - gfirst[t]);
+    const bool h = sfirst[t] == t;
+    const bool hn = t + 1 == m || keys[t + 1] != k || (uint32_t)keys[t + 1] == 0;
+    active[t] = (h && hn) ? 0 : 1;
+}
+
+// ---------------------------------------------------------------- nearest smaller positions
+// 64-ary min tree over the suffix array's values (text positions)
+__global__ void __launch_bounds__(256) k_psa_minlvl(uint32_t n_in, const uint32_t *in, uint32_t n_out, uint32_t *out) {
+    const uint32_t lane = lane_id();
+    const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (w >= n_out) return;
+    const uint32_t i = w * 64 + lane;
+    uint32_t v = i < n_in ? in[i] : kNoPos;
+    for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
+    if (lane == 0) out[w] = v;
+}
+
+struct MinTree {
+    const uint32_t *lvl[8];
+    uint32_t n[8];
+    uint32_t levels;  // lvl[0] = the suffix array
+};
+
+// nearest index left (dir 0) / right (dir 1) of element i whose value is < v, or kNoPos
+// (wave-cooperative: every lane calls it with the same i and v)
+PSA_DEV uint32_t tree_find(const MinTree &t, uint32_t i, uint32_t v, int dir) {
+    const uint32_t lane = lane_id();
+    uint32_t x = i;  // node index at level L
+    for (uint32_t L = 0; L < t.levels; ++L) {
+        const uint32_t base = x & ~63u, at = x & 63u;
+        const uint32_t j = base + lane;
+        const uint32_t s = j < t.n[L] ? t.lvl[L][j] : kNoPos;
+        const bool side = dir == 0 ? lane < at : lane > at;
+        const uint64_t mm = __ballot(side && s < v);
+        if (mm) {
+            uint32_t y = base + (dir == 0 ? 63u - (uint32_t)__clzll((long long)mm) : (uint32_t)__ffsll((long long)mm) - 1u);
+            for (uint32_t D = L; D-- > 0;) {  // descend to the element
+                const uint32_t c = y * 64 + lane;
+                const uint32_t cv = c < t.n[D] ? t.lvl[D][c] : kNoPos;
+                const uint64_t cm = __ballot(cv < v);
+                y = y * 64 + (dir == 0 ? 63u - (uint32_t)__clzll((long long)cm) : (uint32_t)__ffsll((long long)cm) - 1u);
+            }
+            return y;
+        }
+        x >>= 6;
+    }
+    return kNoPos;
+}
+
+// psv / nsv: for the suffix at rank r, the nearest rank to its left / right (inside its
+// shard's range) whose position is smaller; written per position
+__global__ void __launch_bounds__(256) k_psa_ansv(uint32_t N, MinTree t, const uint32_t *pdoc, const PsaDoc *docs,
+                                                  const PsaShard *shards, uint32_t *psvp, uint32_t *nsvp) {
+    const uint32_t lane = lane_id();
+    const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (w * 64 >= N) return;
+    const uint32_t *sa = t.lvl[0];
+    const uint32_t r = w * 64 + lane;
+    const bool live = r < N;
+    const uint32_t v = live ? sa[r] : kNoPos;
+    uint32_t lo = 0, hi = 0;
+    if (live) {
+        const PsaShard sh = shards[docs[pdoc[v]].shard];
+        lo = sh.base;
+        hi = sh.base + sh.len;
+    }
+    // inside the 64-rank block
+    uint32_t ps = kNoPos, ns = kNoPos;
+    for (uint32_t k = 1; k < 64; ++k) {
+        const uint32_t ul = (uint32_t)__shfl((int)v, (int)((lane - k) & 63u));
+        const uint32_t ur = (uint32_t)__shfl((int)v, (int)((lane + k) & 63u));
+        if (ps == kNoPos && lane >= k && ul < v) ps = r - k;
+        if (ns == kNoPos && lane + k < 64 && ur < v) ns = r + k;
+    }
+    // the rest through the min tree, one element at a time (few per block: the block's
+    // prefix / suffix minima)
+    uint64_t need = __ballot(live && (ps == kNoPos || ns == kNoPos));
+    while (need) {
+        const uint32_t l = (uint32_t)__ffsll((long long)need) - 1u;
+        need &= need - 1;
+        const uint32_t ri = w * 64 + l;
+        const uint32_t vi = (uint32_t)__shfl((int)v, (int)l);
+        const uint32_t pi = (uint32_t)__shfl((int)ps, (int)l);
+        const uint32_t ni = (uint32_t)__shfl((int)ns, (int)l);
+        const uint32_t fp = pi == kNoPos ? tree_find(t, ri, vi, 0) : pi;
+        const uint32_t fn = ni == kNoPos ? tree_find(t, ri, vi, 1) : ni;
+        if (lane == l) {
+            ps = fp;
+            ns = fn;
+        }
+    }
+    if (live) {
+        psvp[v] = (ps != kNoPos && ps >= lo) ? sa[ps] : kNoPos;
+        nsvp[v] = (ns != kNoPos && ns < hi) ? sa[ns] : kNoPos;
+    }
+}
+
+// ---------------------------------------------------------------- lcp with those neighbours
+constexpr uint32_t kLceSpan = 256;  // text positions per thread (Kasai-style amortisation)
+
+PSA_DEV uint32_t lce(const uint8_t *G, uint32_t p, uint32_t q, uint32_t k, uint32_t lim) {
+    // bytes equal from offset k on, up to lim (both suffixes stay inside their docs)
+    while (k + 8 <= lim) {
+        uint64_t a, b;
+        __builtin_memcpy(&a, G + p + k, 8);
+        __builtin_memcpy(&b, G + q + k, 8);
+        if (a != b) return k + (uint32_t)(__builtin_ctzll(a ^ b) >> 3);
+        k += 8;
+    }
+    while (k < lim && G[p + k] == G[q + k]) ++k;
+    return k;
+}
+
+__global__ void __launch_bounds__(256) k_psa_lce(uint32_t N, const uint8_t *G, const uint32_t *pdoc, const PsaDoc *docs,
+                                                 const uint32_t *psvp, const uint32_t *nsvp, uint16_t *lcp_p,
+                                                 uint16_t *lcp_n) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t p0 = t * kLceSpan;
+    if (p0 >= N) return;
+    const uint32_t p1 = min(N, p0 + kLceSpan);
+    uint32_t kp = 0, kn = 0;
+    for (uint32_t p = p0; p < p1; ++p) {
+        const uint32_t endp = doc_end(docs, pdoc, p);
+        const uint32_t q = psvp[p], s = nsvp[p];
+        kp = kp ? kp - 1 : 0;
+        kn = kn ? kn - 1 : 0;
+        if (q == kNoPos) {
+            kp = 0;
+        } else {
+            const uint32_t lim = min(endp - p, doc_end(docs, pdoc, q) - q);
+            kp = lce(G, p, q, min(kp, lim), lim);
+        }
+        if (s == kNoPos) {
+            kn = 0;
+        } else {
+            const uint32_t lim = min(endp - p, doc_end(docs, pdoc, s) - s);
+            kn = lce(G, p, s, min(kn, lim), lim);
+        }
+        lcp_p[p] = (uint16_t)kp;
+        lcp_n[p] = (uint16_t)kn;
+    }
+}
+
+// ---------------------------------------------------------------- messages
+PSA_DEV uint32_t lpf_at(const uint16_t *lp, const uint16_t *ln, uint32_t p) { return max((uint32_t)lp[p], (uint32_t)ln[p]); }
+
+// earliest occurrence of T[j .. j+l): climb the nearest-smaller-position links while the
+// neighbour still shares l symbols (positions strictly decrease)
+PSA_DEV uint32_t earliest(const uint32_t *psvp, const uint32_t *nsvp, const uint16_t *lp, const uint16_t *ln, uint32_t j,
+                          uint32_t l) {
+    uint32_t p = j;
+    for (;;) {
+        if (lp[p] >= l) p = psvp[p];
+        else if (ln[p] >= l) p = nsvp[p];
+        else return p;
+    }
+}
+
+PSA_DEV uint32_t msg_of(const PsaDoc *docs, const uint32_t *pdoc, uint32_t e, uint32_t l) {
+    const PsaDoc &d = docs[pdoc[e]];
+    return d.slot << 16 | (e - d.start + l - 1);
+}
+
+// every byte of a new doc: COMPRESS (placeholder 0) when lpf >= 1, else PASS
+__global__ void __launch_bounds__(256) k_psa_msg0(uint32_t N, const uint32_t *pdoc, const PsaDoc *docs,
+                                                  const uint16_t *lp, const uint16_t *ln) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= N) return;
+    const PsaDoc &d = docs[pdoc[p]];
+    if (!d.msg) return;
+    d.msg[p - d.start] = lpf_at(lp, ln, p) >= 1 ? 0u : kPass;
+}
+
+__global__ void __launch_bounds__(256) k_psa_runs(uint32_t N, const uint8_t *G, const uint32_t *pdoc, const PsaDoc *docs,
+                                                  const uint32_t *psvp, const uint32_t *nsvp, const uint16_t *lp,
+                                                  const uint16_t *ln, uint32_t *shard_flag) {
+    const uint32_t J = blockIdx.x * blockDim.x + threadIdx.x;
+    if (J >= N) return;
+    const uint32_t g = pdoc[J];
+    const PsaDoc &d = docs[g];
+    const uint32_t end = d.start + d.len;
+    const uint32_t lJ = lpf_at(lp, ln, J);
+    const uint32_t lq = J > d.start ? lpf_at(lp, ln, J - 1) : 0;
+    const bool restart = J > d.start && lJ >= lq;  // a non-empty active-point range starts at J
+    if (d.msg) {
+        if (restart && J - 1 + lq < end) d.msg[J - 1 + lq - d.start] = kPass;
+        if (lJ >= lq + 7) {  // a COMPRESS run of >= 7 bytes: a reference token can end here
+            const uint32_t b = J + lJ - 1;
+            d.msg[b - d.start] = msg_of(docs, pdoc, earliest(psvp, nsvp, lp, ln, J, lJ), lJ);
+            if (G[b] == 251) d.msg[b - 1 - d.start] = msg_of(docs, pdoc, earliest(psvp, nsvp, lp, ln, J, lJ - 1), lJ - 1);
+        }
+        // stale-pair check (see the file comment): the restart at J-1+lq leaves the split
+        // loop inside an edge only if T[J-1 .. J-1+lq)'s earliest occurrence ends its doc
+        if (restart && lq >= 2) {
+            const uint32_t fe = J - 1 + lq;
+            if (G[fe - 2] == 251 && (G[fe - 1] == 0 || G[fe - 1] == 2)) {
+                const uint32_t e = earliest(psvp, nsvp, lp, ln, J - 1, lq);
+                if (e + lq == doc_end(docs, pdoc, e)) shard_flag[d.shard] = 1;
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_psa_place(uint32_t ndocs, const PsaDoc *docs, const PsaShard *shards,
+                                                   uint32_t *rec_chunk, uint32_t *rec_idx, uint32_t *rec_status) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= ndocs) return;
+    const PsaDoc d = docs[g];
+    if (!d.msg) return;
+    rec_chunk[d.rec] = shards[d.shard].chunk;
+    rec_idx[d.rec] = d.slot;
+    rec_status[d.rec] = kOk;
+}
+
+struct Max {
+    PSA_DEV uint32_t operator()(uint32_t a, uint32_t b) const { return a > b ? a : b; }
+};
+
+}  // namespace
+
+#define PSA_CHECK(x)                         \
+    do {                                     \
+        hipError_t e_ = (x);                 \
+        if (e_ != hipSuccess) return e_;     \
+    } while (0)
+
+// Runs the pipeline; messages land in every new doc's msg array, the new records' chunk /
+// slot / status in rec_*, and shard_flag[k] (device, zeroed by the caller) is set for shards
+// whose stream may differ from the reference's (walk them with k_gst_encode instead).
+hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDoc *docs, uint32_t nshards,
+                   const PsaShard *shards, uint32_t N, uint32_t *rec_chunk, uint32_t *rec_idx, uint32_t *rec_status,
+                   uint32_t *shard_flag, PsaStats *st) {
+    (void)nshards;
+    if (!N || !ndocs) return hipSuccess;
+    auto get = [&](uint64_t n) { return A.alloc(A.self, n); };
+    auto put = [&](void *p, uint64_t n) { A.release(A.self, p, n); };
+    hipEvent_t e0, e1, e2, e3;
+    PSA_CHECK(hipEventCreate(&e0));
+    PSA_CHECK(hipEventCreate(&e1));
+    PSA_CHECK(hipEventCreate(&e2));
+    PSA_CHECK(hipEventCreate(&e3));
+    PSA_CHECK(hipEventRecord(e0, s));
+    const uint64_t n64 = N;
+    auto *G = (uint8_t *)get(n64 + 64);
+    auto *pdoc = (uint32_t *)get(n64 * 4);
+    auto *rank = (uint32_t *)get(n64 * 4);
+    auto *sa = (uint32_t *)get(n64 * 4);
+    auto *keys = (uint64_t *)get(n64 * 8);
+    auto *keys2 = (uint64_t *)get(n64 * 8);
+    auto *vals = (uint32_t *)get(n64 * 4);
+    auto *vals2 = (uint32_t *)get(n64 * 4);
+    auto *f1 = (uint32_t *)get(n64 * 4);
+    auto *f2 = (uint32_t *)get(n64 * 4);
+    auto *act = (uint8_t *)get(n64);
+    auto *cnt = (uint32_t *)get(64);
+    PSA_CHECK(hipMemsetAsync(G + N, 0, 64, s));
+    const uint32_t tb = 256;
+    auto blocks = [&](uint64_t n) { return (uint32_t)((n + tb - 1) / tb); };
+    k_psa_gather<<<std::min<uint32_t>((ndocs + 3) / 4, 65535u), 256, 0, s>>>(ndocs, docs, G, pdoc);
+    k_psa_key0<<<blocks(N), tb, 0, s>>>(N, G, pdoc, docs, keys, vals);
+    // temp storage: the largest of sort / scan / select over N elements
+    size_t t_sort = 0, t_scan = 0, t_sel = 0;
+    PSA_CHECK(rocprim::radix_sort_pairs(nullptr, t_sort, keys, keys2, vals, sa, (size_t)N, 0, 64, s));
+    PSA_CHECK(rocprim::inclusive_scan(nullptr, t_scan, f1, f1, (size_t)N, Max(), s));
+    PSA_CHECK(rocprim::select(nullptr, t_sel, sa, act, vals, cnt, (size_t)N, s));
+    const size_t t_bytes = std::max({t_sort, t_scan, t_sel}) + 256;
+    void *tmp = get(t_bytes);
+    int shard_bits = 1;
+    while ((1u << shard_bits) <= nshards && shard_bits < 19) ++shard_bits;
+    size_t tb_ = t_bytes;
+    PSA_CHECK(rocprim::radix_sort_pairs(tmp, tb_, keys, keys2, vals, sa, (size_t)N, 0, 45 + shard_bits, s));
+    k_psa_head0<<<blocks(N), tb, 0, s>>>(N, keys2, sa, pdoc, docs, f1);
+    tb_ = t_bytes;
+    PSA_CHECK(rocprim::inclusive_scan(tmp, tb_, f1, vals2, (size_t)N, Max(), s));
+    k_psa_rank0<<<blocks(N), tb, 0, s>>>(N, sa, vals2, rank, act);
+    tb_ = t_bytes;
+    uint32_t *alist = vals;  // active suffixes, in suffix-array order
+    PSA_CHECK(rocprim::select(tmp, tb_, sa, act, alist, cnt, (size_t)N, s));
+    uint32_t m = 0;
+    // (counts come back through a synchronous copy after the stream drained: no async
+    // copy into pageable memory, see px_runtime.cpp d2h)
+    PSA_CHECK(hipStreamSynchronize(s));
+    PSA_CHECK(hipMemcpy(&m, cnt, 4, hipMemcpyDeviceToHost));
+    int rank_bits = 1;
+    while (rank_bits < 32 && (1ull << rank_bits) <= n64) ++rank_bits;
+    uint32_t it = 0;
+    for (uint32_t h = kSym0; m > 0; h *= 2, ++it) {
+        if (st && it < 24) st->active[it] = m;
+        if (it >= 20) return hipErrorUnknown;  // cannot happen: docs are <= 65,535 bytes
+        k_psa_key2<<<blocks(m), tb, 0, s>>>(m, alist, rank, pdoc, docs, h, keys, vals2);
+        tb_ = t_bytes;
+        PSA_CHECK(rocprim::radix_sort_pairs(tmp, tb_, keys, keys2, vals2, f2, (size_t)m, 0, 32 + rank_bits, s));
+        // f2 = positions in the new order; group heads f1 -> vals2, subgroup heads in the
+        // (now free) unsorted key buffer: flags in its first half, scan in its second
+        uint32_t *sfl = (uint32_t *)keys, *sfirst = (uint32_t *)keys + N;
+        k_psa_head2<<<blocks(m), tb, 0, s>>>(m, keys2, f1, sfl);
+        tb_ = t_bytes;
+        PSA_CHECK(rocprim::inclusive_scan(tmp, tb_, f1, vals2, (size_t)m, Max(), s));
+        tb_ = t_bytes;
+        PSA_CHECK(rocprim::inclusive_scan(tmp, tb_, sfl, sfirst, (size_t)m, Max(), s));
+        k_psa_rank2<<<blocks(m), tb, 0, s>>>(m, keys2, f2, vals2, sfirst, sa, rank, act);
+        tb_ = t_bytes;
+        PSA_CHECK(rocprim::select(tmp, tb_, f2, act, alist, cnt, (size_t)m, s));
+        PSA_CHECK(hipStreamSynchronize(s));
+        PSA_CHECK(hipMemcpy(&m, cnt, 4, hipMemcpyDeviceToHost));
+    }
+    if (st) st->iterations = it;
+    put(keys2, n64 * 8);
+    put(vals2, n64 * 4);
+    put(act, n64);
+    put(tmp, t_bytes);
+    PSA_CHECK(hipEventRecord(e1, s));
+    // ---- nearest smaller positions in suffix-array order (min tree over sa)
+    MinTree t{};
+    t.lvl[0] = sa;
+    t.n[0] = N;
+    t.levels = 1;
+    uint32_t *lv_buf = (uint32_t *)keys;  // the key buffer is free now: tree levels live in it
+    uint64_t lv_off = 0;
+    while (t.n[t.levels - 1] > 1 && t.levels < 8) {
+        const uint32_t nin = t.n[t.levels - 1];
+        const uint32_t nout = (nin + 63) / 64;
+        uint32_t *out = lv_buf + lv_off;
+        lv_off += nout;
+        k_psa_minlvl<<<(nout + 3) / 4, 256, 0, s>>>(nin, t.lvl[t.levels - 1], nout, out);
+        t.lvl[t.levels] = out;
+        t.n[t.levels] = nout;
+        ++t.levels;
+    }
+    uint32_t *psvp = f1, *nsvp = f2;
+    k_psa_ansv<<<(uint32_t)((n64 + 255) / 256), 256, 0, s>>>(N, t, pdoc, docs, shards, psvp, nsvp);
+    auto *lcp_p = (uint16_t *)rank;  // ranks are no longer needed: two u16 arrays in their place
+    auto *lcp_n = (uint16_t *)get(n64 * 2);
+    k_psa_lce<<<blocks((n64 + kLceSpan - 1) / kLceSpan), tb, 0, s>>>(N, G, pdoc, docs, psvp, nsvp, lcp_p, lcp_n);
+    PSA_CHECK(hipEventRecord(e2, s));
+    // ---- messages
+    k_psa_msg0<<<blocks(N), tb, 0, s>>>(N, pdoc, docs, lcp_p, lcp_n);
+    k_psa_runs<<<blocks(N), tb, 0, s>>>(N, G, pdoc, docs, psvp, nsvp, lcp_p, lcp_n, shard_flag);
+    k_psa_place<<<blocks(ndocs), tb, 0, s>>>(ndocs, docs, shards, rec_chunk, rec_idx, rec_status);
+    PSA_CHECK(hipEventRecord(e3, s));
+    PSA_CHECK(hipEventSynchronize(e3));
+    if (st) {
+        PSA_CHECK(hipEventElapsedTime(&st->ms_sort, e0, e1));
+        PSA_CHECK(hipEventElapsedTime(&st->ms_lcp, e1, e2));
+        PSA_CHECK(hipEventElapsedTime(&st->ms_msg, e2, e3));
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipEventDestroy(e2);
+    (void)hipEventDestroy(e3);
+    put(lcp_n, n64 * 2);
+    put(G, n64 + 64);
+    put(pdoc, n64 * 4);
+    put(rank, n64 * 4);
+    put(sa, n64 * 4);
+    put(keys, n64 * 8);
+    put(vals, n64 * 4);
+    put(f1, n64 * 4);
+    put(f2, n64 * 4);
+    put(cnt, 64);
+    return hipGetLastError();
+}
+
+}  // namespace px

@@ -30,7 +30,10 @@ hipError_t launch_doc_write(hipStream_t, uint32_t, const uint8_t *, const uint64
 hipError_t launch_shard_init(hipStream_t, uint32_t, const ShardInit *);
 hipError_t launch_scatter_slots(hipStream_t, uint32_t, const SlotPut *);
 hipError_t launch_gst_encode(hipStream_t, const GstShard *, uint32_t, const uint32_t *, uint8_t *const *,
-                             const uint8_t *, uint32_t *, uint32_t *, uint32_t *, uint32_t *, ShardState *);
+                             const uint8_t *, uint32_t *, uint32_t *, uint32_t *, uint32_t *, ShardState *,
+                             uint32_t *);
+hipError_t psa_run(hipStream_t, const PsaAlloc &, uint32_t, const PsaDoc *, uint32_t, const PsaShard *, uint32_t,
+                   uint32_t *, uint32_t *, uint32_t *, uint32_t *, PsaStats *);
 hipError_t launch_gst_emit(hipStream_t, uint32_t, const uint8_t *const *, const uint32_t *, uint8_t *const *,
                            const uint8_t *, const uint32_t *, uint32_t *, uint32_t *);
 hipError_t launch_compact(hipStream_t, uint32_t, uint8_t *const *, const uint32_t *, uint8_t *, const uint64_t *);
@@ -319,6 +322,9 @@ struct Shard {
     uint64_t hash_cap = 0, text_cap = 0;
     ShardState hs{};      // host mirror after the last batch
     uint64_t text_end = 0;  // end of written text (relative to the arena text section)
+    // the live chunk was encoded by the suffix-array path (px_psa.hip): hs.n_docs docs,
+    // no tree; the arena is then text only (text_only) until a walk needs the tree
+    bool psa = false, text_only = false;
     uint32_t records = 0;
     std::vector<uint32_t> chunks;  // global chunk ids by chunk_seq
     // CritBit
@@ -356,6 +362,13 @@ struct px_ctx {
     DevBuf scratch_frames, dq_buf, dstat_buf, dlen_buf, in_buf, tmp_buf, link_buf, iter_buf, init_buf, stout_buf,
         slotput_buf;
     HostBuf hq_buf, hres_buf;  // pinned: decode queries up, lengths + statuses down
+    DevBuf sink_buf;           // k_gst_encode's message sink for replayed docs
+    PsaStats psa_stats{};      // the last set batch's suffix-array pass
+    // PX_PSA=0 sends every shard through k_gst_encode (A/B comparisons, tests)
+    static bool psa_enabled() {
+        const char *e = std::getenv("PX_PSA");
+        return !(e && *e == '0');
+    }
     uint32_t host_threads() const {
         const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
         return opts.host_threads ? opts.host_threads : std::min(16u, hw);
@@ -526,6 +539,60 @@ struct px_ctx {
         pending_init.clear();
         for (auto &ps : pending_state) h2d(ps.first, &ps.second, sizeof(ShardState));
         pending_state.clear();
+    }
+
+    // text-only arena of a PSA shard: the live chunk's docs and room for B more bytes
+    void text_reserve(Shard &s, uint64_t B) {
+        const uint64_t need = s.text_end + B;
+        if (s.arena && s.text_only && need <= s.text_cap) return;
+        const uint64_t cap = round_up(std::max(need, s.text_cap * 3 / 2) + 1024, 256);
+        auto *a = (uint8_t *)heap.alloc(cap);
+        if (s.arena) {
+            if (s.text_end) hcheck(hipMemcpyAsync(a, s.text, s.text_end, hipMemcpyDeviceToDevice, stream));
+            deferred_release.emplace_back(s.arena, s.arena_bytes);
+        }
+        s.arena = a;
+        s.arena_bytes = cap;
+        s.text = a;
+        s.text_cap = cap - 1024;
+        s.text_only = true;
+        s.st = nullptr;
+        s.root_tab = nullptr;
+        s.doc_base = nullptr;
+        s.nodes = nullptr;
+        s.hash = nullptr;
+        s.node_cap = s.doc_cap = 0;
+        s.hash_cap = 0;
+    }
+    std::vector<std::pair<void *, uint64_t>> deferred_release;  // freed at the end of a set batch
+
+    // a PSA shard's live chunk goes back to the walk: full arena, text copied, the live
+    // docs' starts uploaded; returns the docs k_gst_encode must re-walk first
+    uint32_t upgrade_to_walk(Shard &s, uint64_t B, uint32_t D) {
+        const uint64_t live = s.text_end;  // PSA shards keep ctext_off == 0
+        const uint32_t docs = s.hs.n_docs;
+        std::vector<uint32_t> base(docs + 1, 0);
+        if (docs) {
+            const Chunk &ch = chunks[s.chunks[s.hs.chunk_seq]];
+            for (uint32_t i = 0; i < docs; ++i) base[i + 1] = base[i] + ch.doc_len[i];
+        }
+        void *old_arena = s.arena;
+        const uint64_t old_bytes = s.arena_bytes;
+        uint8_t *old_text = s.text;
+        const uint32_t seq = s.hs.chunk_seq;
+        s.arena = nullptr;
+        s.text_only = false;
+        s.psa = false;
+        s.text_cap = 0;
+        s.hs = ShardState{};
+        s.hs.chunk_seq = seq;
+        s.text_end = 0;
+        shard_reserve(s, live + B, docs + D);
+        if (live) hcheck(hipMemcpyAsync(s.text, old_text, live, hipMemcpyDeviceToDevice, stream));
+        h2d(s.doc_base, base.data(), base.size() * 4);
+        s.text_end = live;
+        if (old_arena) deferred_release.emplace_back(old_arena, old_bytes);
+        return docs;
     }
 
     // (re)build a shard's arena so the next batch (B new bytes, D new docs) fits
@@ -1250,6 +1317,23 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             return PX_ECAPACITY;
         }
 
+    // ---- which shards take the suffix-array path (px_psa.hip)
+    // A live chunk is encoded by PSA while it provably cannot rotate (<= 65,535 docs and
+    // <= kPsaMaxText doc bytes): its suffix tree is then never built.  A live chunk that
+    // outgrows that, or whose stream the PSA check flags, goes to k_gst_encode, which
+    // first re-walks (replays) the docs PSA encoded.
+    const bool psa_on = psa_enabled();
+    std::vector<uint8_t> wpsa(work.size(), 0);
+    std::vector<uint32_t> wreplay(work.size(), 0);
+    for (size_t k = 0; k < work.size(); ++k) {
+        const Work &w = work[k];
+        const Shard &sh = *w.s;
+        const bool fresh = sh.psa || (sh.hs.epoch == 0 && sh.hs.n_docs == 0);
+        const uint64_t live_text = sh.psa ? sh.text_end : 0;
+        wpsa[k] = psa_on && fresh && w.docs > 0 && (uint64_t)sh.hs.n_docs + w.docs <= (uint64_t)kChunkSlots &&
+                  live_text + w.bytes <= kPsaMaxText;
+    }
+
     // ---- arenas, doc destinations, comp scratch
     std::vector<uint8_t *> dst(n, nullptr), cdst(n, nullptr);
     uint64_t scratch_bytes = 0;
@@ -1259,10 +1343,11 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     // encoder messages: one u32 per doc byte, at 4x the record's comp scratch offset
     auto *msgs = (uint32_t *)heap.alloc(scratch_bytes * 4 + 256);
     uint64_t so = 0;
-    std::vector<GstShard> gs;
-    gs.reserve(work.size());
-    for (auto &w : work) {
-        shard_reserve(*w.s, w.bytes, w.docs);
+    for (size_t k = 0; k < work.size(); ++k) {
+        Work &w = work[k];
+        if (wpsa[k]) text_reserve(*w.s, w.bytes);
+        else if (w.s->text_only) wreplay[k] = upgrade_to_walk(*w.s, w.bytes, w.docs);
+        else shard_reserve(*w.s, w.bytes, w.docs);
         uint64_t t = w.s->text_end;
         for (uint32_t r = w.r0; r < w.r1; ++r) {
             if (doc_len[r] == 0xffffffffu) continue;
@@ -1272,6 +1357,90 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             so += round_up(doc_len[r], 16);
         }
         w.s->text_end = t;
+    }
+    auto *d_dst = (uint8_t **)heap.alloc((uint64_t)n * 8);
+    auto *d_cdst = (uint8_t **)heap.alloc((uint64_t)n * 8);
+    h2d(d_dst, dst.data(), (size_t)n * 8);
+    h2d(d_cdst, cdst.data(), (size_t)n * 8);
+    flush_shard_init();
+    hcheck(launch_doc_write(stream, n, dkeys, dkoff, dvals, dvoff, d_dst));
+
+    // ---- the suffix-array path over the PSA shards (messages, placement, check flags)
+    hcheck(hipEventRecord(ev0, stream));
+    uint32_t psa_shards = 0, walk_shards = 0;
+    double psa_ms = 0;
+    {
+        std::vector<PsaDoc> pd;
+        std::vector<PsaShard> ps;
+        std::vector<size_t> pwork;
+        uint64_t gpos = 0;
+        for (size_t k = 0; k < work.size(); ++k) {
+            if (!wpsa[k]) continue;
+            const Work &w = work[k];
+            Shard &sh = *w.s;
+            const uint32_t si = (uint32_t)ps.size();
+            uint32_t slot = 0;
+            uint64_t off = 0;
+            if (sh.psa && sh.hs.n_docs) {  // the live chunk's earlier docs: text, no messages
+                const Chunk &ch = chunks[sh.chunks[sh.hs.chunk_seq]];
+                for (uint32_t i = 0; i < sh.hs.n_docs; ++i) {
+                    pd.push_back(PsaDoc{sh.text + off, nullptr, (uint32_t)(gpos + off), ch.doc_len[i], si, slot++, 0, 0});
+                    off += ch.doc_len[i];
+                }
+            }
+            for (uint32_t r = w.r0; r < w.r1; ++r) {
+                if (doc_len[r] == 0xffffffffu) continue;
+                pd.push_back(PsaDoc{dst[r], msgs + (cdst[r] - comp_scratch), (uint32_t)(gpos + off), doc_len[r], si,
+                                    slot++, r, 0});
+                off += doc_len[r];
+            }
+            ps.push_back(PsaShard{(uint32_t)gpos, (uint32_t)off, sh.hs.chunk_seq, 0});
+            pwork.push_back(k);
+            gpos += off;
+        }
+        if (!ps.empty()) {
+            if (gpos >= 0xfffffff0ull) throw PxFail{PX_ECAPACITY};  // a batch is split far below this
+            auto *d_pd = (PsaDoc *)heap.alloc(pd.size() * sizeof(PsaDoc));
+            auto *d_ps = (PsaShard *)heap.alloc(ps.size() * sizeof(PsaShard) + ps.size() * 4 + 64);
+            auto *d_flag = (uint32_t *)(d_ps + ps.size());
+            h2d(d_pd, pd.data(), pd.size() * sizeof(PsaDoc));
+            h2d(d_ps, ps.data(), ps.size() * sizeof(PsaShard));
+            hcheck(hipMemsetAsync(d_flag, 0, ps.size() * 4, stream));
+            PsaAlloc A{[](void *self, uint64_t b) { return static_cast<px_ctx *>(self)->heap.alloc(b); },
+                       [](void *self, void *p, uint64_t b) { static_cast<px_ctx *>(self)->heap.release(p, b); }, this};
+            PsaStats pst{};
+            const auto tp = std::chrono::steady_clock::now();
+            hcheck(psa_run(stream, A, (uint32_t)pd.size(), d_pd, (uint32_t)ps.size(), d_ps, (uint32_t)gpos, d_chunk,
+                           d_idx, d_status, d_flag, &pst));
+            std::vector<uint32_t> flag(ps.size());
+            d2h(flag.data(), d_flag, ps.size() * 4);
+            sync();
+            psa_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp).count();
+            psa_stats = pst;
+            heap.release(d_pd, pd.size() * sizeof(PsaDoc));
+            heap.release(d_ps, ps.size() * sizeof(PsaShard) + ps.size() * 4 + 64);
+            for (size_t i = 0; i < ps.size(); ++i) {
+                const size_t k = pwork[i];
+                if (!flag[i]) {
+                    ++psa_shards;
+                    continue;
+                }
+                // the stale-pair check fired: this shard's live chunk goes to the walk
+                // (the text copied includes this batch's docs; its records keep reading their
+                // docs from the old arena, released at the end of the batch)
+                wpsa[k] = 0;
+                wreplay[k] = upgrade_to_walk(*work[k].s, 0, work[k].docs);
+            }
+            flush_shard_init();
+        }
+    }
+
+    // ---- the GST walk for the other shards (encoder messages)
+    std::vector<GstShard> gs;
+    std::vector<size_t> gwork;
+    for (size_t k = 0; k < work.size(); ++k) {
+        if (wpsa[k]) continue;
+        const Work &w = work[k];
         GstShard g{};
         g.text = w.s->text;
         g.doc_base = w.s->doc_base;
@@ -1284,22 +1453,20 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         g.doc_cap = w.s->doc_cap;
         g.r0 = w.r0;
         g.r1 = w.r1;
+        g.replay = wreplay[k];
         gs.push_back(g);
+        gwork.push_back(k);
     }
-    auto *d_dst = (uint8_t **)heap.alloc((uint64_t)n * 8);
-    auto *d_cdst = (uint8_t **)heap.alloc((uint64_t)n * 8);
-    auto *d_gs = (GstShard *)heap.alloc(gs.size() * sizeof(GstShard));
-    h2d(d_dst, dst.data(), (size_t)n * 8);
-    h2d(d_cdst, cdst.data(), (size_t)n * 8);
-    h2d(d_gs, gs.data(), gs.size() * sizeof(GstShard));
-    flush_shard_init();
-    hcheck(launch_doc_write(stream, n, dkeys, dkoff, dvals, dvoff, d_dst));
-
-    // ---- the GST walk (encoder messages), then the stream encoder
-    auto *d_stout = (ShardState *)stout_buf.get(gs.size() * sizeof(ShardState));
-    hcheck(hipEventRecord(ev0, stream));
-    hcheck(launch_gst_encode(stream, d_gs, (uint32_t)gs.size(), d_doclen, d_cdst, comp_scratch, msgs, d_chunk,
-                             d_idx, d_status, d_stout));
+    walk_shards = (uint32_t)gs.size();
+    GstShard *d_gs = nullptr;
+    auto *d_stout = (ShardState *)stout_buf.get(std::max<size_t>(gs.size(), 1) * sizeof(ShardState));
+    if (!gs.empty()) {
+        d_gs = (GstShard *)heap.alloc(gs.size() * sizeof(GstShard));
+        h2d(d_gs, gs.data(), gs.size() * sizeof(GstShard));
+        auto *sink = (uint32_t *)sink_buf.get((uint64_t)(kMaxDoc + 64) * 4);
+        hcheck(launch_gst_encode(stream, d_gs, (uint32_t)gs.size(), d_doclen, d_cdst, comp_scratch, msgs, d_chunk,
+                                 d_idx, d_status, d_stout, sink));
+    }
     hcheck(hipEventRecord(ev_mid, stream));
     hcheck(launch_gst_emit(stream, n, d_dst, d_doclen, d_cdst, comp_scratch, msgs, d_status, d_complen));
     hcheck(hipEventRecord(ev1, stream));
@@ -1311,7 +1478,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     d2h(ridx.data(), d_idx, n * 4);
     d2h(rstatus.data(), d_status, n * 4);
     std::vector<ShardState> stout(gs.size());
-    d2h(stout.data(), d_stout, gs.size() * sizeof(ShardState));
+    if (!gs.empty()) d2h(stout.data(), d_stout, gs.size() * sizeof(ShardState));
     sync();
     // Invariants of the walk + encoder: a record the walk placed (chunk/slot written)
     // has a compressed form of 1..2*doc_len+8 bytes; a record it did not place has a
@@ -1337,7 +1504,16 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         const uint32_t r = (uint32_t)std::atoi(e);
         if (r < n && rstatus[r] == kOk) rstatus[r] = kErrCorrupt;
     }
-    for (size_t k = 0; k < work.size(); ++k) work[k].s->hs = stout[k];
+    for (size_t i = 0; i < gwork.size(); ++i) work[gwork[i]].s->hs = stout[i];
+    for (size_t k = 0; k < work.size(); ++k)
+        if (wpsa[k]) {  // the PSA shard's live chunk grew by this batch's docs (no tree)
+            work[k].s->psa = true;
+            work[k].s->hs.n_docs += work[k].docs;
+        }
+    stats.last_psa_ms = psa_ms;
+    stats.last_psa_shards = psa_shards;
+    stats.last_walk_shards = walk_shards;
+    if (d_gs) heap.release(d_gs, gs.size() * sizeof(GstShard));
     {
         float ms = 0;
         hcheck(hipEventElapsedTime(&ms, ev0, ev1));
@@ -1402,7 +1578,6 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     heap.release(msgs, scratch_bytes * 4 + 256);
     heap.release(d_dst, (uint64_t)n * 8);
     heap.release(d_cdst, (uint64_t)n * 8);
-    heap.release(d_gs, gs.size() * sizeof(GstShard));
     heap.release(d_coff, (uint64_t)n * 8);
     heap.release(d_slots, (uint64_t)n * sizeof(RecSlot));
 
@@ -1511,6 +1686,9 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         }
         replaced[r] |= (uint32_t)cbt_insert(s, q, Leaf{rgchunk[r], ridx[r]});
     }
+
+    for (auto &b : deferred_release) heap.release(b.first, b.second);
+    deferred_release.clear();
 
     // ---- results
     int rc = corrupt;

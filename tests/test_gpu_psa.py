@@ -1,0 +1,105 @@
+"""The suffix-array setitem path (pixiu_amd/csrc/px_psa.hip) against the
+GST walk it replaces and against the oracle:
+
+* every BASELINE config: the same compressed bytes and placement with PX_PSA=0 (every
+  shard walked by k_gst_encode) and with the default (shards encoded by PSA);
+* a live chunk that outgrows the PSA bound in a later batch is handed to the walk,
+  which re-walks (replays) the docs PSA encoded: bytes equal the oracle's single
+  instance across the switch;
+* inputs on which the stale-pair check fires (small alphabets) still match the oracle.
+"""
+import os
+import random
+
+import numpy as np
+import pytest
+
+from _oracle import assemble
+
+pytestmark = pytest.mark.gpu
+px = pytest.importorskip("pixiu_amd")
+
+
+def _run(cp, rps, psa, store_factory):
+    old = os.environ.get("PX_PSA")
+    os.environ["PX_PSA"] = "1" if psa else "0"
+    try:
+        st = store_factory(records_per_shard=rps)
+        r = st.set_batch((cp.keys, cp.koff.astype(np.uint64)), (cp.vals, cp.voff.astype(np.uint64)))
+        stats = st.stats()
+        comp = st.export(px.records_of(r))
+        got = st.get_batch([cp.key(i) for i in range(0, cp.n, max(1, cp.n // 200))])
+        return r, stats, comp, got
+    finally:
+        if old is None:
+            os.environ.pop("PX_PSA", None)
+        else:
+            os.environ["PX_PSA"] = old
+
+
+@pytest.mark.parametrize("cfg,n,rps", [(1, 1000, 0), (2, 3000, 500), (3, 60, 16), (4, 20000, 2000), (5, 48, 16)])
+def test_psa_equals_walk(cfg, n, rps, store_factory):
+    from pixiu_amd import synth
+    cp = synth.make(cfg, n)
+    ra, sa, ca, ga = _run(cp, rps, False, store_factory)
+    rb, sb, cb, gb = _run(cp, rps, True, store_factory)
+    assert sa["last_psa_shards"] == 0 and sb["last_psa_shards"] >= 1
+    assert int(ra["status"].max()) == 0 and int(rb["status"].max()) == 0
+    assert ca == cb
+    assert ra["chunk"].tolist() == rb["chunk"].tolist() and ra["idx"].tolist() == rb["idx"].tolist()
+    assert ga == gb
+
+
+def test_psa_chunk_outgrows_bound_then_walk(store_factory, oracle):
+    """rps = 0: two batches encoded by PSA (6 MB), a third pushes the live chunk past
+    kPsaMaxText: the walk replays the 6,000 PSA docs, then continues; every record
+    equals the oracle's single instance."""
+    from pixiu_amd import synth
+    cp = synth.make(2, 9000)
+    st = store_factory(records_per_shard=0)
+    res = []
+    for a in (0, 3000, 6000):
+        res.append(st.set_batch([cp.key(i) for i in range(a, a + 3000)], [cp.val(i) for i in range(a, a + 3000)]))
+        s = st.stats()
+        assert (s["last_psa_shards"], s["last_walk_shards"]) == ((1, 0) if a < 6000 else (0, 1))
+    r = np.concatenate(res)
+    assert int(r["status"].max()) == 0
+    oc, ochunk, oidx = oracle.encode_docs([assemble(cp.key(i), cp.val(i)) for i in range(cp.n)])
+    assert st.export(px.records_of(r)) == oc
+    assert r["chunk"].tolist() == ochunk and r["idx"].tolist() == oidx
+
+
+def test_psa_small_alphabets_match_oracle(store_factory, oracle):
+    """Random small-alphabet shards (where the reference's stale active-edge pair can
+    change the output and the PSA check hands shards to the walk), batch of many shards."""
+    rng = random.Random(20261016)
+    keys, vals, groups = [], [], []
+    seen = set()
+    rps = 24
+    for g in range(40):
+        alpha = rng.choice([b"ab", b"abc", b"ABCDE", bytes([97, 98, 251]), bytes([251, 0, 2, 1, 97])])
+        rows = []
+        while len(rows) < rps:
+            k = bytes(rng.choice(alpha) for _ in range(rng.randint(1, 10))) + b"%d" % g
+            if k in seen:
+                continue
+            seen.add(k)
+            rows.append(len(keys))
+            keys.append(k)
+            vals.append(bytes(rng.choice(alpha) for _ in range(rng.randint(0, 60))))
+        groups.append(rows)
+    st = store_factory(records_per_shard=rps)
+    r = st.set_batch(keys, vals, check=False)
+    s = st.stats()
+    assert s["last_psa_shards"] + s["last_walk_shards"] == len(groups)
+    comp = st.export(px.records_of(r[r["status"] == 0]))
+    ok_rows = [i for i in range(len(keys)) if r["status"][i] == 0]
+    pos = {i: k for k, i in enumerate(ok_rows)}
+    for rows in groups:
+        want = None
+        try:
+            want = oracle.run([keys[i] for i in rows], [vals[i] for i in rows], do_get=False)
+        except RuntimeError:  # the reference would crash on this shard (PX_EREFCRASH here)
+            assert any(int(r["status"][i]) != 0 for i in rows)
+            continue
+        assert [comp[pos[i]] for i in rows] == want["comp"]

@@ -189,6 +189,45 @@ long lpf_messages(int ndocs, const uint8_t *docs, const uint64_t *off, uint32_t 
             prev_doc = edoc;
         }
     }
+    // the same stream from lpf alone (the GPU formulation): C(i) = lpf(i) >= 1
+    // unless i = reach(J-1) = J-1+lpf(J-1) for a J whose range is non-empty (lpf(J) >=
+    // lpf(J-1)); a run of lpf(J) - lpf(J-1) >= 7 COMPRESS steps ends at b = J+lpf(J)-1 with
+    // the earliest occurrence of T[J..J+lpf(J)) (and of one byte less at b-1 if T[b] is 251)
+    long alt_diff = 0;
+    for (int d = 0; d < ndocs; ++d) {
+        const uint32_t b0 = start_of[d], e = b0 + (uint32_t)(off[d + 1] - off[d]);
+        std::vector<uint32_t> m2(e - b0);
+        for (uint32_t i = b0; i < e; ++i) m2[i - b0] = lpf[i] >= 1 ? 0u : 0xffffffffu;
+        auto E = [&](uint32_t J, uint32_t l) {
+            const uint32_t r = s.isa[J];
+            uint32_t a = 0, z = r;
+            while (a < z) { uint32_t mid = (a + z) / 2; if (lcp_min.q(mid + 1, r) >= l) z = mid; else a = mid + 1; }
+            const uint32_t lo = a;
+            a = r; z = n - 1;
+            while (a < z) { uint32_t mid = (a + z + 1) / 2; if (lcp_min.q(r + 1, mid) >= l) a = mid; else z = mid - 1; }
+            const uint32_t Ep = pos_min.q(lo, a);
+            return (uint32_t)doc_of[Ep] << 16 | (Ep - start_of[doc_of[Ep]] + l - 1);
+        };
+        for (uint32_t J = b0; J < e; ++J) {
+            const uint32_t lp = J > b0 ? lpf[J - 1] : 0;
+            if (J > b0 && lpf[J] + 0 >= lp && J - 1 + lp < e) m2[J - 1 + lp - b0] = 0xffffffffu;
+        }
+        for (uint32_t J = b0; J < e; ++J) {
+            const uint32_t lp = J > b0 ? lpf[J - 1] : 0;
+            if (lpf[J] >= lp + 7) {
+                const uint32_t b = J + lpf[J] - 1;
+                m2[b - b0] = E(J, lpf[J]);
+                if (t[b] == 251) m2[b - 1 - b0] = E(J, lpf[J] - 1);
+            }
+        }
+        for (uint32_t i = b0; i < e; ++i) {
+            const uint32_t a = msg[off[d] + (i - b0)], b = m2[i - b0];
+            if ((a == 0xffffffffu) != (b == 0xffffffffu)) ++alt_diff;
+        }
+        if (stats) stats[31] += alt_diff;
+        // the GPU formulation's stream replaces the scan's (tokens only use run ends)
+        for (uint32_t i = b0; i < e; ++i) msg[off[d] + (i - b0)] = m2[i - b0];
+    }
     return flagged;
 }
 
