@@ -253,7 +253,8 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
         t1 = time.perf_counter()
         sst = st.stats()
         set_kms, walk_kms, emit_kms = sst["last_set_kernel_ms"], sst["last_walk_kernel_ms"], sst["last_emit_kernel_ms"]
-        psa = (sst["last_psa_ms"], int(sst["last_psa_shards"]), int(sst["last_walk_shards"]))
+        psa = (sst["last_psa_ms"], int(sst["last_psa_shards"]), int(sst["last_walk_shards"]),
+               sst["last_psa_sort_ms"], sst["last_psa_lcp_ms"], sst["last_psa_msg_ms"], int(sst["last_psa_iters"]))
         rc, off, ln, sts, need = st.get_batch_device(keys_host, out.data_ptr(), out_cap, px.COMPAT)
         t2 = time.perf_counter()
         gst = st.stats()
@@ -376,7 +377,11 @@ def summarize(cfg, r, rps, world, a, pmc_path):
         "kernel_ms": {"encode_stage": round(walk_kms, 3), "k_gst_emit": round(emit_kms, 3),
                       "k_decode": round(dec_kms, 3), "k_decode_exact": round(r["exact_dec_kms"], 3)},
         "encode_stage": {"kernels": enc_name, "psa_shards": psa_shards, "walked_shards": walk_shards,
-                         "psa_host_ms": round(float(np.mean([x["psa"][0] for x in runs])), 3)},
+                         "psa_host_ms": round(float(np.mean([x["psa"][0] for x in runs])), 3),
+                         "psa_split_ms": {"sort": round(float(np.mean([x["psa"][3] for x in runs])), 3),
+                                          "links_lcp": round(float(np.mean([x["psa"][4] for x in runs])), 3),
+                                          "messages": round(float(np.mean([x["psa"][5] for x in runs])), 3)},
+                         "doubling_steps": runs[-1]["psa"][6]},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 3), "peak": PEAK_HBM_GBPS,
                      "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBPS, 6), "traffic": traffic,
                      "traffic_source": tsrc},

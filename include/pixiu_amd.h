@@ -94,6 +94,10 @@ typedef struct px_stats {
     double last_psa_ms;           /* the suffix-array pass of the last px_set_batch (host wall) */
     uint64_t last_psa_shards;     /* shards the last px_set_batch encoded by the suffix-array pass */
     uint64_t last_walk_shards;    /* shards it walked with k_gst_encode */
+    double last_psa_sort_ms;      /* suffix-array pass: text gather + suffix sorting (GPU events) */
+    double last_psa_lcp_ms;       /*   nearest-smaller-position links + their lcp values */
+    double last_psa_msg_ms;       /*   messages, earliest occurrences, placement */
+    uint64_t last_psa_iters;      /*   prefix-doubling steps after the first sort */
 } px_stats;
 
 px_ctx *px_open(const px_opts *opts);

@@ -32,6 +32,8 @@
 //                  (lcp(p) >= lcp(p-1) - 1 for both neighbours)
 //   k_psa_msg0 / k_psa_runs   messages, earliest occurrences (neighbour chains), the
 //                  stale-pair check; k_psa_place   chunk / slot / status per record
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include <hip/hip_runtime.h>
@@ -53,7 +55,9 @@ constexpr uint32_t kPass = 0xffffffffu;
 PSA_DEV uint32_t lane_id() { return threadIdx.x & 63u; }
 
 // ---------------------------------------------------------------- text
-__global__ void __launch_bounds__(256) k_psa_gather(uint32_t ndocs, const PsaDoc *docs, uint8_t *G, uint32_t *pdoc) {
+// G = the text, pdoc = doc id and dist = bytes to the doc's end, per position
+__global__ void __launch_bounds__(256) k_psa_gather(uint32_t ndocs, const PsaDoc *docs, uint8_t *G, uint32_t *pdoc,
+                                                    uint16_t *dist) {
     const uint32_t lane = lane_id();
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);
     for (uint32_t g = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); g < ndocs; g += waves) {
@@ -62,30 +66,23 @@ __global__ void __launch_bounds__(256) k_psa_gather(uint32_t ndocs, const PsaDoc
         for (uint32_t o = lane; o < d.len; o += 64) {
             G[d.start + o] = src[o];
             pdoc[d.start + o] = g;
+            dist[d.start + o] = (uint16_t)(d.len - o);  // 1..65,535
         }
     }
 }
 
-// doc end (exclusive, global) of position p
-PSA_DEV uint32_t doc_end(const PsaDoc *docs, const uint32_t *pdoc, uint32_t p) {
-    const uint32_t g = pdoc[p];
-    return docs[g].start + docs[g].len;
-}
-
-// initial keys: shard (top 19 bits) | 5 symbols of 9 bits (byte + 1; 0 past the doc end)
-constexpr int kSym0 = 5;
+// initial keys: shard (top bits) | `syms` symbols of 9 bits (byte + 1; 0 past the doc end):
+// as many symbols as the shard count leaves room for (5 to 6)
 __global__ void __launch_bounds__(256) k_psa_key0(uint32_t N, const uint8_t *G, const uint32_t *pdoc,
-                                                  const PsaDoc *docs, uint64_t *keys, uint32_t *vals) {
+                                                  const PsaDoc *docs, const uint16_t *dist, uint32_t syms,
+                                                  uint64_t *keys, uint32_t *vals) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= N) return;
-    const uint32_t g = pdoc[p];
-    const uint32_t end = docs[g].start + docs[g].len;
-    uint64_t k = (uint64_t)docs[g].shard << 45;
-#pragma unroll
-    for (int s = 0; s < kSym0; ++s) {
-        const uint32_t q = p + s;
-        const uint64_t sym = q < end ? (uint64_t)G[q] + 1 : 0;
-        k |= sym << (36 - 9 * s);
+    const uint32_t left = dist[p];
+    uint64_t k = (uint64_t)docs[pdoc[p]].shard << (9 * syms);
+    for (uint32_t s = 0; s < syms; ++s) {
+        const uint64_t sym = s < left ? (uint64_t)G[p + s] + 1 : 0;
+        k |= sym << (9 * (syms - 1 - s));
     }
     keys[p] = k;
     vals[p] = p;
@@ -95,11 +92,11 @@ __global__ void __launch_bounds__(256) k_psa_key0(uint32_t N, const uint8_t *G, 
 // than 5 symbols (its key holds its whole string: equal ones are equal strings, kept
 // in position order by the stable sort and resolved as they are)
 __global__ void __launch_bounds__(256) k_psa_head0(uint32_t N, const uint64_t *keys, const uint32_t *sa,
-                                                   const uint32_t *pdoc, const PsaDoc *docs, uint32_t *hflag) {
+                                                   const uint16_t *dist, uint32_t syms, uint32_t *hflag) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= N) return;
     const uint32_t p = sa[r];
-    const bool complete = doc_end(docs, pdoc, p) - p < (uint32_t)kSym0;
+    const bool complete = dist[p] < syms;
     hflag[r] = (r == 0 || keys[r] != keys[r - 1] || complete) ? r : 0u;
 }
 
@@ -116,14 +113,12 @@ __global__ void __launch_bounds__(256) k_psa_rank0(uint32_t N, const uint32_t *s
 
 // doubling step h: key (group, rank of the suffix h further, 0 past the doc end)
 __global__ void __launch_bounds__(256) k_psa_key2(uint32_t m, const uint32_t *act, const uint32_t *rank,
-                                                  const uint32_t *pdoc, const PsaDoc *docs, uint32_t h,
-                                                  uint64_t *keys, uint32_t *vals) {
+                                                  const uint16_t *dist, uint32_t h, uint64_t *keys, uint32_t *vals) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= m) return;
     const uint32_t p = act[t];
-    const uint32_t end = doc_end(docs, pdoc, p);
     const uint64_t hi = rank[p];
-    const uint64_t lo = p + h < end ? (uint64_t)rank[p + h] + 1 : 0;
+    const uint64_t lo = h < dist[p] ? (uint64_t)rank[p + h] + 1 : 0;
     keys[t] = hi << 32 | lo;
     vals[t] = p;
 }
@@ -214,14 +209,29 @@ __global__ void __launch_bounds__(256) k_psa_ansv(uint32_t N, MinTree t, const u
         lo = sh.base;
         hi = sh.base + sh.len;
     }
-    // inside the 64-rank block
-    uint32_t ps = kNoPos, ns = kNoPos;
-    for (uint32_t k = 1; k < 64; ++k) {
-        const uint32_t ul = (uint32_t)__shfl((int)v, (int)((lane - k) & 63u));
-        const uint32_t ur = (uint32_t)__shfl((int)v, (int)((lane + k) & 63u));
-        if (ps == kNoPos && lane >= k && ul < v) ps = r - k;
-        if (ns == kNoPos && lane + k < 64 && ur < v) ns = r + k;
+    // inside the 64-rank block: binary lifting over window minima.  ml[k] = min of the
+    // 2^k lanes ending at this lane, mr[k] = of the 2^k lanes starting at it
+    uint32_t ml[6], mr[6];
+    ml[0] = mr[0] = v;
+    for (int k = 1; k < 6; ++k) {
+        const uint32_t w = 1u << (k - 1);
+        const uint32_t a = (uint32_t)__shfl((int)ml[k - 1], (int)((lane - w) & 63u));
+        const uint32_t b = (uint32_t)__shfl((int)mr[k - 1], (int)((lane + w) & 63u));
+        ml[k] = lane >= w ? min(ml[k - 1], a) : ml[k - 1];
+        mr[k] = lane + w < 64 ? min(mr[k - 1], b) : mr[k - 1];
     }
+    // nearest smaller to the left: extend (pl, lane) while its minimum stays >= v
+    int pl = (int)lane - 1, pr = (int)lane + 1;
+    for (int k = 5; k >= 0; --k) {
+        const int w = 1 << k;
+        const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute(max(pl, 0) << 2, (int)ml[k]);
+        if (pl - w + 1 >= 0 && a >= v) pl -= w;
+        const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(min(pr, 63) << 2, (int)mr[k]);
+        if (pr + w - 1 <= 63 && b >= v) pr += w;
+    }
+    uint32_t ps = pl >= 0 ? r - (lane - (uint32_t)pl) : kNoPos;
+    uint32_t ns = pr <= 63 ? r + ((uint32_t)pr - lane) : kNoPos;
+    if (ns != kNoPos && ns >= N) ns = kNoPos;
     // the rest through the min tree, one element at a time (few per block: the block's
     // prefix / suffix minima)
     uint64_t need = __ballot(live && (ps == kNoPos || ns == kNoPos));
@@ -248,20 +258,26 @@ __global__ void __launch_bounds__(256) k_psa_ansv(uint32_t N, MinTree t, const u
 // ---------------------------------------------------------------- lcp with those neighbours
 constexpr uint32_t kLceSpan = 256;  // text positions per thread (Kasai-style amortisation)
 
-PSA_DEV uint32_t lce(const uint8_t *G, uint32_t p, uint32_t q, uint32_t k, uint32_t lim) {
-    // bytes equal from offset k on, up to lim (both suffixes stay inside their docs)
-    while (k + 8 <= lim) {
-        uint64_t a, b;
-        __builtin_memcpy(&a, G + p + k, 8);
-        __builtin_memcpy(&b, G + q + k, 8);
-        if (a != b) return k + (uint32_t)(__builtin_ctzll(a ^ b) >> 3);
-        k += 8;
-    }
-    while (k < lim && G[p + k] == G[q + k]) ++k;
-    return k;
+// 8 text bytes from any offset: two aligned 8-byte loads and a funnel shift
+PSA_DEV uint64_t ld8(const uint64_t *G8, uint32_t off) {
+    const uint32_t w = off >> 3, sh = (off & 7u) * 8u;
+    const uint64_t a = G8[w];
+    if (!sh) return a;
+    const uint64_t b = G8[w + 1];
+    return (a >> sh) | (b << (64u - sh));
 }
 
-__global__ void __launch_bounds__(256) k_psa_lce(uint32_t N, const uint8_t *G, const uint32_t *pdoc, const PsaDoc *docs,
+PSA_DEV uint32_t lce(const uint64_t *G8, uint32_t p, uint32_t q, uint32_t k, uint32_t lim) {
+    // bytes equal from offset k on, up to lim (both suffixes stay inside their docs)
+    while (k < lim) {
+        const uint64_t x = ld8(G8, p + k) ^ ld8(G8, q + k);
+        if (x) return min(lim, k + (uint32_t)(__builtin_ctzll(x) >> 3));
+        k += 8;
+    }
+    return lim;
+}
+
+__global__ void __launch_bounds__(256) k_psa_lce(uint32_t N, const uint64_t *G8, const uint16_t *dist,
                                                  const uint32_t *psvp, const uint32_t *nsvp, uint16_t *lcp_p,
                                                  uint16_t *lcp_n) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -270,21 +286,21 @@ __global__ void __launch_bounds__(256) k_psa_lce(uint32_t N, const uint8_t *G, c
     const uint32_t p1 = min(N, p0 + kLceSpan);
     uint32_t kp = 0, kn = 0;
     for (uint32_t p = p0; p < p1; ++p) {
-        const uint32_t endp = doc_end(docs, pdoc, p);
+        const uint32_t dp = dist[p];
         const uint32_t q = psvp[p], s = nsvp[p];
         kp = kp ? kp - 1 : 0;
         kn = kn ? kn - 1 : 0;
         if (q == kNoPos) {
             kp = 0;
         } else {
-            const uint32_t lim = min(endp - p, doc_end(docs, pdoc, q) - q);
-            kp = lce(G, p, q, min(kp, lim), lim);
+            const uint32_t lim = min(dp, (uint32_t)dist[q]);
+            kp = lce(G8, p, q, min(kp, lim), lim);
         }
         if (s == kNoPos) {
             kn = 0;
         } else {
-            const uint32_t lim = min(endp - p, doc_end(docs, pdoc, s) - s);
-            kn = lce(G, p, s, min(kn, lim), lim);
+            const uint32_t lim = min(dp, (uint32_t)dist[s]);
+            kn = lce(G8, p, s, min(kn, lim), lim);
         }
         lcp_p[p] = (uint16_t)kp;
         lcp_n[p] = (uint16_t)kn;
@@ -322,8 +338,8 @@ __global__ void __launch_bounds__(256) k_psa_msg0(uint32_t N, const uint32_t *pd
 }
 
 __global__ void __launch_bounds__(256) k_psa_runs(uint32_t N, const uint8_t *G, const uint32_t *pdoc, const PsaDoc *docs,
-                                                  const uint32_t *psvp, const uint32_t *nsvp, const uint16_t *lp,
-                                                  const uint16_t *ln, uint32_t *shard_flag) {
+                                                  const uint16_t *dist, const uint32_t *psvp, const uint32_t *nsvp,
+                                                  const uint16_t *lp, const uint16_t *ln, uint32_t *shard_flag) {
     const uint32_t J = blockIdx.x * blockDim.x + threadIdx.x;
     if (J >= N) return;
     const uint32_t g = pdoc[J];
@@ -345,7 +361,7 @@ __global__ void __launch_bounds__(256) k_psa_runs(uint32_t N, const uint8_t *G, 
             const uint32_t fe = J - 1 + lq;
             if (G[fe - 2] == 251 && (G[fe - 1] == 0 || G[fe - 1] == 2)) {
                 const uint32_t e = earliest(psvp, nsvp, lp, ln, J - 1, lq);
-                if (e + lq == doc_end(docs, pdoc, e)) shard_flag[d.shard] = 1;
+                if (lq == dist[e]) shard_flag[d.shard] = 1;
             }
         }
     }
@@ -393,6 +409,7 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     const uint64_t n64 = N;
     auto *G = (uint8_t *)get(n64 + 64);
     auto *pdoc = (uint32_t *)get(n64 * 4);
+    auto *dist = (uint16_t *)get(n64 * 2);
     auto *rank = (uint32_t *)get(n64 * 4);
     auto *sa = (uint32_t *)get(n64 * 4);
     auto *keys = (uint64_t *)get(n64 * 8);
@@ -403,11 +420,14 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     auto *f2 = (uint32_t *)get(n64 * 4);
     auto *act = (uint8_t *)get(n64);
     auto *cnt = (uint32_t *)get(64);
-    PSA_CHECK(hipMemsetAsync(G + N, 0, 64, s));
+    PSA_CHECK(hipMemsetAsync(G + N, 0, 64, s));  // (ld8 reads up to 15 bytes past the text)
     const uint32_t tb = 256;
     auto blocks = [&](uint64_t n) { return (uint32_t)((n + tb - 1) / tb); };
-    k_psa_gather<<<std::min<uint32_t>((ndocs + 3) / 4, 65535u), 256, 0, s>>>(ndocs, docs, G, pdoc);
-    k_psa_key0<<<blocks(N), tb, 0, s>>>(N, G, pdoc, docs, keys, vals);
+    int shard_bits = 1;
+    while ((1u << shard_bits) <= nshards && shard_bits < 19) ++shard_bits;
+    const uint32_t syms = std::min<uint32_t>(6, (64 - shard_bits) / 9);  // 5 or 6 symbols
+    k_psa_gather<<<std::min<uint32_t>((ndocs + 3) / 4, 65535u), 256, 0, s>>>(ndocs, docs, G, pdoc, dist);
+    k_psa_key0<<<blocks(N), tb, 0, s>>>(N, G, pdoc, docs, dist, syms, keys, vals);
     // temp storage: the largest of sort / scan / select over N elements
     size_t t_sort = 0, t_scan = 0, t_sel = 0;
     PSA_CHECK(rocprim::radix_sort_pairs(nullptr, t_sort, keys, keys2, vals, sa, (size_t)N, 0, 64, s));
@@ -415,11 +435,9 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     PSA_CHECK(rocprim::select(nullptr, t_sel, sa, act, vals, cnt, (size_t)N, s));
     const size_t t_bytes = std::max({t_sort, t_scan, t_sel}) + 256;
     void *tmp = get(t_bytes);
-    int shard_bits = 1;
-    while ((1u << shard_bits) <= nshards && shard_bits < 19) ++shard_bits;
     size_t tb_ = t_bytes;
-    PSA_CHECK(rocprim::radix_sort_pairs(tmp, tb_, keys, keys2, vals, sa, (size_t)N, 0, 45 + shard_bits, s));
-    k_psa_head0<<<blocks(N), tb, 0, s>>>(N, keys2, sa, pdoc, docs, f1);
+    PSA_CHECK(rocprim::radix_sort_pairs(tmp, tb_, keys, keys2, vals, sa, (size_t)N, 0, 9 * syms + shard_bits, s));
+    k_psa_head0<<<blocks(N), tb, 0, s>>>(N, keys2, sa, dist, syms, f1);
     tb_ = t_bytes;
     PSA_CHECK(rocprim::inclusive_scan(tmp, tb_, f1, vals2, (size_t)N, Max(), s));
     k_psa_rank0<<<blocks(N), tb, 0, s>>>(N, sa, vals2, rank, act);
@@ -434,10 +452,10 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     int rank_bits = 1;
     while (rank_bits < 32 && (1ull << rank_bits) <= n64) ++rank_bits;
     uint32_t it = 0;
-    for (uint32_t h = kSym0; m > 0; h *= 2, ++it) {
+    for (uint32_t h = syms; m > 0; h *= 2, ++it) {
         if (st && it < 24) st->active[it] = m;
         if (it >= 20) return hipErrorUnknown;  // cannot happen: docs are <= 65,535 bytes
-        k_psa_key2<<<blocks(m), tb, 0, s>>>(m, alist, rank, pdoc, docs, h, keys, vals2);
+        k_psa_key2<<<blocks(m), tb, 0, s>>>(m, alist, rank, dist, h, keys, vals2);
         tb_ = t_bytes;
         PSA_CHECK(rocprim::radix_sort_pairs(tmp, tb_, keys, keys2, vals2, f2, (size_t)m, 0, 32 + rank_bits, s));
         // f2 = positions in the new order; group heads f1 -> vals2, subgroup heads in the
@@ -481,11 +499,12 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     k_psa_ansv<<<(uint32_t)((n64 + 255) / 256), 256, 0, s>>>(N, t, pdoc, docs, shards, psvp, nsvp);
     auto *lcp_p = (uint16_t *)rank;  // ranks are no longer needed: two u16 arrays in their place
     auto *lcp_n = (uint16_t *)get(n64 * 2);
-    k_psa_lce<<<blocks((n64 + kLceSpan - 1) / kLceSpan), tb, 0, s>>>(N, G, pdoc, docs, psvp, nsvp, lcp_p, lcp_n);
+    k_psa_lce<<<blocks((n64 + kLceSpan - 1) / kLceSpan), tb, 0, s>>>(N, (const uint64_t *)G, dist, psvp, nsvp, lcp_p,
+                                                                     lcp_n);
     PSA_CHECK(hipEventRecord(e2, s));
     // ---- messages
     k_psa_msg0<<<blocks(N), tb, 0, s>>>(N, pdoc, docs, lcp_p, lcp_n);
-    k_psa_runs<<<blocks(N), tb, 0, s>>>(N, G, pdoc, docs, psvp, nsvp, lcp_p, lcp_n, shard_flag);
+    k_psa_runs<<<blocks(N), tb, 0, s>>>(N, G, pdoc, docs, dist, psvp, nsvp, lcp_p, lcp_n, shard_flag);
     k_psa_place<<<blocks(ndocs), tb, 0, s>>>(ndocs, docs, shards, rec_chunk, rec_idx, rec_status);
     PSA_CHECK(hipEventRecord(e3, s));
     PSA_CHECK(hipEventSynchronize(e3));
@@ -493,12 +512,19 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         PSA_CHECK(hipEventElapsedTime(&st->ms_sort, e0, e1));
         PSA_CHECK(hipEventElapsedTime(&st->ms_lcp, e1, e2));
         PSA_CHECK(hipEventElapsedTime(&st->ms_msg, e2, e3));
+        if (const char *v = std::getenv("PX_PSA_VERBOSE"); v && *v == '1') {
+            fprintf(stderr, "psa: N=%u docs=%u shards=%u syms=%u sort %.2f ms, links+lcp %.2f ms, msgs %.2f ms; active:",
+                    N, ndocs, nshards, syms, st->ms_sort, st->ms_lcp, st->ms_msg);
+            for (uint32_t k = 0; k < it && k < 24; ++k) fprintf(stderr, " %u", st->active[k]);
+            fprintf(stderr, "\n");
+        }
     }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     (void)hipEventDestroy(e2);
     (void)hipEventDestroy(e3);
     put(lcp_n, n64 * 2);
+    put(dist, n64 * 2);
     put(G, n64 + 64);
     put(pdoc, n64 * 4);
     put(rank, n64 * 4);

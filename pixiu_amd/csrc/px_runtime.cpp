@@ -1511,6 +1511,10 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             work[k].s->hs.n_docs += work[k].docs;
         }
     stats.last_psa_ms = psa_ms;
+    stats.last_psa_sort_ms = psa_shards ? psa_stats.ms_sort : 0;
+    stats.last_psa_lcp_ms = psa_shards ? psa_stats.ms_lcp : 0;
+    stats.last_psa_msg_ms = psa_shards ? psa_stats.ms_msg : 0;
+    stats.last_psa_iters = psa_shards ? psa_stats.iterations : 0;
     stats.last_psa_shards = psa_shards;
     stats.last_walk_shards = walk_shards;
     if (d_gs) heap.release(d_gs, gs.size() * sizeof(GstShard));
