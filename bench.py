@@ -30,7 +30,8 @@ sys.path.insert(0, ROOT)
 PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 # records per shard (independent GST instances) benchmarked for each BASELINE config;
 # DESIGN.md §6 has the compression-vs-shard-size curve
-DEFAULT_RPS = {1: 0, 2: 500, 3: 2, 4: 2000, 5: 16}
+# (the suffix-array path keeps shards up to 8.4 MB of text at GPU speed: DESIGN.md §9)
+DEFAULT_RPS = {1: 0, 2: 2000, 3: 64, 4: 8000, 5: 126}
 
 
 def parse():

@@ -1381,7 +1381,13 @@ __global__ void __launch_bounds__(256) k_link(uint32_t n, const LinkJob *jobs) {
 // exceed what it asked for, an unlinked token) ends the batch; that one segment
 // then goes through the serial frame machine (a stack of Frames in scratch memory),
 // which is the reference's generator nesting restated.
-constexpr uint32_t kLaneDepth = 10;  // 10 KB of LDS per wave: 4 blocks (16 waves) per CU
+#ifndef PX_LANE_DEPTH
+#define PX_LANE_DEPTH 10
+#endif
+#ifndef PX_DEC_WAVES
+#define PX_DEC_WAVES 4
+#endif
+constexpr uint32_t kLaneDepth = PX_LANE_DEPTH;  // 10: 10 KB of LDS per wave, 4 blocks (16 waves) per CU
 constexpr uint32_t kLaneCopyMax = 512;  // plain pieces up to this size are copied by one lane
 constexpr uint32_t kAssignMin = 24;      // idle lanes that trigger an assignment round
 
@@ -1531,7 +1537,7 @@ struct DecLds {
     uint32_t stk[kLaneDepth * 4][64];
 };
 
-constexpr uint32_t kDecWaves = 4;  // independent query waves per block (see kGstWaves)
+constexpr uint32_t kDecWaves = PX_DEC_WAVES;  // independent query waves per block (see kGstWaves)
 
 // the body of k_decode (getitem queries) and k_decode_keys (the stored-key prefixes
 // setitem and prefix iteration decode): one code, two kernel names in the profiles

@@ -1672,23 +1672,47 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             }
     }
 
-    // ---- CritBit inserts (per shard, in arrival order)
+    // ---- CritBit inserts: every shard's own records in arrival order, shards on host
+    // threads (their tries are independent); then a key that moved to a newer shard is
+    // deleted from its older one, in record order (a shard's records all precede a newer
+    // shard's, so this is the order the sequential loop would have used)
     std::vector<uint32_t> replaced(n, 0);
-    for (uint32_t r = 0; r < n; ++r) {
-        if (!live[r]) continue;
-        Shard &s = *shards[rec_shard[r]];
-        const uint8_t *kp = hkeys.data() + hkoff[r];
-        uint64_t klen = hkoff[r + 1] - hkoff[r];
-        std::string q = esc_key(kp, klen);
-        if (opts.records_per_shard != 0) {
+    std::vector<std::pair<uint32_t, uint32_t>> moved;  // (record, older shard)
+    if (opts.records_per_shard != 0)
+        for (uint32_t r = 0; r < n; ++r) {
+            if (!live[r]) continue;
+            const uint8_t *kp = hkeys.data() + hkoff[r];
+            const uint64_t klen = hkoff[r + 1] - hkoff[r];
             const int64_t prev = keymap.find(kp, klen);
-            if (prev >= 0 && (uint32_t)prev != s.id) {
-                cbt_delete(*shards[(size_t)prev], q);  // cross-shard replace
-                replaced[r] = 1;
-            }
-            keymap.put(kp, klen, s.id);
+            if (prev >= 0 && (uint32_t)prev != rec_shard[r]) moved.emplace_back(r, (uint32_t)prev);
+            keymap.put(kp, klen, rec_shard[r]);
         }
-        replaced[r] |= (uint32_t)cbt_insert(s, q, Leaf{rgchunk[r], ridx[r]});
+    auto insert_work = [&](size_t k) {
+        const Work &w = work[k];
+        Shard &s = *w.s;
+        std::string q;
+        for (uint32_t r = w.r0; r < w.r1; ++r) {
+            if (!live[r]) continue;
+            esc_key_into(q, hkeys.data() + hkoff[r], hkoff[r + 1] - hkoff[r]);
+            replaced[r] |= (uint32_t)cbt_insert(s, q, Leaf{rgchunk[r], ridx[r]});
+        }
+    };
+    const uint32_t nthr = std::min<uint32_t>(host_threads(), (uint32_t)work.size());
+    if (nthr <= 1 || n < 2048) {
+        for (size_t k = 0; k < work.size(); ++k) insert_work(k);
+    } else {
+        std::atomic<size_t> next{0};
+        std::vector<std::thread> pool;
+        for (uint32_t t = 0; t < nthr; ++t)
+            pool.emplace_back([&] {
+                for (size_t k; (k = next.fetch_add(1)) < work.size();) insert_work(k);
+            });
+        for (auto &th : pool) th.join();
+    }
+    for (const auto &mv : moved) {  // cross-shard replace
+        const uint32_t r = mv.first;
+        cbt_delete(*shards[mv.second], esc_key(hkeys.data() + hkoff[r], hkoff[r + 1] - hkoff[r]));
+        replaced[r] = 1;
     }
 
     for (auto &b : deferred_release) heap.release(b.first, b.second);
