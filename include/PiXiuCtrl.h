@@ -14,7 +14,8 @@
 // including the CLI's `ctrl.st.cbt_chunk->getitem(ctrl.st.local_chunk.used_num - 1)->len`
 // (main.cpp:67).  Semantics are the reference's single instance (one shard);
 // getitem and iter stream the compat expansion (PXSGen byte-for-byte).  Difference:
-// `reinsert` is a no-op (compaction policy out of scope).
+// reinsert compaction runs inside setitem/delitem; calling
+// `reinsert` directly does nothing.
 #ifndef PIXIU_CTRL_FACADE_H
 #define PIXIU_CTRL_FACADE_H
 

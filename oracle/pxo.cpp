@@ -437,6 +437,8 @@ class Gst {
 struct Chunk {
     std::vector<Bytes> recs;
     std::vector<uint8_t> dead;
+    int used = 0;   // PiXiuChunk::used_num: records placed minus deleted (PiXiuStr.h:76)
+    int total = 0;  // PiXiuChunk::total_num: set when the chunk is closed (PiXiuCtrl.cpp:15)
     std::vector<Bytes> exact;          // memo of exact expansions
     std::vector<uint8_t> exact_state;  // 0 none, 1 in progress, 2 done
 };
@@ -631,20 +633,89 @@ struct pxo_shard {
     bool has_root = false;
     CbtRef root;
 
+    // Glob_Reinsert_Chunk (PiXiuStr.cpp:4), per instance here: the last chunk a delete
+    // left under 80 % of PXC_STR_NUM live records (PiXiuStr.cpp:178-187), or -1
+    int glob = -1;
+
     pxo_shard() { chunks.emplace_back(); }
 
-    // PiXiuCtrl::setitem minus CritBit: rotation check (PiXiuCtrl.cpp:13), then
-    // SuffixTree::setitem
-    void store(const Bytes &doc, uint32_t *chunk_no, uint32_t *idx) {
-        if (gst.pools() >= kRotatePools || gst.num_docs() == (size_t)kChunkSlots) {
-            gst.clear();
-            chunks.emplace_back();
-        }
+    bool rotation_due() const { return gst.pools() >= kRotatePools || gst.num_docs() == (size_t)kChunkSlots; }
+    // SuffixTree::setitem into the live chunk
+    void place(const Bytes &doc, uint32_t *chunk_no, uint32_t *idx) {
         Chunk &ch = chunks.back();
         ch.recs.push_back(gst.add_doc(doc));
         ch.dead.push_back(0);
+        ch.used++;
         *chunk_no = (uint32_t)chunks.size() - 1;
         *idx = (uint32_t)ch.recs.size() - 1;
+    }
+    // PiXiuCtrl::setitem minus CritBit and reinsert: rotation check (PiXiuCtrl.cpp:13),
+    // then SuffixTree::setitem (the encoder-only driver)
+    void store(const Bytes &doc, uint32_t *chunk_no, uint32_t *idx) {
+        if (rotation_due()) {
+            gst.clear();
+            chunks.emplace_back();
+        }
+        place(doc, chunk_no, idx);
+    }
+
+    // need_reinsert (PiXiuCtrl.cpp:7-8): live records under half of the closed total
+    bool need_reinsert(int c) const { return chunks[(size_t)c].used < 0.5 * chunks[(size_t)c].total; }
+    int live_chunk() const { return (int)chunks.size() - 1; }
+
+    // PiXiuChunk::delitem (PiXiuStr.cpp:178-187)
+    void chunk_delitem(const Leaf &l) {
+        Chunk &ch = chunks[l.chunk];
+        if (ch.dead[l.idx]) throw FAIL(PXO_ECORRUPT);  // the reference asserts
+        ch.dead[l.idx] = 1;
+        ch.used--;
+        if (ch.used < 0.8 * kChunkSlots) glob = (int)l.chunk;
+    }
+
+    // PiXiuCtrl::setitem (PiXiuCtrl.cpp:12-47) with its reinsert triggers
+    int ctrl_set(const Bytes &doc, bool reinsert, uint32_t *c, uint32_t *i) {
+        if (rotation_due()) {
+            const int last = live_chunk();
+            chunks[(size_t)last].total = (int)gst.num_docs();
+            gst.clear();
+            chunks.emplace_back();
+            if (need_reinsert(last)) {
+                if (last == glob) glob = -1;
+                reinsert_chunk(last, false);
+            }
+        }
+        if (!reinsert && glob >= 0 && glob != live_chunk() && need_reinsert(glob)) reinsert_chunk(glob, true);
+        place(doc, c, i);
+        return index_insert(doc, Leaf{*c, *i});
+    }
+
+    // PiXiuCtrl::delitem's trigger (PiXiuCtrl.cpp:63-69), before the CritBit delete
+    void delete_trigger() {
+        if (glob >= 0 && glob != live_chunk() && need_reinsert(glob)) reinsert_chunk(glob, true);
+    }
+
+    // PiXiuCtrl::reinsert (PiXiuCtrl.cpp:88-114): every live record of chunk c, decoded
+    // through PXSGen (compat), goes back in through setitem as a ready doc; the CritBit
+    // replace deletes the old copy.  The loop visits all PXC_STR_NUM slots and the
+    // reference asserts each is set (PiXiuStr.cpp:189-193): only a slot-full chunk is
+    // well defined, and only that case is carried out (any other is a no-op here).
+    // `via_glob`: called as reinsert(Glob_Reinsert_Chunk), whose reference argument the
+    // final `chunk = NULL` clears.
+    void reinsert_chunk(int c, bool via_glob) {
+        if (chunks[(size_t)c].recs.size() != (size_t)kChunkSlots) return;
+        const int curr = glob;
+        for (uint32_t i = 0; i < (uint32_t)kChunkSlots; ++i) {
+            if (chunks[(size_t)c].dead[i]) continue;
+            Sink sk;
+            sk.limit = (size_t)kMaxDoc;
+            decode_into((uint32_t)c, i, 0, kMaxDoc, PXO_COMPAT, sk);
+            uint32_t cc, ii;
+            ctrl_set(sk.out, true, &cc, &ii);
+        }
+        Chunk &ch = chunks[(size_t)c];  // PiXiuChunk_free: the chunk's records are gone
+        std::fill(ch.dead.begin(), ch.dead.end(), 1);
+        ch.used = 0;
+        glob = via_glob ? -1 : curr;
     }
 
     void decode_into(uint32_t c, uint32_t i, int from, int to, int mode, Sink &s) {
@@ -686,7 +757,6 @@ struct pxo_shard {
         return b;
     }
 
-    void mark_dead(const Leaf &l) { chunks[l.chunk].dead[l.idx] = 1; }
 
     int32_t new_inner() {
         if (!cbt_free.empty()) {
@@ -725,7 +795,7 @@ struct pxo_shard {
                 spec = true;
             } else if (spec) {
                 if (crit_rv == kKeyEnd) {  // same key: replace (CBT_SET_REPLACE)
-                    mark_dead(b.crit);
+                    chunk_delitem(b.crit);
                     if (b.pa < 0) root = nref;
                     else cbt[(size_t)b.pa].kid[b.dir] = nref;
                     return 1;
@@ -805,7 +875,7 @@ struct pxo_shard {
             }
             cbt_free.push_back(b.pa);
         }
-        mark_dead(b.crit);
+        chunk_delitem(b.crit);
         return 0;
     }
 
@@ -890,10 +960,10 @@ int pxo_set(pxo_shard *s, const uint8_t *k, int klen, const uint8_t *v, int vlen
         int rc = assemble_doc(k, klen, v, vlen, doc);
         if (rc) return rc;
         uint32_t c, i;
-        s->store(doc, &c, &i);
+        rc = s->ctrl_set(doc, false, &c, &i);
         if (chunk_no) *chunk_no = c;
         if (idx) *idx = i;
-        return s->index_insert(doc, Leaf{c, i});
+        return rc;
     } catch (const Fail &f) {
         return f.code;
     }
@@ -913,6 +983,7 @@ int pxo_delete(pxo_shard *s, const uint8_t *k, int klen) {
     try {
         Bytes key;
         escape_append(k, klen, true, key);
+        s->delete_trigger();
         return s->remove(key);
     } catch (const Fail &f) {
         return f.code;
@@ -946,6 +1017,22 @@ int pxo_get(pxo_shard *s, const uint8_t *k, int klen, int mode, uint8_t *out, in
         Sink sk;
         s->decode_into(l.chunk, l.idx, 0, kMaxDoc, mode, sk);
         return copy_out(sk.out, out, cap);
+    } catch (const Fail &f) {
+        return f.code;
+    }
+}
+
+// CritBitTree::find_best_match + key_eq (CritBitTree.cpp:185-195): where the key's
+// record lives (chunk number, slot), for state comparisons after reinsert.
+int pxo_locate(pxo_shard *s, const uint8_t *k, int klen, uint32_t *chunk, uint32_t *idx) {
+    try {
+        Bytes key;
+        escape_append(k, klen, true, key);
+        Leaf l;
+        if (!s->lookup(key, &l)) return PXO_NOTFOUND;
+        *chunk = l.chunk;
+        *idx = l.idx;
+        return 0;
     } catch (const Fail &f) {
         return f.code;
     }

@@ -49,6 +49,9 @@ int pxo_parse(pxo_shard *s, uint32_t chunk, uint32_t idx, int from, int to, int 
 #define PXO_NOTFOUND -5
 int pxo_get(pxo_shard *s, const uint8_t *k, int klen, int mode, uint8_t *out, int cap);
 
+/* where the key's record lives (chunk number, slot); PXO_NOTFOUND if absent */
+int pxo_locate(pxo_shard *s, const uint8_t *k, int klen, uint32_t *chunk, uint32_t *idx);
+
 /* PiXiuCtrl::contains (1/0) and ::delitem (0 deleted, 1 not found) */
 int pxo_contains(pxo_shard *s, const uint8_t *k, int klen);
 int pxo_delete(pxo_shard *s, const uint8_t *k, int klen);

@@ -83,6 +83,26 @@ int refx_delitem(const uint8_t *k, int klen) {
     return g_ctrl.delitem((uint8_t *)k, klen);
 }
 
+// CritBitTree::getitem's lookup (CritBitTree.cpp:185-195) stopped before the parse: the
+// located record's slot and compressed bytes; -5 when the key is absent.
+int refx_locate(const uint8_t *k, int klen, uint8_t *out, int cap, uint32_t *idx) {
+    if (g_ctrl.cbt.root == NULL) return -5;
+    PiXiuStr *src = PiXiuStr_init_key((uint8_t *)k, klen);
+    auto ret = g_ctrl.cbt.find_best_match(src);
+    auto pa = (CBTInner *)ret.pa;
+    auto chunk = (PiXiuChunk *)ret.crit_node;
+    int ci = pa == NULL ? g_ctrl.cbt.chunk_idx : pa->chunk_idx_arr[ret.pa_direct];
+    PiXiuStr *p = chunk->getitem(ci);
+    bool eq = p->key_eq(src, chunk);
+    PiXiuStr_free(src);
+    if (!eq) return -5;
+    int n = p->len;
+    if (n > cap) return -2;
+    memcpy(out, p->data, (size_t)n);
+    *idx = (uint32_t)ci;
+    return n;
+}
+
 // PiXiuCtrl::iter: drains every yielded generator into out (CSR offsets in off[]).
 // Returns the record count, -1 for a NULL generator, -2 on overflow.
 int refx_iter(const uint8_t *prefix, int plen, uint8_t *out, int cap, uint64_t *off, int max_recs) {

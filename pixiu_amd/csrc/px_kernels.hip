@@ -122,6 +122,18 @@ __global__ void __launch_bounds__(256) k_doc_len(uint32_t n, const uint8_t *keys
     const uint32_t lane = lane_id();
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);
     for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < n; r += waves) {
+        if (!vals) {  // ready docs (reinsert, PiXiuCtrl.cpp:39-40): taken as they are
+            if (lane == 0) {
+                const uint64_t len = koff[r + 1] - koff[r];
+                const bool bad = len == 0 || len > (uint64_t)kMaxDoc;
+                doc_len[r] = bad ? 0xffffffffu : (uint32_t)len;
+                if (rec_init) {
+                    rec_init[r] = rec_init[n + r] = rec_init[2 * n + r] = 0xffffffffu;
+                    rec_init[3 * n + r] = bad ? (uint32_t)kErrInval : (uint32_t)kOk;
+                }
+            }
+            continue;
+        }
         uint64_t ka = koff[r], kb = koff[r + 1], va = voff[r], vb = voff[r + 1];
         uint32_t cnt = 0;
         for (uint64_t p = ka + lane; p < kb; p += 64) cnt += keys[p] == kEsc;
@@ -172,6 +184,10 @@ __global__ void __launch_bounds__(256) k_doc_write(uint32_t n, const uint8_t *ke
     for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < n; r += waves) {
         uint8_t *dst = dst_ptr[r];
         if (dst == nullptr) continue;
+        if (!vals) {  // a ready doc: copied verbatim
+            for (uint64_t p = koff[r] + lane; p < koff[r + 1]; p += 64) dst[p - koff[r]] = keys[p];
+            continue;
+        }
         uint64_t ka = koff[r], kb = koff[r + 1], va = voff[r], vb = voff[r + 1];
         uint32_t w = escape_span(keys, ka, kb, dst);
         if (lane == 0) {

@@ -17,6 +17,7 @@
 #include <string>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/pixiu_amd.h"
@@ -297,6 +298,8 @@ inline int crit_dir(uint8_t mask, uint8_t byte) { return (1 + (mask | byte)) >> 
 struct Chunk {
     uint32_t shard = 0;
     uint32_t n = 0;
+    uint32_t used = 0;   // PiXiuChunk::used_num: live records (placed, not deleted)
+    uint32_t total = 0;  // PiXiuChunk::total_num: records when the chunk was closed (0: live)
     std::vector<RecSlot> slots;  // host mirror (device pointers inside)
     RecSlot *dev = nullptr;      // device slot table
     uint32_t dev_cap = 0;
@@ -325,6 +328,10 @@ struct Shard {
     // the live chunk was encoded by the suffix-array path (px_psa.hip): hs.n_docs docs,
     // no tree; the arena is then text only (text_only) until a walk needs the tree
     bool psa = false, text_only = false;
+    // Glob_Reinsert_Chunk of this shard's PiXiuCtrl (PiXiuStr.cpp:4, 178-187): the last
+    // chunk a delete left under 80 % of 65,535 live records; -1 = NULL
+    int64_t glob = -1;
+    int64_t closed = -1;  // slot-full live chunk whose rotation trigger has run
     uint32_t records = 0;
     std::vector<uint32_t> chunks;  // global chunk ids by chunk_seq
     // CritBit
@@ -707,7 +714,7 @@ struct px_ctx {
                 spec = true;
             } else if (spec) {
                 if (crit_rv == kKeyEnd) {
-                    chunks[b.crit.chunk].dead[b.crit.idx] = 1;
+                    chunk_delitem(s, b.crit);
                     if (b.pa < 0) s.root = nref;
                     else s.cbt[(size_t)b.pa].kid[b.dir] = nref;
                     return 1;
@@ -752,6 +759,16 @@ struct px_ctx {
         else s.cbt[(size_t)parent].kid[pdir] = iref;
         s.cbt[(size_t)in].kid[1 - dir] = p;
         return 0;
+    }
+
+    // PiXiuChunk::delitem (PiXiuStr.cpp:178-187): dead mark, live count, Glob
+    void chunk_delitem(Shard &s, const Leaf &l) {
+        Chunk &ch = chunks[l.chunk];
+        if (!ch.dead[l.idx]) {
+            ch.dead[l.idx] = 1;
+            if (ch.used) ch.used--;
+        }
+        if (ch.used < 0.8 * kChunkSlots) s.glob = l.chunk;
     }
 
     // CritBitTree::getitem's key_eq (PiXiuStr.cpp:129-143)
@@ -822,7 +839,7 @@ struct px_ctx {
                         }
                         s.cbt_free.push_back(b.pa);
                     }
-                    chunks[b.crit.chunk].dead[b.crit.idx] = 1;
+                    chunk_delitem(s, b.crit);
                     return 0;
                 }
                 spec = false;
@@ -1153,6 +1170,15 @@ struct px_ctx {
             qo = ao;
         }
     }
+    // PiXiuCtrl-level setitem / delitem with the reinsert compaction (PiXiuCtrl.cpp:12-29,
+    // 63-69, 88-114); set_batch is the batch SuffixTree::setitem + CritBit underneath
+    bool raw_docs = false;  // set_batch input is ready docs (reinserted records)
+    int set_ctrl(uint32_t n, const uint8_t *keys, const uint64_t *koff, const uint8_t *vals, const uint64_t *voff,
+                 int on_device, px_set_result *res);
+    void reinsert_chunk(Shard &s, uint32_t c, bool via_glob);
+    enum { kTrigSet, kTrigReinsert, kTrigDel };
+    void reinsert_triggers(Shard &s, int when);
+    int del_ctrl(uint32_t n, const uint8_t *keys, const uint64_t *koff, uint32_t *result);
     // chunk blob (include/pixiu_amd.h: px_save / px_load)
     int save(uint8_t *dst, uint64_t cap, int dst_on_device, uint64_t *bytes);
     int load(const uint8_t *src, uint64_t len, int src_on_device, uint32_t *first_shard);
@@ -1280,7 +1306,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     uint32_t *d_doclen = tmp, *d_complen = tmp + n, *d_chunk = tmp + 2 * n, *d_idx = tmp + 3 * n,
              *d_status = tmp + 4 * n, *d_nseg = tmp + 5 * n, *d_nesc = tmp + 6 * n;
     if (debug_poison()) hcheck(hipMemsetAsync(tmp, 0xa5, (size_t)n * 28 + 64, stream));  // stale-scratch test
-    hcheck(launch_doc_len(stream, n, dkeys, dkoff, dvals, dvoff, d_doclen, d_complen));
+    hcheck(launch_doc_len(stream, n, dkeys, dkoff, raw_docs ? nullptr : dvals, dvoff, d_doclen, d_complen));
     std::vector<uint32_t> doc_len(n);
     d2h(doc_len.data(), d_doclen, n * 4);
     sync();
@@ -1323,6 +1349,16 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     // outgrows that, or whose stream the PSA check flags, goes to k_gst_encode, which
     // first re-walks (replays) the docs PSA encoded.
     const bool psa_on = psa_enabled();
+    // a PSA live chunk that is slot-full rotates at this batch's first doc (PiXiuCtrl.cpp:13):
+    // the new chunk starts empty, so the rotation is done here and the batch stays on PSA
+    for (const Work &w : work) {
+        Shard &sh = *w.s;
+        if (sh.psa && w.docs > 0 && sh.hs.n_docs == (uint32_t)kChunkSlots) {
+            sh.hs.chunk_seq++;
+            sh.hs.n_docs = 0;
+            sh.text_end = 0;
+        }
+    }
     std::vector<uint8_t> wpsa(work.size(), 0);
     std::vector<uint32_t> wreplay(work.size(), 0);
     for (size_t k = 0; k < work.size(); ++k) {
@@ -1363,7 +1399,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     h2d(d_dst, dst.data(), (size_t)n * 8);
     h2d(d_cdst, cdst.data(), (size_t)n * 8);
     flush_shard_init();
-    hcheck(launch_doc_write(stream, n, dkeys, dkoff, dvals, dvoff, d_dst));
+    hcheck(launch_doc_write(stream, n, dkeys, dkoff, raw_docs ? nullptr : dvals, dvoff, d_dst));
 
     // ---- the suffix-array path over the PSA shards (messages, placement, check flags)
     hcheck(hipEventRecord(ev0, stream));
@@ -1593,7 +1629,10 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         if (!placed[r]) continue;
         if (rstatus[r] == kOk && tstat[r] != kOk) rstatus[r] = tstat[r];
         Shard &s = *shards[rec_shard[r]];
-        while (s.chunks.size() <= rchunk[r]) s.chunks.push_back(new_chunk(s.id));
+        while (s.chunks.size() <= rchunk[r]) {
+            if (!s.chunks.empty()) chunks[s.chunks.back()].total = chunks[s.chunks.back()].n;  // closed
+            s.chunks.push_back(new_chunk(s.id));
+        }
         uint32_t c = s.chunks[rchunk[r]];
         Chunk &ch = chunks[c];
         if (ridx[r] != ch.n) {  // the device numbered slots differently: fail loudly
@@ -1611,6 +1650,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         ch.kp_off.push_back(0);
         ch.kp_len.push_back(0);
         ch.n++;
+        ch.used += ok ? 1 : 0;
         rgchunk[r] = c;
         live[r] = ok;
         if (!ok) continue;
@@ -1668,6 +1708,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
                 const uint32_t r = jrec[i];
                 rstatus[r] = kst[i];
                 chunks[rgchunk[r]].dead[ridx[r]] = 1;
+                if (chunks[rgchunk[r]].used) chunks[rgchunk[r]].used--;
                 live[r] = 0;
             }
     }
@@ -1693,7 +1734,12 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         std::string q;
         for (uint32_t r = w.r0; r < w.r1; ++r) {
             if (!live[r]) continue;
-            esc_key_into(q, hkeys.data() + hkoff[r], hkoff[r + 1] - hkoff[r]);
+            if (raw_docs) {  // a ready doc: its escaped key is its prefix through 251,0
+                const uint8_t *d = hkeys.data() + hkoff[r];
+                q.assign(reinterpret_cast<const char *>(d), key_end(d, (uint32_t)(hkoff[r + 1] - hkoff[r])));
+            } else {
+                esc_key_into(q, hkeys.data() + hkoff[r], hkoff[r + 1] - hkoff[r]);
+            }
             replaced[r] |= (uint32_t)cbt_insert(s, q, Leaf{rgchunk[r], ridx[r]});
         }
     };
@@ -1794,6 +1840,213 @@ int px_ctx::expand(const std::vector<DecodeQuery> &q0, uint8_t *out, uint64_t ou
         sync();
     }
     return rc;
+}
+
+// ====================================================================== reinsert
+// PiXiuCtrl::setitem / delitem with the reinsert compaction (PiXiuCtrl.cpp:12-29, 63-69,
+// 88-114).  A chunk closed with fewer than half of its records live is re-inserted: every
+// live record, decoded through PXSGen (compat), goes back in through setitem as a ready
+// doc and the CritBit replace deletes the old copy.  Triggers: the rotation that closes a
+// chunk, and before every setitem / delitem the shard's Glob_Reinsert_Chunk (the last
+// chunk a delete left under 80 % live).  The reference's loop visits all 65,535 slots and
+// asserts each is set (PiXiuStr.cpp:189-193), so only slot-full chunks are defined; a
+// chunk closed by the pool rule is left alone here (the reference dereferences NULL).
+// Slot-full chunks exist only when a shard's live chunk can reach 65,535 records:
+// records_per_shard = 0 (the reference's single instance).
+
+namespace {
+bool need_reinsert(const Chunk &c) { return c.total && c.used < 0.5 * c.total; }
+}  // namespace
+
+void px_ctx::reinsert_triggers(Shard &s, int when) {
+    if (s.chunks.empty()) return;
+    const uint32_t live = s.chunks.back();
+    // the live chunk is slot-full: the next setitem rotates it (PiXiuCtrl.cpp:13-25).  The
+    // rotation itself happens at the next doc the encoder places, so `closed` remembers
+    // that this chunk's rotation trigger already ran (the reinsert below goes through
+    // setitem again and would otherwise see the same full chunk).
+    const bool rotating = s.hs.n_docs == (uint32_t)kChunkSlots;
+    if (rotating && when != kTrigDel && s.closed != (int64_t)live) {
+        s.closed = live;
+        Chunk &ch = chunks[live];
+        ch.total = ch.n;
+        if (need_reinsert(ch)) {
+            if (s.glob == (int64_t)live) s.glob = -1;
+            reinsert_chunk(s, live, false);
+        }
+    }
+    if (when == kTrigReinsert) return;
+    // Glob_Reinsert_Chunk != st.cbt_chunk: delitem compares with the live chunk, setitem
+    // with the chunk its record goes to (a new one when the live chunk is full)
+    const int64_t cur = rotating && when == kTrigSet ? -2 : (int64_t)live;
+    if (s.glob >= 0 && s.glob != cur && need_reinsert(chunks[(size_t)s.glob]))
+        reinsert_chunk(s, (uint32_t)s.glob, true);
+}
+
+void px_ctx::reinsert_chunk(Shard &s, uint32_t c, bool via_glob) {
+    if (chunks[c].n != (uint32_t)kChunkSlots) return;
+    const int64_t curr = s.glob;
+    // every live record, PXSGen-decoded over [0, 65535) (PiXiuCtrl.cpp:94-101)
+    std::vector<DecodeQuery> q;
+    uint64_t qo = 0;
+    for (uint32_t i = 0; i < chunks[c].n; ++i) {
+        if (chunks[c].dead[i]) continue;
+        const uint32_t cap = (uint32_t)round_up(chunks[c].doc_len[i] + 64, 16);
+        q.push_back(DecodeQuery{c, i, 0, kMaxDoc, qo, cap, 0});
+        qo += cap;
+    }
+    std::vector<uint8_t> docs;
+    std::vector<uint64_t> doff(1, 0);
+    if (!q.empty()) {
+        auto *dbuf = (uint8_t *)heap.alloc(qo + 64);
+        std::vector<uint32_t> len, st;
+        run_decode(q, dbuf, len, st, false);
+        std::vector<uint8_t> h(qo);
+        d2h(h.data(), dbuf, qo);
+        sync();
+        heap.release(dbuf, qo + 64);
+        // a compat expansion longer than the doc (PXSGen's bug-compatible output) is
+        // redone with the whole PXSG_MAX_TO window
+        std::vector<DecodeQuery> q2;
+        std::vector<uint32_t> which;
+        uint64_t qo2 = 0;
+        for (size_t k = 0; k < q.size(); ++k)
+            if (st[k] == kErrSpace) {
+                DecodeQuery d = q[k];
+                d.out_off = qo2;
+                d.out_cap = (uint32_t)round_up(kMaxDoc + 64, 16);
+                qo2 += d.out_cap;
+                q2.push_back(d);
+                which.push_back((uint32_t)k);
+            }
+        std::vector<uint8_t> h2;
+        std::vector<uint32_t> len2, st2;
+        if (!q2.empty()) {
+            auto *dbuf2 = (uint8_t *)heap.alloc(qo2 + 64);
+            run_decode(q2, dbuf2, len2, st2, false);
+            h2.resize(qo2);
+            d2h(h2.data(), dbuf2, qo2);
+            sync();
+            heap.release(dbuf2, qo2 + 64);
+        }
+        for (size_t k = 0, j = 0; k < q.size(); ++k) {
+            const uint8_t *src = h.data() + q[k].out_off;
+            uint32_t l = len[k], stk = st[k];
+            if (j < which.size() && which[j] == k) {
+                src = h2.data() + q2[j].out_off;
+                l = len2[j];
+                stk = st2[j];
+                ++j;
+            }
+            if (stk != kOk) throw PxFail{(int)map_status(stk)};
+            l = std::min<uint32_t>(l, (uint32_t)kMaxDoc);  // the reference's uint16_t len
+            docs.insert(docs.end(), src, src + l);
+            doff.push_back(docs.size());
+        }
+    }
+    // setitem(doc, reinsert = true) each, in slot order: rotation triggers only
+    const bool saved = raw_docs;
+    raw_docs = true;
+    const uint32_t n = (uint32_t)q.size();
+    std::vector<uint64_t> zero(n + 1, 0);
+    uint8_t dummy = 0;
+    for (uint32_t pos = 0; pos < n;) {
+        reinsert_triggers(s, kTrigReinsert);
+        const uint32_t room = (uint32_t)kChunkSlots - std::min<uint32_t>(s.hs.n_docs, kChunkSlots);
+        const uint32_t end = std::min(n, pos + std::max(room, 1u));
+        std::vector<uint64_t> off(doff.begin() + pos, doff.begin() + end + 1);
+        const int rc = set_batch(end - pos, docs.data(), off.data(), &dummy, zero.data(), 0, nullptr);
+        if (rc != PX_OK) {
+            raw_docs = saved;
+            throw PxFail{rc};
+        }
+        pos = end;
+    }
+    raw_docs = saved;
+    // PiXiuChunk_free: the chunk's records are gone
+    Chunk &ch = chunks[c];
+    std::fill(ch.dead.begin(), ch.dead.end(), (uint8_t)1);
+    ch.used = 0;
+    s.glob = via_glob ? -1 : curr;
+}
+
+int px_ctx::set_ctrl(uint32_t n, const uint8_t *keys, const uint64_t *koff, const uint8_t *vals,
+                     const uint64_t *voff, int on_device, px_set_result *res) {
+    if (opts.records_per_shard != 0 || n == 0) return set_batch(n, keys, koff, vals, voff, on_device, res);
+    // one shard (the reference's single instance): evaluate the triggers between records
+    std::vector<uint64_t> ko(n + 1), vo(n + 1);
+    std::vector<uint8_t> hk, hv;
+    if (on_device) {
+        d2h(ko.data(), koff, (size_t)(n + 1) * 8);
+        d2h(vo.data(), voff, (size_t)(n + 1) * 8);
+        sync();
+    } else {
+        std::memcpy(ko.data(), koff, (size_t)(n + 1) * 8);
+        std::memcpy(vo.data(), voff, (size_t)(n + 1) * 8);
+    }
+    Shard *s = shards.empty() ? nullptr : shards[0].get();
+    bool full_closed = false;  // a slot-full closed chunk exists: a replace may move Glob onto it
+    if (s)
+        for (uint32_t c : s->chunks) full_closed |= chunks[c].total == (uint32_t)kChunkSlots;
+    const bool fast = !s || (s->hs.n_docs + (uint64_t)n < (uint64_t)kChunkSlots && !full_closed);
+    if (fast) return set_batch(n, keys, koff, vals, voff, on_device, res);
+    if (on_device) {  // the slow path reads keys on the host
+        hk.resize(ko[n] - ko[0]);
+        hv.resize(vo[n] - vo[0]);
+        d2h(hk.data(), keys + ko[0], hk.size());
+        d2h(hv.data(), vals + vo[0], hv.size());
+        sync();
+        const uint64_t k0 = ko[0], v0 = vo[0];
+        for (auto &o : ko) o -= k0;
+        for (auto &o : vo) o -= v0;
+        keys = hk.data();
+        vals = hv.data();
+        on_device = 0;
+    }
+    int rc = PX_OK;
+    for (uint32_t pos = 0; pos < n;) {
+        s = shards.empty() ? nullptr : shards[0].get();
+        uint32_t end = n;
+        if (s) {
+            reinsert_triggers(*s, kTrigSet);
+            const uint32_t room = (uint32_t)kChunkSlots - std::min<uint32_t>(s->hs.n_docs, kChunkSlots);
+            end = std::min(n, pos + std::max(room, 1u));
+            full_closed = false;
+            for (uint32_t c : s->chunks) full_closed |= chunks[c].total == (uint32_t)kChunkSlots;
+            if (full_closed) {
+                // stop after the first record whose replace leaves a slot-full closed chunk
+                // under half live: Glob then triggers before the next record
+                std::unordered_map<uint32_t, uint32_t> dec;
+                std::unordered_set<std::string> seen;
+                for (uint32_t r = pos; r < end; ++r) {
+                    std::string q = esc_key(keys + ko[r], ko[r + 1] - ko[r]);
+                    Leaf l;
+                    if (!seen.insert(q).second || !cbt_lookup(*s, q, &l)) continue;
+                    const Chunk &ch = chunks[l.chunk];
+                    if (ch.total != (uint32_t)kChunkSlots || ch.dead[l.idx]) continue;
+                    const uint32_t d = ++dec[l.chunk];
+                    if (ch.used - std::min(d, ch.used) < 0.5 * ch.total) {
+                        end = r + 1;
+                        break;
+                    }
+                }
+            }
+        }
+        const int r2 = set_batch(end - pos, keys, ko.data() + pos, vals, vo.data() + pos, on_device,
+                                 res ? res + pos : nullptr);
+        if (rc == PX_OK) rc = r2;
+        pos = end;
+    }
+    return rc;
+}
+
+int px_ctx::del_ctrl(uint32_t n, const uint8_t *keys, const uint64_t *koff, uint32_t *result) {
+    for (uint32_t i = 0; i < n; ++i) {
+        Shard *s = shard_for_key(keys + koff[i], koff[i + 1] - koff[i]);
+        if (s && opts.records_per_shard == 0) reinsert_triggers(*s, kTrigDel);  // PiXiuCtrl.cpp:64-67
+        result[i] = s ? (uint32_t)cbt_delete(*s, esc_key(keys + koff[i], koff[i + 1] - koff[i])) : 1u;
+    }
+    return PX_OK;
 }
 
 // ====================================================================== chunk blob
@@ -2015,6 +2268,8 @@ int px_ctx::load(const uint8_t *src, uint64_t len, int src_on_device, uint32_t *
             rshard[i] = s;
         }
         ch.n = c.n;
+        for (uint32_t i = 0; i < c.n; ++i) ch.used += ch.dead[i] ? 0 : 1;
+        ch.total = c.n;  // a loaded chunk is closed
         s->records += c.n;
         // the next set batch starts this shard's GST in a fresh chunk after the loaded ones
         s->hs.chunk_seq = (uint32_t)s->chunks.size();
@@ -2055,6 +2310,7 @@ int px_ctx::load(const uint8_t *src, uint64_t len, int src_on_device, uint32_t *
         uint32_t kl = 0;
         const uint8_t *kp = kp_of(Leaf{jobs[j].chunk, k}, &kl);
         if (kst[j] != kOk || kl < 2 || kp[kl - 2] != kEsc || kp[kl - 1] != kKeyEnd) {
+            if (!ch.dead[k] && ch.used) ch.used--;
             ch.dead[k] = 1;  // no decodable key: not indexed
             if (rc == PX_OK) rc = kst[j] != kOk ? (int)map_status(kst[j]) : PX_ECORRUPT;
             continue;
@@ -2150,7 +2406,7 @@ const char *px_strerror(int s) {
 int px_set_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff, const uint8_t *vals,
                  const uint64_t *voff, int on_device, px_set_result *res) {
     if (!ctx || (n && (!keys || !koff || !voff))) return PX_EINVAL;
-    PX_GUARD(return ctx->set_batch(n, keys, koff, vals, voff, on_device, res);)
+    PX_GUARD(return ctx->set_ctrl(n, keys, koff, vals, voff, on_device, res);)
 }
 
 int px_get_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff, int mode, uint8_t *out,
@@ -2229,13 +2485,7 @@ int px_contains_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64
 
 int px_del_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff, uint32_t *result) {
     if (!ctx || (n && (!keys || !koff || !result))) return PX_EINVAL;
-    PX_GUARD({
-        for (uint32_t i = 0; i < n; ++i) {
-            Shard *s = ctx->shard_for_key(keys + koff[i], koff[i + 1] - koff[i]);
-            result[i] = s ? (uint32_t)ctx->cbt_delete(*s, px_ctx::esc_key(keys + koff[i], koff[i + 1] - koff[i])) : 1u;
-        }
-        return PX_OK;
-    })
+    PX_GUARD(return ctx->del_ctrl(n, keys, koff, result);)
 }
 
 int px_iter(px_ctx *ctx, const uint8_t *prefix, uint64_t prefix_len, px_rec *recs, uint32_t cap, uint32_t *n_out) {

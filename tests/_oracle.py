@@ -184,6 +184,16 @@ class _Shard:
     def delete(self, k: bytes) -> int:
         return self.lib.pxo_delete(self.h, k, len(k))
 
+    def locate(self, k: bytes):
+        """(chunk, idx) of the key's record, or None."""
+        cn, ix = C.c_uint32(), C.c_uint32()
+        rc = self.lib.pxo_locate(self.h, k, len(k), C.byref(cn), C.byref(ix))
+        if rc == PXO_NOTFOUND:
+            return None
+        if rc < 0:
+            raise RuntimeError(f"pxo_locate: {rc}")
+        return cn.value, ix.value
+
     def comp(self, chunk, idx):
         out = C.create_string_buffer(1 << 17)
         n = self.lib.pxo_comp(self.h, chunk, idx, out, len(out))
@@ -202,6 +212,41 @@ class Reference(_Runner):
         self.lib = C.CDLL(REF_SO)
         self.run_fn = "refx_run"
         self.has_mode = False
+
+    # incremental API over the library's single global controller (PiXiuCtrl.cpp:12-69)
+    def init(self):
+        self.lib.refx_init()
+        return self
+
+    def set(self, k: bytes, v: bytes) -> int:
+        cn, ix = C.c_uint32(), C.c_uint32()
+        return self.lib.refx_setitem(k, len(k), v, len(v), C.byref(cn), C.byref(ix))
+
+    def delete(self, k: bytes) -> int:
+        return self.lib.refx_delitem(k, len(k))
+
+    def contains(self, k: bytes) -> int:
+        return self.lib.refx_contains(k, len(k))
+
+    def get(self, k: bytes):
+        out = C.create_string_buffer(1 << 17)
+        n = self.lib.refx_getitem(k, len(k), out, len(out))
+        if n == -1:
+            return None
+        if n < 0:
+            raise RuntimeError(f"refx_getitem: {n}")
+        return out.raw[:n]
+
+    def locate_comp(self, k: bytes):
+        """(idx, compressed bytes) of the key's record, or None."""
+        out = C.create_string_buffer(1 << 17)
+        ix = C.c_uint32()
+        n = self.lib.refx_locate(k, len(k), out, len(out), C.byref(ix))
+        if n == -5:
+            return None
+        if n < 0:
+            raise RuntimeError(f"refx_locate: {n}")
+        return ix.value, out.raw[:n]
 
 
 def have_reference() -> bool:

@@ -103,3 +103,21 @@ def test_psa_small_alphabets_match_oracle(store_factory, oracle):
             assert any(int(r["status"][i]) != 0 for i in rows)
             continue
         assert [comp[pos[i]] for i in rows] == want["comp"]
+
+
+def test_psa_slot_full_chunk_then_next_batch(store_factory, oracle):
+    """A PSA live chunk filled to 65,535 docs: the next batch rotates at its first doc and
+    stays on PSA (new chunk), bytes and placement equal the oracle's single instance."""
+    from pixiu_amd import synth
+    cp = synth.tiny_keys(70000)
+    st = store_factory(records_per_shard=0)
+    res = []
+    for a, b in ((0, 65535), (65535, 70000)):
+        res.append(st.set_batch([cp.key(i) for i in range(a, b)], [cp.val(i) for i in range(a, b)]))
+        s = st.stats()
+        assert (s["last_psa_shards"], s["last_walk_shards"]) == (1, 0)
+    r = np.concatenate(res)
+    assert int(r["status"].max()) == 0
+    oc, ochunk, oidx = oracle.encode_docs([assemble(cp.key(i), cp.val(i)) for i in range(cp.n)])
+    assert r["chunk"].tolist() == ochunk and r["idx"].tolist() == oidx
+    assert st.export(px.records_of(r)) == oc

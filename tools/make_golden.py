@@ -13,6 +13,8 @@ Fixtures:
   corpus_c{1..5}.npz per-config mini corpora: compressed bytes, chunk/slot, compat getitem
   rotation.json      >= 12 MB single-shard corpora crossing a chunk rotation (pool count
                      and slot count): per-chunk record counts + sha256 of every chunk's bytes
+  reinsert.json      slot-full chunks compacted by reinsert (PiXiuCtrl.cpp:12-29, 63-69, 88-114):
+                     digests of per-record returns and of the end state (tests/_reinsert.py)
 """
 from __future__ import annotations
 
@@ -223,15 +225,38 @@ def rotation():
     return out
 
 
+def reinsert():
+    """tests/_reinsert.py scenarios through the reference, one record at a time: digests
+    of every record's return and of the end state (presence, compat getitem, slot,
+    compressed bytes of every touched key), and where a few keys ended up."""
+    import _reinsert as R
+    out = {}
+    for name, ops in R.scenarios().items():
+        REF.init()
+        rets = R.run_scalar(REF, ops)
+        keys = R.touched(ops)
+        state = R.reference_state(REF, keys)
+        d = R.digest(rets, state)
+        d["ops_sha256"] = R.ops_sha256(ops)
+        d["sample"] = [[k.decode(), int(p), hx(g) if p else None, i, hx(c) if p else None]
+                       for k, p, g, i, c in state[:: max(1, len(state) // 40)]]
+        out[name] = d
+        print(name, {k: v for k, v in d.items() if k != "sample"})
+    REF.lib.refx_free()
+    return out
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
-    what = set(sys.argv[1:]) or {"kats", "corpora", "rotation"}
+    what = set(sys.argv[1:]) or {"kats", "corpora", "rotation", "reinsert"}
     if "kats" in what:
         json.dump(kats(), open(os.path.join(OUT, "kats.json"), "w"))
     if "corpora" in what:
         corpora()
     if "rotation" in what:
         json.dump(rotation(), open(os.path.join(OUT, "rotation.json"), "w"), indent=1)
+    if "reinsert" in what:
+        json.dump(reinsert(), open(os.path.join(OUT, "reinsert.json"), "w"), indent=1)
 
 
 if __name__ == "__main__":
