@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--no-checks", action="store_true", help="skip the compat/exact/original parity counts")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) leg")
+    ap.add_argument("--no-exact", action="store_true",
+                    help="skip the exact-mode getitem (profiling runs: one compat batch per step only)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r02.json"),
                     help="per-kernel PMC summary (tools/pmc_summary.py); used only if its workload matches")
@@ -260,6 +262,8 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
         t2 = time.perf_counter()
         gst = st.stats()
         dec_kms, look_ms, call_ms = gst["last_decode_kernel_ms"], gst["last_get_lookup_ms"], gst["last_get_call_ms"]
+        spans = (int(gst["last_gather_queries"]), int(sst["span_entries"]), sst["last_span_build_ms"],
+                 int(sst["device_bytes"]))
         g_ms = 0.0
         if world > 1:  # every rank's chunk blob (pixiu_amd/blob.py) to rank 0, RCCL over xGMI
             tg = time.perf_counter()
@@ -277,7 +281,7 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
         return {"set_s": t1 - t0 + g_ms * 1e-3, "get_s": t2 - t1, "set_kms": set_kms, "walk_kms": walk_kms,
                 "emit_kms": emit_kms, "dec_kms": dec_kms, "gather_ms": g_ms, "look_ms": look_ms,
                 "call_ms": call_ms, "comp": int(res["comp_len"].sum()), "exp": int(ln.sum()), "res": res,
-                "off": off, "len": ln, "psa": psa}
+                "off": off, "len": ln, "psa": psa, "spans": spans}
 
     for _ in range(warmup):
         step()
@@ -294,12 +298,16 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
          "out": out, "out_cap": out_cap, "keys_host": keys_host}
     # exact-mode getitem (one timed call, outside the step loop) and parity counts
     last = runs[-1]
+    if a.no_exact:
+        r["exact_s"], r["exact_dec_kms"], r["exact_exp"], r["exact_gather"] = 0.0, 0.0, 0, 0
+        return r
     out2 = torch.empty(out_cap, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
     te = time.perf_counter()
     rc, eoff, eln, ests, _ = st.get_batch_device(keys_host, out2.data_ptr(), out_cap, px.EXACT)
     r["exact_s"] = time.perf_counter() - te
     r["exact_dec_kms"] = st.stats()["last_decode_kernel_ms"]
+    r["exact_gather"] = int(st.stats()["last_gather_queries"])
     r["exact_exp"] = int(eln.sum())
     if rc != px.PX_OK:
         raise SystemExit(f"config {cfg}: exact getitem rc={rc}")
@@ -346,8 +354,9 @@ def summarize(cfg, r, rps, world, a, pmc_path):
         else "k_gst_encode"
     set_gbps = (raw + comp) / (walk_kms * 1e-3) / 1e9   # encode stage: raw in + compressed out
     emit_gbps = (raw * 5 + comp) / (emit_kms * 1e-3) / 1e9
-    dec_gbps = (comp + exp) / (dec_kms * 1e-3) / 1e9     # k_decode: compressed in + expanded out
-    dominant = enc_name if walk_kms >= dec_kms else "k_decode"
+    dec_gbps = (comp + exp) / (dec_kms * 1e-3) / 1e9     # getitem stage: compressed in + expanded out
+    dec_name = "k_gather + k_decode"
+    dominant = enc_name if walk_kms >= dec_kms else dec_name
     ach = set_gbps if dominant == enc_name else dec_gbps
     traffic, tsrc = None, None
     if pmc_path and os.path.exists(pmc_path):
@@ -356,8 +365,10 @@ def summarize(cfg, r, rps, world, a, pmc_path):
             w = pmc.get("workload", {})
             # only a profile of this exact workload counts (config, shard size, records)
             if w.get("config") == cfg and w.get("rps") == rps and w.get("records") == r["n"]:
-                if dominant == "k_decode":
-                    traffic = pmc.get("k_decode", {}).get("hbm_bytes_per_launch")
+                if dominant == dec_name:  # the stage's launches (one compat batch in the profile run)
+                    tot_b = sum(v["hbm_bytes_per_launch"] * v["dispatches"] for k, v in pmc.items()
+                                if isinstance(v, dict) and k in ("k_decode", "k_gather"))
+                    traffic = tot_b or None
                 else:  # every kernel of the encode stage, summed over its launches
                     tot_b = 0.0
                     for k, v in pmc.items():
@@ -373,10 +384,16 @@ def summarize(cfg, r, rps, world, a, pmc_path):
         "value": round(set_MBps + get_MBps, 3), "unit": "MB/s",
         "ms_per_step": round(elapsed / steps * 1e3, 3),
         "setitem_MBps": round(set_MBps, 3), "getitem_MBps": round(get_MBps, 3),
-        "getitem_exact_MBps": round(job_exact / exact_s / 1e6, 3),
+        "getitem_exact_MBps": round(job_exact / exact_s / 1e6, 3) if exact_s else None,
         "compression_ratio": round(job_comp / job_raw, 4),
         "kernel_ms": {"encode_stage": round(walk_kms, 3), "k_gst_emit": round(emit_kms, 3),
-                      "k_decode": round(dec_kms, 3), "k_decode_exact": round(r["exact_dec_kms"], 3)},
+                      "getitem_stage": round(dec_kms, 3), "getitem_stage_exact": round(r["exact_dec_kms"], 3)},
+        "getitem_path": {"kernels": dec_name, "gather_queries": runs[-1]["spans"][0],
+                         "exact_gather_queries": r.get("exact_gather", 0), "queries": r["n"],
+                         "span_entries": runs[-1]["spans"][1],
+                         "span_table_vs_comp": round(runs[-1]["spans"][1] * 8 / max(comp, 1), 4),
+                         "span_build_ms": round(float(np.mean([x["spans"][2] for x in runs])), 3),
+                         "device_bytes": runs[-1]["spans"][3]},
         "encode_stage": {"kernels": enc_name, "psa_shards": psa_shards, "walked_shards": walk_shards,
                          "psa_host_ms": round(float(np.mean([x["psa"][0] for x in runs])), 3),
                          "psa_split_ms": {"sort": round(float(np.mean([x["psa"][3] for x in runs])), 3),
@@ -387,7 +404,7 @@ def summarize(cfg, r, rps, world, a, pmc_path):
                      "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBPS, 6), "traffic": traffic,
                      "traffic_source": tsrc},
         "roofline_kernels_GBps": {"encode_stage": round(set_gbps, 3), "k_gst_emit": round(emit_gbps, 3),
-                                  "k_decode": round(dec_gbps, 3)},
+                                  "getitem_stage": round(dec_gbps, 3)},
         "gather_ms": round(float(np.mean([x["gather_ms"] for x in runs])), 3),
     }
     if "parity_counts" in r:
@@ -453,7 +470,7 @@ def main():
                    "parallelism": f"dp{world} (record-range shards, no cross-GPU refs)"},
     }
     for k in ("setitem_MBps", "getitem_MBps", "getitem_exact_MBps", "compression_ratio", "kernel_ms",
-              "encode_stage", "roofline", "roofline_kernels_GBps", "gather_ms", "parity_counts"):
+              "encode_stage", "getitem_path", "roofline", "roofline_kernels_GBps", "gather_ms", "parity_counts"):
         if k in main_sum:
             line[k] = main_sum[k]
     line["getitem_split_ms"] = {k: round(v, 3) for k, v in get_split.items()}

@@ -98,6 +98,9 @@ typedef struct px_stats {
     double last_psa_lcp_ms;       /*   nearest-smaller-position links + their lcp values */
     double last_psa_msg_ms;       /*   messages, earliest occurrences, placement */
     uint64_t last_psa_iters;      /*   prefix-doubling steps after the first sort */
+    uint64_t span_entries;        /* span-table entries held (8 bytes each) */
+    uint64_t last_gather_queries; /* queries of the last get/parse batch served by k_gather */
+    double last_span_build_ms;    /* span-table build of the last px_set_batch (host wall) */
 } px_stats;
 
 px_ctx *px_open(const px_opts *opts);

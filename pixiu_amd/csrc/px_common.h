@@ -180,6 +180,38 @@ struct DecodeQuery {
     uint32_t pad;
 };
 
+// Span table (fast full-range getitem): a record's compat expansion
+// as literal runs of compressed bytes.  Entry k covers output [start_k, start_{k+1})
+// and copies it from (the record's comp pointer + rel); a sentinel entry {0, len}
+// closes the table.
+struct SpanEnt {
+    int32_t rel;
+    uint32_t start;
+};
+constexpr int32_t kAddrNone = (int32_t)0x80000000;  // a source beyond +-2 GiB of the record
+
+// span build work item: the address decode of one record (k_decode_addr's output)
+struct SpanJob {
+    const int32_t *addr;  // per output byte: source address relative to the record's comp
+    const uint8_t *base;  // the record's comp pointer
+    const uint8_t *doc;   // the escaped doc (compat == exact test), or null
+    SpanEnt *out;         // span entries (count pass: null)
+    uint32_t len;         // output bytes (k_decode_addr's length)
+    uint32_t doc_len;
+    uint32_t *count;      // count pass: spans | kSpanBad, eq flag in bit 30
+    uint32_t pad;
+};
+constexpr uint32_t kSpanBad = 1u << 31, kSpanEq = 1u << 30;
+
+// gather query: one full-range getitem served from a span table
+struct GatherQuery {
+    const SpanEnt *span;
+    const uint8_t *base;
+    uint64_t out_off;
+    uint32_t nspan, len, cap;
+    uint32_t slot;  // result index (out_len / status)
+};
+
 // decode frame (scratch, one stack per wave)
 struct alignas(16) Frame {
     uint32_t rec;     // chunk-local idx of the record being parsed ("self")

@@ -1548,6 +1548,30 @@ PX_DEV uint32_t seg_find(const SlotV &s, int32_t from) {
     return uni(lo + (uint32_t)__popcll(ballot(le)));
 }
 
+// Output writers of the decoder.  Byte output (getitem) copies bytes; address output
+// (k_decode_addr, the span build) writes, per output byte, the address of the
+// compressed byte it is copied from, relative to the query record's comp pointer.
+PX_DEV int32_t addr_of(const PX_GAS uint8_t *p, const PX_GAS uint8_t *qb) {
+    const int64_t d = (int64_t)((uint64_t)p - (uint64_t)qb);
+    return (d == (int64_t)(int32_t)d && (int32_t)d != kAddrNone) ? (int32_t)d : kAddrNone;
+}
+PX_DEV void out_wave_copy(PX_GAS uint8_t *dst, const PX_GAS uint8_t *src, uint32_t n, const PX_GAS uint8_t *) {
+    wave_copy(dst, src, n);
+}
+PX_DEV void out_wave_copy(PX_GAS int32_t *dst, const PX_GAS uint8_t *src, uint32_t n, const PX_GAS uint8_t *qb) {
+    for (uint32_t i = lane_id(); i < n; i += 64) dst[i] = addr_of(src + i, qb);
+}
+PX_DEV void out_lane_copy(PX_GAS uint8_t *dst, const PX_GAS uint8_t *src, uint32_t n, const PX_GAS uint8_t *) {
+    lane_copy(dst, src, n);
+}
+PX_DEV void out_lane_copy(PX_GAS int32_t *dst, const PX_GAS uint8_t *src, uint32_t n, const PX_GAS uint8_t *qb) {
+    for (uint32_t i = 0; i < n; ++i) dst[i] = addr_of(src + i, qb);
+}
+PX_DEV void out_one(PX_GAS uint8_t *dst, const PX_GAS uint8_t *src, const PX_GAS uint8_t *) { *dst = *src; }
+PX_DEV void out_one(PX_GAS int32_t *dst, const PX_GAS uint8_t *src, const PX_GAS uint8_t *qb) {
+    *dst = addr_of(src, qb);
+}
+
 struct DecLds {
     // per-lane frames, 4 words: entry address | rec << 48, from | len << 16, ret
     uint32_t stk[kLaneDepth * 4][64];
@@ -1557,12 +1581,23 @@ constexpr uint32_t kDecWaves = PX_DEC_WAVES;  // independent query waves per blo
 
 // the body of k_decode (getitem queries) and k_decode_keys (the stored-key prefixes
 // setitem and prefix iteration decode): one code, two kernel names in the profiles
-PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const *chunk_slots, uint8_t *out_,
+template <class OutT>
+PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const *chunk_slots, OutT *out_,
                         uint32_t *out_len, uint32_t *status, Frame *scratch, uint32_t depth_cap,
                         uint32_t n_waves) {
     __shared__ DecLds lds_w[kDecWaves];
     const uint32_t wv = uni(threadIdx.x >> 6);
-    const uint32_t gw = blockIdx.x * kDecWaves + wv;
+    // bit 31: XCD-aware order.  Blocks are dealt round-robin over the 8 XCDs (b and
+    // b + 8 share one); with the remap, XCD x takes a contiguous range of queries
+    // (the host sorts them by chunk), so each chunk's compressed bytes and entries are
+    // read through one XCD's L2 instead of all eight
+    uint32_t lb = blockIdx.x;
+    if (n_waves >> 31) {
+        const uint32_t nb = gridDim.x, x = blockIdx.x & 7u, per = nb >> 3, rem = nb & 7u;
+        lb = x * per + min(x, rem) + (blockIdx.x >> 3);
+    }
+    n_waves &= 0x7fffffffu;
+    const uint32_t gw = lb * kDecWaves + wv;
     if (gw >= n_waves) return;
     DecLds &lds = lds_w[wv];
     const uint32_t lane = lane_id();
@@ -1577,7 +1612,9 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
         const PX_GAS RecSlot *slots = qchunk == kNone ? nullptr : (const PX_GAS RecSlot *)chunk_slots[qchunk];
         const bool compat = uni(q.mode) == 0;
         const uint32_t nrec = uni(q.nrec);
-        PX_GAS uint8_t *o = (PX_GAS uint8_t *)out_ + uni64(q.out_off);
+        PX_GAS OutT *o = (PX_GAS OutT *)out_ + uni64(q.out_off);
+        const PX_GAS uint8_t *qb =
+            slots && uni(q.idx) < nrec ? (const PX_GAS uint8_t *)uni64((uint64_t)slot_at(slots, uni(q.idx)).comp) : nullptr;
         const uint32_t qcap = uni(q.out_cap);
         uint32_t outp = 0, err = 0, depth = 0;
         bool capped = false;
@@ -1731,7 +1768,7 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                     while (lm) {
                         const uint32_t j = ffs64(lm);
                         lm &= lm - 1;
-                        wave_copy(o + readlane(b, j), sv.comp + readlane(csrc, j), readlane((uint32_t)reqc, j));
+                        out_wave_copy(o + readlane(b, j), sv.comp + readlane(csrc, j), readlane((uint32_t)reqc, j), qb);
                     }
                     if (active && !fl && kind == 0 && reqc > 0 && reqc <= (int32_t)kLaneCopyMax) {
                         // a shorter plain piece: copied by its lane in the walk steps below,
@@ -1862,7 +1899,7 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                         if (nb) {
                             const PX_GAS uint8_t *cp = seg0 + poff;
                             const uint32_t last = ov ? cp[nb - 1] : 0u;
-                            lane_copy(o + base + w, cp, nb);
+                            out_lane_copy(o + base + w, cp, nb, qb);
                             w += nb;
                             ret += (int32_t)nb;
                             // a range ending inside a 251 pair writes the pair whole
@@ -1872,7 +1909,7 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                                     flag = true;
                                     busy = false;
                                 } else {
-                                    o[base + w] = cp[nb];
+                                    out_one(o + base + w, cp + nb, qb);
                                     ++w;
                                     ++ret;
                                 }
@@ -2046,7 +2083,7 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                         }
                         uint32_t room = f.cap > outp ? f.cap - outp : 0;
                         uint32_t w = min(nb, room);
-                        wave_copy(o + outp, sv.comp + cs + (uint32_t)(p0 - sx), w);
+                        out_wave_copy(o + outp, sv.comp + cs + (uint32_t)(p0 - sx), w, qb);
                         outp += w;
                         f.ret += (int32_t)nb;
                         if (w < nb || outp >= f.cap) {
@@ -2087,6 +2124,107 @@ __global__ void __launch_bounds__(64 * kDecWaves) k_decode_keys(const DecodeQuer
                                                               uint32_t *out_len, uint32_t *status, Frame *scratch,
                                                               uint32_t depth_cap, uint32_t n_waves) {
     decode_body(qs, nq, chunk_slots, out, out_len, status, scratch, depth_cap, n_waves);
+}
+// the same decode with address output (span build; out_off counts 4-byte elements)
+__global__ void __launch_bounds__(64 * kDecWaves) k_decode_addr(const DecodeQuery *qs, uint32_t nq,
+                                                              const RecSlot *const *chunk_slots, int32_t *out,
+                                                              uint32_t *out_len, uint32_t *status, Frame *scratch,
+                                                              uint32_t depth_cap, uint32_t n_waves) {
+    decode_body(qs, nq, chunk_slots, out, out_len, status, scratch, depth_cap, n_waves);
+}
+
+// ====================================================================== spans
+// Span build: one wave per record scans its address decode.  A span starts where the
+// address is not the previous one + 1.  Count pass: spans (| kSpanBad for a source out
+// of the relative range, | kSpanEq when the expansion equals the doc, i.e. compat ==
+// exact).  Write pass: {rel, start} entries plus the {0, len} sentinel.
+__global__ void __launch_bounds__(256) k_span_build(uint32_t n, const SpanJob *jobs) {
+    const uint32_t lane = lane_id();
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t j = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); j < n; j += waves) {
+        const SpanJob jb = jobs[j];
+        const PX_GAS int32_t *a = (const PX_GAS int32_t *)jb.addr;
+        const PX_GAS uint8_t *base = (const PX_GAS uint8_t *)jb.base;
+        const PX_GAS uint8_t *doc = (const PX_GAS uint8_t *)jb.doc;
+        PX_GAS SpanEnt *out = (PX_GAS SpanEnt *)jb.out;
+        const uint32_t len = uni(jb.len);
+        uint32_t cnt = 0;
+        bool bad = false, eq = doc && len == uni(jb.doc_len);
+        int32_t prev_last = kAddrNone;  // address of byte k0 - 1 (lane 63 of the last step)
+        for (uint32_t k0 = 0; k0 < len; k0 += 64) {
+            const uint32_t k = k0 + lane;
+            const bool in = k < len;
+            const int32_t v = in ? a[k] : 0;
+            int32_t pv = __shfl_up(v, 1);
+            if (lane == 0) pv = prev_last;
+            const bool start = in && (k == 0 || pv == kAddrNone || v != pv + 1);
+            bad = bad || (bool)ballot(in && v == kAddrNone);
+            if (eq) eq = !ballot(in && (v == kAddrNone || base[v] != doc[k]));
+            const uint64_t m = ballot(start);
+            if (out && !bad) {
+                const uint32_t rank =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                if (start) {
+                    PX_GAS uint32_t *e = (PX_GAS uint32_t *)(out + cnt + rank);
+                    e[0] = (uint32_t)v;
+                    e[1] = k;
+                }
+            }
+            cnt += (uint32_t)__popcll(m);
+            prev_last = __shfl(v, 63);
+        }
+        if (out && !bad && lane == 0) {
+            PX_GAS uint32_t *e = (PX_GAS uint32_t *)(out + cnt);
+            e[0] = 0;
+            e[1] = len;
+        }
+        if (!out && lane == 0) jb.count[0] = cnt | (bad ? kSpanBad : 0u) | (eq ? kSpanEq : 0u);
+    }
+}
+
+// Gather: one wave per query; lane l takes span k0 + l.  Spans up to kLaneCopyMax are
+// copied by their lane, longer ones by the whole wave.  Output stops at the query's cap.
+__global__ void __launch_bounds__(256) k_gather(uint32_t nq, const GatherQuery *qs, uint8_t *out_,
+                                                uint32_t *out_len, uint32_t *status, uint32_t remap) {
+    const uint32_t lane = lane_id();
+    uint32_t lb = blockIdx.x;
+    if (remap) {  // XCD-aware order, as k_decode
+        const uint32_t nb = gridDim.x, x = blockIdx.x & 7u, per = nb >> 3, rem = nb & 7u;
+        lb = x * per + min(x, rem) + (blockIdx.x >> 3);
+    }
+    const uint32_t qi = lb * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (qi >= nq) return;
+    const GatherQuery q = qs[qi];
+    const PX_GAS SpanEnt *sp = (const PX_GAS SpanEnt *)uni64((uint64_t)q.span);
+    const PX_GAS uint8_t *base = (const PX_GAS uint8_t *)uni64((uint64_t)q.base);
+    PX_GAS uint8_t *o = (PX_GAS uint8_t *)out_ + uni64(q.out_off);
+    const uint32_t nspan = uni(q.nspan), cap = uni(q.cap), len = uni(q.len);
+    for (uint32_t k0 = 0; k0 < nspan; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        uint32_t st = 0, en = 0;
+        int32_t rel = 0;
+        if (k < nspan) {
+            const PX_GAS uint32_t *e = (const PX_GAS uint32_t *)(sp + k);
+            rel = (int32_t)e[0];
+            st = e[1];
+            en = ((const PX_GAS uint32_t *)(sp + k + 1))[1];
+        }
+        if (uni(st) >= cap) break;  // spans are in output order: lane 0's start is the lowest
+        en = min(en, cap);
+        const uint32_t nb = en > st ? en - st : 0;
+        const bool lng = nb > kLaneCopyMax;
+        if (nb && !lng) lane_copy(o + st, base + rel, nb);
+        uint64_t lm = ballot(lng);
+        while (lm) {
+            const uint32_t j = ffs64(lm);
+            lm &= lm - 1;
+            wave_copy(o + readlane(st, j), base + (int32_t)readlane((uint32_t)rel, j), readlane(nb, j));
+        }
+    }
+    if (lane == 0) {  // result slot: the query's position in the k_decode launch it was taken from
+        out_len[q.slot] = min(len, cap);
+        status[q.slot] = len > cap ? (uint32_t)kErrSpace : (uint32_t)kOk;
+    }
 }
 
 // ====================================================================== migrate
@@ -2201,13 +2339,36 @@ hipError_t launch_decode(hipStream_t s, const DecodeQuery *qs, uint32_t nq, cons
                          uint8_t *out, uint32_t *out_len, uint32_t *status, Frame *scratch, uint32_t depth_cap,
                          uint32_t n_waves, bool keys) {
     if (!nq) return hipSuccess;
-    const uint32_t blocks = (n_waves + kDecWaves - 1) / kDecWaves;
+    const uint32_t blocks = ((n_waves & 0x7fffffffu) + kDecWaves - 1) / kDecWaves;
     if (keys)
         k_decode_keys<<<blocks, 64 * kDecWaves, 0, s>>>(qs, nq, chunk_slots, out, out_len, status, scratch,
                                                           depth_cap, n_waves);
     else
         k_decode<<<blocks, 64 * kDecWaves, 0, s>>>(qs, nq, chunk_slots, out, out_len, status, scratch, depth_cap,
                                                      n_waves);
+    return hipGetLastError();
+}
+
+hipError_t launch_decode_addr(hipStream_t s, const DecodeQuery *qs, uint32_t nq, const RecSlot *const *chunk_slots,
+                              int32_t *out, uint32_t *out_len, uint32_t *status, Frame *scratch, uint32_t depth_cap,
+                              uint32_t n_waves) {
+    if (!nq) return hipSuccess;
+    const uint32_t blocks = ((n_waves & 0x7fffffffu) + kDecWaves - 1) / kDecWaves;
+    k_decode_addr<<<blocks, 64 * kDecWaves, 0, s>>>(qs, nq, chunk_slots, out, out_len, status, scratch, depth_cap,
+                                                      n_waves);
+    return hipGetLastError();
+}
+
+hipError_t launch_span_build(hipStream_t s, uint32_t n, const SpanJob *jobs) {
+    if (!n) return hipSuccess;
+    k_span_build<<<std::min<uint32_t>((n + 3) / 4, 16384), 256, 0, s>>>(n, jobs);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather(hipStream_t s, uint32_t nq, const GatherQuery *qs, uint8_t *out, uint32_t *out_len,
+                         uint32_t *status, bool remap) {
+    if (!nq) return hipSuccess;
+    k_gather<<<(nq + 3) / 4, 256, 0, s>>>(nq, qs, out, out_len, status, remap ? 1u : 0u);
     return hipGetLastError();
 }
 

@@ -277,6 +277,11 @@ PSA_DEV uint32_t lce(const uint64_t *G8, uint32_t p, uint32_t q, uint32_t k, uin
     return lim;
 }
 
+// One thread per kLceSpan consecutive positions.  The per-position arrays are read and
+// written 8 positions at a time with 16-byte accesses: a wave's 64 threads sit 256
+// positions apart, so per-position 2- and 4-byte accesses would each touch a different
+// cache line (and 64 threads x 5 arrays of such lines do not stay cached between the
+// thread's consecutive positions).
 __global__ void __launch_bounds__(256) k_psa_lce(uint32_t N, const uint64_t *G8, const uint16_t *dist,
                                                  const uint32_t *psvp, const uint32_t *nsvp, uint16_t *lcp_p,
                                                  uint16_t *lcp_n) {
@@ -285,25 +290,53 @@ __global__ void __launch_bounds__(256) k_psa_lce(uint32_t N, const uint64_t *G8,
     if (p0 >= N) return;
     const uint32_t p1 = min(N, p0 + kLceSpan);
     uint32_t kp = 0, kn = 0;
-    for (uint32_t p = p0; p < p1; ++p) {
-        const uint32_t dp = dist[p];
-        const uint32_t q = psvp[p], s = nsvp[p];
-        kp = kp ? kp - 1 : 0;
-        kn = kn ? kn - 1 : 0;
-        if (q == kNoPos) {
-            kp = 0;
+    for (uint32_t b = p0; b < p1; b += 8) {
+        const uint32_t nb = min(8u, p1 - b);
+        uint16_t dv[8], op[8], on[8];
+        uint32_t qv[8], sv[8];
+        if (nb == 8) {  // b is a multiple of 8: aligned vector loads
+            *(uint4 *)dv = *(const uint4 *)(dist + b);
+            *(uint4 *)qv = *(const uint4 *)(psvp + b);
+            *(uint4 *)(qv + 4) = *(const uint4 *)(psvp + b + 4);
+            *(uint4 *)sv = *(const uint4 *)(nsvp + b);
+            *(uint4 *)(sv + 4) = *(const uint4 *)(nsvp + b + 4);
         } else {
-            const uint32_t lim = min(dp, (uint32_t)dist[q]);
-            kp = lce(G8, p, q, min(kp, lim), lim);
+            for (uint32_t i = 0; i < nb; ++i) {
+                dv[i] = dist[b + i];
+                qv[i] = psvp[b + i];
+                sv[i] = nsvp[b + i];
+            }
         }
-        if (s == kNoPos) {
-            kn = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 8; ++i) {
+            if (i >= nb) break;
+            const uint32_t p = b + i, dp = dv[i], q = qv[i], sn = sv[i];
+            kp = kp ? kp - 1 : 0;
+            kn = kn ? kn - 1 : 0;
+            if (q == kNoPos) {
+                kp = 0;
+            } else {
+                const uint32_t lim = min(dp, (uint32_t)dist[q]);
+                kp = lce(G8, p, q, min(kp, lim), lim);
+            }
+            if (sn == kNoPos) {
+                kn = 0;
+            } else {
+                const uint32_t lim = min(dp, (uint32_t)dist[sn]);
+                kn = lce(G8, p, sn, min(kn, lim), lim);
+            }
+            op[i] = (uint16_t)kp;
+            on[i] = (uint16_t)kn;
+        }
+        if (nb == 8) {
+            *(uint4 *)(lcp_p + b) = *(const uint4 *)op;
+            *(uint4 *)(lcp_n + b) = *(const uint4 *)on;
         } else {
-            const uint32_t lim = min(dp, (uint32_t)dist[s]);
-            kn = lce(G8, p, s, min(kn, lim), lim);
+            for (uint32_t i = 0; i < nb; ++i) {
+                lcp_p[b + i] = op[i];
+                lcp_n[b + i] = on[i];
+            }
         }
-        lcp_p[p] = (uint16_t)kp;
-        lcp_n[p] = (uint16_t)kn;
     }
 }
 

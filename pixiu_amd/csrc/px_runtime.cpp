@@ -44,6 +44,10 @@ hipError_t launch_link(hipStream_t, uint32_t, const LinkJob *);
 hipError_t launch_decode(hipStream_t, const DecodeQuery *, uint32_t, const RecSlot *const *, uint8_t *,
                          uint32_t *, uint32_t *, Frame *, uint32_t, uint32_t, bool);
 hipError_t launch_rehash(hipStream_t, const uint4 *, uint32_t, uint32_t, uint4 *, uint32_t);
+hipError_t launch_decode_addr(hipStream_t, const DecodeQuery *, uint32_t, const RecSlot *const *, int32_t *,
+                              uint32_t *, uint32_t *, Frame *, uint32_t, uint32_t);
+hipError_t launch_span_build(hipStream_t, uint32_t, const SpanJob *);
+hipError_t launch_gather(hipStream_t, uint32_t, const GatherQuery *, uint8_t *, uint32_t *, uint32_t *, bool);
 int debug_trace_take(int32_t *, uint32_t);
 int debug_prof_take(unsigned long long *, uint32_t);
 }  // namespace px
@@ -308,6 +312,15 @@ struct Chunk {
     std::string kp;  // concatenated compat key prefixes
     std::vector<uint64_t> kp_off;
     std::vector<uint32_t> kp_len;
+    // span tables (full-range getitem as a gather); sized lazily
+    struct Span {
+        const SpanEnt *p = nullptr;  // device; null: decode through the segment walk
+        uint32_t n = 0, len = 0;     // spans, compat expansion length
+        bool eq = false;             // the compat expansion equals the doc (== exact)
+        const SpanEnt *xp = nullptr;  // exact expansion's table when it differs (!eq)
+        uint32_t xn = 0, xlen = 0;
+    };
+    std::vector<Span> span;
 };
 
 struct Shard {
@@ -927,8 +940,55 @@ struct px_ctx {
 
     // ------------------------------------------------------------ decode
     // Runs decode queries; out_dev is a device buffer.  Returns per-query len/status.
+    static bool spans_enabled() {  // PX_SPANS=0: no span tables, every getitem walks
+        const char *e = std::getenv("PX_SPANS");
+        return !(e && e[0] == '0');
+    }
+    // the table serving query q: {entries, count, expansion length}, or entries == null
+    struct SpanView {
+        const SpanEnt *p;
+        uint32_t n, len;
+    };
+    SpanView span_view(const DecodeQuery &q) const {
+        if (q.chunk == kNone || q.from != 0 || q.to < kMaxDoc) return SpanView{nullptr, 0, 0};
+        const Chunk &ch = chunks[q.chunk];
+        if (q.idx >= ch.span.size()) return SpanView{nullptr, 0, 0};
+        const Chunk::Span &sp = ch.span[q.idx];
+        if (!sp.p) return SpanView{nullptr, 0, 0};
+        if (q.mode == 0 || sp.eq) return SpanView{sp.p, sp.n, sp.len};
+        return SpanView{sp.xp, sp.xn, sp.xlen};
+    }
+
+    // Full-range getitem queries on records with span tables go to k_gather: they are
+    // taken out of qn[lo, hi) (chunk -> kNone: k_decode's wave skips them) and returned
+    // as gather queries whose result slot is their position in the launch's arrays.
+    std::vector<GatherQuery> take_gathers(DecodeQuery *qn, uint32_t lo, uint32_t hi, uint32_t slot0) {
+        std::vector<GatherQuery> g;
+        if (!spans_enabled()) return g;
+        for (uint32_t j = lo; j < hi; ++j) {
+            const SpanView sp = span_view(qn[j]);
+            if (!sp.p) continue;
+            g.push_back(GatherQuery{sp.p, chunks[qn[j].chunk].slots[qn[j].idx].comp, qn[j].out_off, sp.n, sp.len,
+                                    qn[j].out_cap, j - lo + slot0});
+            qn[j].chunk = kNone;
+            qn[j].nrec = 0;
+        }
+        return g;
+    }
+    // after the k_decode launch on the same stream (its skipped-query results are overwritten)
+    void launch_gathers(hipStream_t st, const std::vector<GatherQuery> &g, uint8_t *out, uint32_t *dl, uint32_t *ds,
+                        GatherQuery *&dbuf) {
+        if (g.empty()) return;
+        dbuf = (GatherQuery *)heap.alloc(g.size() * sizeof(GatherQuery));
+        hcheck(hipMemcpyAsync(dbuf, g.data(), g.size() * sizeof(GatherQuery), hipMemcpyHostToDevice, st));
+        hcheck(launch_gather(st, (uint32_t)g.size(), dbuf, out, dl, ds, true));
+    }
+
+    // Runs decode queries; out_dev is a device buffer.  Returns per-query len/status.
+    // `addr` runs k_decode_addr instead (the span build: 4-byte address elements,
+    // out_off in elements); getitem batches (timed) send span-served queries to k_gather.
     void run_decode(const std::vector<DecodeQuery> &q, uint8_t *out_dev, std::vector<uint32_t> &len,
-                    std::vector<uint32_t> &st, bool timed) {
+                    std::vector<uint32_t> &st, bool timed, int32_t *addr = nullptr) {
         uint32_t nq = (uint32_t)q.size();
         len.assign(nq, 0);
         st.assign(nq, 0);
@@ -943,26 +1003,148 @@ struct px_ctx {
         auto *dl = (uint32_t *)dlen_buf.get((uint64_t)nq * 8);
         uint32_t *ds = dl + nq;
         auto *qn = (DecodeQuery *)hq_buf.get((uint64_t)nq * sizeof(DecodeQuery));
-        for (uint32_t i = 0; i < nq; ++i) {
-            qn[i] = q[i];
-            qn[i].nrec = q[i].chunk == kNone ? 0 : chunks[q[i].chunk].n;
+        // queries grouped by chunk (stable), so that one chunk's queries run together on
+        // one XCD (k_decode's remap); results are mapped back below
+        std::vector<uint32_t> perm;
+        bool sorted = true;
+        for (uint32_t i = 1; i < nq && sorted; ++i) sorted = q[i - 1].chunk <= q[i].chunk;
+        if (!sorted) {
+            perm.resize(nq);
+            for (uint32_t i = 0; i < nq; ++i) perm[i] = i;
+            std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) { return q[a].chunk < q[b].chunk; });
         }
+        for (uint32_t j = 0; j < nq; ++j) {
+            const DecodeQuery &src = q[perm.empty() ? j : perm[j]];
+            qn[j] = src;
+            qn[j].nrec = src.chunk == kNone ? 0 : chunks[src.chunk].n;
+        }
+        std::vector<GatherQuery> gq;
+        if (timed && !addr) gq = take_gathers(qn, 0, nq, 0);
+        stats.last_gather_queries = timed ? (uint32_t)gq.size() : stats.last_gather_queries;
         hcheck(hipMemcpyAsync(dq, qn, (size_t)nq * sizeof(DecodeQuery), hipMemcpyHostToDevice, stream));
         flush_tab();
         if (timed) hcheck(hipEventRecord(ev0, stream));
         // timed == a getitem batch (k_decode); otherwise stored-key prefixes (k_decode_keys)
-        hcheck(launch_decode(stream, dq, nq, (const RecSlot *const *)chunk_tab, out_dev, dl, ds, frames, depth,
-                             waves, !timed));
+        static const bool xcd = [] {
+            const char *e = std::getenv("PX_DEC_XCD");
+            return !(e && e[0] == '0');
+        }();
+        if (addr)
+            hcheck(launch_decode_addr(stream, dq, nq, (const RecSlot *const *)chunk_tab, addr, dl, ds, frames, depth,
+                                      waves | (xcd ? 0x80000000u : 0u)));
+        else
+            hcheck(launch_decode(stream, dq, nq, (const RecSlot *const *)chunk_tab, out_dev, dl, ds, frames, depth,
+                                 waves | (xcd ? 0x80000000u : 0u), !timed));
+        GatherQuery *dgq = nullptr;
+        launch_gathers(stream, gq, out_dev, dl, ds, dgq);
         if (timed) hcheck(hipEventRecord(ev1, stream));
         auto *hr = (uint32_t *)hres_buf.get((uint64_t)nq * 8);
         hcheck(hipMemcpyAsync(hr, dl, (size_t)nq * 8, hipMemcpyDeviceToHost, stream));  // lengths, then statuses
         sync();
-        std::memcpy(len.data(), hr, (size_t)nq * 4);
-        std::memcpy(st.data(), hr + nq, (size_t)nq * 4);
+        if (dgq) heap.release(dgq, gq.size() * sizeof(GatherQuery));
         if (timed) {
             float ms = 0;
             hcheck(hipEventElapsedTime(&ms, ev0, ev1));
             stats.last_decode_kernel_ms = ms;
+        }
+        if (perm.empty()) {
+            std::memcpy(len.data(), hr, (size_t)nq * 4);
+            std::memcpy(st.data(), hr + nq, (size_t)nq * 4);
+        } else {
+            for (uint32_t j = 0; j < nq; ++j) {
+                len[perm[j]] = hr[j];
+                st[perm[j]] = hr[nq + j];
+            }
+        }
+    }
+
+    // Span tables for new records (k_decode_addr -> k_span_build count -> allocate ->
+    // k_span_build write).  docs: each record's escaped doc on the device (for the
+    // compat == exact flag), or null.  A record whose compat expansion overran its
+    // doc + 64 bytes, or reaches a source beyond +-2 GiB, keeps using the walk.
+    struct SpanReq {
+        uint32_t chunk, idx;
+        const uint8_t *doc;
+    };
+    void build_spans(const std::vector<SpanReq> &reqs, uint32_t mode = 0) {
+        if (reqs.empty() || !spans_enabled()) return;
+        std::vector<DecodeQuery> q;
+        q.reserve(reqs.size());
+        uint64_t tot = 0;
+        for (const SpanReq &r : reqs) {
+            const uint32_t cap = (uint32_t)round_up(chunks[r.chunk].doc_len[r.idx] + 64, 16);
+            q.push_back(DecodeQuery{r.chunk, r.idx, 0, kMaxDoc, tot, cap, mode});
+            tot += cap;
+        }
+        auto *addr = (int32_t *)heap.alloc(tot * 4 + 64);
+        std::vector<uint32_t> len, st;
+        run_decode(q, nullptr, len, st, false, addr);
+        std::vector<SpanJob> jobs;
+        std::vector<uint32_t> ji;
+        for (size_t k = 0; k < reqs.size(); ++k) {
+            if (st[k] != kOk) continue;
+            const Chunk &ch = chunks[reqs[k].chunk];
+            jobs.push_back(SpanJob{addr + q[k].out_off, ch.slots[reqs[k].idx].comp, reqs[k].doc, nullptr, len[k],
+                                   ch.doc_len[reqs[k].idx], nullptr, 0});
+            ji.push_back((uint32_t)k);
+        }
+        if (!jobs.empty()) {
+            const size_t nj = jobs.size();
+            auto *dcnt = (uint32_t *)heap.alloc(nj * 4 + 64);
+            for (size_t j = 0; j < nj; ++j) jobs[j].count = dcnt + j;
+            auto *djobs = (SpanJob *)heap.alloc(nj * sizeof(SpanJob));
+            h2d(djobs, jobs.data(), nj * sizeof(SpanJob));
+            hcheck(launch_span_build(stream, (uint32_t)nj, djobs));
+            std::vector<uint32_t> cnt(nj);
+            d2h(cnt.data(), dcnt, nj * 4);
+            sync();
+            uint64_t ents = 0;
+            for (size_t j = 0; j < nj; ++j)
+                if (!(cnt[j] & kSpanBad)) ents += (cnt[j] & ~(kSpanBad | kSpanEq)) + 1;
+            if (ents) {
+                auto *tab = (SpanEnt *)heap.alloc(ents * sizeof(SpanEnt) + 64);
+                store_blocks.emplace_back(tab, ents * sizeof(SpanEnt) + 64);
+                uint64_t o = 0;
+                for (size_t j = 0; j < nj; ++j) {
+                    const uint32_t k = ji[j];
+                    Chunk &ch = chunks[reqs[k].chunk];
+                    if (ch.span.size() < ch.n) ch.span.resize(ch.n);
+                    if (cnt[j] & kSpanBad) {
+                        jobs[j].out = nullptr;
+                        jobs[j].len = 0;
+                        continue;
+                    }
+                    const uint32_t ns = cnt[j] & ~(kSpanBad | kSpanEq);
+                    jobs[j].out = tab + o;
+                    Chunk::Span &sp = ch.span[reqs[k].idx];
+                    if (mode == 0) {
+                        sp.p = tab + o;
+                        sp.n = ns;
+                        sp.len = len[k];
+                        sp.eq = (cnt[j] & kSpanEq) != 0;
+                    } else {
+                        sp.xp = tab + o;
+                        sp.xn = ns;
+                        sp.xlen = len[k];
+                    }
+                    o += ns + 1;
+                    stats.span_entries += ns + 1;
+                }
+                h2d(djobs, jobs.data(), nj * sizeof(SpanJob));
+                hcheck(launch_span_build(stream, (uint32_t)nj, djobs));
+            }
+            sync();
+            heap.release(djobs, nj * sizeof(SpanJob));
+            heap.release(dcnt, nj * 4 + 64);
+        }
+        heap.release(addr, tot * 4 + 64);
+        if (mode == 0) {  // exact tables for the records whose compat expansion is not the doc
+            std::vector<SpanReq> x;
+            for (const SpanReq &r : reqs) {
+                const Chunk &ch = chunks[r.chunk];
+                if (r.idx < ch.span.size() && ch.span[r.idx].p && !ch.span[r.idx].eq) x.push_back(r);
+            }
+            build_spans(x, 1);
         }
     }
 
@@ -1035,11 +1217,14 @@ struct px_ctx {
         auto *qn = (DecodeQuery *)hq_buf.get((uint64_t)n * sizeof(DecodeQuery));
         auto *hr = (uint32_t *)hres_buf.get((uint64_t)n * 8);
         std::memcpy(qn, q.data(), (size_t)head * sizeof(DecodeQuery));
+        const std::vector<GatherQuery> g1 = take_gathers(qn, 0, head, 0);
         hcheck(hipMemcpyAsync(dq, qn, (size_t)head * sizeof(DecodeQuery), hipMemcpyHostToDevice, stream));
         flush_tab();
         hcheck(hipEventRecord(ev0, stream));
-        hcheck(launch_decode(stream, dq, head, (const RecSlot *const *)chunk_tab, out, dl, ds, frames, depth, w1,
-                             false));
+        hcheck(launch_decode(stream, dq, head, (const RecSlot *const *)chunk_tab, out, dl, ds, frames, depth,
+                             w1 | 0x80000000u, false));
+        GatherQuery *dg1 = nullptr, *dg2 = nullptr;
+        launch_gathers(stream, g1, out, dl, ds, dg1);
         // the tail: resolved while the head decodes
         auto t1 = clk::now();
         parallel_ranges(n - head, host_threads(), [&](uint32_t lo, uint32_t hi) { resolve(head + lo, head + hi); });
@@ -1051,16 +1236,21 @@ struct px_ctx {
             return PX_ESPACE;
         }
         std::memcpy(qn + head, q.data() + head, (size_t)(n - head) * sizeof(DecodeQuery));
+        const std::vector<GatherQuery> g2 = take_gathers(qn, head, n, 0);
+        stats.last_gather_queries = (uint32_t)(g1.size() + g2.size());
         hcheck(hipStreamWaitEvent(stream2, ev0, 0));  // chunk table and head queries uploaded
         hcheck(hipMemcpyAsync(dq + head, qn + head, (size_t)(n - head) * sizeof(DecodeQuery), hipMemcpyHostToDevice,
                               stream2));
         hcheck(launch_decode(stream2, dq + head, n - head, (const RecSlot *const *)chunk_tab, out, dl + head,
-                             ds + head, frames + (uint64_t)w1 * depth, depth, w2, false));
+                             ds + head, frames + (uint64_t)w1 * depth, depth, w2 | 0x80000000u, false));
+        launch_gathers(stream2, g2, out, dl + head, ds + head, dg2);
         hcheck(hipEventRecord(ev_join, stream2));
         hcheck(hipStreamWaitEvent(stream, ev_join, 0));
         hcheck(hipEventRecord(ev1, stream));
         hcheck(hipMemcpyAsync(hr, dl, (size_t)n * 8, hipMemcpyDeviceToHost, stream));  // lengths, then statuses
         sync();
+        if (dg1) heap.release(dg1, g1.size() * sizeof(GatherQuery));
+        if (dg2) heap.release(dg2, g2.size() * sizeof(GatherQuery));
         float ms = 0;
         hcheck(hipEventElapsedTime(&ms, ev0, ev1));
         stats.last_decode_kernel_ms = ms;
@@ -1711,6 +1901,16 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
                 if (chunks[rgchunk[r]].used) chunks[rgchunk[r]].used--;
                 live[r] = 0;
             }
+    }
+
+    // ---- span tables of the new records (full-range getitem as a gather)
+    {
+        std::vector<SpanReq> reqs;
+        for (uint32_t r = 0; r < n; ++r)
+            if (live[r]) reqs.push_back(SpanReq{rgchunk[r], ridx[r], dst[r]});
+        const auto ts = std::chrono::steady_clock::now();
+        build_spans(reqs);
+        stats.last_span_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts).count();
     }
 
     // ---- CritBit inserts: every shard's own records in arrival order, shards on host
