@@ -289,7 +289,7 @@ __global__ void __launch_bounds__(256) k_psa_lce(uint32_t N, const uint64_t *G8,
     const uint32_t p0 = t * kLceSpan;
     if (p0 >= N) return;
     const uint32_t p1 = min(N, p0 + kLceSpan);
-    uint32_t kp = 0, kn = 0;
+    uint32_t kp = 0, kn = 0, qprev = kNoPos - 1, sprev = kNoPos - 1;
     for (uint32_t b = p0; b < p1; b += 8) {
         const uint32_t nb = min(8u, p1 - b);
         uint16_t dv[8], op[8], on[8];
@@ -311,20 +311,27 @@ __global__ void __launch_bounds__(256) k_psa_lce(uint32_t N, const uint64_t *G8,
         for (uint32_t i = 0; i < 8; ++i) {
             if (i >= nb) break;
             const uint32_t p = b + i, dp = dv[i], q = qv[i], sn = sv[i];
+            // the shifted pair: lcp(p-1, q') = L >= 2 gives lcp(p, q'+1) = L - 1 exactly
+            // (same mismatch, or the same doc end, one byte on; both stay in their docs),
+            // so a neighbour that continues the previous one needs no text at all
+            const bool shp = q != kNoPos && q == qprev + 1 && kp >= 2;
+            const bool shn = sn != kNoPos && sn == sprev + 1 && kn >= 2;
             kp = kp ? kp - 1 : 0;
             kn = kn ? kn - 1 : 0;
             if (q == kNoPos) {
                 kp = 0;
-            } else {
+            } else if (!shp) {
                 const uint32_t lim = min(dp, (uint32_t)dist[q]);
                 kp = lce(G8, p, q, min(kp, lim), lim);
             }
             if (sn == kNoPos) {
                 kn = 0;
-            } else {
+            } else if (!shn) {
                 const uint32_t lim = min(dp, (uint32_t)dist[sn]);
                 kn = lce(G8, p, sn, min(kn, lim), lim);
             }
+            qprev = q;
+            sprev = sn;
             op[i] = (uint16_t)kp;
             on[i] = (uint16_t)kn;
         }
