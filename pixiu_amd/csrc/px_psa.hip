@@ -40,6 +40,7 @@
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_select.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 
 #include "px_common.h"
 
@@ -146,6 +147,178 @@ __global__ void __launch_bounds__(256) k_psa_rank2(uint32_t m, const uint64_t *k
     const bool h = sfirst[t] == t;
     const bool hn = t + 1 == m || keys[t + 1] != k || (uint32_t)keys[t + 1] == 0;
     active[t] = (h && hn) ? 0 : 1;
+}
+
+// ---------------------------------------------------------------- segmented doubling sort
+// A doubling step's keys arrive in suffix-array order, so each group (equal high word) is
+// a contiguous range and only needs sorting by the low word inside it.  From the third
+// step on almost every group is small (config 3: every group <= 113 suffixes from h = 24
+// on, 90 % of suffixes in groups <= 1,024 at h = 12), so groups are sorted where they lie:
+// <= 64 by one wave (bitonic over lanes), <= kSegBlock by one workgroup (bitonic in LDS),
+// and only the rest go through the global radix sort.  Ties (equal low words: identical
+// complete strings) keep their input order, as the stable radix sort keeps them.
+constexpr uint32_t kSegBlock = 1024;
+
+__global__ void __launch_bounds__(256) k_seg_flag(uint32_t m, const uint64_t *keys, uint8_t *fl) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= m) return;
+    fl[t] = (t == 0 || (keys[t] >> 32) != (keys[t - 1] >> 32)) ? 1 : 0;
+}
+
+// group sizes -> class lists (wave-aggregated appends; a list's order does not matter):
+// class c < 6: size <= 2^(c+1) (sorted 64 / 2^(c+1) groups per wave), 6: <= kSegBlock, 7: larger
+constexpr int kSegClasses = 8;
+__global__ void __launch_bounds__(256) k_seg_class(uint32_t ng, const uint32_t *gs, uint32_t m, uint32_t *lists,
+                                                   uint64_t stride, uint32_t *cnt) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = lane_id();
+    uint32_t sz = 0;
+    if (g < ng) sz = (g + 1 < ng ? gs[g + 1] : m) - gs[g];
+    int cls = -1;
+    if (g < ng) {
+        cls = 7;
+        if (sz <= kSegBlock) cls = 6;
+        for (int c = 5; c >= 0; --c)
+            if (sz <= (2u << c)) cls = c;
+    }
+    for (int c = 0; c < kSegClasses; ++c) {
+        const uint64_t mm = __ballot(cls == c);
+        if (!mm) continue;
+        const uint32_t leader = (uint32_t)__ffsll((long long)mm) - 1u;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&cnt[c], (uint32_t)__popcll(mm));
+        base = (uint32_t)__shfl((int)base, (int)leader);
+        const uint32_t rank =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0));
+        if (cls == c) lists[(uint64_t)c * stride + base + rank] = g;
+    }
+}
+
+PSA_DEV void cas_shfl(uint64_t &k, uint32_t &v, uint32_t lane, uint32_t j, bool up) {
+    const uint64_t ok = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(k >> 32), (int)j) << 32) |
+                        (uint32_t)__shfl_xor((int)(uint32_t)k, (int)j);
+    const uint32_t ov = (uint32_t)__shfl_xor((int)v, (int)j);
+    const bool lower = (lane & j) == 0;
+    const bool take = up == lower ? ok < k : ok > k;
+    if (take) {
+        k = ok;
+        v = ov;
+    }
+}
+
+// groups of <= S suffixes, 64 / S per wave: bitonic over S-lane segments, sort key
+// (low word << 6 | input index)
+template <uint32_t S>
+__global__ void __launch_bounds__(256) k_seg_sortS(uint32_t n, const uint32_t *list, const uint32_t *gs, uint32_t ng,
+                                                   uint32_t m, const uint64_t *keys, const uint32_t *vals,
+                                                   uint64_t *keys_out, uint32_t *vals_out) {
+    // grid-stride: a dispatch holds fewer than 2^32 work-items, and there can be ~10^8 groups
+    constexpr uint32_t G = 64 / S;
+    const uint32_t lane = lane_id(), i = lane & (S - 1);
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); w * G < n; w += waves) {
+        const uint32_t slot = w * G + lane / S;
+        uint32_t a = 0, sz = 0;
+        if (slot < n) {
+            const uint32_t g = list[slot];
+            a = gs[g];
+            sz = (g + 1 < ng ? gs[g + 1] : m) - a;
+        }
+        uint64_t k = ~0ull, hi = 0;
+        uint32_t v = 0;
+        if (i < sz) {
+            const uint64_t key = keys[a + i];
+            hi = key >> 32;
+            k = (key & 0xffffffffull) << 6 | i;
+            v = vals[a + i];
+        }
+        for (uint32_t kk = 2; kk <= S; kk <<= 1)
+            for (uint32_t j = kk >> 1; j > 0; j >>= 1) cas_shfl(k, v, lane, j, (i & kk) == 0);
+        if (i < sz) {
+            keys_out[a + i] = hi << 32 | (k >> 6);
+            vals_out[a + i] = v;
+        }
+    }
+}
+
+// one workgroup per group of 65..kSegBlock: bitonic sort in LDS
+__global__ void __launch_bounds__(256) k_seg_sortblk(const uint32_t *list, const uint32_t *gs, uint32_t ng, uint32_t m,
+                                                     const uint64_t *keys, const uint32_t *vals, uint64_t *keys_out,
+                                                     uint32_t *vals_out) {
+    __shared__ uint64_t sk[kSegBlock];
+    __shared__ uint32_t sv[kSegBlock];
+    const uint32_t g = list[blockIdx.x];
+    const uint32_t a = gs[g], sz = (g + 1 < ng ? gs[g + 1] : m) - a;
+    uint32_t P = 128;
+    while (P < sz) P <<= 1;
+    const uint64_t hi = keys[a] >> 32;
+    for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
+        if (i < sz) {
+            sk[i] = (keys[a + i] & 0xffffffffull) << 10 | i;
+            sv[i] = vals[a + i];
+        } else {
+            sk[i] = ~0ull;
+            sv[i] = 0;
+        }
+    }
+    __syncthreads();
+    for (uint32_t kk = 2; kk <= P; kk <<= 1)
+        for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const bool up = (i & kk) == 0;
+                    const uint64_t x = sk[i], y = sk[l];
+                    if (up ? x > y : x < y) {
+                        sk[i] = y;
+                        sk[l] = x;
+                        const uint32_t t = sv[i];
+                        sv[i] = sv[l];
+                        sv[l] = t;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    for (uint32_t i = threadIdx.x; i < sz; i += blockDim.x) {
+        keys_out[a + i] = hi << 32 | (sk[i] >> 10);
+        vals_out[a + i] = sv[i];
+    }
+}
+
+// big groups: mark their elements, then gather / radix sort / scatter back
+__global__ void __launch_bounds__(256) k_seg_mark(const uint32_t *list, const uint32_t *gs, uint32_t ng, uint32_t m,
+                                                  uint8_t *fl) {
+    const uint32_t g = list[blockIdx.x];
+    const uint32_t a = gs[g], sz = (g + 1 < ng ? gs[g + 1] : m) - a;
+    for (uint32_t i = threadIdx.x; i < sz; i += blockDim.x) fl[a + i] = 1;
+}
+__global__ void __launch_bounds__(256) k_seg_gather(uint32_t n, const uint32_t *idx, const uint64_t *keys,
+                                                    const uint32_t *vals, uint64_t *ck, uint32_t *cv) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    ck[i] = keys[idx[i]];
+    cv[i] = vals[idx[i]];
+}
+__global__ void __launch_bounds__(256) k_seg_scatter(uint32_t n, const uint32_t *idx, const uint64_t *ck,
+                                                     const uint32_t *cv, uint64_t *keys_out, uint32_t *vals_out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    keys_out[idx[i]] = ck[i];
+    vals_out[idx[i]] = cv[i];
+}
+
+// debug (PX_PSA_SEGCHECK=1): compare the segmented sort with the radix sort
+__global__ void k_seg_cmp(uint32_t m, const uint64_t *k1, const uint32_t *v1, const uint64_t *k2, const uint32_t *v2,
+                          uint32_t *out) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= m) return;
+    if (k1[t] != k2[t] || v1[t] != v2[t]) {
+        const uint32_t c = atomicAdd(&out[0], 1u);
+        if (c == 0) {
+            out[1] = t;
+        }
+    }
 }
 
 // ---------------------------------------------------------------- nearest smaller positions
@@ -473,6 +646,9 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     PSA_CHECK(rocprim::radix_sort_pairs(nullptr, t_sort, keys, keys2, vals, sa, (size_t)N, 0, 64, s));
     PSA_CHECK(rocprim::inclusive_scan(nullptr, t_scan, f1, f1, (size_t)N, Max(), s));
     PSA_CHECK(rocprim::select(nullptr, t_sel, sa, act, vals, cnt, (size_t)N, s));
+    size_t t_sel2 = 0;
+    PSA_CHECK(rocprim::select(nullptr, t_sel2, rocprim::counting_iterator<uint32_t>(0), act, vals, cnt, (size_t)N, s));
+    t_sel = std::max(t_sel, t_sel2);
     const size_t t_bytes = std::max({t_sort, t_scan, t_sel}) + 256;
     void *tmp = get(t_bytes);
     size_t tb_ = t_bytes;
@@ -491,13 +667,104 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     PSA_CHECK(hipMemcpy(&m, cnt, 4, hipMemcpyDeviceToHost));
     int rank_bits = 1;
     while (rank_bits < 32 && (1ull << rank_bits) <= n64) ++rank_bits;
+    const bool verbose = [] {
+        const char *v = std::getenv("PX_PSA_VERBOSE");
+        return v && *v == '1';
+    }();
+    const bool segcheck = [] {
+        const char *v = std::getenv("PX_PSA_SEGCHECK");
+        return v && *v == '1';
+    }();
+    const bool segsort = [] {  // PX_PSA_SEGSORT=1: groups sorted in place
+        const char *e = std::getenv("PX_PSA_SEGSORT");
+        return e && e[0] == '1';
+    }();
+    // group starts and the three group lists (an active group has >= 2 suffixes: <= m/2 groups)
+    const uint64_t half = n64 / 2 + 64;
+    auto *gsl = segsort ? (uint32_t *)get(half * 4 * (1 + kSegClasses)) : nullptr;
     uint32_t it = 0;
     for (uint32_t h = syms; m > 0; h *= 2, ++it) {
         if (st && it < 24) st->active[it] = m;
         if (it >= 20) return hipErrorUnknown;  // cannot happen: docs are <= 65,535 bytes
         k_psa_key2<<<blocks(m), tb, 0, s>>>(m, alist, rank, dist, h, keys, vals2);
-        tb_ = t_bytes;
-        PSA_CHECK(rocprim::radix_sort_pairs(tmp, tb_, keys, keys2, vals2, f2, (size_t)m, 0, 32 + rank_bits, s));
+        if (segsort) {
+            // groups are ranges of the (suffix-array ordered) keys: sort each where it lies
+            k_seg_flag<<<blocks(m), tb, 0, s>>>(m, keys, act);
+            tb_ = t_bytes;
+            PSA_CHECK(rocprim::select(tmp, tb_, rocprim::counting_iterator<uint32_t>(0), act, gsl, cnt, (size_t)m, s));
+            PSA_CHECK(hipMemsetAsync(cnt + 1, 0, 4 * kSegClasses, s));
+            PSA_CHECK(hipStreamSynchronize(s));
+            uint32_t ng = 0;
+            PSA_CHECK(hipMemcpy(&ng, cnt, 4, hipMemcpyDeviceToHost));
+            uint32_t *lists = gsl + half;
+            k_seg_class<<<blocks(ng), tb, 0, s>>>(ng, gsl, m, lists, half, cnt + 1);
+            PSA_CHECK(hipStreamSynchronize(s));
+            uint32_t c8[kSegClasses] = {};
+            PSA_CHECK(hipMemcpy(c8, cnt + 1, sizeof c8, hipMemcpyDeviceToHost));
+            if (verbose)
+                fprintf(stderr, "psa: step %u h=%u m=%u groups=%u (<=2..64: %u %u %u %u %u %u, <=%u: %u, larger: %u)\n",
+                        it, h, m, ng, c8[0], c8[1], c8[2], c8[3], c8[4], c8[5], kSegBlock, c8[6], c8[7]);
+            auto grid = [&](uint32_t n, uint32_t per_wave) {
+                return std::min<uint32_t>((n + 4 * per_wave - 1) / (4 * per_wave), 1u << 16);
+            };
+            if (c8[0]) k_seg_sortS<2><<<grid(c8[0], 32), 256, 0, s>>>(c8[0], lists, gsl, ng, m, keys, vals2, keys2, f2);
+            if (c8[1]) k_seg_sortS<4><<<grid(c8[1], 16), 256, 0, s>>>(c8[1], lists + half, gsl, ng, m, keys, vals2, keys2, f2);
+            if (c8[2]) k_seg_sortS<8><<<grid(c8[2], 8), 256, 0, s>>>(c8[2], lists + 2 * half, gsl, ng, m, keys, vals2, keys2, f2);
+            if (c8[3]) k_seg_sortS<16><<<grid(c8[3], 4), 256, 0, s>>>(c8[3], lists + 3 * half, gsl, ng, m, keys, vals2, keys2, f2);
+            if (c8[4]) k_seg_sortS<32><<<grid(c8[4], 2), 256, 0, s>>>(c8[4], lists + 4 * half, gsl, ng, m, keys, vals2, keys2, f2);
+            if (c8[5]) k_seg_sortS<64><<<grid(c8[5], 1), 256, 0, s>>>(c8[5], lists + 5 * half, gsl, ng, m, keys, vals2, keys2, f2);
+            if (c8[6]) k_seg_sortblk<<<c8[6], 256, 0, s>>>(lists + 6 * half, gsl, ng, m, keys, vals2, keys2, f2);
+            PSA_CHECK(hipGetLastError());
+            uint32_t c3[3] = {0, 0, c8[7]};
+            uint32_t *lbig = lists + 7 * half;
+            if (c3[2]) {
+                PSA_CHECK(hipMemsetAsync(act, 0, m, s));
+                k_seg_mark<<<c3[2], 256, 0, s>>>(lbig, gsl, ng, m, act);
+                uint32_t *tl = f1;  // free until the group-head scan below
+                tb_ = t_bytes;
+                PSA_CHECK(rocprim::select(tmp, tb_, rocprim::counting_iterator<uint32_t>(0), act, tl, cnt, (size_t)m, s));
+                PSA_CHECK(hipStreamSynchronize(s));
+                uint32_t ml = 0;
+                PSA_CHECK(hipMemcpy(&ml, cnt, 4, hipMemcpyDeviceToHost));
+                auto *ck = (uint64_t *)get((uint64_t)ml * 24 + 64);
+                uint64_t *ck2 = ck + ml;
+                auto *cv = (uint32_t *)(ck2 + ml), *cv2 = cv + ml;
+                k_seg_gather<<<blocks(ml), tb, 0, s>>>(ml, tl, keys, vals2, ck, cv);
+                tb_ = t_bytes;
+                PSA_CHECK(rocprim::radix_sort_pairs(tmp, tb_, ck, ck2, cv, cv2, (size_t)ml, 0, 32 + rank_bits, s));
+                k_seg_scatter<<<blocks(ml), tb, 0, s>>>(ml, tl, ck2, cv2, keys2, f2);
+                PSA_CHECK(hipStreamSynchronize(s));
+                put(ck, (uint64_t)ml * 24 + 64);
+            }
+            if (segcheck) {
+                auto *k3 = (uint64_t *)get((uint64_t)m * 12 + 64);
+                auto *v3 = (uint32_t *)(k3 + m);
+                tb_ = t_bytes;
+                PSA_CHECK(rocprim::radix_sort_pairs(tmp, tb_, keys, k3, vals2, v3, (size_t)m, 0, 32 + rank_bits, s));
+                PSA_CHECK(hipMemsetAsync(cnt + 12, 0, 8, s));
+                k_seg_cmp<<<blocks(m), tb, 0, s>>>(m, keys2, f2, k3, v3, cnt + 12);
+                PSA_CHECK(hipStreamSynchronize(s));
+                uint32_t r2[2];
+                PSA_CHECK(hipMemcpy(r2, cnt + 12, 8, hipMemcpyDeviceToHost));
+                if (r2[0]) {
+                    uint64_t a[4], b[4];
+                    uint32_t va[4], vb[4];
+                    const uint32_t t0 = r2[1] > 1 ? r2[1] - 1 : 0;
+                    PSA_CHECK(hipMemcpy(a, keys2 + t0, 32, hipMemcpyDeviceToHost));
+                    PSA_CHECK(hipMemcpy(b, k3 + t0, 32, hipMemcpyDeviceToHost));
+                    PSA_CHECK(hipMemcpy(va, f2 + t0, 16, hipMemcpyDeviceToHost));
+                    PSA_CHECK(hipMemcpy(vb, v3 + t0, 16, hipMemcpyDeviceToHost));
+                    fprintf(stderr, "psa segcheck step %u: %u mismatches, first at t=%u\n", it, r2[0], r2[1]);
+                    for (int q = 0; q < 4; ++q)
+                        fprintf(stderr, "  t=%u seg %016llx/%u radix %016llx/%u\n", t0 + q, (unsigned long long)a[q], va[q],
+                                (unsigned long long)b[q], vb[q]);
+                }
+                put(k3, (uint64_t)m * 12 + 64);
+            }
+        } else {
+            tb_ = t_bytes;
+            PSA_CHECK(rocprim::radix_sort_pairs(tmp, tb_, keys, keys2, vals2, f2, (size_t)m, 0, 32 + rank_bits, s));
+        }
         // f2 = positions in the new order; group heads f1 -> vals2, subgroup heads in the
         // (now free) unsorted key buffer: flags in its first half, scan in its second
         uint32_t *sfl = (uint32_t *)keys, *sfirst = (uint32_t *)keys + N;
@@ -516,6 +783,7 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     put(keys2, n64 * 8);
     put(vals2, n64 * 4);
     put(act, n64);
+    if (gsl) put(gsl, half * 4 * (1 + kSegClasses));
     put(tmp, t_bytes);
     PSA_CHECK(hipEventRecord(e1, s));
     // ---- nearest smaller positions in suffix-array order (min tree over sa)
