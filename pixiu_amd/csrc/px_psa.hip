@@ -165,33 +165,44 @@ __global__ void __launch_bounds__(256) k_seg_flag(uint32_t m, const uint64_t *ke
     fl[t] = (t == 0 || (keys[t] >> 32) != (keys[t - 1] >> 32)) ? 1 : 0;
 }
 
-// group sizes -> class lists (wave-aggregated appends; a list's order does not matter):
-// class c < 6: size <= 2^(c+1) (sorted 64 / 2^(c+1) groups per wave), 6: <= kSegBlock, 7: larger
+// group sizes -> size classes: c < 6: size <= 2^(c+1) (sorted 64 / 2^(c+1) groups per
+// wave), 6: <= kSegBlock (one workgroup), 7: larger (radix).  The class lists are one
+// array partitioned class-major: per-block class counts, one exclusive scan over them
+// (class-major), then every block writes its groups at its offsets.
 constexpr int kSegClasses = 8;
-__global__ void __launch_bounds__(256) k_seg_class(uint32_t ng, const uint32_t *gs, uint32_t m, uint32_t *lists,
-                                                   uint64_t stride, uint32_t *cnt) {
+PSA_DEV uint32_t seg_class_of(uint32_t g, uint32_t ng, const uint32_t *gs, uint32_t m) {
+    const uint32_t sz = (g + 1 < ng ? gs[g + 1] : m) - gs[g];
+    uint32_t c = sz <= kSegBlock ? 6 : 7;
+    for (int k = 5; k >= 0; --k)
+        if (sz <= (2u << k)) c = (uint32_t)k;
+    return c;
+}
+__global__ void __launch_bounds__(256) k_seg_hist(uint32_t ng, const uint32_t *gs, uint32_t m, uint32_t nb,
+                                                  uint32_t *hist) {
+    __shared__ uint32_t h[kSegClasses];
+    if (threadIdx.x < kSegClasses) h[threadIdx.x] = 0;
+    __syncthreads();
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t lane = lane_id();
-    uint32_t sz = 0;
-    if (g < ng) sz = (g + 1 < ng ? gs[g + 1] : m) - gs[g];
-    int cls = -1;
+    if (g < ng) atomicAdd(&h[seg_class_of(g, ng, gs, m)], 1u);
+    __syncthreads();
+    if (threadIdx.x < kSegClasses) hist[threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
+}
+__global__ void __launch_bounds__(256) k_seg_part(uint32_t ng, const uint32_t *gs, uint32_t m, uint32_t nb,
+                                                  const uint32_t *offs, uint32_t *lists) {
+    __shared__ uint32_t h[kSegClasses];
+    if (threadIdx.x < kSegClasses) h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g < ng) {
-        cls = 7;
-        if (sz <= kSegBlock) cls = 6;
-        for (int c = 5; c >= 0; --c)
-            if (sz <= (2u << c)) cls = c;
+        const uint32_t c = seg_class_of(g, ng, gs, m);
+        lists[offs[c * nb + blockIdx.x] + atomicAdd(&h[c], 1u)] = g;  // order inside a class is free
     }
-    for (int c = 0; c < kSegClasses; ++c) {
-        const uint64_t mm = __ballot(cls == c);
-        if (!mm) continue;
-        const uint32_t leader = (uint32_t)__ffsll((long long)mm) - 1u;
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(&cnt[c], (uint32_t)__popcll(mm));
-        base = (uint32_t)__shfl((int)base, (int)leader);
-        const uint32_t rank =
-            __builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0));
-        if (cls == c) lists[(uint64_t)c * stride + base + rank] = g;
-    }
+}
+// class start offsets -> out[0..8] (out[8] = ng)
+__global__ void k_seg_bounds(uint32_t nb, const uint32_t *offs, uint32_t ng, uint32_t *out) {
+    const uint32_t c = threadIdx.x;
+    if (c < kSegClasses) out[c] = offs[c * nb];
+    if (c == kSegClasses) out[c] = ng;
 }
 
 PSA_DEV void cas_shfl(uint64_t &k, uint32_t &v, uint32_t lane, uint32_t j, bool up) {
@@ -646,9 +657,10 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     PSA_CHECK(rocprim::radix_sort_pairs(nullptr, t_sort, keys, keys2, vals, sa, (size_t)N, 0, 64, s));
     PSA_CHECK(rocprim::inclusive_scan(nullptr, t_scan, f1, f1, (size_t)N, Max(), s));
     PSA_CHECK(rocprim::select(nullptr, t_sel, sa, act, vals, cnt, (size_t)N, s));
-    size_t t_sel2 = 0;
+    size_t t_sel2 = 0, t_sel3 = 0;
     PSA_CHECK(rocprim::select(nullptr, t_sel2, rocprim::counting_iterator<uint32_t>(0), act, vals, cnt, (size_t)N, s));
-    t_sel = std::max(t_sel, t_sel2);
+    PSA_CHECK(rocprim::exclusive_scan(nullptr, t_sel3, f1, f2, 0u, (size_t)N, rocprim::plus<uint32_t>(), s));
+    t_sel = std::max({t_sel, t_sel2, t_sel3});
     const size_t t_bytes = std::max({t_sort, t_scan, t_sel}) + 256;
     void *tmp = get(t_bytes);
     size_t tb_ = t_bytes;
@@ -675,13 +687,13 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         const char *v = std::getenv("PX_PSA_SEGCHECK");
         return v && *v == '1';
     }();
-    const bool segsort = [] {  // PX_PSA_SEGSORT=1: groups sorted in place
+    const bool segsort = [] {  // PX_PSA_SEGSORT=0: every doubling step through the radix sort
         const char *e = std::getenv("PX_PSA_SEGSORT");
-        return e && e[0] == '1';
+        return !(e && e[0] == '0');
     }();
     // group starts and the three group lists (an active group has >= 2 suffixes: <= m/2 groups)
     const uint64_t half = n64 / 2 + 64;
-    auto *gsl = segsort ? (uint32_t *)get(half * 4 * (1 + kSegClasses)) : nullptr;
+    auto *gsl = segsort ? (uint32_t *)get(half * 12) : nullptr;
     uint32_t it = 0;
     for (uint32_t h = syms; m > 0; h *= 2, ++it) {
         if (st && it < 24) st->active[it] = m;
@@ -692,31 +704,42 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
             k_seg_flag<<<blocks(m), tb, 0, s>>>(m, keys, act);
             tb_ = t_bytes;
             PSA_CHECK(rocprim::select(tmp, tb_, rocprim::counting_iterator<uint32_t>(0), act, gsl, cnt, (size_t)m, s));
-            PSA_CHECK(hipMemsetAsync(cnt + 1, 0, 4 * kSegClasses, s));
             PSA_CHECK(hipStreamSynchronize(s));
             uint32_t ng = 0;
             PSA_CHECK(hipMemcpy(&ng, cnt, 4, hipMemcpyDeviceToHost));
             uint32_t *lists = gsl + half;
-            k_seg_class<<<blocks(ng), tb, 0, s>>>(ng, gsl, m, lists, half, cnt + 1);
+            const uint32_t nbk = blocks(ng);
+            uint32_t *hist = gsl + 2 * half, *offs = hist + (uint64_t)kSegClasses * nbk;
+            k_seg_hist<<<nbk, tb, 0, s>>>(ng, gsl, m, nbk, hist);
+            tb_ = t_bytes;
+            PSA_CHECK(rocprim::exclusive_scan(tmp, tb_, hist, offs, 0u, (size_t)kSegClasses * nbk, rocprim::plus<uint32_t>(), s));
+            k_seg_part<<<nbk, tb, 0, s>>>(ng, gsl, m, nbk, offs, lists);
+            k_seg_bounds<<<1, 64, 0, s>>>(nbk, offs, ng, cnt + 1);
             PSA_CHECK(hipStreamSynchronize(s));
-            uint32_t c8[kSegClasses] = {};
-            PSA_CHECK(hipMemcpy(c8, cnt + 1, sizeof c8, hipMemcpyDeviceToHost));
+            uint32_t cb[kSegClasses + 1] = {};
+            PSA_CHECK(hipMemcpy(cb, cnt + 1, sizeof cb, hipMemcpyDeviceToHost));
+            uint32_t c8[kSegClasses];
+            uint32_t *lc[kSegClasses];
+            for (int c = 0; c < kSegClasses; ++c) {
+                c8[c] = cb[c + 1] - cb[c];
+                lc[c] = lists + cb[c];
+            }
             if (verbose)
                 fprintf(stderr, "psa: step %u h=%u m=%u groups=%u (<=2..64: %u %u %u %u %u %u, <=%u: %u, larger: %u)\n",
                         it, h, m, ng, c8[0], c8[1], c8[2], c8[3], c8[4], c8[5], kSegBlock, c8[6], c8[7]);
             auto grid = [&](uint32_t n, uint32_t per_wave) {
                 return std::min<uint32_t>((n + 4 * per_wave - 1) / (4 * per_wave), 1u << 16);
             };
-            if (c8[0]) k_seg_sortS<2><<<grid(c8[0], 32), 256, 0, s>>>(c8[0], lists, gsl, ng, m, keys, vals2, keys2, f2);
-            if (c8[1]) k_seg_sortS<4><<<grid(c8[1], 16), 256, 0, s>>>(c8[1], lists + half, gsl, ng, m, keys, vals2, keys2, f2);
-            if (c8[2]) k_seg_sortS<8><<<grid(c8[2], 8), 256, 0, s>>>(c8[2], lists + 2 * half, gsl, ng, m, keys, vals2, keys2, f2);
-            if (c8[3]) k_seg_sortS<16><<<grid(c8[3], 4), 256, 0, s>>>(c8[3], lists + 3 * half, gsl, ng, m, keys, vals2, keys2, f2);
-            if (c8[4]) k_seg_sortS<32><<<grid(c8[4], 2), 256, 0, s>>>(c8[4], lists + 4 * half, gsl, ng, m, keys, vals2, keys2, f2);
-            if (c8[5]) k_seg_sortS<64><<<grid(c8[5], 1), 256, 0, s>>>(c8[5], lists + 5 * half, gsl, ng, m, keys, vals2, keys2, f2);
-            if (c8[6]) k_seg_sortblk<<<c8[6], 256, 0, s>>>(lists + 6 * half, gsl, ng, m, keys, vals2, keys2, f2);
+            if (c8[0]) k_seg_sortS<2><<<grid(c8[0], 32), 256, 0, s>>>(c8[0], lc[0], gsl, ng, m, keys, vals2, keys2, f2);
+            if (c8[1]) k_seg_sortS<4><<<grid(c8[1], 16), 256, 0, s>>>(c8[1], lc[1], gsl, ng, m, keys, vals2, keys2, f2);
+            if (c8[2]) k_seg_sortS<8><<<grid(c8[2], 8), 256, 0, s>>>(c8[2], lc[2], gsl, ng, m, keys, vals2, keys2, f2);
+            if (c8[3]) k_seg_sortS<16><<<grid(c8[3], 4), 256, 0, s>>>(c8[3], lc[3], gsl, ng, m, keys, vals2, keys2, f2);
+            if (c8[4]) k_seg_sortS<32><<<grid(c8[4], 2), 256, 0, s>>>(c8[4], lc[4], gsl, ng, m, keys, vals2, keys2, f2);
+            if (c8[5]) k_seg_sortS<64><<<grid(c8[5], 1), 256, 0, s>>>(c8[5], lc[5], gsl, ng, m, keys, vals2, keys2, f2);
+            if (c8[6]) k_seg_sortblk<<<c8[6], 256, 0, s>>>(lc[6], gsl, ng, m, keys, vals2, keys2, f2);
             PSA_CHECK(hipGetLastError());
             uint32_t c3[3] = {0, 0, c8[7]};
-            uint32_t *lbig = lists + 7 * half;
+            uint32_t *lbig = lc[7];
             if (c3[2]) {
                 PSA_CHECK(hipMemsetAsync(act, 0, m, s));
                 k_seg_mark<<<c3[2], 256, 0, s>>>(lbig, gsl, ng, m, act);
@@ -783,7 +806,7 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     put(keys2, n64 * 8);
     put(vals2, n64 * 4);
     put(act, n64);
-    if (gsl) put(gsl, half * 4 * (1 + kSegClasses));
+    if (gsl) put(gsl, half * 12);
     put(tmp, t_bytes);
     PSA_CHECK(hipEventRecord(e1, s));
     // ---- nearest smaller positions in suffix-array order (min tree over sa)
