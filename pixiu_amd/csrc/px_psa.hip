@@ -319,6 +319,68 @@ __global__ void __launch_bounds__(256) k_seg_scatter(uint32_t n, const uint32_t 
     vals_out[idx[i]] = cv[i];
 }
 
+// ---------------------------------------------------------------- stream compaction
+// out = values[i] (or i itself when values is null) for every i < n with flags[i] != 0, in
+// order.  Three passes: per-tile counts, a scan over the tiles, per-tile writes.  A
+// tile is 4,096 elements (16 per thread, read as one 16-byte flag vector).
+constexpr uint32_t kCmpTile = 4096;
+PSA_DEV uint32_t nflags16(const uint8_t *f, uint32_t i, uint32_t n, uint32_t &bits) {
+    bits = 0;
+    if (i + 16 <= n) {
+        const uint4 v = *(const uint4 *)(f + i);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        for (int q = 0; q < 4; ++q)
+            for (int b = 0; b < 4; ++b)
+                if ((w[q] >> (8 * b)) & 0xffu) bits |= 1u << (4 * q + b);
+    } else {
+        for (uint32_t k = 0; k < 16 && i + k < n; ++k)
+            if (f[i + k]) bits |= 1u << k;
+    }
+    return (uint32_t)__popc(bits);
+}
+__global__ void __launch_bounds__(256) k_cmp_count(uint32_t n, const uint8_t *flags, uint32_t *tile_cnt) {
+    __shared__ uint32_t red[4];
+    const uint32_t i = blockIdx.x * kCmpTile + threadIdx.x * 16;
+    uint32_t bits;
+    uint32_t c = i < n ? nflags16(flags, i, n, bits) : 0;
+    for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+__global__ void __launch_bounds__(256) k_cmp_write(uint32_t n, const uint8_t *flags, const uint32_t *values,
+                                                   const uint32_t *tile_off, uint32_t *out) {
+    __shared__ uint32_t wsum[4];
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    const uint32_t i = blockIdx.x * kCmpTile + threadIdx.x * 16;
+    uint32_t bits = 0;
+    const uint32_t c = i < n ? nflags16(flags, i, n, bits) : 0;
+    // exclusive prefix of c over the block
+    uint32_t x = c;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+        if ((int)lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    uint32_t base = tile_off[blockIdx.x] + x - c;
+    for (uint32_t k = 0; k < wv; ++k) base += wsum[k];
+    if (!bits) return;
+    if (values && i + 16 <= n) {
+        uint32_t v[16];
+        for (int q = 0; q < 4; ++q) *(uint4 *)(v + 4 * q) = *(const uint4 *)(values + i + 4 * q);
+        for (uint32_t k = 0; k < 16; ++k)
+            if (bits >> k & 1u) out[base++] = v[k];
+    } else {
+        for (uint32_t k = 0; k < 16; ++k)
+            if (bits >> k & 1u) out[base++] = values ? values[i + k] : i + k;
+    }
+}
+
+__global__ void k_cmp_total(uint32_t nt, const uint32_t *tile_cnt, const uint32_t *tile_off, uint32_t *total) {
+    *total = nt ? tile_off[nt - 1] + tile_cnt[nt - 1] : 0;
+}
+
 // debug (PX_PSA_SEGCHECK=1): compare the segmented sort with the radix sort
 __global__ void k_seg_cmp(uint32_t m, const uint64_t *k1, const uint32_t *v1, const uint64_t *k2, const uint32_t *v2,
                           uint32_t *out) {
@@ -663,6 +725,21 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     t_sel = std::max({t_sel, t_sel2, t_sel3});
     const size_t t_bytes = std::max({t_sort, t_scan, t_sel}) + 256;
     void *tmp = get(t_bytes);
+    // stream compaction (k_cmp_*): out = the flagged values (or indices), count -> cnt[0]
+    const uint64_t n_tiles = (n64 + kCmpTile - 1) / kCmpTile + 1;
+    auto *tcnt = (uint32_t *)get(n_tiles * 8);
+    uint32_t *toff = tcnt + n_tiles;
+    auto compact = [&](const uint8_t *fl, const uint32_t *vin, uint32_t *out, uint32_t n) -> hipError_t {
+        const uint32_t nt = (n + kCmpTile - 1) / kCmpTile;
+        if (!nt) return hipMemsetAsync(cnt, 0, 4, s);
+        k_cmp_count<<<nt, 256, 0, s>>>(n, fl, tcnt);
+        size_t b = t_bytes;
+        const hipError_t e = rocprim::exclusive_scan(tmp, b, tcnt, toff, 0u, (size_t)nt, rocprim::plus<uint32_t>(), s);
+        if (e != hipSuccess) return e;
+        k_cmp_write<<<nt, 256, 0, s>>>(n, fl, vin, toff, out);
+        k_cmp_total<<<1, 1, 0, s>>>(nt, tcnt, toff, cnt);
+        return hipGetLastError();
+    };
     size_t tb_ = t_bytes;
     PSA_CHECK(rocprim::radix_sort_pairs(tmp, tb_, keys, keys2, vals, sa, (size_t)N, 0, 9 * syms + shard_bits, s));
     k_psa_head0<<<blocks(N), tb, 0, s>>>(N, keys2, sa, dist, syms, f1);
@@ -671,7 +748,7 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     k_psa_rank0<<<blocks(N), tb, 0, s>>>(N, sa, vals2, rank, act);
     tb_ = t_bytes;
     uint32_t *alist = vals;  // active suffixes, in suffix-array order
-    PSA_CHECK(rocprim::select(tmp, tb_, sa, act, alist, cnt, (size_t)N, s));
+    PSA_CHECK(compact(act, sa, alist, N));
     uint32_t m = 0;
     // (counts come back through a synchronous copy after the stream drained: no async
     // copy into pageable memory, see px_runtime.cpp d2h)
@@ -703,7 +780,7 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
             // groups are ranges of the (suffix-array ordered) keys: sort each where it lies
             k_seg_flag<<<blocks(m), tb, 0, s>>>(m, keys, act);
             tb_ = t_bytes;
-            PSA_CHECK(rocprim::select(tmp, tb_, rocprim::counting_iterator<uint32_t>(0), act, gsl, cnt, (size_t)m, s));
+            PSA_CHECK(compact(act, nullptr, gsl, m));
             PSA_CHECK(hipStreamSynchronize(s));
             uint32_t ng = 0;
             PSA_CHECK(hipMemcpy(&ng, cnt, 4, hipMemcpyDeviceToHost));
@@ -745,7 +822,7 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
                 k_seg_mark<<<c3[2], 256, 0, s>>>(lbig, gsl, ng, m, act);
                 uint32_t *tl = f1;  // free until the group-head scan below
                 tb_ = t_bytes;
-                PSA_CHECK(rocprim::select(tmp, tb_, rocprim::counting_iterator<uint32_t>(0), act, tl, cnt, (size_t)m, s));
+                PSA_CHECK(compact(act, nullptr, tl, m));
                 PSA_CHECK(hipStreamSynchronize(s));
                 uint32_t ml = 0;
                 PSA_CHECK(hipMemcpy(&ml, cnt, 4, hipMemcpyDeviceToHost));
@@ -798,7 +875,7 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         PSA_CHECK(rocprim::inclusive_scan(tmp, tb_, sfl, sfirst, (size_t)m, Max(), s));
         k_psa_rank2<<<blocks(m), tb, 0, s>>>(m, keys2, f2, vals2, sfirst, sa, rank, act);
         tb_ = t_bytes;
-        PSA_CHECK(rocprim::select(tmp, tb_, f2, act, alist, cnt, (size_t)m, s));
+        PSA_CHECK(compact(act, f2, alist, m));
         PSA_CHECK(hipStreamSynchronize(s));
         PSA_CHECK(hipMemcpy(&m, cnt, 4, hipMemcpyDeviceToHost));
     }
@@ -807,6 +884,7 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     put(vals2, n64 * 4);
     put(act, n64);
     if (gsl) put(gsl, half * 12);
+    put(tcnt, n_tiles * 8);
     put(tmp, t_bytes);
     PSA_CHECK(hipEventRecord(e1, s));
     // ---- nearest smaller positions in suffix-array order (min tree over sa)
