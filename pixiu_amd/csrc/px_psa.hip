@@ -440,8 +440,20 @@ PSA_DEV uint32_t tree_find(const MinTree &t, uint32_t i, uint32_t v, int dir) {
 
 // psv / nsv: for the suffix at rank r, the nearest rank to its left / right (inside its
 // shard's range) whose position is smaller; written per position
-__global__ void __launch_bounds__(256) k_psa_ansv(uint32_t N, MinTree t, const uint32_t *pdoc, const PsaDoc *docs,
-                                                  const PsaShard *shards, uint32_t *psvp, uint32_t *nsvp) {
+// the shard whose range holds suffix-array index r (shards are contiguous and in order in
+// both position and rank space)
+PSA_DEV uint32_t shard_of_rank(const PsaShard *shards, uint32_t nshards, uint32_t r) {
+    uint32_t a = 0, b = nshards;  // shards[a].base <= r < shards[b].base
+    while (b - a > 1) {
+        const uint32_t c = (a + b) >> 1;
+        if (shards[c].base <= r) a = c;
+        else b = c;
+    }
+    return a;
+}
+
+__global__ void __launch_bounds__(256) k_psa_ansv(uint32_t N, MinTree t, const PsaShard *shards, uint32_t nshards,
+                                                  uint32_t *psvp, uint32_t *nsvp) {
     const uint32_t lane = lane_id();
     const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (w * 64 >= N) return;
@@ -449,9 +461,13 @@ __global__ void __launch_bounds__(256) k_psa_ansv(uint32_t N, MinTree t, const u
     const uint32_t r = w * 64 + lane;
     const bool live = r < N;
     const uint32_t v = live ? sa[r] : kNoPos;
-    uint32_t lo = 0, hi = 0;
-    if (live) {
-        const PsaShard sh = shards[docs[pdoc[v]].shard];
+    // this block of 64 ranks lies in one shard unless it straddles a boundary
+    const uint32_t r0 = w * 64, r1 = min(N, r0 + 64) - 1;
+    const uint32_t s0 = shard_of_rank(shards, nshards, __builtin_amdgcn_readfirstlane(r0));
+    const PsaShard sh0 = shards[s0];
+    uint32_t lo = sh0.base, hi = sh0.base + sh0.len;
+    if (r1 >= hi && live && r >= hi) {
+        const PsaShard sh = shards[shard_of_rank(shards, nshards, r)];
         lo = sh.base;
         hi = sh.base + sh.len;
     }
@@ -682,7 +698,6 @@ struct Max {
 hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDoc *docs, uint32_t nshards,
                    const PsaShard *shards, uint32_t N, uint32_t *rec_chunk, uint32_t *rec_idx, uint32_t *rec_status,
                    uint32_t *shard_flag, PsaStats *st) {
-    (void)nshards;
     if (!N || !ndocs) return hipSuccess;
     auto get = [&](uint64_t n) { return A.alloc(A.self, n); };
     auto put = [&](void *p, uint64_t n) { A.release(A.self, p, n); };
@@ -905,7 +920,7 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         ++t.levels;
     }
     uint32_t *psvp = f1, *nsvp = f2;
-    k_psa_ansv<<<(uint32_t)((n64 + 255) / 256), 256, 0, s>>>(N, t, pdoc, docs, shards, psvp, nsvp);
+    k_psa_ansv<<<(uint32_t)((n64 + 255) / 256), 256, 0, s>>>(N, t, shards, nshards, psvp, nsvp);
     auto *lcp_p = (uint16_t *)rank;  // ranks are no longer needed: two u16 arrays in their place
     auto *lcp_n = (uint16_t *)get(n64 * 2);
     k_psa_lce<<<blocks((n64 + kLceSpan - 1) / kLceSpan), tb, 0, s>>>(N, (const uint64_t *)G, dist, psvp, nsvp, lcp_p,

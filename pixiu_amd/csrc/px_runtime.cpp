@@ -1445,6 +1445,32 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             return rc;
         }
     }
+    struct PhaseClock {  // PX_SET_VERBOSE=1: host wall time per set-batch phase on stderr
+        bool on = false;
+        std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), t = t0;
+        std::string out;
+        const char *cur = "setup";
+        void mark(const char *next) {  // closes the running phase, starts `next`
+            if (!on) return;
+            const auto now = std::chrono::steady_clock::now();
+            char b[128];
+            snprintf(b, sizeof b, "\n  %8.2f ms  %s", std::chrono::duration<double, std::milli>(now - t).count(), cur);
+            out += b;
+            t = now;
+            cur = next;
+        }
+        ~PhaseClock() {
+            if (!on) return;
+            mark("");
+            fprintf(stderr, "set_batch:%s\n  %8.2f ms  total\n", out.c_str(),
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+        }
+    } phase;
+    {
+        const char *v = std::getenv("PX_SET_VERBOSE");
+        phase.on = v && *v == '1';
+    }
+    phase.mark("inputs on device; raw keys also on host ");
     // ---- inputs on device; raw keys also on host (the CritBit needs them)
     std::vector<uint64_t> hkoff(n + 1), hvoff(n + 1);
     const uint8_t *dkeys, *dvals;
@@ -1491,6 +1517,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         dvoff = dvo;
     }
 
+    phase.mark("pass 1: escaped doc lengths");
     // ---- pass 1: escaped doc lengths
     auto *tmp = (uint32_t *)tmp_buf.get((uint64_t)n * 28 + 64);
     uint32_t *d_doclen = tmp, *d_complen = tmp + n, *d_chunk = tmp + 2 * n, *d_idx = tmp + 3 * n,
@@ -1501,6 +1528,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     d2h(doc_len.data(), d_doclen, n * 4);
     sync();
 
+    phase.mark("shard assignment: contiguous, in arrival");
     // ---- shard assignment: contiguous, in arrival order
     std::vector<uint32_t> rec_shard(n);
     struct Work {
@@ -1533,6 +1561,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             return PX_ECAPACITY;
         }
 
+    phase.mark("which shards take the suffix-array path ");
     // ---- which shards take the suffix-array path (px_psa.hip)
     // A live chunk is encoded by PSA while it provably cannot rotate (<= 65,535 docs and
     // <= kPsaMaxText doc bytes): its suffix tree is then never built.  A live chunk that
@@ -1560,6 +1589,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
                   live_text + w.bytes <= kPsaMaxText;
     }
 
+    phase.mark("arenas, doc destinations, comp scratch");
     // ---- arenas, doc destinations, comp scratch
     std::vector<uint8_t *> dst(n, nullptr), cdst(n, nullptr);
     uint64_t scratch_bytes = 0;
@@ -1591,6 +1621,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     flush_shard_init();
     hcheck(launch_doc_write(stream, n, dkeys, dkoff, raw_docs ? nullptr : dvals, dvoff, d_dst));
 
+    phase.mark("the suffix-array path over the PSA shard");
     // ---- the suffix-array path over the PSA shards (messages, placement, check flags)
     hcheck(hipEventRecord(ev0, stream));
     uint32_t psa_shards = 0, walk_shards = 0;
@@ -1661,6 +1692,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         }
     }
 
+    phase.mark("the GST walk for the other shards (encod");
     // ---- the GST walk for the other shards (encoder messages)
     std::vector<GstShard> gs;
     std::vector<size_t> gwork;
@@ -1754,6 +1786,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         stats.last_emit_kernel_ms = ms;
     }
 
+    phase.mark("packed store + segment index");
     // ---- packed store + segment index
     // Every record the walk placed gets its bytes stored and its slot registered, even
     // if it failed later (emit / tokenize / the check above): later records of its
@@ -1811,6 +1844,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     heap.release(d_coff, (uint64_t)n * 8);
     heap.release(d_slots, (uint64_t)n * sizeof(RecSlot));
 
+    phase.mark("register records in their chunks");
     // ---- register records in their chunks
     std::vector<uint32_t> rgchunk(n, kNone);  // chunk of every placed record
     std::vector<uint8_t> live(n, 0);          // placed, OK and indexed
@@ -1880,6 +1914,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         link(jobs);
     }
 
+    phase.mark("compat key prefixes (GPU decode of each ");
     // ---- compat key prefixes (GPU decode of each new record's key region)
     {
         std::vector<KpJob> jobs;
@@ -1903,6 +1938,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             }
     }
 
+    phase.mark("span tables of the new records (full-ran");
     // ---- span tables of the new records (full-range getitem as a gather)
     {
         std::vector<SpanReq> reqs;
@@ -1913,6 +1949,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         stats.last_span_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts).count();
     }
 
+    phase.mark("CritBit inserts: every shard's own recor");
     // ---- CritBit inserts: every shard's own records in arrival order, shards on host
     // threads (their tries are independent); then a key that moved to a newer shard is
     // deleted from its older one, in record order (a shard's records all precede a newer
@@ -1964,6 +2001,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     for (auto &b : deferred_release) heap.release(b.first, b.second);
     deferred_release.clear();
 
+    phase.mark("results");
     // ---- results
     int rc = corrupt;
     uint64_t ub = 0;
