@@ -1200,7 +1200,7 @@ struct px_ctx {
         };
         const uint32_t head = std::max<uint32_t>(1024, (uint32_t)((uint64_t)n * opts_head_frac() / 64));
         auto t0 = clk::now();
-        resolve(0, head);
+        parallel_ranges(head, host_threads(), [&](uint32_t lo, uint32_t hi) { resolve(lo, hi); });
         place(0, head);
         double head_ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
         if (total > out_cap) {  // cannot launch the head: plain path (reports PX_ESPACE)
