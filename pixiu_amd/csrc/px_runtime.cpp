@@ -10,6 +10,9 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -262,22 +265,96 @@ class KeyMap {
     }
 };
 
+// Persistent host workers (created once per process): spawning threads per call cost
+// more than a 10k-key lookup batch itself.  run(n, f) calls f(0..n-1) on the workers
+// and the caller, and returns when every call has returned.
+class WorkerPool {
+  public:
+    static WorkerPool &get() {
+        static WorkerPool pool(std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1);
+        return pool;
+    }
+    uint32_t size() const { return (uint32_t)workers_.size() + 1; }
+    void run(uint32_t ntask, const std::function<void(uint32_t)> &f) {
+        std::lock_guard<std::mutex> one(run_mu_);  // one job at a time (callers from several threads)
+        std::unique_lock<std::mutex> lk(m_);
+        busy_.wait(lk, [&] { return active_ == 0; });  // no worker still holds the last job
+        fn_ = &f;
+        ntask_ = ntask;
+        next_.store(0);
+        done_ = 0;
+        ++gen_;
+        lk.unlock();
+        work_.notify_all();
+        uint32_t mine = 0;
+        for (uint32_t t; (t = next_.fetch_add(1)) < ntask;) {
+            f(t);
+            ++mine;
+        }
+        lk.lock();
+        done_ += mine;
+        busy_.wait(lk, [&] { return done_ == ntask_ && active_ == 0; });
+    }
+    ~WorkerPool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            quit_ = true;
+        }
+        work_.notify_all();
+        for (auto &t : workers_) t.join();
+    }
+
+  private:
+    explicit WorkerPool(uint32_t n) {
+        for (uint32_t i = 0; i < n; ++i) workers_.emplace_back([this] { loop(); });
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            std::unique_lock<std::mutex> lk(m_);
+            work_.wait(lk, [&] { return quit_ || gen_ != seen; });
+            if (quit_) return;
+            seen = gen_;
+            ++active_;
+            const std::function<void(uint32_t)> *f = fn_;
+            const uint32_t nt = ntask_;
+            lk.unlock();
+            uint32_t mine = 0;
+            for (uint32_t t; (t = next_.fetch_add(1)) < nt;) {
+                (*f)(t);
+                ++mine;
+            }
+            lk.lock();
+            done_ += mine;
+            --active_;
+            busy_.notify_all();
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex m_, run_mu_;
+    std::condition_variable work_, busy_;
+    const std::function<void(uint32_t)> *fn_ = nullptr;
+    uint32_t ntask_ = 0, done_ = 0, active_ = 0;
+    std::atomic<uint32_t> next_{0};
+    uint64_t gen_ = 0;
+    bool quit_ = false;
+};
+
 // fn(lo, hi) over [0, n) on up to `threads` host threads (inline for small n)
 template <class F>
 void parallel_ranges(uint32_t n, uint32_t threads, F fn) {
-    if (threads <= 1 || n < 4096) {
+    if (threads <= 1 || n < 2048) {
         fn(0u, n);
         return;
     }
-    threads = std::min<uint32_t>(threads, n / 1024);
-    std::vector<std::thread> pool;
-    const uint32_t per = (n + threads - 1) / threads;
-    for (uint32_t t = 1; t < threads; ++t) {
+    threads = std::min<uint32_t>({threads, WorkerPool::get().size(), n / 512});
+    const uint32_t tasks = threads * 4;  // a few ranges per thread: uneven keys balance out
+    const uint32_t per = (n + tasks - 1) / tasks;
+    const std::function<void(uint32_t)> job = [&](uint32_t t) {
         const uint32_t lo = t * per, hi = std::min(n, lo + per);
-        if (lo < hi) pool.emplace_back([=] { fn(lo, hi); });
-    }
-    fn(0u, std::min(n, per));
-    for (auto &th : pool) th.join();
+        if (lo < hi) fn(lo, hi);
+    };
+    WorkerPool::get().run(tasks, job);
 }
 
 // ---------------------------------------------------------------- crit-bit index
@@ -1984,13 +2061,8 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     if (nthr <= 1 || n < 2048) {
         for (size_t k = 0; k < work.size(); ++k) insert_work(k);
     } else {
-        std::atomic<size_t> next{0};
-        std::vector<std::thread> pool;
-        for (uint32_t t = 0; t < nthr; ++t)
-            pool.emplace_back([&] {
-                for (size_t k; (k = next.fetch_add(1)) < work.size();) insert_work(k);
-            });
-        for (auto &th : pool) th.join();
+        const std::function<void(uint32_t)> job = [&](uint32_t k) { insert_work(k); };
+        WorkerPool::get().run((uint32_t)work.size(), job);
     }
     for (const auto &mv : moved) {  // cross-shard replace
         const uint32_t r = mv.first;
