@@ -50,7 +50,8 @@ hipError_t launch_rehash(hipStream_t, const uint4 *, uint32_t, uint32_t, uint4 *
 hipError_t launch_decode_addr(hipStream_t, const DecodeQuery *, uint32_t, const RecSlot *const *, int32_t *,
                               uint32_t *, uint32_t *, Frame *, uint32_t, uint32_t);
 hipError_t launch_span_build(hipStream_t, uint32_t, const SpanJob *);
-hipError_t launch_gather(hipStream_t, uint32_t, const GatherQuery *, uint8_t *, uint32_t *, uint32_t *, bool);
+hipError_t launch_gather(hipStream_t, uint32_t, const uint2 *, const GatherQuery *, uint8_t *, uint32_t *, uint32_t *,
+                         bool);
 int debug_trace_take(int32_t *, uint32_t);
 int debug_prof_take(unsigned long long *, uint32_t);
 }  // namespace px
@@ -195,6 +196,7 @@ class KeyMap {
     struct Slot {
         uint64_t h, off;
         uint32_t len, shard;  // len == kFree: empty
+        uint32_t chunk, idx;  // the record last stored under the key (a hint: verified on use)
     };
     static constexpr uint32_t kFree = ~0u;
     std::vector<Slot> tab_;
@@ -216,7 +218,7 @@ class KeyMap {
         }
     }
     void grow() {
-        std::vector<Slot> old(std::max<size_t>(tab_.size() * 2, 1024), Slot{0, 0, kFree, 0});
+        std::vector<Slot> old(std::max<size_t>(tab_.size() * 2, 1024), Slot{0, 0, kFree, 0, ~0u, 0});
         old.swap(tab_);
         const size_t m = tab_.size() - 1;
         for (const Slot &e : old)
@@ -246,22 +248,62 @@ class KeyMap {
         const Slot &e = tab_[probe(hash(k, n), k, n)];
         return e.len == kFree ? -1 : (int64_t)e.shard;
     }
-    void put(const uint8_t *k, size_t n, uint32_t shard) {
+    // shard and record hint of k; false when k was never stored
+    bool find_hint(const uint8_t *k, size_t n, uint32_t *shard, uint32_t *chunk, uint32_t *idx) const {
+        if (tab_.empty()) return false;
+        const Slot &e = tab_[probe(hash(k, n), k, n)];
+        if (e.len == kFree) return false;
+        *shard = e.shard;
+        *chunk = e.chunk;
+        *idx = e.idx;
+        return true;
+    }
+    void put(const uint8_t *k, size_t n, uint32_t shard, uint32_t chunk = ~0u, uint32_t idx = 0) {
         if ((n_ + 1) * 2 > tab_.size()) grow();
         const uint64_t h = hash(k, n);
         Slot &e = tab_[probe(h, k, n)];
         if (e.len == kFree) {
-            e = Slot{h, bytes_.size(), (uint32_t)n, shard};
+            e = Slot{h, bytes_.size(), (uint32_t)n, shard, chunk, idx};
             bytes_.insert(bytes_.end(), k, k + n);
             ++n_;
         } else {
             e.shard = shard;
+            e.chunk = chunk;
+            e.idx = idx;
         }
     }
     void clear() {
         tab_.clear();
         bytes_.clear();
         n_ = 0;
+    }
+};
+
+// host wall time per phase of one call, printed on stderr when `env` is 1
+struct PhaseClock {
+    bool on = false;
+    const char *name;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), t = t0;
+    std::string out;
+    const char *cur = "setup";
+    PhaseClock(const char *nm, const char *env) : name(nm) {
+        const char *v = std::getenv(env);
+        on = v && *v == '1';
+    }
+    void mark(const char *next) {  // closes the running phase, starts `next`
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        char b[128];
+        snprintf(b, sizeof b, "\n  %8.2f ms  %s", std::chrono::duration<double, std::milli>(now - t).count(), cur);
+        out += b;
+        t = now;
+        cur = next;
+    }
+    ~PhaseClock() {
+        if (!on) return;
+        mark("");
+        fprintf(stderr, "%s:%s\n  %8.2f ms  total\n", name, out.c_str(),
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     }
 };
 
@@ -862,25 +904,28 @@ struct px_ctx {
     }
 
     // CritBitTree::getitem's key_eq (PiXiuStr.cpp:129-143)
-    bool cbt_lookup(const Shard &s, const std::string &q, Leaf *out) const {
-        if (!s.has_root) return false;
-        Best b = best_match(s, q);
+    // PXSGen_key_eq on the stored compat key prefix: equal through the key terminator
+    bool kp_matches(const Leaf &l, const std::string &q) const {
         uint32_t clen;
-        const uint8_t *crit = kp_of(b.crit, &clen);
+        const uint8_t *crit = kp_of(l, &clen);
         bool spec = false;
         for (size_t k = 0; k < clen && k < q.size() && crit[k] == (uint8_t)q[k]; ++k) {
             uint8_t v = crit[k];
             if (!spec && v == kEsc) {
                 spec = true;
             } else if (spec) {
-                if (v == kKeyEnd) {
-                    *out = b.crit;
-                    return true;
-                }
+                if (v == kKeyEnd) return true;
                 spec = false;
             }
         }
         return false;
+    }
+    bool cbt_lookup(const Shard &s, const std::string &q, Leaf *out) const {
+        if (!s.has_root) return false;
+        Best b = best_match(s, q);
+        if (!kp_matches(b.crit, q)) return false;
+        *out = b.crit;
+        return true;
     }
 
     // CritBitTree::contains (CritBitTree.cpp:154-178): crit stream vs the escaped key bytes
@@ -1053,12 +1098,34 @@ struct px_ctx {
         return g;
     }
     // after the k_decode launch on the same stream (its skipped-query results are overwritten)
+    // tasks: one query, or consecutive queries of 1..64 spans each with <= 64 spans in all
+    // (one wave serves them together: small records leave most lanes idle otherwise)
     void launch_gathers(hipStream_t st, const std::vector<GatherQuery> &g, uint8_t *out, uint32_t *dl, uint32_t *ds,
                         GatherQuery *&dbuf) {
         if (g.empty()) return;
-        dbuf = (GatherQuery *)heap.alloc(g.size() * sizeof(GatherQuery));
+        std::vector<uint2> tasks;
+        tasks.reserve(g.size());
+        for (uint32_t i = 0; i < (uint32_t)g.size();) {
+            uint32_t j = i, tot = 0;
+            while (j < g.size() && j - i < 64 && g[j].nspan >= 1 && tot + g[j].nspan <= 64) tot += g[j++].nspan;
+            if (j == i) j = i + 1;  // a large (or empty) one alone
+            tasks.push_back(make_uint2(i, j - i));
+            i = j;
+        }
+        const uint64_t qb = round_up(g.size() * sizeof(GatherQuery), 64);
+        dbuf = (GatherQuery *)heap.alloc(qb + tasks.size() * sizeof(uint2));
+        auto *dt = (uint2 *)((uint8_t *)dbuf + qb);
         hcheck(hipMemcpyAsync(dbuf, g.data(), g.size() * sizeof(GatherQuery), hipMemcpyHostToDevice, st));
-        hcheck(launch_gather(st, (uint32_t)g.size(), dbuf, out, dl, ds, true));
+        hcheck(hipMemcpyAsync(dt, tasks.data(), tasks.size() * sizeof(uint2), hipMemcpyHostToDevice, st));
+        hcheck(launch_gather(st, (uint32_t)tasks.size(), dt, dbuf, out, dl, ds, true));
+        gather_bytes[dbuf] = qb + tasks.size() * sizeof(uint2);
+    }
+    std::map<void *, uint64_t> gather_bytes;  // launch_gathers' device buffers -> their sizes
+    void release_gathers(GatherQuery *d) {
+        if (!d) return;
+        auto it = gather_bytes.find(d);
+        heap.release(d, it->second);
+        gather_bytes.erase(it);
     }
 
     // Runs decode queries; out_dev is a device buffer.  Returns per-query len/status.
@@ -1098,7 +1165,10 @@ struct px_ctx {
         std::vector<GatherQuery> gq;
         if (timed && !addr) gq = take_gathers(qn, 0, nq, 0);
         stats.last_gather_queries = timed ? (uint32_t)gq.size() : stats.last_gather_queries;
-        hcheck(hipMemcpyAsync(dq, qn, (size_t)nq * sizeof(DecodeQuery), hipMemcpyHostToDevice, stream));
+        // every found key gathered: no walk launch (the host answers the missing keys)
+        bool walk = false;
+        for (uint32_t j = 0; j < nq && !walk; ++j) walk = qn[j].chunk != kNone;
+        if (walk) hcheck(hipMemcpyAsync(dq, qn, (size_t)nq * sizeof(DecodeQuery), hipMemcpyHostToDevice, stream));
         flush_tab();
         if (timed) hcheck(hipEventRecord(ev0, stream));
         // timed == a getitem batch (k_decode); otherwise stored-key prefixes (k_decode_keys)
@@ -1106,19 +1176,21 @@ struct px_ctx {
             const char *e = std::getenv("PX_DEC_XCD");
             return !(e && e[0] == '0');
         }();
-        if (addr)
+        if (!walk) {
+        } else if (addr) {
             hcheck(launch_decode_addr(stream, dq, nq, (const RecSlot *const *)chunk_tab, addr, dl, ds, frames, depth,
                                       waves | (xcd ? 0x80000000u : 0u)));
-        else
+        } else {
             hcheck(launch_decode(stream, dq, nq, (const RecSlot *const *)chunk_tab, out_dev, dl, ds, frames, depth,
                                  waves | (xcd ? 0x80000000u : 0u), !timed));
+        }
         GatherQuery *dgq = nullptr;
         launch_gathers(stream, gq, out_dev, dl, ds, dgq);
         if (timed) hcheck(hipEventRecord(ev1, stream));
         auto *hr = (uint32_t *)hres_buf.get((uint64_t)nq * 8);
         hcheck(hipMemcpyAsync(hr, dl, (size_t)nq * 8, hipMemcpyDeviceToHost, stream));  // lengths, then statuses
         sync();
-        if (dgq) heap.release(dgq, gq.size() * sizeof(GatherQuery));
+        release_gathers(dgq);
         if (timed) {
             float ms = 0;
             hcheck(hipEventElapsedTime(&ms, ev0, ev1));
@@ -1228,10 +1300,28 @@ struct px_ctx {
     // key -> decode query (CritBit lookup, CritBitTree.cpp:13-40); pre = PX_ENOTFOUND when absent
     void resolve_key(const uint8_t *k, uint64_t kn, int mode, std::string &ek, DecodeQuery &q, uint32_t &pre) const {
         esc_key_into(ek, k, kn);
-        const Shard *s = shard_for_key(k, kn);
-        Leaf l;
         q = DecodeQuery{kNone, 0, 0, kMaxDoc, 0, 0, (uint32_t)mode};
         pre = PX_OK;
+        const Shard *s = nullptr;
+        if (opts.records_per_shard != 0) {
+            // the key map's record hint: a live record whose stored key equals the query
+            // is the one the CritBit walk would reach (a trie holds one live leaf per key)
+            uint32_t sh, c, i;
+            if (!keymap.find_hint(k, kn, &sh, &c, &i)) {
+                pre = PX_ENOTFOUND;
+                return;
+            }
+            if (c < chunks.size() && i < chunks[c].n && !chunks[c].dead[i] && kp_matches(Leaf{c, i}, ek)) {
+                q.chunk = c;
+                q.idx = i;
+                q.out_cap = (uint32_t)round_up(chunks[c].doc_len[i] + 64, 16);
+                return;
+            }
+            s = shards[sh].get();
+        } else {
+            s = shard_for_key(k, kn);
+        }
+        Leaf l;
         if (!s || !cbt_lookup(*s, ek, &l)) {
             pre = PX_ENOTFOUND;
             return;
@@ -1276,6 +1366,8 @@ struct px_ctx {
             }
         };
         const uint32_t head = std::max<uint32_t>(1024, (uint32_t)((uint64_t)n * opts_head_frac() / 64));
+        PhaseClock phase("get_overlapped", "PX_GET_VERBOSE");
+        phase.mark("head lookups");
         auto t0 = clk::now();
         parallel_ranges(head, host_threads(), [&](uint32_t lo, uint32_t hi) { resolve(lo, hi); });
         place(0, head);
@@ -1294,15 +1386,24 @@ struct px_ctx {
         auto *qn = (DecodeQuery *)hq_buf.get((uint64_t)n * sizeof(DecodeQuery));
         auto *hr = (uint32_t *)hres_buf.get((uint64_t)n * 8);
         std::memcpy(qn, q.data(), (size_t)head * sizeof(DecodeQuery));
+        phase.mark("head gathers + launch");
         const std::vector<GatherQuery> g1 = take_gathers(qn, 0, head, 0);
-        hcheck(hipMemcpyAsync(dq, qn, (size_t)head * sizeof(DecodeQuery), hipMemcpyHostToDevice, stream));
+        auto any_walk = [&](uint32_t lo, uint32_t hi) {
+            for (uint32_t j = lo; j < hi; ++j)
+                if (qn[j].chunk != kNone) return true;
+            return false;
+        };
+        const bool walk1 = any_walk(0, head);
+        if (walk1) hcheck(hipMemcpyAsync(dq, qn, (size_t)head * sizeof(DecodeQuery), hipMemcpyHostToDevice, stream));
         flush_tab();
         hcheck(hipEventRecord(ev0, stream));
-        hcheck(launch_decode(stream, dq, head, (const RecSlot *const *)chunk_tab, out, dl, ds, frames, depth,
-                             w1 | 0x80000000u, false));
+        if (walk1)
+            hcheck(launch_decode(stream, dq, head, (const RecSlot *const *)chunk_tab, out, dl, ds, frames, depth,
+                                 w1 | 0x80000000u, false));
         GatherQuery *dg1 = nullptr, *dg2 = nullptr;
         launch_gathers(stream, g1, out, dl, ds, dg1);
         // the tail: resolved while the head decodes
+        phase.mark("tail lookups");
         auto t1 = clk::now();
         parallel_ranges(n - head, host_threads(), [&](uint32_t lo, uint32_t hi) { resolve(head + lo, head + hi); });
         place(head, n);
@@ -1310,24 +1411,30 @@ struct px_ctx {
         if (needed) *needed = total;
         if (total > out_cap) {
             sync();
+            release_gathers(dg1);
             return PX_ESPACE;
         }
+        phase.mark("tail gathers + launch");
         std::memcpy(qn + head, q.data() + head, (size_t)(n - head) * sizeof(DecodeQuery));
         const std::vector<GatherQuery> g2 = take_gathers(qn, head, n, 0);
         stats.last_gather_queries = (uint32_t)(g1.size() + g2.size());
         hcheck(hipStreamWaitEvent(stream2, ev0, 0));  // chunk table and head queries uploaded
-        hcheck(hipMemcpyAsync(dq + head, qn + head, (size_t)(n - head) * sizeof(DecodeQuery), hipMemcpyHostToDevice,
-                              stream2));
-        hcheck(launch_decode(stream2, dq + head, n - head, (const RecSlot *const *)chunk_tab, out, dl + head,
-                             ds + head, frames + (uint64_t)w1 * depth, depth, w2 | 0x80000000u, false));
+        if (any_walk(head, n)) {
+            hcheck(hipMemcpyAsync(dq + head, qn + head, (size_t)(n - head) * sizeof(DecodeQuery),
+                                  hipMemcpyHostToDevice, stream2));
+            hcheck(launch_decode(stream2, dq + head, n - head, (const RecSlot *const *)chunk_tab, out, dl + head,
+                                 ds + head, frames + (uint64_t)w1 * depth, depth, w2 | 0x80000000u, false));
+        }
         launch_gathers(stream2, g2, out, dl + head, ds + head, dg2);
         hcheck(hipEventRecord(ev_join, stream2));
         hcheck(hipStreamWaitEvent(stream, ev_join, 0));
         hcheck(hipEventRecord(ev1, stream));
+        phase.mark("sync");
         hcheck(hipMemcpyAsync(hr, dl, (size_t)n * 8, hipMemcpyDeviceToHost, stream));  // lengths, then statuses
         sync();
-        if (dg1) heap.release(dg1, g1.size() * sizeof(GatherQuery));
-        if (dg2) heap.release(dg2, g2.size() * sizeof(GatherQuery));
+        phase.mark("results");
+        release_gathers(dg1);
+        release_gathers(dg2);
         float ms = 0;
         hcheck(hipEventElapsedTime(&ms, ev0, ev1));
         stats.last_decode_kernel_ms = ms;
@@ -1522,31 +1629,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             return rc;
         }
     }
-    struct PhaseClock {  // PX_SET_VERBOSE=1: host wall time per set-batch phase on stderr
-        bool on = false;
-        std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), t = t0;
-        std::string out;
-        const char *cur = "setup";
-        void mark(const char *next) {  // closes the running phase, starts `next`
-            if (!on) return;
-            const auto now = std::chrono::steady_clock::now();
-            char b[128];
-            snprintf(b, sizeof b, "\n  %8.2f ms  %s", std::chrono::duration<double, std::milli>(now - t).count(), cur);
-            out += b;
-            t = now;
-            cur = next;
-        }
-        ~PhaseClock() {
-            if (!on) return;
-            mark("");
-            fprintf(stderr, "set_batch:%s\n  %8.2f ms  total\n", out.c_str(),
-                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
-        }
-    } phase;
-    {
-        const char *v = std::getenv("PX_SET_VERBOSE");
-        phase.on = v && *v == '1';
-    }
+    PhaseClock phase("set_batch", "PX_SET_VERBOSE");
     phase.mark("inputs on device; raw keys also on host ");
     // ---- inputs on device; raw keys also on host (the CritBit needs them)
     std::vector<uint64_t> hkoff(n + 1), hvoff(n + 1);
@@ -2040,7 +2123,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             const uint64_t klen = hkoff[r + 1] - hkoff[r];
             const int64_t prev = keymap.find(kp, klen);
             if (prev >= 0 && (uint32_t)prev != rec_shard[r]) moved.emplace_back(r, (uint32_t)prev);
-            keymap.put(kp, klen, rec_shard[r]);
+            keymap.put(kp, klen, rec_shard[r], rgchunk[r], ridx[r]);
         }
     auto insert_work = [&](size_t k) {
         const Work &w = work[k];
@@ -2636,7 +2719,7 @@ int px_ctx::load(const uint8_t *src, uint64_t len, int src_on_device, uint32_t *
             const auto *rk = reinterpret_cast<const uint8_t *>(raw.data());
             const int64_t prev = keymap.find(rk, raw.size());
             if (prev >= 0 && (uint32_t)prev != s.id) cbt_delete(*shards[(size_t)prev], q);
-            keymap.put(rk, raw.size(), s.id);
+            keymap.put(rk, raw.size(), s.id, jobs[j].chunk, k);
         }
         if (cbt_insert(s, q, Leaf{jobs[j].chunk, k})) {
             // a duplicate key inside the blob: the later record replaced the earlier
