@@ -121,3 +121,26 @@ def test_psa_slot_full_chunk_then_next_batch(store_factory, oracle):
     oc, ochunk, oidx = oracle.encode_docs([assemble(cp.key(i), cp.val(i)) for i in range(cp.n)])
     assert r["chunk"].tolist() == ochunk and r["idx"].tolist() == oidx
     assert st.export(px.records_of(r)) == oc
+
+
+@pytest.mark.parametrize("cfg,n,rps", [(3, 128, 64), (5, 64, 32), (2, 4000, 1000)])
+def test_segmented_sort_equals_radix(cfg, n, rps, store_factory):
+    """The in-place segmented doubling sort (default) and the all-radix sort
+    (PX_PSA_SEGSORT=0) give the same suffix array, hence the same bytes."""
+    from pixiu_amd import synth
+    cp = synth.make(cfg, n)
+    out = []
+    for seg in ("1", "0"):
+        old = os.environ.get("PX_PSA_SEGSORT")
+        os.environ["PX_PSA_SEGSORT"] = seg
+        try:
+            st = store_factory(records_per_shard=rps)
+            r = st.set_batch((cp.keys, cp.koff.astype(np.uint64)), (cp.vals, cp.voff.astype(np.uint64)))
+            assert int(r["status"].max()) == 0 and st.stats()["last_psa_shards"] >= 1
+            out.append(st.export(px.records_of(r)))
+        finally:
+            if old is None:
+                os.environ.pop("PX_PSA_SEGSORT", None)
+            else:
+                os.environ["PX_PSA_SEGSORT"] = old
+    assert out[0] == out[1]
