@@ -2182,33 +2182,37 @@ __global__ void __launch_bounds__(256) k_span_build(uint32_t n, const SpanJob *j
     }
 }
 
-// Gather: one wave per query; lane l takes span k0 + l.  Spans up to kLaneCopyMax are
-// copied by their lane, longer ones by the whole wave.  Output stops at the query's cap.
-__global__ void __launch_bounds__(256) k_gather(uint32_t nq, const GatherQuery *qs, uint8_t *out_,
-                                                uint32_t *out_len, uint32_t *status, uint32_t remap) {
+// Gather: one wave per task.  A task is one query (lane l takes span k0 + l, 64 spans a
+// step), or several consecutive queries whose spans total <= 64 (small records: one
+// span per lane, each lane finds its query from the queries' span offsets).  Spans up
+// to kLaneCopyMax bytes are copied by their lane, longer ones by the whole wave.
+// Output stops at each query's cap.
+PX_DEV void gather_one(const GatherQuery &q0, uint8_t *out_, uint32_t *out_len, uint32_t *status) {
     const uint32_t lane = lane_id();
-    uint32_t lb = blockIdx.x;
-    if (remap) {  // XCD-aware order, as k_decode
-        const uint32_t nb = gridDim.x, x = blockIdx.x & 7u, per = nb >> 3, rem = nb & 7u;
-        lb = x * per + min(x, rem) + (blockIdx.x >> 3);
-    }
-    const uint32_t qi = lb * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (qi >= nq) return;
-    const GatherQuery q = qs[qi];
-    const PX_GAS SpanEnt *sp = (const PX_GAS SpanEnt *)uni64((uint64_t)q.span);
-    const PX_GAS uint8_t *base = (const PX_GAS uint8_t *)uni64((uint64_t)q.base);
-    PX_GAS uint8_t *o = (PX_GAS uint8_t *)out_ + uni64(q.out_off);
-    const uint32_t nspan = uni(q.nspan), cap = uni(q.cap), len = uni(q.len);
-    for (uint32_t k0 = 0; k0 < nspan; k0 += 64) {
-        const uint32_t k = k0 + lane;
-        uint32_t st = 0, en = 0;
-        int32_t rel = 0;
+    const PX_GAS SpanEnt *sp = (const PX_GAS SpanEnt *)uni64((uint64_t)q0.span);
+    const PX_GAS uint8_t *base = (const PX_GAS uint8_t *)uni64((uint64_t)q0.base);
+    PX_GAS uint8_t *o = (PX_GAS uint8_t *)out_ + uni64(q0.out_off);
+    const uint32_t nspan = uni(q0.nspan), cap = uni(q0.cap), len = uni(q0.len);
+    // the next step's entries are loaded before this step's copies (one round trip per
+    // step instead of two)
+    auto load_ent = [&](uint32_t k, int32_t &rel, uint32_t &st, uint32_t &en) {
+        rel = 0;
+        st = en = 0;
         if (k < nspan) {
             const PX_GAS uint32_t *e = (const PX_GAS uint32_t *)(sp + k);
             rel = (int32_t)e[0];
             st = e[1];
-            en = ((const PX_GAS uint32_t *)(sp + k + 1))[1];
+            en = e[3];  // the next entry's start (the table ends with a sentinel)
         }
+    };
+    int32_t nrel;
+    uint32_t nst, nen;
+    load_ent(lane, nrel, nst, nen);
+    for (uint32_t k0 = 0; k0 < nspan; k0 += 64) {
+        const int32_t rel = nrel;
+        const uint32_t st = nst;
+        uint32_t en = nen;
+        if (k0 + 64 < nspan) load_ent(k0 + 64 + lane, nrel, nst, nen);
         if (uni(st) >= cap) break;  // spans are in output order: lane 0's start is the lowest
         en = min(en, cap);
         const uint32_t nb = en > st ? en - st : 0;
@@ -2222,8 +2226,60 @@ __global__ void __launch_bounds__(256) k_gather(uint32_t nq, const GatherQuery *
         }
     }
     if (lane == 0) {  // result slot: the query's position in the k_decode launch it was taken from
-        out_len[q.slot] = min(len, cap);
-        status[q.slot] = len > cap ? (uint32_t)kErrSpace : (uint32_t)kOk;
+        out_len[q0.slot] = min(len, cap);
+        status[q0.slot] = len > cap ? (uint32_t)kErrSpace : (uint32_t)kOk;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_gather(uint32_t ntask, const uint2 *tasks, const GatherQuery *qs,
+                                                uint8_t *out_, uint32_t *out_len, uint32_t *status, uint32_t remap) {
+    const uint32_t lane = lane_id();
+    uint32_t lb = blockIdx.x;
+    if (remap) {  // XCD-aware order, as k_decode
+        const uint32_t nb = gridDim.x, x = blockIdx.x & 7u, per = nb >> 3, rem = nb & 7u;
+        lb = x * per + min(x, rem) + (blockIdx.x >> 3);
+    }
+    const uint32_t ti = lb * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (ti >= ntask) return;
+    const uint2 task = tasks[ti];
+    const uint32_t first = uni(task.x), count = uni(task.y);
+    if (count == 1) {
+        gather_one(qs[first], out_, out_len, status);
+        return;
+    }
+    // several small queries (each >= 1 span, <= 64 spans in all): lane i holds query i
+    GatherQuery q{};
+    if (lane < count) q = qs[first + lane];
+    const uint32_t ns = lane < count ? q.nspan : 0;
+    const uint32_t st0 = wave_excl_scan((int32_t)ns);  // this query's first lane
+    uint64_t starts = lane < count ? (1ull << st0) : 0;
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint64_t y = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(starts >> 32), o) << 32) |
+                           (uint32_t)__shfl_xor((int)(uint32_t)starts, o);
+        starts |= y;
+    }
+    const uint32_t total = uni(readlane(st0 + ns, count - 1));
+    const uint32_t qi = (uint32_t)__popcll(starts & (lane == 63 ? ~0ull : ((2ull << lane) - 1))) - 1u;
+    const int src = (int)min(qi, 63u);
+    const uint64_t spp = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uint64_t)q.span >> 32), src) << 32) |
+                         (uint32_t)__shfl((int)(uint32_t)(uint64_t)q.span, src);
+    const uint64_t bp = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uint64_t)q.base >> 32), src) << 32) |
+                        (uint32_t)__shfl((int)(uint32_t)(uint64_t)q.base, src);
+    const uint64_t oo = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(q.out_off >> 32), src) << 32) |
+                        (uint32_t)__shfl((int)(uint32_t)q.out_off, src);
+    const uint32_t qcap = (uint32_t)__shfl((int)q.cap, src), qst = (uint32_t)__shfl((int)st0, src);
+    if (lane < total) {
+        const PX_GAS SpanEnt *sp = (const PX_GAS SpanEnt *)spp;
+        const uint32_t k = lane - qst;
+        const PX_GAS uint32_t *e = (const PX_GAS uint32_t *)(sp + k);
+        const int32_t rel = (int32_t)e[0];
+        const uint32_t s0 = e[1];
+        const uint32_t en = min(((const PX_GAS uint32_t *)(sp + k + 1))[1], qcap);
+        if (en > s0) lane_copy((PX_GAS uint8_t *)out_ + oo + s0, (const PX_GAS uint8_t *)bp + rel, en - s0);
+    }
+    if (lane < count) {
+        out_len[q.slot] = min(q.len, q.cap);
+        status[q.slot] = q.len > q.cap ? (uint32_t)kErrSpace : (uint32_t)kOk;
     }
 }
 
@@ -2365,10 +2421,10 @@ hipError_t launch_span_build(hipStream_t s, uint32_t n, const SpanJob *jobs) {
     return hipGetLastError();
 }
 
-hipError_t launch_gather(hipStream_t s, uint32_t nq, const GatherQuery *qs, uint8_t *out, uint32_t *out_len,
-                         uint32_t *status, bool remap) {
-    if (!nq) return hipSuccess;
-    k_gather<<<(nq + 3) / 4, 256, 0, s>>>(nq, qs, out, out_len, status, remap ? 1u : 0u);
+hipError_t launch_gather(hipStream_t s, uint32_t ntask, const uint2 *tasks, const GatherQuery *qs, uint8_t *out,
+                         uint32_t *out_len, uint32_t *status, bool remap) {
+    if (!ntask) return hipSuccess;
+    k_gather<<<(ntask + 3) / 4, 256, 0, s>>>(ntask, tasks, qs, out, out_len, status, remap ? 1u : 0u);
     return hipGetLastError();
 }
 

@@ -1107,7 +1107,9 @@ struct px_ctx {
         tasks.reserve(g.size());
         for (uint32_t i = 0; i < (uint32_t)g.size();) {
             uint32_t j = i, tot = 0;
-            while (j < g.size() && j - i < 64 && g[j].nspan >= 1 && tot + g[j].nspan <= 64) tot += g[j++].nspan;
+            // (small records only: a packed span is copied by one lane, however long)
+            while (j < g.size() && j - i < 64 && g[j].nspan >= 1 && g[j].len <= 4096 && tot + g[j].nspan <= 64)
+                tot += g[j++].nspan;
             if (j == i) j = i + 1;  // a large (or empty) one alone
             tasks.push_back(make_uint2(i, j - i));
             i = j;
