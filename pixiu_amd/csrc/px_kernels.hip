@@ -2187,12 +2187,13 @@ __global__ void __launch_bounds__(256) k_span_build(uint32_t n, const SpanJob *j
 // span per lane, each lane finds its query from the queries' span offsets).  Spans up
 // to kLaneCopyMax bytes are copied by their lane, longer ones by the whole wave.
 // Output stops at each query's cap.
-PX_DEV void gather_one(const GatherQuery &q0, uint8_t *out_, uint32_t *out_len, uint32_t *status) {
+PX_DEV void gather_one(const GatherQuery &q0, uint32_t k_lo, uint32_t k_hi, uint8_t *out_, uint32_t *out_len,
+                       uint32_t *status) {
     const uint32_t lane = lane_id();
     const PX_GAS SpanEnt *sp = (const PX_GAS SpanEnt *)uni64((uint64_t)q0.span);
     const PX_GAS uint8_t *base = (const PX_GAS uint8_t *)uni64((uint64_t)q0.base);
     PX_GAS uint8_t *o = (PX_GAS uint8_t *)out_ + uni64(q0.out_off);
-    const uint32_t nspan = uni(q0.nspan), cap = uni(q0.cap), len = uni(q0.len);
+    const uint32_t nspan = min(uni(q0.nspan), k_hi), cap = uni(q0.cap), len = uni(q0.len);
     // the next step's entries are loaded before this step's copies (one round trip per
     // step instead of two)
     auto load_ent = [&](uint32_t k, int32_t &rel, uint32_t &st, uint32_t &en) {
@@ -2207,8 +2208,8 @@ PX_DEV void gather_one(const GatherQuery &q0, uint8_t *out_, uint32_t *out_len, 
     };
     int32_t nrel;
     uint32_t nst, nen;
-    load_ent(lane, nrel, nst, nen);
-    for (uint32_t k0 = 0; k0 < nspan; k0 += 64) {
+    load_ent(k_lo + lane, nrel, nst, nen);
+    for (uint32_t k0 = k_lo; k0 < nspan; k0 += 64) {
         const int32_t rel = nrel;
         const uint32_t st = nst;
         uint32_t en = nen;
@@ -2225,13 +2226,13 @@ PX_DEV void gather_one(const GatherQuery &q0, uint8_t *out_, uint32_t *out_len, 
             wave_copy(o + readlane(st, j), base + (int32_t)readlane((uint32_t)rel, j), readlane(nb, j));
         }
     }
-    if (lane == 0) {  // result slot: the query's position in the k_decode launch it was taken from
+    if (lane == 0 && k_lo == 0) {  // result slot: the query's position in the k_decode launch
         out_len[q0.slot] = min(len, cap);
         status[q0.slot] = len > cap ? (uint32_t)kErrSpace : (uint32_t)kOk;
     }
 }
 
-__global__ void __launch_bounds__(256) k_gather(uint32_t ntask, const uint2 *tasks, const GatherQuery *qs,
+__global__ void __launch_bounds__(256) k_gather(uint32_t ntask, const uint4 *tasks, const GatherQuery *qs,
                                                 uint8_t *out_, uint32_t *out_len, uint32_t *status, uint32_t remap) {
     const uint32_t lane = lane_id();
     uint32_t lb = blockIdx.x;
@@ -2241,10 +2242,10 @@ __global__ void __launch_bounds__(256) k_gather(uint32_t ntask, const uint2 *tas
     }
     const uint32_t ti = lb * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (ti >= ntask) return;
-    const uint2 task = tasks[ti];
+    const uint4 task = tasks[ti];
     const uint32_t first = uni(task.x), count = uni(task.y);
-    if (count == 1) {
-        gather_one(qs[first], out_, out_len, status);
+    if (count == 1) {  // one query, or the span range [z, w) of a long one
+        gather_one(qs[first], uni(task.z), uni(task.w), out_, out_len, status);
         return;
     }
     // several small queries (each >= 1 span, <= 64 spans in all): lane i holds query i
@@ -2421,7 +2422,7 @@ hipError_t launch_span_build(hipStream_t s, uint32_t n, const SpanJob *jobs) {
     return hipGetLastError();
 }
 
-hipError_t launch_gather(hipStream_t s, uint32_t ntask, const uint2 *tasks, const GatherQuery *qs, uint8_t *out,
+hipError_t launch_gather(hipStream_t s, uint32_t ntask, const uint4 *tasks, const GatherQuery *qs, uint8_t *out,
                          uint32_t *out_len, uint32_t *status, bool remap) {
     if (!ntask) return hipSuccess;
     k_gather<<<(ntask + 3) / 4, 256, 0, s>>>(ntask, tasks, qs, out, out_len, status, remap ? 1u : 0u);

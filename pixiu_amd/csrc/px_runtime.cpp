@@ -50,7 +50,7 @@ hipError_t launch_rehash(hipStream_t, const uint4 *, uint32_t, uint32_t, uint4 *
 hipError_t launch_decode_addr(hipStream_t, const DecodeQuery *, uint32_t, const RecSlot *const *, int32_t *,
                               uint32_t *, uint32_t *, Frame *, uint32_t, uint32_t);
 hipError_t launch_span_build(hipStream_t, uint32_t, const SpanJob *);
-hipError_t launch_gather(hipStream_t, uint32_t, const uint2 *, const GatherQuery *, uint8_t *, uint32_t *, uint32_t *,
+hipError_t launch_gather(hipStream_t, uint32_t, const uint4 *, const GatherQuery *, uint8_t *, uint32_t *, uint32_t *,
                          bool);
 int debug_trace_take(int32_t *, uint32_t);
 int debug_prof_take(unsigned long long *, uint32_t);
@@ -1103,24 +1103,36 @@ struct px_ctx {
     void launch_gathers(hipStream_t st, const std::vector<GatherQuery> &g, uint8_t *out, uint32_t *dl, uint32_t *ds,
                         GatherQuery *&dbuf) {
         if (g.empty()) return;
-        std::vector<uint2> tasks;
+        // a long record is split into pieces of kPiece spans (one wave each: more waves in
+        // flight to hide the entry -> bytes round trips)
+        static const uint32_t kPiece = [] {
+            const char *e = std::getenv("PX_GATHER_PIECE");
+            const int v = e ? std::atoi(e) : 0;
+            return v >= 64 ? (uint32_t)v : 1024u;
+        }();
+        std::vector<uint4> tasks;
         tasks.reserve(g.size());
         for (uint32_t i = 0; i < (uint32_t)g.size();) {
             uint32_t j = i, tot = 0;
             // (small records only: a packed span is copied by one lane, however long)
             while (j < g.size() && j - i < 64 && g[j].nspan >= 1 && g[j].len <= 4096 && tot + g[j].nspan <= 64)
                 tot += g[j++].nspan;
-            if (j == i) j = i + 1;  // a large (or empty) one alone
-            tasks.push_back(make_uint2(i, j - i));
+            if (j > i + 1) {
+                tasks.push_back(make_uint4(i, j - i, 0, 0));
+            } else {  // one query alone, in pieces
+                j = i + 1;
+                const uint32_t ns = g[i].nspan;
+                for (uint32_t k = 0; k == 0 || k < ns; k += kPiece) tasks.push_back(make_uint4(i, 1, k, k + kPiece));
+            }
             i = j;
         }
         const uint64_t qb = round_up(g.size() * sizeof(GatherQuery), 64);
-        dbuf = (GatherQuery *)heap.alloc(qb + tasks.size() * sizeof(uint2));
-        auto *dt = (uint2 *)((uint8_t *)dbuf + qb);
+        dbuf = (GatherQuery *)heap.alloc(qb + tasks.size() * sizeof(uint4));
+        auto *dt = (uint4 *)((uint8_t *)dbuf + qb);
         hcheck(hipMemcpyAsync(dbuf, g.data(), g.size() * sizeof(GatherQuery), hipMemcpyHostToDevice, st));
-        hcheck(hipMemcpyAsync(dt, tasks.data(), tasks.size() * sizeof(uint2), hipMemcpyHostToDevice, st));
+        hcheck(hipMemcpyAsync(dt, tasks.data(), tasks.size() * sizeof(uint4), hipMemcpyHostToDevice, st));
         hcheck(launch_gather(st, (uint32_t)tasks.size(), dt, dbuf, out, dl, ds, true));
-        gather_bytes[dbuf] = qb + tasks.size() * sizeof(uint2);
+        gather_bytes[dbuf] = qb + tasks.size() * sizeof(uint4);
     }
     std::map<void *, uint64_t> gather_bytes;  // launch_gathers' device buffers -> their sizes
     void release_gathers(GatherQuery *d) {
