@@ -402,7 +402,13 @@ def summarize(cfg, r, rps, world, a, pmc_path):
                          "doubling_steps": runs[-1]["psa"][6]},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 3), "peak": PEAK_HBM_GBPS,
                      "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBPS, 6), "traffic": traffic,
-                     "traffic_source": tsrc},
+                     "traffic_source": tsrc,
+                     # what the stage's kernels actually move (PMC bytes / stage time): how busy
+                     # HBM is, next to the algorithmic rate above
+                     "traffic_GBps": round(traffic / ((walk_kms if dominant == enc_name else dec_kms) * 1e-3) / 1e9, 1)
+                     if traffic else None,
+                     "traffic_per_algorithmic_byte": round(traffic / ((raw + comp) if dominant == enc_name
+                                                                      else (comp + exp)), 1) if traffic else None},
         "roofline_kernels_GBps": {"encode_stage": round(set_gbps, 3), "k_gst_emit": round(emit_gbps, 3),
                                   "getitem_stage": round(dec_gbps, 3)},
         "gather_ms": round(float(np.mean([x["gather_ms"] for x in runs])), 3),
