@@ -62,10 +62,12 @@ namespace {
 
 struct HipFail {
     hipError_t e;
+    int line;  // px_runtime.cpp line of the failed call
 };
-inline void hcheck(hipError_t e) {
-    if (e != hipSuccess) throw HipFail{e};
+inline void hcheck_at(hipError_t e, int line) {
+    if (e != hipSuccess) throw HipFail{e, line};
 }
+#define hcheck(x) hcheck_at((x), __LINE__)
 struct PxFail {
     int code;
 };
@@ -103,47 +105,86 @@ inline uint64_t pow2_at_least(uint64_t v) {
 }
 
 // ---------------------------------------------------------------- device heap
-// Slab bump allocator with exact-size free lists: no hipMalloc per shard.
+// Best-fit allocator over 1 GiB slabs: a free block is split on allocation and merged
+// with its free neighbours (inside its slab) on release, so batches of varying sizes
+// reuse the same memory instead of growing the footprint.  No hipMalloc per shard.
 class DevHeap {
   public:
     ~DevHeap() {
-        for (void *s : slabs_) (void)hipFree(s);
+        for (auto &s : slabs_) (void)hipFree(s.first);
     }
     void *alloc(uint64_t n) {
         n = round_up(std::max<uint64_t>(n, 256), 256);
-        auto it = free_.find(n);
-        if (it != free_.end() && !it->second.empty()) {
-            void *p = it->second.back();
-            it->second.pop_back();
-            return p;
-        }
-        if (n > left_) {
-            uint64_t sz = std::max<uint64_t>(n, kSlab);
-            void *s = nullptr;
-            if (hipMalloc(&s, sz) != hipSuccess) throw PxFail{PX_ENOMEM};
-            slabs_.push_back(s);
+        auto it = by_size_.lower_bound(n);
+        if (it == by_size_.end()) {
+            const uint64_t sz = std::max<uint64_t>(n, kSlab);
+            void *v = nullptr;
+            if (hipMalloc(&v, sz) != hipSuccess) throw PxFail{PX_ENOMEM};
+            char *s = static_cast<char *>(v);
+            slabs_.emplace(s, s + sz);
             held_ += sz;
-            cur_ = static_cast<char *>(s);
-            left_ = sz;
+            add_free(s, sz);
+            it = by_size_.lower_bound(n);
         }
-        void *p = cur_;
-        cur_ += n;
-        left_ -= n;
+        char *p = it->second;
+        uint64_t sz = it->first;
+        by_size_.erase(it);
+        by_addr_.erase(p);
+        if (sz - n >= 256) {  // split: the tail stays free
+            add_free(p + n, sz - n);
+            sz = n;
+        }
+        live_[p] = sz;
         return p;
     }
-    void release(void *p, uint64_t n) {
-        if (!p) return;
-        n = round_up(std::max<uint64_t>(n, 256), 256);
-        free_[n].push_back(p);
+    void release(void *v, uint64_t) {
+        if (!v) return;
+        char *p = static_cast<char *>(v);
+        auto lv = live_.find(p);
+        if (lv == live_.end()) return;
+        uint64_t sz = lv->second;
+        live_.erase(lv);
+        auto slab = std::prev(slabs_.upper_bound(p));  // the slab holding p
+        // merge with the free block right after and right before, inside the slab
+        auto nx = by_addr_.find(p + sz);
+        if (nx != by_addr_.end() && nx->first < slab->second) {
+            sz += nx->second;
+            erase_free(nx->first, nx->second);
+        }
+        auto pv = by_addr_.lower_bound(p);
+        if (pv != by_addr_.begin()) {
+            --pv;
+            if (pv->first >= slab->first && pv->first + pv->second == p) {
+                char *q = pv->first;
+                const uint64_t qs = pv->second;
+                erase_free(q, qs);
+                p = q;
+                sz += qs;
+            }
+        }
+        add_free(p, sz);
     }
     uint64_t held() const { return held_; }
 
   private:
+    void add_free(char *p, uint64_t sz) {
+        by_addr_[p] = sz;
+        by_size_.emplace(sz, p);
+    }
+    void erase_free(char *p, uint64_t sz) {
+        by_addr_.erase(p);
+        for (auto r = by_size_.equal_range(sz); r.first != r.second; ++r.first)
+            if (r.first->second == p) {
+                by_size_.erase(r.first);
+                break;
+            }
+    }
     static constexpr uint64_t kSlab = 1ull << 30;
-    std::vector<void *> slabs_;
-    char *cur_ = nullptr;
-    uint64_t left_ = 0, held_ = 0;
-    std::map<uint64_t, std::vector<void *>> free_;
+    std::map<char *, char *> slabs_;  // start -> end
+    std::map<char *, uint64_t> by_addr_;
+    std::multimap<uint64_t, char *> by_size_;
+    std::unordered_map<void *, uint64_t> live_;
+    uint64_t held_ = 0;
 };
 
 // pinned-free scratch buffer that only grows
@@ -650,7 +691,10 @@ struct px_ctx {
         cap = std::min<uint32_t>(cap, kChunkSlots);
         auto *nt = (RecSlot *)heap.alloc((uint64_t)cap * sizeof(RecSlot));
         if (ch.dev) {
-            hcheck(hipMemcpyAsync(nt, ch.dev, (size_t)ch.n * sizeof(RecSlot), hipMemcpyDeviceToDevice, stream));
+            // the old table's slots (new ones are scattered in afterwards; ch.n may already
+            // count them, and reading past the old allocation is out of bounds)
+            hcheck(hipMemcpyAsync(nt, ch.dev, (size_t)std::min(ch.n, ch.dev_cap) * sizeof(RecSlot),
+                                  hipMemcpyDeviceToDevice, stream));
             heap.release(ch.dev, (uint64_t)ch.dev_cap * sizeof(RecSlot));
         }
         ch.dev = nt;
@@ -2803,6 +2847,7 @@ const char *px_strerror(int s) {
         __VA_ARGS__                                      \
     } catch (const HipFail &f) {                         \
         ctx->last_hip = (int)f.e;                        \
+        fprintf(stderr, "pixiu_amd: HIP error %s at px_runtime.cpp:%d\n", hipGetErrorName(f.e), f.line); \
         return PX_EHIP;                                  \
     } catch (const PxFail &f) {                          \
         return f.code;                                   \
