@@ -299,6 +299,27 @@ class KeyMap {
         *idx = e.idx;
         return true;
     }
+    // room for `more` keys without rehashing on the way
+    void reserve(size_t more) {
+        while ((n_ + more) * 2 > tab_.size()) grow();
+    }
+    // put, returning the shard k was stored under before (-1: new key)
+    int64_t upsert(const uint8_t *k, size_t n, uint32_t shard, uint32_t chunk, uint32_t idx) {
+        if ((n_ + 1) * 2 > tab_.size()) grow();
+        const uint64_t h = hash(k, n);
+        Slot &e = tab_[probe(h, k, n)];
+        if (e.len == kFree) {
+            e = Slot{h, bytes_.size(), (uint32_t)n, shard, chunk, idx};
+            bytes_.insert(bytes_.end(), k, k + n);
+            ++n_;
+            return -1;
+        }
+        const int64_t prev = e.shard;
+        e.shard = shard;
+        e.chunk = chunk;
+        e.idx = idx;
+        return prev;
+    }
     void put(const uint8_t *k, size_t n, uint32_t shard, uint32_t chunk = ~0u, uint32_t idx = 0) {
         if ((n_ + 1) * 2 > tab_.size()) grow();
         const uint64_t h = hash(k, n);
@@ -318,6 +339,28 @@ class KeyMap {
         bytes_.clear();
         n_ = 0;
     }
+};
+
+// KeyMap split into 16 partitions by key hash: a batch's upserts run one partition per
+// host thread, each seeing its keys in record order
+class PartKeyMap {
+  public:
+    static constexpr uint32_t kParts = 16;
+    static uint32_t part_of(const uint8_t *k, size_t n) { return (uint32_t)(KeyMap::hash(k, n) >> 60); }
+    int64_t find(const uint8_t *k, size_t n) const { return p_[part_of(k, n)].find(k, n); }
+    bool find_hint(const uint8_t *k, size_t n, uint32_t *shard, uint32_t *chunk, uint32_t *idx) const {
+        return p_[part_of(k, n)].find_hint(k, n, shard, chunk, idx);
+    }
+    void put(const uint8_t *k, size_t n, uint32_t shard, uint32_t chunk = ~0u, uint32_t idx = 0) {
+        p_[part_of(k, n)].put(k, n, shard, chunk, idx);
+    }
+    KeyMap &part(uint32_t i) { return p_[i]; }
+    void clear() {
+        for (auto &m : p_) m.clear();
+    }
+
+  private:
+    KeyMap p_[kParts];
 };
 
 // host wall time per phase of one call, printed on stderr when `env` is 1
@@ -535,7 +578,7 @@ struct px_ctx {
     uint32_t tab_lo = ~0u, tab_hi = 0;      // chunk_tab entries not yet uploaded
     std::vector<ShardInit> pending_init;    // new shard arenas to zero (k_shard_init)
     std::vector<std::pair<ShardState *, ShardState>> pending_state;  // states set after the zeroing (loaded shards)
-    KeyMap keymap;  // raw key -> shard (multi-shard only)
+    PartKeyMap keymap;  // raw key -> shard (multi-shard only)
     std::vector<std::pair<void *, uint64_t>> store_blocks;  // packed record stores + segment indexes
     uint8_t *last_store = nullptr;  // packed compressed bytes of the last set batch
     uint64_t last_store_bytes = 0;
@@ -602,6 +645,7 @@ struct px_ctx {
     }
     void h2d(void *d, const void *h, size_t n) {
         if (!n) return;
+        if (n >= kRingSlot) return h2d_bulk(d, h, n);  // large: pinned ring, no staging copy
         const uint8_t *b = static_cast<const uint8_t *>(h);
         staged.emplace_back(b, b + n);
         hcheck(hipMemcpyAsync(d, staged.back().data(), n, hipMemcpyHostToDevice, stream));
@@ -616,7 +660,12 @@ struct px_ctx {
     hipEvent_t ring_ev[kRingSlots] = {};
     bool ring_busy[kRingSlots] = {};
     void h2d_bulk(void *d, const void *h, size_t n) {
-        if (n < kRingSlot) return h2d(d, h, n);
+        if (n < kRingSlot) {
+            const uint8_t *b = static_cast<const uint8_t *>(h);
+            staged.emplace_back(b, b + n);
+            hcheck(hipMemcpyAsync(d, staged.back().data(), n, hipMemcpyHostToDevice, stream));
+            return;
+        }
         auto *slots = static_cast<uint8_t *>(ring_buf.get(kRingSlot * kRingSlots));
         const auto *src = static_cast<const uint8_t *>(h);
         auto *dst = static_cast<uint8_t *>(d);
@@ -1574,28 +1623,52 @@ struct px_ctx {
             std::vector<DecodeQuery> again;
             std::vector<uint32_t> again_j;
             uint64_t ao = 0;
+            // the first pass's overruns go again with room; everything else is appended to
+            // its chunk's prefix store, chunks in parallel (a chunk's queries are contiguous)
+            std::vector<uint8_t> redo(q.size(), 0);
             for (size_t i = 0; i < q.size(); ++i) {
-                const KpJob &j = jobs[qj[i]];
-                const uint8_t *p = hk.data() + q[i].out_off;
-                uint32_t ke = key_end(p, ql[i]);
                 if (qs[i] != kOk && qs[i] != kErrSpace) {
                     st[qj[i]] = qs[i];
+                    redo[i] = 2;
                     continue;
                 }
-                if (ke == 0 && qs[i] == kErrSpace && pass == 0) {  // decoded key ran past the cap
+                if (pass == 0 && qs[i] == kErrSpace && key_end(hk.data() + q[i].out_off, ql[i]) == 0) {
                     DecodeQuery d = q[i];
                     d.out_off = ao;
-                    d.out_cap = j.doc_len + 256;
+                    d.out_cap = jobs[qj[i]].doc_len + 256;
                     ao += round_up(d.out_cap, 16);
                     again.push_back(d);
                     again_j.push_back(qj[i]);
-                    continue;
+                    redo[i] = 1;
                 }
-                uint32_t keep = ke ? ke : ql[i];
-                Chunk &ch = chunks[j.chunk];
-                ch.kp_off[j.idx] = ch.kp.size();
-                ch.kp_len[j.idx] = keep;
-                ch.kp.append(reinterpret_cast<const char *>(p), keep);
+            }
+            std::vector<uint32_t> runs;  // [runs[k], runs[k+1]): one chunk's queries
+            for (uint32_t i = 0; i < (uint32_t)q.size(); ++i)
+                if (i == 0 || q[i].chunk != q[i - 1].chunk) runs.push_back(i);
+            runs.push_back((uint32_t)q.size());
+            auto append_run = [&](uint32_t k) {
+                for (uint32_t i = runs[k]; i < runs[k + 1]; ++i) {
+                    if (redo[i]) continue;
+                    const KpJob &j = jobs[qj[i]];
+                    const uint8_t *p = hk.data() + q[i].out_off;
+                    const uint32_t ke = key_end(p, ql[i]);
+                    const uint32_t keep = ke ? ke : ql[i];
+                    Chunk &ch = chunks[j.chunk];
+                    ch.kp_off[j.idx] = ch.kp.size();
+                    ch.kp_len[j.idx] = keep;
+                    ch.kp.append(reinterpret_cast<const char *>(p), keep);
+                }
+            };
+            bool distinct = true;  // a chunk in two runs (possible in the second pass): in order
+            {
+                std::unordered_set<uint32_t> seen;
+                for (uint32_t k = 0; k + 1 < runs.size() && distinct; ++k) distinct = seen.insert(q[runs[k]].chunk).second;
+            }
+            if (distinct && runs.size() > 2 && q.size() >= 4096) {
+                const std::function<void(uint32_t)> job = [&](uint32_t k) { append_run(k); };
+                WorkerPool::get().run((uint32_t)runs.size() - 1, job);
+            } else {
+                for (uint32_t k = 0; k + 1 < runs.size(); ++k) append_run(k);
             }
             q.swap(again);
             qj.swap(again_j);
@@ -2174,15 +2247,31 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     // shard's, so this is the order the sequential loop would have used)
     std::vector<uint32_t> replaced(n, 0);
     std::vector<std::pair<uint32_t, uint32_t>> moved;  // (record, older shard)
-    if (opts.records_per_shard != 0)
-        for (uint32_t r = 0; r < n; ++r) {
-            if (!live[r]) continue;
-            const uint8_t *kp = hkeys.data() + hkoff[r];
-            const uint64_t klen = hkoff[r + 1] - hkoff[r];
-            const int64_t prev = keymap.find(kp, klen);
-            if (prev >= 0 && (uint32_t)prev != rec_shard[r]) moved.emplace_back(r, (uint32_t)prev);
-            keymap.put(kp, klen, rec_shard[r], rgchunk[r], ridx[r]);
+    if (opts.records_per_shard != 0) {
+        // key -> shard upserts, one key-map partition per task (keys in record order)
+        std::vector<uint8_t> part(n);
+        for (uint32_t r = 0; r < n; ++r)
+            if (live[r]) part[r] = (uint8_t)PartKeyMap::part_of(hkeys.data() + hkoff[r], hkoff[r + 1] - hkoff[r]);
+        std::vector<std::vector<std::pair<uint32_t, uint32_t>>> mv(PartKeyMap::kParts);
+        const std::function<void(uint32_t)> job = [&](uint32_t pi) {
+            KeyMap &m = keymap.part(pi);
+            m.reserve(n / PartKeyMap::kParts + 64);
+            for (uint32_t r = 0; r < n; ++r) {
+                if (!live[r] || part[r] != pi) continue;
+                const uint8_t *kp = hkeys.data() + hkoff[r];
+                const uint64_t klen = hkoff[r + 1] - hkoff[r];
+                const int64_t prev = m.upsert(kp, klen, rec_shard[r], rgchunk[r], ridx[r]);
+                if (prev >= 0 && (uint32_t)prev != rec_shard[r]) mv[pi].emplace_back(r, (uint32_t)prev);
+            }
+        };
+        if (n >= 4096) {
+            WorkerPool::get().run(PartKeyMap::kParts, job);
+        } else {
+            for (uint32_t pi = 0; pi < PartKeyMap::kParts; ++pi) job(pi);
         }
+        for (auto &v : mv) moved.insert(moved.end(), v.begin(), v.end());
+        std::sort(moved.begin(), moved.end());  // record order
+    }
     auto insert_work = [&](size_t k) {
         const Work &w = work[k];
         Shard &s = *w.s;
