@@ -1489,6 +1489,47 @@ PX_DEV void lane_copy(PX_GAS uint8_t *dst, const PX_GAS uint8_t *src, uint32_t n
     }
 }
 
+// the first r < 16 bytes of v to dst: one predicated store per set bit of r (8, 4, 2,
+// 1 bytes), the same four store instructions for every lane whatever its r
+PX_DEV uint32_t dw_at(u32x4 v, uint32_t i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
+PX_DEV void st_tail(PX_GAS uint8_t *dst, u32x4 v, uint32_t r) {
+    if (r & 8) {
+        const uint64_t x = ((uint64_t)v.y << 32) | v.x;
+        __builtin_memcpy((PX_GAS void *)dst, &x, 8);
+    }
+    const uint32_t o8 = r & 8, o4 = r & 12, o2 = r & 14;
+    if (r & 4) {
+        const uint32_t x = dw_at(v, o8 >> 2);
+        __builtin_memcpy((PX_GAS void *)(dst + o8), &x, 4);
+    }
+    if (r & 2) {
+        const uint16_t x = (uint16_t)dw_at(v, o4 >> 2);
+        __builtin_memcpy((PX_GAS void *)(dst + o4), &x, 2);
+    }
+    if (r & 1) dst[o2] = (uint8_t)(dw_at(v, o2 >> 2) >> (8 * (o2 & 3)));
+}
+// one lane copies a piece of n bytes.  Below 64 bytes: the 16-byte blocks and the tail
+// block are loaded together (the tail load may read up to 15 bytes past the piece: every
+// source is compressed bytes with >= 64 bytes of slack behind them in its store), then
+// stored, so a wave of mixed piece sizes issues at most 4 loads and 7 stores instead of
+// one load/store pair per size class.  Longer pieces take lane_copy.
+PX_DEV void span_copy(PX_GAS uint8_t *dst, const PX_GAS uint8_t *src, uint32_t n) {
+    if (n >= 64) {
+        lane_copy(dst, src, n);
+        return;
+    }
+    const uint32_t f = n & ~15u;
+    const u32x4 t = ld16(src + f);
+    u32x4 a0{}, a1{}, a2{};
+    if (f >= 16) a0 = ld16(src);
+    if (f >= 32) a1 = ld16(src + 16);
+    if (f >= 48) a2 = ld16(src + 32);
+    if (f >= 16) st16(dst, a0);
+    if (f >= 32) st16(dst + 16, a1);
+    if (f >= 48) st16(dst + 32, a2);
+    st_tail(dst + f, t, n & 15);
+}
+
 PX_DEV int32_t wave_excl_scan(int32_t v) {
     int32_t x = v;
     for (int o = 1; o < 64; o <<= 1) {
@@ -2199,11 +2240,11 @@ PX_DEV void gather_one(const GatherQuery &q0, uint32_t k_lo, uint32_t k_hi, uint
     auto load_ent = [&](uint32_t k, int32_t &rel, uint32_t &st, uint32_t &en) {
         rel = 0;
         st = en = 0;
-        if (k < nspan) {
-            const PX_GAS uint32_t *e = (const PX_GAS uint32_t *)(sp + k);
-            rel = (int32_t)e[0];
-            st = e[1];
-            en = e[3];  // the next entry's start (the table ends with a sentinel)
+        if (k < nspan) {  // this entry and the next one's start (the table ends with a sentinel)
+            const u32x4 e = *(const PX_GAS u32x4_u *)(sp + k);
+            rel = (int32_t)e.x;
+            st = e.y;
+            en = e.w;
         }
     };
     int32_t nrel;
@@ -2218,7 +2259,7 @@ PX_DEV void gather_one(const GatherQuery &q0, uint32_t k_lo, uint32_t k_hi, uint
         en = min(en, cap);
         const uint32_t nb = en > st ? en - st : 0;
         const bool lng = nb > kLaneCopyMax;
-        if (nb && !lng) lane_copy(o + st, base + rel, nb);
+        if (nb && !lng) span_copy(o + st, base + rel, nb);
         uint64_t lm = ballot(lng);
         while (lm) {
             const uint32_t j = ffs64(lm);
@@ -2272,11 +2313,11 @@ __global__ void __launch_bounds__(256) k_gather(uint32_t ntask, const uint4 *tas
     if (lane < total) {
         const PX_GAS SpanEnt *sp = (const PX_GAS SpanEnt *)spp;
         const uint32_t k = lane - qst;
-        const PX_GAS uint32_t *e = (const PX_GAS uint32_t *)(sp + k);
-        const int32_t rel = (int32_t)e[0];
-        const uint32_t s0 = e[1];
-        const uint32_t en = min(((const PX_GAS uint32_t *)(sp + k + 1))[1], qcap);
-        if (en > s0) lane_copy((PX_GAS uint8_t *)out_ + oo + s0, (const PX_GAS uint8_t *)bp + rel, en - s0);
+        const u32x4 e = *(const PX_GAS u32x4_u *)(sp + k);
+        const int32_t rel = (int32_t)e.x;
+        const uint32_t s0 = e.y;
+        const uint32_t en = min(e.w, qcap);
+        if (en > s0) span_copy((PX_GAS uint8_t *)out_ + oo + s0, (const PX_GAS uint8_t *)bp + rel, en - s0);
     }
     if (lane < count) {
         out_len[q.slot] = min(q.len, q.cap);
