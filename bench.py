@@ -257,7 +257,8 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
         sst = st.stats()
         set_kms, walk_kms, emit_kms = sst["last_set_kernel_ms"], sst["last_walk_kernel_ms"], sst["last_emit_kernel_ms"]
         psa = (sst["last_psa_ms"], int(sst["last_psa_shards"]), int(sst["last_walk_shards"]),
-               sst["last_psa_sort_ms"], sst["last_psa_lcp_ms"], sst["last_psa_msg_ms"], int(sst["last_psa_iters"]))
+               sst["last_psa_sort_ms"], sst["last_psa_lcp_ms"], sst["last_psa_msg_ms"], int(sst["last_psa_iters"]),
+               int(sst["last_psa_rounds"]), int(sst["last_psa_rotations"]), sst["last_psa_pool_ms"], int(sst["chunks"]))
         rc, off, ln, sts, need = st.get_batch_device(keys_host, out.data_ptr(), out_cap, px.COMPAT)
         t2 = time.perf_counter()
         gst = st.stats()
@@ -398,8 +399,13 @@ def summarize(cfg, r, rps, world, a, pmc_path):
                          "psa_host_ms": round(float(np.mean([x["psa"][0] for x in runs])), 3),
                          "psa_split_ms": {"sort": round(float(np.mean([x["psa"][3] for x in runs])), 3),
                                           "links_lcp": round(float(np.mean([x["psa"][4] for x in runs])), 3),
-                                          "messages": round(float(np.mean([x["psa"][5] for x in runs])), 3)},
-                         "doubling_steps": runs[-1]["psa"][6]},
+                                          "messages": round(float(np.mean([x["psa"][5] for x in runs])), 3),
+                                          "pool_emulation": round(float(np.mean([x["psa"][9] for x in runs])), 3)},
+                         "doubling_steps": runs[-1]["psa"][6],
+                         # last set batch: suffix-array rounds (chunk windows) and the rotations
+                         # the MemPool emulation found; chunks = the store's chunk count
+                         "psa_rounds": runs[-1]["psa"][7], "psa_rotations": runs[-1]["psa"][8],
+                         "chunks": runs[-1]["psa"][10]},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 3), "peak": PEAK_HBM_GBPS,
                      "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBPS, 6), "traffic": traffic,
                      "traffic_source": tsrc,

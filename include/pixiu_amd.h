@@ -101,6 +101,9 @@ typedef struct px_stats {
     uint64_t span_entries;        /* span-table entries held (8 bytes each) */
     uint64_t last_gather_queries; /* queries of the last get/parse batch served by k_gather */
     double last_span_build_ms;    /* span-table build of the last px_set_batch (host wall) */
+    uint64_t last_psa_rounds;     /* suffix-array rounds of the last px_set_batch (one per chunk window) */
+    uint64_t last_psa_rotations;  /* chunk rotations the suffix-array path found in it (MemPool emulation) */
+    double last_psa_pool_ms;      /* MemPool emulation: leaves, split candidates, pool scan (GPU events) */
 } px_stats;
 
 px_ctx *px_open(const px_opts *opts);

@@ -1176,4 +1176,25 @@ int pxo_encode_docs(int n, const uint8_t *docs, const uint64_t *doc_off,
     }
 }
 
+// MemPool state (pools, used blocks) after every doc, docs stored one after another as
+// the single-instance reference does (rotation included): chunk_no[i] / pools[i] /
+// used[i] after doc i.  Checks the suffix-array path's pool emulation (px_psa.hip).
+int pxo_pool_trace(int n, const uint8_t *docs, const uint64_t *doc_off, uint32_t *chunk_no, int32_t *pools,
+                   int32_t *used) {
+    try {
+        pxo_shard s;
+        for (int i = 0; i < n; ++i) {
+            Bytes doc(docs + doc_off[i], docs + doc_off[i + 1]);
+            if (doc.size() > (size_t)kMaxDoc) return PXO_EINVAL;
+            uint32_t idx = 0;
+            s.store(doc, &chunk_no[i], &idx);
+            pools[i] = s.gst.pools();
+            used[i] = s.gst.used_blocks();
+        }
+        return 0;
+    } catch (const Fail &f) {
+        return f.code;
+    }
+}
+
 }  // extern "C"

@@ -63,6 +63,8 @@ uint32_t pxo_num_chunks(pxo_shard *s);
 uint32_t pxo_chunk_records(pxo_shard *s, uint32_t chunk);
 /* pool counters of the live GST (MemPool.h:14-22: nth, used_num) */
 void pxo_pool_state(pxo_shard *s, int *pools, int *used_blocks);
+int pxo_pool_trace(int n, const uint8_t *docs, const uint64_t *doc_off, uint32_t *chunk_no, int32_t *pools,
+                   int32_t *used);
 
 /* PiXiuStr_init / PiXiuStr_init_key (PiXiuStr.cpp:8-14, 228-271) */
 int pxo_escape(const uint8_t *src, int n, int is_key, uint8_t *out, int cap);

@@ -68,7 +68,8 @@ class PxStats(C.Structure):
                 ("last_psa_ms", C.c_double), ("last_psa_shards", C.c_uint64), ("last_walk_shards", C.c_uint64),
                 ("last_psa_sort_ms", C.c_double), ("last_psa_lcp_ms", C.c_double), ("last_psa_msg_ms", C.c_double),
                 ("last_psa_iters", C.c_uint64), ("span_entries", C.c_uint64), ("last_gather_queries", C.c_uint64),
-                ("last_span_build_ms", C.c_double)]
+                ("last_span_build_ms", C.c_double), ("last_psa_rounds", C.c_uint64),
+                ("last_psa_rotations", C.c_uint64), ("last_psa_pool_ms", C.c_double)]
 
 
 SET_RESULT_DTYPE = np.dtype([("status", "<u4"), ("replaced", "<u4"), ("shard", "<u4"), ("chunk", "<u4"),

@@ -87,7 +87,17 @@ static_assert(sizeof(PsaDoc) == 40, "PsaDoc layout");
 struct PsaShard {
     uint32_t base, len;  // global positions [base, base + len): also its suffix-array range
     uint32_t chunk;      // chunk sequence number of the live chunk
-    uint32_t pad;
+    uint32_t pools;      // 1: emulate MemPool (the live chunk can rotate inside this window)
+    uint32_t doc0, ndocs;  // its docs in the PsaDoc list (the live chunk's, then the new ones)
+    uint32_t pad[2];
+};
+static_assert(sizeof(PsaShard) == 32, "PsaShard layout");
+// MemPool emulation result per PSA shard: the first doc (PsaDoc index) that goes to the
+// next chunk (kNone: every doc stays), and the pool state after the last doc that stays
+struct PsaPoolOut {
+    uint32_t rot_doc;
+    int32_t pools, used;
+    uint32_t splits;  // split leaves (inner nodes) in the docs that stay
 };
 // device scratch for px_psa.hip, borrowed from the runtime's heap
 struct PsaAlloc {
@@ -98,7 +108,8 @@ struct PsaAlloc {
 struct PsaStats {
     uint32_t iterations;  // prefix-doubling steps after the first sort
     uint32_t active[24];  // unsorted suffixes entering each doubling step
-    float ms_sort, ms_lcp, ms_msg;
+    float ms_sort, ms_lcp, ms_msg, ms_pool;
+    uint32_t candidates;  // split candidates of the MemPool emulation
 };
 // a live chunk of at most this many doc bytes cannot rotate by pool count: MemPool charges
 // <= 16 blocks per inserted leaf (leaf 5 + entry 3, split node 5 + entry 3) and at most one

@@ -680,6 +680,159 @@ __global__ void __launch_bounds__(256) k_psa_place(uint32_t ndocs, const PsaDoc 
     rec_status[d.rec] = kOk;
 }
 
+// ---------------------------------------------------------------- MemPool emulation
+// The walk charges MemPool blocks per leaf it creates (MemPool.cpp:7-37; SuffixTree.cpp:
+// 148-227): a leaf under the root or under an existing node [5, 3] (STNode 40 B, child-map
+// entry 24 B), a leaf that splits an edge [5, 5, 3, 3] (leaf, inner node, two entries).
+// Leaf j of a doc ending at e exists iff j + lpf(j) < e; leaves are created in position
+// order.  With sigma = T[j .. j+lpf(j)), E its earliest occurrence and a = T[E + |sigma|]:
+// sigma is already a node iff an earlier leaf had the same sigma or E's doc ends right after
+// sigma (E's leaf node).  The leaves with a given sigma are the first occurrences of
+// sigma.c (c != a), so the split happens at the smallest of them: the minimum of sigma's
+// suffix-array interval outside sigma.a's.  That is the minimum of one side of sigma.a,
+// and a side minimum has its nearest smaller position on one side outside sigma (or among
+// the terminated copies of sigma, which sort first and are implicit doc ends, not leaves)
+// and on the other inside sigma.a: at most two candidates per sigma, the smaller splits.
+// (tools/proto/pool_proto.cpp is the CPU prototype, checked doc by doc against the walk.)
+// code: 0 no leaf, 1 leaf [5, 3], 2 split candidate, 3 split leaf [5, 5, 3, 3]
+__global__ void __launch_bounds__(256) k_pool_leaf(uint32_t N, const uint8_t *G, const uint32_t *pdoc, const PsaDoc *docs,
+                                                   const PsaShard *shards, const uint16_t *dist, const uint32_t *psvp,
+                                                   const uint32_t *nsvp, const uint16_t *lp, const uint16_t *ln,
+                                                   uint8_t *code, uint32_t *E, uint32_t *ncand) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t c = 0;
+    if (p < N) {
+        const PsaDoc &d = docs[pdoc[p]];
+        if (shards[d.shard].pools) {
+            const uint32_t lpv = lp[p], lnv = ln[p], l = max(lpv, lnv);
+            if (p + l < d.start + d.len) {
+                c = 1;
+                if (l) {
+                    uint32_t q = kNoPos;
+                    if (lnv < l) q = psvp[p];
+                    else if (lpv < l || dist[psvp[p]] == l) q = nsvp[p];
+                    if (q != kNoPos) {
+                        const uint32_t e = earliest(psvp, nsvp, lp, ln, q, l);
+                        if (dist[e] > l && dist[q] > l && G[q + l] == G[e + l]) {
+                            c = 2;
+                            E[p] = e;
+                        }
+                    }
+                }
+            }
+        }
+        code[p] = (uint8_t)c;
+    }
+    const uint64_t m = __ballot(c == 2);
+    if (lane_id() == 0 && m) atomicAdd(ncand, (uint32_t)__popcll(m));
+}
+
+struct PoolSlot {
+    unsigned long long key;  // (E << 16 | l), ~0: empty
+    uint32_t min;            // smallest candidate position
+    uint32_t pad;
+};
+PSA_DEV uint32_t pool_hash(uint64_t k, uint32_t mask) {
+    k *= 0x9E3779B97F4A7C15ull;
+    return (uint32_t)(k >> 32) & mask;
+}
+__global__ void __launch_bounds__(256) k_pool_insert(uint32_t N, const uint8_t *code, const uint32_t *E, const uint16_t *lp,
+                                                     const uint16_t *ln, PoolSlot *tab, uint32_t mask) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= N || code[p] != 2) return;
+    const unsigned long long key = (unsigned long long)E[p] << 16 | max(lp[p], ln[p]);
+    for (uint32_t h = pool_hash(key, mask);; h = (h + 1) & mask) {
+        const unsigned long long old = atomicCAS(&tab[h].key, ~0ull, key);
+        if (old == ~0ull || old == key) {
+            atomicMin(&tab[h].min, p);
+            return;
+        }
+    }
+}
+// split decision and blocks per position (u32, for the scan)
+__global__ void __launch_bounds__(256) k_pool_blocks(uint32_t N, uint8_t *code, const uint32_t *E, const uint16_t *lp,
+                                                     const uint16_t *ln, const PoolSlot *tab, uint32_t mask,
+                                                     uint32_t *blk) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= N) return;
+    uint32_t c = code[p];
+    if (c == 2) {
+        const unsigned long long key = (unsigned long long)E[p] << 16 | max(lp[p], ln[p]);
+        uint32_t h = pool_hash(key, mask);
+        while (tab[h].key != key) h = (h + 1) & mask;
+        c = tab[h].min == p ? 3 : 1;
+        code[p] = (uint8_t)c;
+    }
+    blk[p] = c == 1 ? 8u : c == 3 ? 16u : 0u;
+}
+
+// first x in [lo, hi) with P[x] - base > cap (exists: P[hi - 1] - base > cap); wave-uniform
+PSA_DEV uint32_t pool_search(const uint32_t *P, uint32_t lo, uint32_t hi, uint32_t base, uint32_t cap) {
+    const uint32_t lane = lane_id();
+    while (hi - lo > 64) {
+        const uint32_t stride = (hi - lo + 63) / 64;
+        const uint32_t x = lo + lane * stride;
+        const uint64_t m = __ballot(x < hi && P[x] - base > cap);
+        if (!m) {
+            lo = lo + 63 * stride + 1;
+            continue;
+        }
+        const uint32_t t = (uint32_t)__ffsll((long long)m) - 1u;
+        if (t == 0) return lo;
+        hi = min(hi, lo + t * stride + 1);
+        lo = lo + (t - 1) * stride + 1;
+    }
+    const uint32_t x = lo + lane;
+    const uint64_t m = __ballot(x < hi && P[x] - base > cap);
+    return lo + (uint32_t)__ffsll((long long)m) - 1u;
+}
+
+// one wave per emulating shard: the pool state from the chunk's root node on, doc by doc;
+// before a new doc, rotation if 2,048 pools are open or 65,535 docs placed (PiXiuCtrl.cpp:13)
+__global__ void __launch_bounds__(64) k_pool_scan(uint32_t nshards, const PsaShard *shards, const PsaDoc *docs,
+                                                  const uint32_t *P, PsaPoolOut *out) {
+    const uint32_t s = blockIdx.x;
+    if (s >= nshards) return;
+    const PsaShard sh = shards[s];
+    PsaPoolOut o{kNone, 0, 0, 0};
+    if (sh.pools) {
+        auto S = [&](uint32_t x) { return x ? P[x - 1] : 0u; };  // blocks before position x
+        int32_t pools = 1, used = kNodeBlocks;  // the root (SuffixTree::init_prop)
+        for (uint32_t g = sh.doc0; g < sh.doc0 + sh.ndocs; ++g) {
+            const PsaDoc d = docs[g];
+            if (g > sh.doc0 && d.msg && (pools >= kRotatePools || g - sh.doc0 == (uint32_t)kChunkSlots)) {
+                o.rot_doc = g;
+                break;
+            }
+            uint32_t cur = d.start;
+            const uint32_t end = d.start + d.len, send = S(end);
+            uint32_t base = S(cur);
+            while ((uint32_t)used + (send - base) > (uint32_t)kPoolBlocks) {
+                const uint32_t k = pool_search(P, cur, end, base, (uint32_t)(kPoolBlocks - used));
+                const uint32_t sk = S(k);
+                int32_t u = used + (int32_t)(sk - base);
+                const bool split = P[k] - sk == 16u;
+                const int32_t ch[4] = {kNodeBlocks, split ? kNodeBlocks : kEdgeBlocks, kEdgeBlocks, kEdgeBlocks};
+                for (int i = 0; i < (split ? 4 : 2); ++i) {
+                    if (u + ch[i] > kPoolBlocks) {
+                        ++pools;
+                        u = ch[i];
+                    } else {
+                        u += ch[i];
+                    }
+                }
+                used = u;
+                cur = k + 1;
+                base = P[k];
+            }
+            used += (int32_t)(send - base);
+        }
+        o.pools = pools;
+        o.used = used;
+    }
+    if (lane_id() == 0) out[s] = o;
+}
+
 struct Max {
     PSA_DEV uint32_t operator()(uint32_t a, uint32_t b) const { return a > b ? a : b; }
 };
@@ -695,13 +848,16 @@ struct Max {
 // Runs the pipeline; messages land in every new doc's msg array, the new records' chunk /
 // slot / status in rec_*, and shard_flag[k] (device, zeroed by the caller) is set for shards
 // whose stream may differ from the reference's (walk them with k_gst_encode instead).
+// With any_pools, the shards marked `pools` get the MemPool emulation: pool_out[k] (device)
+// says where shard k's live chunk rotates inside this window (see k_pool_scan).
 hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDoc *docs, uint32_t nshards,
                    const PsaShard *shards, uint32_t N, uint32_t *rec_chunk, uint32_t *rec_idx, uint32_t *rec_status,
-                   uint32_t *shard_flag, PsaStats *st) {
+                   uint32_t *shard_flag, bool any_pools, PsaPoolOut *pool_out, PsaStats *st) {
     if (!N || !ndocs) return hipSuccess;
     auto get = [&](uint64_t n) { return A.alloc(A.self, n); };
     auto put = [&](void *p, uint64_t n) { A.release(A.self, p, n); };
-    hipEvent_t e0, e1, e2, e3;
+    hipEvent_t e0, e1, e2, e3, e4;
+    PSA_CHECK(hipEventCreate(&e4));
     PSA_CHECK(hipEventCreate(&e0));
     PSA_CHECK(hipEventCreate(&e1));
     PSA_CHECK(hipEventCreate(&e2));
@@ -931,8 +1087,38 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     k_psa_runs<<<blocks(N), tb, 0, s>>>(N, G, pdoc, docs, dist, psvp, nsvp, lcp_p, lcp_n, shard_flag);
     k_psa_place<<<blocks(ndocs), tb, 0, s>>>(ndocs, docs, shards, rec_chunk, rec_idx, rec_status);
     PSA_CHECK(hipEventRecord(e3, s));
-    PSA_CHECK(hipEventSynchronize(e3));
+    if (any_pools) {  // ---- MemPool emulation (rotation points)
+        auto *code = (uint8_t *)get(n64 + 64);
+        auto *E = (uint32_t *)keys, *blk = (uint32_t *)keys + N;  // the key buffer is free
+        uint32_t *P = vals;
+        PSA_CHECK(hipMemsetAsync(cnt + 14, 0, 4, s));
+        k_pool_leaf<<<blocks(N), tb, 0, s>>>(N, G, pdoc, docs, shards, dist, psvp, nsvp, lcp_p, lcp_n, code, E, cnt + 14);
+        PSA_CHECK(hipStreamSynchronize(s));
+        uint32_t nc = 0;
+        PSA_CHECK(hipMemcpy(&nc, cnt + 14, 4, hipMemcpyDeviceToHost));
+        uint64_t cap = 1024;
+        while (cap < 2ull * nc) cap <<= 1;
+        auto *tab = (PoolSlot *)get(cap * sizeof(PoolSlot));
+        PSA_CHECK(hipMemsetAsync(tab, 0xff, cap * sizeof(PoolSlot), s));
+        const uint32_t mask = (uint32_t)(cap - 1);
+        k_pool_insert<<<blocks(N), tb, 0, s>>>(N, code, E, lcp_p, lcp_n, tab, mask);
+        k_pool_blocks<<<blocks(N), tb, 0, s>>>(N, code, E, lcp_p, lcp_n, tab, mask, blk);
+        size_t tsz = 0;
+        PSA_CHECK(rocprim::inclusive_scan(nullptr, tsz, blk, P, (size_t)N, rocprim::plus<uint32_t>(), s));
+        void *tmp2 = get(tsz + 256);
+        PSA_CHECK(rocprim::inclusive_scan(tmp2, tsz, blk, P, (size_t)N, rocprim::plus<uint32_t>(), s));
+        k_pool_scan<<<nshards, 64, 0, s>>>(nshards, shards, docs, P, pool_out);
+        PSA_CHECK(hipGetLastError());
+        PSA_CHECK(hipStreamSynchronize(s));
+        put(tmp2, tsz + 256);
+        put(tab, cap * sizeof(PoolSlot));
+        put(code, n64 + 64);
+        if (st) st->candidates = nc;
+    }
+    PSA_CHECK(hipEventRecord(e4, s));
+    PSA_CHECK(hipEventSynchronize(e4));
     if (st) {
+        PSA_CHECK(hipEventElapsedTime(&st->ms_pool, e3, e4));
         PSA_CHECK(hipEventElapsedTime(&st->ms_sort, e0, e1));
         PSA_CHECK(hipEventElapsedTime(&st->ms_lcp, e1, e2));
         PSA_CHECK(hipEventElapsedTime(&st->ms_msg, e2, e3));
@@ -947,6 +1133,7 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     (void)hipEventDestroy(e1);
     (void)hipEventDestroy(e2);
     (void)hipEventDestroy(e3);
+    (void)hipEventDestroy(e4);
     put(lcp_n, n64 * 2);
     put(dist, n64 * 2);
     put(G, n64 + 64);

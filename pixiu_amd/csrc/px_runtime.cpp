@@ -37,7 +37,7 @@ hipError_t launch_gst_encode(hipStream_t, const GstShard *, uint32_t, const uint
                              const uint8_t *, uint32_t *, uint32_t *, uint32_t *, uint32_t *, ShardState *,
                              uint32_t *);
 hipError_t psa_run(hipStream_t, const PsaAlloc &, uint32_t, const PsaDoc *, uint32_t, const PsaShard *, uint32_t,
-                   uint32_t *, uint32_t *, uint32_t *, uint32_t *, PsaStats *);
+                   uint32_t *, uint32_t *, uint32_t *, uint32_t *, bool, PsaPoolOut *, PsaStats *);
 hipError_t launch_gst_emit(hipStream_t, uint32_t, const uint8_t *const *, const uint32_t *, uint8_t *const *,
                            const uint8_t *, const uint32_t *, uint32_t *, uint32_t *);
 hipError_t launch_compact(hipStream_t, uint32_t, uint8_t *const *, const uint32_t *, uint8_t *, const uint64_t *);
@@ -773,16 +773,21 @@ struct px_ctx {
         pending_state.clear();
     }
 
-    // text-only arena of a PSA shard: the live chunk's docs and room for B more bytes
+    // text-only arena of a PSA shard: the live chunk's docs (from hs.ctext_off: a rotation
+    // inside a batch leaves the closed chunks' text in front of it) and room for B more bytes
     void text_reserve(Shard &s, uint64_t B) {
-        const uint64_t need = s.text_end + B;
-        if (s.arena && s.text_only && need <= s.text_cap) return;
+        const uint64_t live_off = s.text_only ? s.hs.ctext_off : 0;
+        const uint64_t live = s.text_end - live_off;
+        if (s.arena && s.text_only && live_off == 0 && s.text_end + B <= s.text_cap) return;
+        const uint64_t need = live + B;
         const uint64_t cap = round_up(std::max(need, s.text_cap * 3 / 2) + 1024, 256);
         auto *a = (uint8_t *)heap.alloc(cap);
         if (s.arena) {
-            if (s.text_end) hcheck(hipMemcpyAsync(a, s.text, s.text_end, hipMemcpyDeviceToDevice, stream));
+            if (live) hcheck(hipMemcpyAsync(a, s.text + live_off, live, hipMemcpyDeviceToDevice, stream));
             deferred_release.emplace_back(s.arena, s.arena_bytes);
         }
+        s.text_end = live;
+        s.hs.ctext_off = 0;
         s.arena = a;
         s.arena_bytes = cap;
         s.text = a;
@@ -801,13 +806,20 @@ struct px_ctx {
     // a PSA shard's live chunk goes back to the walk: full arena, text copied, the live
     // docs' starts uploaded; returns the docs k_gst_encode must re-walk first
     uint32_t upgrade_to_walk(Shard &s, uint64_t B, uint32_t D) {
-        const uint64_t live = s.text_end;  // PSA shards keep ctext_off == 0
-        const uint32_t docs = s.hs.n_docs;
-        std::vector<uint32_t> base(docs + 1, 0);
-        if (docs) {
+        std::vector<uint32_t> lens;
+        if (s.hs.n_docs) {
             const Chunk &ch = chunks[s.chunks[s.hs.chunk_seq]];
-            for (uint32_t i = 0; i < docs; ++i) base[i + 1] = base[i] + ch.doc_len[i];
+            lens.assign(ch.doc_len.begin(), ch.doc_len.begin() + s.hs.n_docs);
         }
+        return upgrade_to_walk(s, B, D, s.text_only ? s.hs.ctext_off : 0, lens);
+    }
+    // the live chunk's docs (lens) start at arena text offset live_off; everything from there
+    // to text_end (this batch's docs included) moves to the walk's arena
+    uint32_t upgrade_to_walk(Shard &s, uint64_t B, uint32_t D, uint64_t live_off, const std::vector<uint32_t> &lens) {
+        const uint64_t live = s.text_end - live_off;
+        const uint32_t docs = (uint32_t)lens.size();
+        std::vector<uint32_t> base(docs + 1, 0);
+        for (uint32_t i = 0; i < docs; ++i) base[i + 1] = base[i] + lens[i];
         void *old_arena = s.arena;
         const uint64_t old_bytes = s.arena_bytes;
         uint8_t *old_text = s.text;
@@ -820,7 +832,7 @@ struct px_ctx {
         s.hs.chunk_seq = seq;
         s.text_end = 0;
         shard_reserve(s, live + B, docs + D);
-        if (live) hcheck(hipMemcpyAsync(s.text, old_text, live, hipMemcpyDeviceToDevice, stream));
+        if (live) hcheck(hipMemcpyAsync(s.text, old_text + live_off, live, hipMemcpyDeviceToDevice, stream));
         h2d(s.doc_base, base.data(), base.size() * 4);
         s.text_end = live;
         if (old_arena) deferred_release.emplace_back(old_arena, old_bytes);
@@ -1854,10 +1866,8 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
 
     phase.mark("which shards take the suffix-array path ");
     // ---- which shards take the suffix-array path (px_psa.hip)
-    // A live chunk is encoded by PSA while it provably cannot rotate (<= 65,535 docs and
-    // <= kPsaMaxText doc bytes): its suffix tree is then never built.  A live chunk that
-    // outgrows that, or whose stream the PSA check flags, goes to k_gst_encode, which
-    // first re-walks (replays) the docs PSA encoded.
+    // A PSA live chunk never has a suffix tree.  One whose stream the PSA check flags goes
+    // to k_gst_encode, which first re-walks (replays) the docs PSA encoded.
     const bool psa_on = psa_enabled();
     // a PSA live chunk that is slot-full rotates at this batch's first doc (PiXiuCtrl.cpp:13):
     // the new chunk starts empty, so the rotation is done here and the batch stays on PSA
@@ -1866,18 +1876,22 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         if (sh.psa && w.docs > 0 && sh.hs.n_docs == (uint32_t)kChunkSlots) {
             sh.hs.chunk_seq++;
             sh.hs.n_docs = 0;
+            sh.hs.ctext_off = 0;
             sh.text_end = 0;
         }
     }
+    // A live chunk is encoded by PSA unless it already has a suffix tree (a walked chunk).
+    // Where the live chunk could rotate inside the batch (more than kPsaMaxText doc bytes),
+    // the MemPool accounting is emulated on the suffix array (k_pool_*) and the docs after a
+    // rotation go to the next chunk in another round.
     std::vector<uint8_t> wpsa(work.size(), 0);
-    std::vector<uint32_t> wreplay(work.size(), 0);
+    std::vector<uint32_t> wreplay(work.size(), 0), wr0(work.size());
     for (size_t k = 0; k < work.size(); ++k) {
         const Work &w = work[k];
         const Shard &sh = *w.s;
         const bool fresh = sh.psa || (sh.hs.epoch == 0 && sh.hs.n_docs == 0);
-        const uint64_t live_text = sh.psa ? sh.text_end : 0;
-        wpsa[k] = psa_on && fresh && w.docs > 0 && (uint64_t)sh.hs.n_docs + w.docs <= (uint64_t)kChunkSlots &&
-                  live_text + w.bytes <= kPsaMaxText;
+        wpsa[k] = psa_on && fresh && w.docs > 0;
+        wr0[k] = w.r0;
     }
 
     phase.mark("arenas, doc destinations, comp scratch");
@@ -1913,40 +1927,108 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     hcheck(launch_doc_write(stream, n, dkeys, dkoff, raw_docs ? nullptr : dvals, dvoff, d_dst));
 
     phase.mark("the suffix-array path over the PSA shard");
-    // ---- the suffix-array path over the PSA shards (messages, placement, check flags)
+    // ---- the suffix-array path over the PSA shards (messages, placement, check flags), in
+    // rounds: a round takes every unfinished shard's live chunk plus a window of its next
+    // docs; a shard whose live chunk rotates inside the window keeps the docs before the
+    // rotation and starts the next round with an empty chunk
     hcheck(hipEventRecord(ev0, stream));
-    uint32_t psa_shards = 0, walk_shards = 0;
+    uint32_t psa_shards = 0, walk_shards = 0, psa_rounds = 0, psa_rotations = 0;
     double psa_ms = 0;
     {
-        std::vector<PsaDoc> pd;
-        std::vector<PsaShard> ps;
-        std::vector<size_t> pwork;
-        uint64_t gpos = 0;
+        struct Run {
+            size_t k;
+            std::vector<uint32_t> recs;  // valid records, in order
+            size_t next = 0;             // first record not placed yet
+            uint32_t seq = 0;
+            std::vector<std::pair<const uint8_t *, uint32_t>> live;  // live chunk docs
+            uint64_t live_bytes = 0, live_off = 0;
+            uint64_t window = 0;  // new doc bytes per round while the chunk may rotate
+            bool done = false;
+        };
+        std::vector<Run> runs;
+        const uint64_t win0 = [] {
+            const char *e = std::getenv("PX_PSA_WINDOW_MB");
+            return (uint64_t)((e ? std::atof(e) : 12.0) * 1048576.0);
+        }();
         for (size_t k = 0; k < work.size(); ++k) {
             if (!wpsa[k]) continue;
             const Work &w = work[k];
             Shard &sh = *w.s;
-            const uint32_t si = (uint32_t)ps.size();
-            uint32_t slot = 0;
-            uint64_t off = 0;
-            if (sh.psa && sh.hs.n_docs) {  // the live chunk's earlier docs: text, no messages
+            Run u;
+            u.k = k;
+            u.seq = sh.hs.chunk_seq;
+            for (uint32_t r = w.r0; r < w.r1; ++r)
+                if (doc_len[r] != 0xffffffffu) u.recs.push_back(r);
+            if (sh.psa && sh.hs.n_docs) {  // the live chunk's earlier docs (text_reserve put them at 0)
                 const Chunk &ch = chunks[sh.chunks[sh.hs.chunk_seq]];
                 for (uint32_t i = 0; i < sh.hs.n_docs; ++i) {
-                    pd.push_back(PsaDoc{sh.text + off, nullptr, (uint32_t)(gpos + off), ch.doc_len[i], si, slot++, 0, 0});
-                    off += ch.doc_len[i];
+                    u.live.emplace_back(sh.text + u.live_bytes, ch.doc_len[i]);
+                    u.live_bytes += ch.doc_len[i];
                 }
             }
-            for (uint32_t r = w.r0; r < w.r1; ++r) {
-                if (doc_len[r] == 0xffffffffu) continue;
-                pd.push_back(PsaDoc{dst[r], msgs + (cdst[r] - comp_scratch), (uint32_t)(gpos + off), doc_len[r], si,
-                                    slot++, r, 0});
-                off += doc_len[r];
-            }
-            ps.push_back(PsaShard{(uint32_t)gpos, (uint32_t)off, sh.hs.chunk_seq, 0});
-            pwork.push_back(k);
-            gpos += off;
+            u.window = win0;
+            runs.push_back(std::move(u));
         }
-        if (!ps.empty()) {
+        auto *d_pool = (PsaPoolOut *)heap.alloc(std::max<size_t>(runs.size(), 1) * sizeof(PsaPoolOut) + 64);
+        const auto tp = std::chrono::steady_clock::now();
+        PsaStats pst{};
+        for (;;) {
+            std::vector<PsaDoc> pd;
+            std::vector<PsaShard> ps;
+            std::vector<size_t> prun;
+            std::vector<uint32_t> pcount;  // new docs in the window
+            uint64_t gpos = 0;
+            bool any_pools = false;
+            for (size_t ri = 0; ri < runs.size(); ++ri) {
+                Run &u = runs[ri];
+                if (u.done) continue;
+                Shard &sh = *work[u.k].s;
+                if (u.live.size() == (size_t)kChunkSlots) {  // slot-full: rotation before the next doc
+                    ++u.seq;
+                    ++psa_rotations;
+                    u.live.clear();
+                    u.live_bytes = 0;
+                    u.live_off = (uint64_t)(dst[u.recs[u.next]] - sh.text);
+                }
+                const uint32_t si = (uint32_t)ps.size();
+                PsaShard psh{};
+                psh.base = (uint32_t)gpos;
+                psh.chunk = u.seq;
+                psh.doc0 = (uint32_t)pd.size();
+                uint64_t off = 0;
+                uint32_t slot = 0;
+                for (const auto &lv : u.live) {
+                    pd.push_back(PsaDoc{lv.first, nullptr, (uint32_t)(gpos + off), lv.second, si, slot++, 0, 0});
+                    off += lv.second;
+                }
+                // the window: every remaining doc if the chunk cannot rotate on them,
+                // else up to u.window new bytes (at least one doc)
+                uint64_t rest = 0;
+                for (size_t i = u.next; i < u.recs.size(); ++i) rest += doc_len[u.recs[i]];
+                const bool may_rotate = u.live_bytes + rest > kPsaMaxText;
+                uint32_t cnt = 0;
+                uint64_t nb = 0;
+                for (size_t i = u.next; i < u.recs.size() && u.live.size() + cnt < (size_t)kChunkSlots; ++i) {
+                    const uint32_t r = u.recs[i];
+                    if (may_rotate && cnt > 0 && u.live_bytes + nb + doc_len[r] > std::max<uint64_t>(u.window, kPsaMaxText))
+                        break;
+                    pd.push_back(PsaDoc{dst[r], msgs + (cdst[r] - comp_scratch), (uint32_t)(gpos + off), doc_len[r], si,
+                                        slot++, r, 0});
+                    off += doc_len[r];
+                    nb += doc_len[r];
+                    ++cnt;
+                }
+                psh.len = (uint32_t)off;
+                psh.ndocs = (uint32_t)(pd.size() - psh.doc0);
+                psh.pools = u.live_bytes + nb > kPsaMaxText ? 1u : 0u;
+                any_pools |= psh.pools != 0;
+                ps.push_back(psh);
+                prun.push_back(ri);
+                pcount.push_back(cnt);
+                gpos += off;
+            }
+            if (ps.empty()) break;
+            ++psa_rounds;
             if (gpos >= 0xfffffff0ull) throw PxFail{PX_ECAPACITY};  // a batch is split far below this
             auto *d_pd = (PsaDoc *)heap.alloc(pd.size() * sizeof(PsaDoc));
             auto *d_ps = (PsaShard *)heap.alloc(ps.size() * sizeof(PsaShard) + ps.size() * 4 + 64);
@@ -1956,31 +2038,75 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             hcheck(hipMemsetAsync(d_flag, 0, ps.size() * 4, stream));
             PsaAlloc A{[](void *self, uint64_t b) { return static_cast<px_ctx *>(self)->heap.alloc(b); },
                        [](void *self, void *p, uint64_t b) { static_cast<px_ctx *>(self)->heap.release(p, b); }, this};
-            PsaStats pst{};
-            const auto tp = std::chrono::steady_clock::now();
+            PsaStats rst{};
             hcheck(psa_run(stream, A, (uint32_t)pd.size(), d_pd, (uint32_t)ps.size(), d_ps, (uint32_t)gpos, d_chunk,
-                           d_idx, d_status, d_flag, &pst));
+                           d_idx, d_status, d_flag, any_pools, d_pool, &rst));
             std::vector<uint32_t> flag(ps.size());
+            std::vector<PsaPoolOut> pout(ps.size());
             d2h(flag.data(), d_flag, ps.size() * 4);
+            if (any_pools) d2h(pout.data(), d_pool, ps.size() * sizeof(PsaPoolOut));
             sync();
-            psa_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp).count();
-            psa_stats = pst;
+            if (psa_rounds == 1) {
+                pst = rst;
+            } else {
+                pst.ms_sort += rst.ms_sort;
+                pst.ms_lcp += rst.ms_lcp;
+                pst.ms_msg += rst.ms_msg;
+                pst.iterations = std::max(pst.iterations, rst.iterations);
+            }
+            pst.ms_pool += any_pools ? rst.ms_pool : 0.f;
             heap.release(d_pd, pd.size() * sizeof(PsaDoc));
             heap.release(d_ps, ps.size() * sizeof(PsaShard) + ps.size() * 4 + 64);
             for (size_t i = 0; i < ps.size(); ++i) {
-                const size_t k = pwork[i];
-                if (!flag[i]) {
-                    ++psa_shards;
+                Run &u = runs[prun[i]];
+                Shard &sh = *work[u.k].s;
+                if (flag[i]) {
+                    // the stale-pair check fired: this shard's live chunk and its remaining docs
+                    // go to the walk (the text copied includes them; their records keep reading
+                    // their docs from the old arena, released at the end of the batch)
+                    std::vector<uint32_t> lens;
+                    for (const auto &lv : u.live) lens.push_back(lv.second);
+                    sh.hs.chunk_seq = u.seq;
+                    wpsa[u.k] = 0;
+                    wr0[u.k] = u.recs[u.next];
+                    wreplay[u.k] = upgrade_to_walk(sh, 0, (uint32_t)(u.recs.size() - u.next), u.live_off, lens);
+                    u.done = true;
                     continue;
                 }
-                // the stale-pair check fired: this shard's live chunk goes to the walk
-                // (the text copied includes this batch's docs; its records keep reading their
-                // docs from the old arena, released at the end of the batch)
-                wpsa[k] = 0;
-                wreplay[k] = upgrade_to_walk(*work[k].s, 0, work[k].docs);
+                const uint32_t first_new = ps[i].doc0 + (uint32_t)u.live.size();
+                const bool rot = ps[i].pools && pout[i].rot_doc != kNone;
+                const uint32_t take = rot ? pout[i].rot_doc - first_new : pcount[i];
+                uint64_t took = 0;
+                for (uint32_t t = 0; t < take; ++t) {
+                    const uint32_t r = u.recs[u.next + t];
+                    u.live.emplace_back(dst[r], doc_len[r]);
+                    took += doc_len[r];
+                }
+                u.live_bytes += took;
+                u.next += take;
+                if (rot) {
+                    // the window for the next chunk: a little more than this one held
+                    u.window = std::max<uint64_t>(kPsaMaxText, u.live_bytes + u.live_bytes / 12);
+                    ++u.seq;
+                    ++psa_rotations;
+                    u.live.clear();
+                    u.live_bytes = 0;
+                    u.live_off = u.next < u.recs.size() ? (uint64_t)(dst[u.recs[u.next]] - sh.text) : sh.text_end;
+                }
+                if (u.next >= u.recs.size()) {
+                    u.done = true;
+                    ++psa_shards;
+                    sh.psa = true;
+                    sh.hs.n_docs = (uint32_t)u.live.size();
+                    sh.hs.chunk_seq = u.seq;
+                    sh.hs.ctext_off = u.live_off;
+                }
             }
             flush_shard_init();
         }
+        heap.release(d_pool, std::max<size_t>(runs.size(), 1) * sizeof(PsaPoolOut) + 64);
+        psa_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp).count();
+        psa_stats = pst;
     }
 
     phase.mark("the GST walk for the other shards (encod");
@@ -2000,7 +2126,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         g.node_cap = w.s->node_cap;
         g.hash_mask = (uint32_t)(w.s->hash_cap - 1);
         g.doc_cap = w.s->doc_cap;
-        g.r0 = w.r0;
+        g.r0 = wr0[k];
         g.r1 = w.r1;
         g.replay = wreplay[k];
         gs.push_back(g);
@@ -2054,17 +2180,15 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         if (r < n && rstatus[r] == kOk) rstatus[r] = kErrCorrupt;
     }
     for (size_t i = 0; i < gwork.size(); ++i) work[gwork[i]].s->hs = stout[i];
-    for (size_t k = 0; k < work.size(); ++k)
-        if (wpsa[k]) {  // the PSA shard's live chunk grew by this batch's docs (no tree)
-            work[k].s->psa = true;
-            work[k].s->hs.n_docs += work[k].docs;
-        }
     stats.last_psa_ms = psa_ms;
     stats.last_psa_sort_ms = psa_shards ? psa_stats.ms_sort : 0;
     stats.last_psa_lcp_ms = psa_shards ? psa_stats.ms_lcp : 0;
     stats.last_psa_msg_ms = psa_shards ? psa_stats.ms_msg : 0;
     stats.last_psa_iters = psa_shards ? psa_stats.iterations : 0;
     stats.last_psa_shards = psa_shards;
+    stats.last_psa_rounds = psa_rounds;
+    stats.last_psa_rotations = psa_rotations;
+    stats.last_psa_pool_ms = psa_shards ? psa_stats.ms_pool : 0;
     stats.last_walk_shards = walk_shards;
     if (d_gs) heap.release(d_gs, gs.size() * sizeof(GstShard));
     {

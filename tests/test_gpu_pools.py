@@ -1,0 +1,106 @@
+"""Chunk rotation on the suffix-array path (px_psa.hip k_pool_*).
+
+The reference rotates its live chunk before a doc once 2,048 MemPool pools are open
+(PiXiuCtrl.cpp:13); the pool count follows the leaves and inner nodes its suffix tree
+creates (MemPool.cpp:7-37, SuffixTree.cpp:148-227).  The suffix-array path emulates that
+accounting and encodes shards of any size in rounds (one chunk window per round).  These
+tests compare it with the oracle's single instance (chunk numbers, slots and compressed
+bytes of every record) on shards that rotate, within one batch and across batches.  The reference's own rotation fixtures
+(tests/golden/rotation.json, test_gpu_golden.py) take the same path.
+"""
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+from _oracle import Oracle, assemble
+
+pytestmark = pytest.mark.gpu
+px = pytest.importorskip("pixiu_amd")
+
+
+def _oracle_shards(cp, rps):
+    """oracle encode_docs per shard of rps records (rps = 0: one shard), on threads"""
+    n = cp.n
+    bounds = [(a, min(n, a + rps)) for a in range(0, n, rps)] if rps else [(0, n)]
+
+    def one(ab):
+        a, b = ab
+        return Oracle().encode_docs([assemble(cp.key(i), cp.val(i)) for i in range(a, b)])
+
+    with ThreadPoolExecutor(min(8, len(bounds))) as ex:
+        parts = list(ex.map(one, bounds))
+    comp, chunk, idx = [], [], []
+    for c, ch, ix in parts:
+        comp += c
+        chunk += ch
+        idx += ix
+    return comp, chunk, idx
+
+
+def _set(st, cp, pieces):
+    res = []
+    for a, b in pieces:
+        res.append(st.set_batch([cp.key(i) for i in range(a, b)], [cp.val(i) for i in range(a, b)]))
+    return np.concatenate(res)
+
+
+def test_single_instance_rotates_like_the_oracle(store_factory):
+    """config 3, 420 records (25 MB) in one batch at rps = 0: two rotations by pool count"""
+    from pixiu_amd import synth
+    cp = synth.make(3, 420)
+    st = store_factory(records_per_shard=0)
+    r = _set(st, cp, [(0, cp.n)])
+    s = st.stats()
+    assert (s["last_psa_shards"], s["last_walk_shards"]) == (1, 0)
+    assert s["last_psa_rotations"] >= 1 and s["last_psa_rounds"] >= 2
+    assert int(r["status"].max()) == 0
+    oc, ochunk, oidx = _oracle_shards(cp, 0)
+    assert r["chunk"].tolist() == ochunk and r["idx"].tolist() == oidx
+    assert max(ochunk) >= 1
+    assert st.export(px.records_of(r)) == oc
+    sample = list(range(0, cp.n, 7))
+    assert st.parse_batch(px.records_of(r[sample]), px.EXACT) == [assemble(cp.key(i), cp.val(i)) for i in sample]
+
+
+def test_rotation_across_batches_and_shards(store_factory):
+    """config 3, two 300-record shards fed in 4 batches of 150: rotations fall inside
+    batches and the live chunk is carried across batch boundaries"""
+    from pixiu_amd import synth
+    cp = synth.make(3, 600)
+    st = store_factory(records_per_shard=300)
+    r = _set(st, cp, [(0, 150), (150, 300), (300, 450), (450, 600)])
+    assert int(r["status"].max()) == 0
+    oc, ochunk, oidx = _oracle_shards(cp, 300)
+    assert r["chunk"].tolist() == ochunk and r["idx"].tolist() == oidx
+    assert max(ochunk) >= 1
+    assert st.export(px.records_of(r)) == oc
+    got = st.get_batch([cp.key(i) for i in range(0, cp.n, 5)])
+    want = _oracle_get(cp, 300, range(0, cp.n, 5))
+    assert got == want
+
+
+def _oracle_get(cp, rps, rows):
+    out = {}
+    for a in range(0, cp.n, rps):
+        want = [i for i in rows if a <= i < a + rps]
+        if not want:
+            continue
+        o = Oracle().run([cp.key(i) for i in range(a, a + rps)], [cp.val(i) for i in range(a, a + rps)])
+        for i in want:
+            out[i] = o["get"][i - a]
+    return [out[i] for i in rows]
+
+
+@pytest.mark.parametrize("cfg,n,rps", [(2, 20000, 0), (4, 60000, 0), (5, 400, 200)])
+def test_pool_emulation_matches_oracle(cfg, n, rps, store_factory):
+    """configs 2 / 4 (byte-251 stress) / 5: every record's chunk, slot and bytes"""
+    from pixiu_amd import synth
+    cp = synth.make(cfg, n)
+    st = store_factory(records_per_shard=rps)
+    r = st.set_batch((cp.keys, cp.koff.astype(np.uint64)), (cp.vals, cp.voff.astype(np.uint64)))
+    assert int(r["status"].max()) == 0
+    oc, ochunk, oidx = _oracle_shards(cp, rps)
+    assert r["chunk"].tolist() == ochunk and r["idx"].tolist() == oidx
+    assert max(ochunk) >= 1
+    assert st.export(px.records_of(r)) == oc

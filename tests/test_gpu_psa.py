@@ -3,9 +3,8 @@ GST walk it replaces and against the oracle:
 
 * every BASELINE config: the same compressed bytes and placement with PX_PSA=0 (every
   shard walked by k_gst_encode) and with the default (shards encoded by PSA);
-* a live chunk that outgrows the PSA bound in a later batch is handed to the walk,
-  which re-walks (replays) the docs PSA encoded: bytes equal the oracle's single
-  instance across the switch;
+* a live chunk that outgrows the no-rotation bound in a later batch stays on PSA with
+  the MemPool emulation: bytes equal the oracle's single instance;
 * inputs on which the stale-pair check fires (small alphabets) still match the oracle.
 """
 import os
@@ -50,9 +49,9 @@ def test_psa_equals_walk(cfg, n, rps, store_factory):
     assert ga == gb
 
 
-def test_psa_chunk_outgrows_bound_then_walk(store_factory, oracle):
-    """rps = 0: two batches encoded by PSA (6 MB), a third pushes the live chunk past
-    kPsaMaxText: the walk replays the 6,000 PSA docs, then continues; every record
+def test_psa_chunk_outgrows_bound_stays_psa(store_factory, oracle):
+    """rps = 0: three batches; the third pushes the live chunk past kPsaMaxText, where the
+    MemPool accounting is emulated on the suffix array (no walk, no replay); every record
     equals the oracle's single instance."""
     from pixiu_amd import synth
     cp = synth.make(2, 9000)
@@ -61,7 +60,7 @@ def test_psa_chunk_outgrows_bound_then_walk(store_factory, oracle):
     for a in (0, 3000, 6000):
         res.append(st.set_batch([cp.key(i) for i in range(a, a + 3000)], [cp.val(i) for i in range(a, a + 3000)]))
         s = st.stats()
-        assert (s["last_psa_shards"], s["last_walk_shards"]) == ((1, 0) if a < 6000 else (0, 1))
+        assert (s["last_psa_shards"], s["last_walk_shards"]) == (1, 0)
     r = np.concatenate(res)
     assert int(r["status"].max()) == 0
     oc, ochunk, oidx = oracle.encode_docs([assemble(cp.key(i), cp.val(i)) for i in range(cp.n)])
