@@ -773,8 +773,8 @@ PSA_DEV uint32_t pool_search(const uint32_t *P, uint32_t lo, uint32_t hi, uint32
         const uint32_t stride = (hi - lo + 63) / 64;
         const uint32_t x = lo + lane * stride;
         const uint64_t m = __ballot(x < hi && P[x] - base > cap);
-        if (!m) {
-            lo = lo + 63 * stride + 1;
+        if (!m) {  // after the last probe inside the range
+            lo += (hi - 1 - lo) / stride * stride + 1;
             continue;
         }
         const uint32_t t = (uint32_t)__ffsll((long long)m) - 1u;
@@ -784,7 +784,7 @@ PSA_DEV uint32_t pool_search(const uint32_t *P, uint32_t lo, uint32_t hi, uint32
     }
     const uint32_t x = lo + lane;
     const uint64_t m = __ballot(x < hi && P[x] - base > cap);
-    return lo + (uint32_t)__ffsll((long long)m) - 1u;
+    return m ? lo + (uint32_t)__ffsll((long long)m) - 1u : hi - 1u;  // (m != 0 by the precondition)
 }
 
 // one wave per emulating shard: the pool state from the chunk's root node on, doc by doc;
@@ -1082,11 +1082,19 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     k_psa_lce<<<blocks((n64 + kLceSpan - 1) / kLceSpan), tb, 0, s>>>(N, (const uint64_t *)G, dist, psvp, nsvp, lcp_p,
                                                                      lcp_n);
     PSA_CHECK(hipEventRecord(e2, s));
+    if (verbose) {
+        PSA_CHECK(hipStreamSynchronize(s));
+        fprintf(stderr, "psa: links + lcp done\n");
+    }
     // ---- messages
     k_psa_msg0<<<blocks(N), tb, 0, s>>>(N, pdoc, docs, lcp_p, lcp_n);
     k_psa_runs<<<blocks(N), tb, 0, s>>>(N, G, pdoc, docs, dist, psvp, nsvp, lcp_p, lcp_n, shard_flag);
     k_psa_place<<<blocks(ndocs), tb, 0, s>>>(ndocs, docs, shards, rec_chunk, rec_idx, rec_status);
     PSA_CHECK(hipEventRecord(e3, s));
+    if (verbose) {
+        PSA_CHECK(hipStreamSynchronize(s));
+        fprintf(stderr, "psa: messages done\n");
+    }
     if (any_pools) {  // ---- MemPool emulation (rotation points)
         auto *code = (uint8_t *)get(n64 + 64);
         auto *E = (uint32_t *)keys, *blk = (uint32_t *)keys + N;  // the key buffer is free
@@ -1096,17 +1104,30 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         PSA_CHECK(hipStreamSynchronize(s));
         uint32_t nc = 0;
         PSA_CHECK(hipMemcpy(&nc, cnt + 14, 4, hipMemcpyDeviceToHost));
+        const bool pv = [] {
+            const char *v = std::getenv("PX_PSA_VERBOSE");
+            return v && *v == '1';
+        }();
+        if (pv) fprintf(stderr, "psa pools: %u split candidates\n", nc);
         uint64_t cap = 1024;
         while (cap < 2ull * nc) cap <<= 1;
         auto *tab = (PoolSlot *)get(cap * sizeof(PoolSlot));
         PSA_CHECK(hipMemsetAsync(tab, 0xff, cap * sizeof(PoolSlot), s));
         const uint32_t mask = (uint32_t)(cap - 1);
         k_pool_insert<<<blocks(N), tb, 0, s>>>(N, code, E, lcp_p, lcp_n, tab, mask);
+        if (pv) {
+            PSA_CHECK(hipStreamSynchronize(s));
+            fprintf(stderr, "psa pools: inserted (table %llu slots)\n", (unsigned long long)cap);
+        }
         k_pool_blocks<<<blocks(N), tb, 0, s>>>(N, code, E, lcp_p, lcp_n, tab, mask, blk);
         size_t tsz = 0;
         PSA_CHECK(rocprim::inclusive_scan(nullptr, tsz, blk, P, (size_t)N, rocprim::plus<uint32_t>(), s));
         void *tmp2 = get(tsz + 256);
         PSA_CHECK(rocprim::inclusive_scan(tmp2, tsz, blk, P, (size_t)N, rocprim::plus<uint32_t>(), s));
+        if (pv) {
+            PSA_CHECK(hipStreamSynchronize(s));
+            fprintf(stderr, "psa pools: blocks scanned\n");
+        }
         k_pool_scan<<<nshards, 64, 0, s>>>(nshards, shards, docs, P, pool_out);
         PSA_CHECK(hipGetLastError());
         PSA_CHECK(hipStreamSynchronize(s));
