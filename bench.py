@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--extra-steps", type=int, default=2, help="timed steps of each further config")
     ap.add_argument("--no-checks", action="store_true", help="skip the compat/exact/original parity counts")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-single", action="store_true",
+                    help="skip the single-instance leg (config 3 as one shard, GPU and CPU)")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) leg")
     ap.add_argument("--no-exact", action="store_true",
                     help="skip the exact-mode getitem (profiling runs: one compat batch per step only)")
@@ -90,6 +92,28 @@ def cpu_baseline(corpus, rps, budget_s):
         s += rps
     return {"set_MBps": raw / t_set / 1e6, "get_MBps": exp / t_get / 1e6, "records": nrec, "raw": raw,
             "shards": shards, "seconds": t_set + t_get}
+
+
+def cpu_single_instance(corpus, budget_s):
+    """The reference-shaped CPU baseline: ONE oracle instance (records_per_shard = 0, the
+    reference's single PiXiuCtrl with its chunk rotation), records set in order until half
+    the budget is spent, then every stored key read back."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _oracle import Oracle
+    sh = Oracle().new()
+    ks, raw = [], 0
+    t0 = time.perf_counter()
+    while len(ks) < corpus.n and time.perf_counter() - t0 < budget_s / 2:
+        k, v = corpus.key(len(ks)), corpus.val(len(ks))
+        if sh.set(k, v)[0] < 0:
+            raise RuntimeError("oracle setitem failed")
+        ks.append(k)
+        raw += len(k) + len(v)
+    t1 = time.perf_counter()
+    exp = sum(len(sh.get(k) or b"") for k in ks)
+    t2 = time.perf_counter()
+    return {"set_MBps": raw / (t1 - t0) / 1e6, "get_MBps": exp / (t2 - t1) / 1e6, "records": len(ks), "raw": raw,
+            "seconds": t2 - t0}
 
 
 def cpu_baseline_mt(corpus, rps, set_MBps_1t, budget_s):
@@ -518,8 +542,30 @@ def main():
                                              f"{mt['seconds']:.1f} s"}
     if not a.no_pcie and world == 1:
         line["pcie_inclusive"] = pcie_leg(st, px, corpus, r["keys_host"], r["out_cap"])
-    print(json.dumps(line), flush=True)
     st.close()
+    if not a.no_single and world == 1 and a.config == 3 and rps != 0:
+        # the same corpus as ONE shard (records_per_shard = 0): the reference's single
+        # instance, chunks rotated by its MemPool rule (suffix-array path with the pool
+        # emulation), next to the oracle's single instance on the CPU
+        torch.cuda.empty_cache()
+        r0 = run_config(a.config, a, rank, world, local, 1, 1, 0, None, checks=False)
+        s0 = summarize(a.config, r0, 0, world, a, None)
+        line["single_instance"] = {
+            "records_per_shard": 0, "setitem_MBps": s0["setitem_MBps"], "getitem_MBps": s0["getitem_MBps"],
+            "getitem_exact_MBps": s0.get("getitem_exact_MBps"), "compression_ratio": s0["compression_ratio"],
+            "ms_per_step": s0.get("ms_per_step"), "chunks": s0["encode_stage"].get("chunks"),
+            "psa_rounds": s0["encode_stage"].get("psa_rounds"),
+            "encode_stage_ms": s0["kernel_ms"]["encode_stage"],
+            "psa_split_ms": s0["encode_stage"].get("psa_split_ms")}
+        if not a.no_cpu:
+            c0 = cpu_single_instance(corpus, a.cpu_seconds)
+            line["single_instance"]["cpu_baseline"] = {
+                "value": round(c0["set_MBps"] + c0["get_MBps"], 4), "unit": "MB/s",
+                "set_MBps": round(c0["set_MBps"], 4), "get_MBps": round(c0["get_MBps"], 4), "cores": 1,
+                "kind": "port", "sample": f"first {c0['records']} records ({c0['raw'] / 1e6:.2f} MB) into one "
+                                          f"oracle instance, {c0['seconds']:.1f} s"}
+        r0["st"].close()
+    print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

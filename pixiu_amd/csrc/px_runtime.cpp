@@ -1786,7 +1786,9 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         hkeys.resize(hkoff[n] - hkoff[0]);
         d2h(hkeys.data(), keys + hkoff[0], hkeys.size());
         sync();
-        for (auto &o : hkoff) o -= hkoff[0];
+        // (rebase by a copy: hkoff[0] itself becomes 0 on the first iteration)
+        const uint64_t k0 = hkoff[0];
+        for (auto &o : hkoff) o -= k0;
         dkeys = keys;
         dvals = vals;
         dkoff = koff;

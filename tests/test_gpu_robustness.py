@@ -98,3 +98,22 @@ def test_single_shard_batch_beyond_16mb(store_factory, oracle):
     oc, ochunk, oidx = oracle.encode_docs(_docs(cp, range(n)))
     assert st.export(px.records_of(r)) == oc
     assert r["chunk"].tolist() == ochunk and r["idx"].tolist() == oidx
+
+
+@pytest.mark.parametrize("rps", [0, 64])
+def test_device_inputs_with_offsets_not_starting_at_zero(rps, store_factory):
+    """set_batch_device over a sub-range of device arrays (koff / voff start past 0, as
+    the pieces of a batch split at kMaxBatchRaw do): every key is found again"""
+    import torch
+    from pixiu_amd import synth
+    cp = synth.make(2, 600)
+    kb = torch.from_numpy(cp.keys).cuda()
+    ko = torch.from_numpy(cp.koff.astype(np.int64)).cuda()
+    vb = torch.from_numpy(cp.vals).cuda()
+    vo = torch.from_numpy(cp.voff.astype(np.int64)).cuda()
+    st = store_factory(records_per_shard=rps)
+    for a, b in ((0, 250), (250, 600)):
+        r = st.set_batch_device(b - a, kb.data_ptr(), ko[a:].data_ptr(), vb.data_ptr(), vo[a:].data_ptr())
+        assert int(r["status"].max()) == 0
+    got = st.get_batch([cp.key(i) for i in range(cp.n)])
+    assert got == [assemble(cp.key(i), cp.val(i)) for i in range(cp.n)]
