@@ -1762,13 +1762,42 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         }
         if ((ko[n] - ko[0]) + (vo[n] - vo[0]) > kMaxBatchRaw) {
             int rc = PX_OK;
+            px_stats acc{};  // the batch's timings: the pieces' sums
             for (uint32_t a = 0; a < n;) {
                 uint32_t b = a + 1;
                 while (b < n && (ko[b + 1] - ko[a]) + (vo[b + 1] - vo[a]) <= kMaxBatchRaw) ++b;
                 const int r2 = set_batch(b - a, keys, koff + a, vals, voff + a, on_device, res ? res + a : nullptr);
                 if (rc == PX_OK) rc = r2;
+                acc.last_set_kernel_ms += stats.last_set_kernel_ms;
+                acc.last_walk_kernel_ms += stats.last_walk_kernel_ms;
+                acc.last_emit_kernel_ms += stats.last_emit_kernel_ms;
+                acc.last_psa_ms += stats.last_psa_ms;
+                acc.last_psa_sort_ms += stats.last_psa_sort_ms;
+                acc.last_psa_lcp_ms += stats.last_psa_lcp_ms;
+                acc.last_psa_msg_ms += stats.last_psa_msg_ms;
+                acc.last_psa_pool_ms += stats.last_psa_pool_ms;
+                acc.last_psa_rounds += stats.last_psa_rounds;
+                acc.last_psa_rotations += stats.last_psa_rotations;
+                acc.last_span_build_ms += stats.last_span_build_ms;
+                acc.last_psa_shards = std::max(acc.last_psa_shards, stats.last_psa_shards);
+                acc.last_walk_shards = std::max(acc.last_walk_shards, stats.last_walk_shards);
+                acc.last_psa_iters = std::max(acc.last_psa_iters, stats.last_psa_iters);
                 a = b;
             }
+            stats.last_set_kernel_ms = acc.last_set_kernel_ms;
+            stats.last_walk_kernel_ms = acc.last_walk_kernel_ms;
+            stats.last_emit_kernel_ms = acc.last_emit_kernel_ms;
+            stats.last_psa_ms = acc.last_psa_ms;
+            stats.last_psa_sort_ms = acc.last_psa_sort_ms;
+            stats.last_psa_lcp_ms = acc.last_psa_lcp_ms;
+            stats.last_psa_msg_ms = acc.last_psa_msg_ms;
+            stats.last_psa_pool_ms = acc.last_psa_pool_ms;
+            stats.last_psa_rounds = acc.last_psa_rounds;
+            stats.last_psa_rotations = acc.last_psa_rotations;
+            stats.last_span_build_ms = acc.last_span_build_ms;
+            stats.last_psa_shards = acc.last_psa_shards;
+            stats.last_walk_shards = acc.last_walk_shards;
+            stats.last_psa_iters = acc.last_psa_iters;
             return rc;
         }
     }
@@ -2048,15 +2077,17 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             d2h(flag.data(), d_flag, ps.size() * 4);
             if (any_pools) d2h(pout.data(), d_pool, ps.size() * sizeof(PsaPoolOut));
             sync();
+            if (!any_pools) rst.ms_pool = 0.f;
             if (psa_rounds == 1) {
                 pst = rst;
             } else {
                 pst.ms_sort += rst.ms_sort;
                 pst.ms_lcp += rst.ms_lcp;
                 pst.ms_msg += rst.ms_msg;
+                pst.ms_pool += rst.ms_pool;
+                pst.candidates += rst.candidates;
                 pst.iterations = std::max(pst.iterations, rst.iterations);
             }
-            pst.ms_pool += any_pools ? rst.ms_pool : 0.f;
             if (const char *v = std::getenv("PX_PSA_VERBOSE"); v && *v == '1') {
                 uint32_t nf = 0, nr = 0;
                 for (size_t i = 0; i < ps.size(); ++i) {

@@ -18,8 +18,10 @@ if [ "$SKIP_TESTS" != 1 ]; then
     > $O/${TAG}_gpu_tests.log 2>&1 || { echo "GPU TESTS FAILED"; tail -30 $O/${TAG}_gpu_tests.log; exit 1; }
   tail -2 $O/${TAG}_gpu_tests.log
 fi
-timeout -k 10 600 python -u bench.py $BENCH_ARGS > $O/${TAG}_bench.log 2>&1 || { echo "BENCH FAILED"; tail -20 $O/${TAG}_bench.log; exit 1; }
-tail -1 $O/${TAG}_bench.log
+if [ "${SKIP_BENCH:-0}" != 1 ]; then
+  timeout -k 10 600 python -u bench.py $BENCH_ARGS > $O/${TAG}_bench.log 2>&1 || { echo "BENCH FAILED"; tail -20 $O/${TAG}_bench.log; exit 1; }
+  tail -1 $O/${TAG}_bench.log
+fi
 PROF="bench.py --steps 1 --warmup 0 --no-cpu --no-pcie --no-checks --no-exact --configs= --config $CFG ${RPS:+--rps $RPS}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/${TAG}_ks -o ks --output-format csv \
   -- python3 $PROF > $O/${TAG}_ks.log 2>&1 || { echo "KTRACE FAILED"; tail -20 $O/${TAG}_ks.log; exit 1; }
@@ -33,4 +35,7 @@ REC=$(python3 -c "from pixiu_amd import synth; print(synth.FULL_SIZES[$CFG])")
 RPSV=${RPS:-$(python3 -c "import bench; print(bench.DEFAULT_RPS[$CFG])")}
 python3 tools/pmc_summary.py "$F" "$W" $O/${TAG}_pmc.json "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), python3 $PROF ($TAG)" $CFG $RPSV $REC > /dev/null
 find $O/${TAG}_ks -name '*kernel_stats.csv' | sort
+# the per-dispatch traces are large (gpurun copies back at most 64 MiB): keep the summaries
+find $O/${TAG}_ks $O/${TAG}_pmc_f $O/${TAG}_pmc_w -name '*kernel_trace.csv' -delete
+gzip -f $O/${TAG}_pmc_f/*counter_collection.csv $O/${TAG}_pmc_w/*counter_collection.csv 2>/dev/null
 echo DONE
