@@ -695,25 +695,45 @@ __global__ void __launch_bounds__(256) k_psa_place(uint32_t ndocs, const PsaDoc 
 // and on the other inside sigma.a: at most two candidates per sigma, the smaller splits.
 // (tools/proto/pool_proto.cpp is the CPU prototype, checked doc by doc against the walk.)
 // code: 0 no leaf, 1 leaf [5, 3], 2 split candidate, 3 split leaf [5, 5, 3, 3]
+// the links of one position packed for the candidates' climbs: one 16-byte load per step
+struct alignas(16) LinkRec {
+    uint32_t psv, nsv;
+    uint16_t lp, ln, dist, pad;
+};
+__global__ void __launch_bounds__(256) k_pool_pack(uint32_t N, const uint32_t *psvp, const uint32_t *nsvp,
+                                                   const uint16_t *lp, const uint16_t *ln, const uint16_t *dist,
+                                                   LinkRec *rec) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= N) return;
+    rec[p] = LinkRec{psvp[p], nsvp[p], lp[p], ln[p], dist[p], 0};
+}
 __global__ void __launch_bounds__(256) k_pool_leaf(uint32_t N, const uint8_t *G, const uint32_t *pdoc, const PsaDoc *docs,
-                                                   const PsaShard *shards, const uint16_t *dist, const uint32_t *psvp,
-                                                   const uint32_t *nsvp, const uint16_t *lp, const uint16_t *ln,
-                                                   uint8_t *code, uint32_t *E, uint32_t *ncand) {
+                                                   const PsaShard *shards, const LinkRec *R, uint8_t *code, uint32_t *E,
+                                                   uint32_t *ncand) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t c = 0;
     if (p < N) {
         const PsaDoc &d = docs[pdoc[p]];
         if (shards[d.shard].pools) {
-            const uint32_t lpv = lp[p], lnv = ln[p], l = max(lpv, lnv);
+            const LinkRec me = R[p];
+            const uint32_t l = max(me.lp, me.ln);
             if (p + l < d.start + d.len) {
                 c = 1;
                 if (l) {
                     uint32_t q = kNoPos;
-                    if (lnv < l) q = psvp[p];
-                    else if (lpv < l || dist[psvp[p]] == l) q = nsvp[p];
+                    if (me.ln < l) q = me.psv;
+                    else if (me.lp < l || R[me.psv].dist == l) q = me.nsv;
                     if (q != kNoPos) {
-                        const uint32_t e = earliest(psvp, nsvp, lp, ln, q, l);
-                        if (dist[e] > l && dist[q] > l && G[q + l] == G[e + l]) {
+                        // climb to E = the earliest occurrence of T[q .. q+l), keeping q's record
+                        LinkRec rq = R[q], r = rq;
+                        uint32_t e = q;
+                        for (;;) {
+                            if (r.lp >= l) e = r.psv;
+                            else if (r.ln >= l) e = r.nsv;
+                            else break;
+                            r = R[e];
+                        }
+                        if (r.dist > l && rq.dist > l && G[q + l] == G[e + l]) {
                             c = 2;
                             E[p] = e;
                         }
@@ -1100,7 +1120,10 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         auto *E = (uint32_t *)keys, *blk = (uint32_t *)keys + N;  // the key buffer is free
         uint32_t *P = vals;
         PSA_CHECK(hipMemsetAsync(cnt + 14, 0, 4, s));
-        k_pool_leaf<<<blocks(N), tb, 0, s>>>(N, G, pdoc, docs, shards, dist, psvp, nsvp, lcp_p, lcp_n, code, E, cnt + 14);
+        auto *rec = (LinkRec *)get(n64 * sizeof(LinkRec));
+        k_pool_pack<<<blocks(N), tb, 0, s>>>(N, psvp, nsvp, lcp_p, lcp_n, dist, rec);
+        k_pool_leaf<<<blocks(N), tb, 0, s>>>(N, G, pdoc, docs, shards, rec, code, E, cnt + 14);
+        put(rec, n64 * sizeof(LinkRec));  // (stream-ordered: the heap hands it out again only later)
         PSA_CHECK(hipStreamSynchronize(s));
         uint32_t nc = 0;
         PSA_CHECK(hipMemcpy(&nc, cnt + 14, 4, hipMemcpyDeviceToHost));
