@@ -2037,12 +2037,15 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
                 uint64_t rest = 0;
                 for (size_t i = u.next; i < u.recs.size(); ++i) rest += doc_len[u.recs[i]];
                 const bool may_rotate = u.live_bytes + rest > kPsaMaxText;
+                // (new bytes: up to the window, and at least half a window once the live
+                // chunk alone has outgrown it without rotating)
+                const uint64_t win = std::max<uint64_t>(u.window, kPsaMaxText);
+                const uint64_t budget = std::max<uint64_t>(win > u.live_bytes ? win - u.live_bytes : 0, win / 2);
                 uint32_t cnt = 0;
                 uint64_t nb = 0;
                 for (size_t i = u.next; i < u.recs.size() && u.live.size() + cnt < (size_t)kChunkSlots; ++i) {
                     const uint32_t r = u.recs[i];
-                    if (may_rotate && cnt > 0 && u.live_bytes + nb + doc_len[r] > std::max<uint64_t>(u.window, kPsaMaxText))
-                        break;
+                    if (may_rotate && cnt > 0 && nb + doc_len[r] > budget) break;
                     pd.push_back(PsaDoc{dst[r], msgs + (cdst[r] - comp_scratch), (uint32_t)(gpos + off), doc_len[r], si,
                                         slot++, r, 0});
                     off += doc_len[r];
@@ -2077,6 +2080,8 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             d2h(flag.data(), d_flag, ps.size() * 4);
             if (any_pools) d2h(pout.data(), d_pool, ps.size() * sizeof(PsaPoolOut));
             sync();
+            if (const char *e = std::getenv("PX_DEBUG_PSA_FLAG_ROUND"))  // test hook: the check fires
+                if ((uint32_t)std::atoi(e) == psa_rounds) std::fill(flag.begin(), flag.end(), 1u);
             if (!any_pools) rst.ms_pool = 0.f;
             if (psa_rounds == 1) {
                 pst = rst;

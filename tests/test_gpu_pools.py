@@ -8,6 +8,7 @@ tests compare it with the oracle's single instance (chunk numbers, slots and com
 bytes of every record) on shards that rotate, within one batch and across batches.  The reference's own rotation fixtures
 (tests/golden/rotation.json, test_gpu_golden.py) take the same path.
 """
+import os
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -104,3 +105,60 @@ def test_pool_emulation_matches_oracle(cfg, n, rps, store_factory):
     assert r["chunk"].tolist() == ochunk and r["idx"].tolist() == oidx
     assert max(ochunk) >= 1
     assert st.export(px.records_of(r)) == oc
+
+
+def _flag_round(k):
+    old = os.environ.get("PX_DEBUG_PSA_FLAG_ROUND")
+    os.environ["PX_DEBUG_PSA_FLAG_ROUND"] = str(k)
+    return old
+
+
+def _unflag(old):
+    if old is None:
+        os.environ.pop("PX_DEBUG_PSA_FLAG_ROUND", None)
+    else:
+        os.environ["PX_DEBUG_PSA_FLAG_ROUND"] = old
+
+
+def test_walk_takes_over_after_a_rotation(store_factory):
+    """The stale-pair check firing in the round after a rotation (test hook): the walk
+    takes the shard's remaining docs in the new chunk, whose text starts past the closed
+    chunk's in the arena; every record equals the oracle's single instance"""
+    from pixiu_amd import synth
+    cp = synth.make(3, 230)
+    st = store_factory(records_per_shard=0)
+    old = _flag_round(2)
+    try:
+        r = _set(st, cp, [(0, cp.n)])
+    finally:
+        _unflag(old)
+    s = st.stats()
+    assert s["last_walk_shards"] == 1 and s["last_psa_rotations"] >= 1
+    assert int(r["status"].max()) == 0
+    oc, ochunk, oidx = _oracle_shards(cp, 0)
+    assert r["chunk"].tolist() == ochunk and r["idx"].tolist() == oidx
+    assert st.export(px.records_of(r)) == oc
+
+
+def test_walk_replays_the_live_chunk(store_factory):
+    """The check firing on a batch whose live chunk came from an earlier batch (test
+    hook): the walk replays the live chunk's docs, then continues; later batches go on
+    from the walked tree"""
+    from pixiu_amd import synth
+    cp = synth.make(2, 3600)
+    st = store_factory(records_per_shard=0)
+    r1 = _set(st, cp, [(0, 2000)])
+    old = _flag_round(1)
+    try:
+        r2 = _set(st, cp, [(2000, 3000)])
+    finally:
+        _unflag(old)
+    assert st.stats()["last_walk_shards"] == 1
+    r3 = _set(st, cp, [(3000, 3600)])
+    r = np.concatenate([r1, r2, r3])
+    assert int(r["status"].max()) == 0
+    oc, ochunk, oidx = _oracle_shards(cp, 0)
+    assert r["chunk"].tolist() == ochunk and r["idx"].tolist() == oidx
+    assert st.export(px.records_of(r)) == oc
+    got = st.get_batch([cp.key(i) for i in range(0, cp.n, 9)])
+    assert got == [assemble(cp.key(i), cp.val(i)) for i in range(0, cp.n, 9)]
