@@ -29,9 +29,10 @@ sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 # records per shard (independent GST instances) benchmarked for each BASELINE config;
-# DESIGN.md §6 has the compression-vs-shard-size curve
-# (the suffix-array path keeps shards up to 8.4 MB of text at GPU speed: DESIGN.md §9)
-DEFAULT_RPS = {1: 0, 2: 2000, 3: 64, 4: 8000, 5: 126}
+# DESIGN.md §6 has the compression-vs-shard-size curve.  Config 3: 139 pages (8.35 MB) is
+# the largest shard whose live chunk cannot rotate (kPsaMaxText), and
+# compresses within 0.5 % of the reference's single instance (0.7734 vs 0.7698)
+DEFAULT_RPS = {1: 0, 2: 2000, 3: 139, 4: 8000, 5: 126}
 
 
 def parse():

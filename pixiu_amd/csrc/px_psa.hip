@@ -1124,16 +1124,21 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         k_pool_pack<<<blocks(N), tb, 0, s>>>(N, psvp, nsvp, lcp_p, lcp_n, dist, rec);
         k_pool_leaf<<<blocks(N), tb, 0, s>>>(N, G, pdoc, docs, shards, rec, code, E, cnt + 14);
         put(rec, n64 * sizeof(LinkRec));  // (stream-ordered: the heap hands it out again only later)
-        PSA_CHECK(hipStreamSynchronize(s));
+        // the candidate table: 2x the candidates, read back for big windows; a small window
+        // (one chunk, the single instance's rounds) sizes it from N and skips the round trip
         uint32_t nc = 0;
-        PSA_CHECK(hipMemcpy(&nc, cnt + 14, 4, hipMemcpyDeviceToHost));
+        uint64_t cap = 1024;
+        const bool small_n = N <= (1u << 26);
         const bool pv = [] {
             const char *v = std::getenv("PX_PSA_VERBOSE");
             return v && *v == '1';
         }();
-        if (pv) fprintf(stderr, "psa pools: %u split candidates\n", nc);
-        uint64_t cap = 1024;
-        while (cap < 2ull * nc) cap <<= 1;
+        if (!small_n || pv) {
+            PSA_CHECK(hipStreamSynchronize(s));
+            PSA_CHECK(hipMemcpy(&nc, cnt + 14, 4, hipMemcpyDeviceToHost));
+            if (pv) fprintf(stderr, "psa pools: %u split candidates\n", nc);
+        }
+        while (cap < 2ull * (small_n ? N : nc)) cap <<= 1;
         auto *tab = (PoolSlot *)get(cap * sizeof(PoolSlot));
         PSA_CHECK(hipMemsetAsync(tab, 0xff, cap * sizeof(PoolSlot), s));
         const uint32_t mask = (uint32_t)(cap - 1);
@@ -1153,14 +1158,13 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         }
         k_pool_scan<<<nshards, 64, 0, s>>>(nshards, shards, docs, P, pool_out);
         PSA_CHECK(hipGetLastError());
-        PSA_CHECK(hipStreamSynchronize(s));
-        put(tmp2, tsz + 256);
+        put(tmp2, tsz + 256);  // (stream-ordered reuse, as above)
         put(tab, cap * sizeof(PoolSlot));
         put(code, n64 + 64);
-        if (st) st->candidates = nc;
     }
     PSA_CHECK(hipEventRecord(e4, s));
     PSA_CHECK(hipEventSynchronize(e4));
+    if (any_pools && st) PSA_CHECK(hipMemcpy(&st->candidates, cnt + 14, 4, hipMemcpyDeviceToHost));
     if (st) {
         PSA_CHECK(hipEventElapsedTime(&st->ms_pool, e3, e4));
         PSA_CHECK(hipEventElapsedTime(&st->ms_sort, e0, e1));
