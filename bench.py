@@ -398,7 +398,10 @@ def summarize(cfg, r, rps, world, a, pmc_path):
                 else:  # every kernel of the encode stage, summed over its launches
                     tot_b = 0.0
                     for k, v in pmc.items():
-                        if isinstance(v, dict) and (k.startswith("k_psa") or "rocprim" in k or k == "k_gst_encode"):
+                        # (tools/pmc_summary.py names rocPRIM's sort / scan kernels by their
+                        # k_id_wrapper / k_scan_determinism template pieces)
+                        if isinstance(v, dict) and (k.startswith(("k_psa", "k_seg", "k_cmp", "k_pool")) or "rocprim" in k
+                                                    or k in ("k_gst_encode", "k_id_wrapper", "k_scan_determinism")):
                             tot_b += v["hbm_bytes_per_launch"] * v["dispatches"]
                     traffic = tot_b or None
                 tsrc = f"{os.path.relpath(pmc_path, ROOT)} ({pmc.get('source', '')})"
