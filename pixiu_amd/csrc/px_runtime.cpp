@@ -2477,7 +2477,9 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     deferred_release.clear();
 
     phase.mark("results");
-    // ---- results
+    // ---- results (the batch's device work is done when the call returns: slot scatters
+    // and span builds are not left running into the caller's next call)
+    hcheck(hipStreamSynchronize(stream));
     int rc = corrupt;
     uint64_t ub = 0;
     for (auto &sp : shards) ub += sp->hs.ub_reads;
