@@ -453,7 +453,7 @@ PSA_DEV uint32_t shard_of_rank(const PsaShard *shards, uint32_t nshards, uint32_
 }
 
 __global__ void __launch_bounds__(256) k_psa_ansv(uint32_t N, MinTree t, const PsaShard *shards, uint32_t nshards,
-                                                  uint32_t *psvp, uint32_t *nsvp) {
+                                                  uint2 *links) {
     const uint32_t lane = lane_id();
     const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (w * 64 >= N) return;
@@ -511,10 +511,19 @@ __global__ void __launch_bounds__(256) k_psa_ansv(uint32_t N, MinTree t, const P
             ns = fn;
         }
     }
-    if (live) {
-        psvp[v] = (ps != kNoPos && ps >= lo) ? sa[ps] : kNoPos;
-        nsvp[v] = (ns != kNoPos && ns < hi) ? sa[ns] : kNoPos;
-    }
+    if (live)  // in rank order (coalesced); k_psa_links_text moves them to text order
+        links[r] = make_uint2((ps != kNoPos && ps >= lo) ? sa[ps] : kNoPos, (ns != kNoPos && ns < hi) ? sa[ns] : kNoPos);
+}
+
+// the links in text order: one scattered 8-byte read per position instead of two
+// scattered 4-byte writes in k_psa_ansv (rank = the inverse suffix array)
+__global__ void __launch_bounds__(256) k_psa_links_text(uint32_t N, const uint32_t *rank, const uint2 *links,
+                                                        uint32_t *psvp, uint32_t *nsvp) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= N) return;
+    const uint2 l = links[rank[p]];
+    psvp[p] = l.x;
+    nsvp[p] = l.y;
 }
 
 // ---------------------------------------------------------------- lcp with those neighbours
@@ -1096,7 +1105,12 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         ++t.levels;
     }
     uint32_t *psvp = f1, *nsvp = f2;
-    k_psa_ansv<<<(uint32_t)((n64 + 255) / 256), 256, 0, s>>>(N, t, shards, nshards, psvp, nsvp);
+    {
+        auto *links = (uint2 *)get(n64 * 8);
+        k_psa_ansv<<<(uint32_t)((n64 + 255) / 256), 256, 0, s>>>(N, t, shards, nshards, links);
+        k_psa_links_text<<<blocks(N), tb, 0, s>>>(N, rank, links, psvp, nsvp);
+        put(links, n64 * 8);  // (stream-ordered reuse)
+    }
     auto *lcp_p = (uint16_t *)rank;  // ranks are no longer needed: two u16 arrays in their place
     auto *lcp_n = (uint16_t *)get(n64 * 2);
     k_psa_lce<<<blocks((n64 + kLceSpan - 1) / kLceSpan), tb, 0, s>>>(N, (const uint64_t *)G, dist, psvp, nsvp, lcp_p,
