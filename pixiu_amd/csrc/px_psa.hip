@@ -795,71 +795,88 @@ __global__ void __launch_bounds__(256) k_pool_blocks(uint32_t N, uint8_t *code, 
     blk[p] = c == 1 ? 8u : c == 3 ? 16u : 0u;
 }
 
-// first x in [lo, hi) with P[x] - base > cap (exists: P[hi - 1] - base > cap); wave-uniform
-PSA_DEV uint32_t pool_search(const uint32_t *P, uint32_t lo, uint32_t hi, uint32_t base, uint32_t cap) {
-    const uint32_t lane = lane_id();
-    while (hi - lo > 64) {
-        const uint32_t stride = (hi - lo + 63) / 64;
-        const uint32_t x = lo + lane * stride;
-        const uint64_t m = __ballot(x < hi && P[x] - base > cap);
-        if (!m) {  // after the last probe inside the range
-            lo += (hi - 1 - lo) / stride * stride + 1;
-            continue;
-        }
-        const uint32_t t = (uint32_t)__ffsll((long long)m) - 1u;
-        if (t == 0) return lo;
-        hi = min(hi, lo + t * stride + 1);
-        lo = lo + (t - 1) * stride + 1;
-    }
-    const uint32_t x = lo + lane;
-    const uint64_t m = __ballot(x < hi && P[x] - base > cap);
-    return m ? lo + (uint32_t)__ffsll((long long)m) - 1u : hi - 1u;  // (m != 0 by the precondition)
+// C[b] = the blocks before the end of the b-th 64-position block (P at 64b + 63)
+__global__ void __launch_bounds__(256) k_pool_coarse(uint32_t N, const uint32_t *P, uint32_t *C) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if ((uint64_t)b * 64 >= N) return;
+    C[b] = P[min(b * 64 + 63, N - 1)];
 }
 
-// one wave per emulating shard: the pool state from the chunk's root node on, doc by doc;
-// before a new doc, rotation if 2,048 pools are open or 65,535 docs placed (PiXiuCtrl.cpp:13)
+// One wave per emulating shard: the pool state from the chunk's root node on, boundary by
+// boundary.  A pool boundary is the first leaf whose pattern does not fit the open pool:
+// the wave keeps 64 coarse prefix values (4,096 positions) in registers, finds the block
+// holding the boundary by one ballot, then its leaf with one 64-position load, and
+// resolves the leaf's [5, 3] / [5, 5, 3, 3] charges.  The 2,048th pool opened inside doc g
+// rotates the chunk before doc g + 1 (PiXiuCtrl.cpp:13); the window's doc count never
+// reaches 65,535 (the host rotates slot-full chunks between rounds).
 __global__ void __launch_bounds__(64) k_pool_scan(uint32_t nshards, const PsaShard *shards, const PsaDoc *docs,
-                                                  const uint32_t *P, PsaPoolOut *out) {
+                                                  const uint32_t *P, const uint32_t *C, uint32_t N, PsaPoolOut *out) {
     const uint32_t s = blockIdx.x;
     if (s >= nshards) return;
+    const uint32_t lane = lane_id();
     const PsaShard sh = shards[s];
     PsaPoolOut o{kNone, 0, 0, 0};
-    if (sh.pools) {
+    if (sh.pools && sh.ndocs) {
         auto S = [&](uint32_t x) { return x ? P[x - 1] : 0u; };  // blocks before position x
+        const uint32_t start = docs[sh.doc0].start, endp = sh.base + sh.len;
         int32_t pools = 1, used = kNodeBlocks;  // the root (SuffixTree::init_prop)
-        for (uint32_t g = sh.doc0; g < sh.doc0 + sh.ndocs; ++g) {
-            const PsaDoc d = docs[g];
-            if (g > sh.doc0 && d.msg && (pools >= kRotatePools || g - sh.doc0 == (uint32_t)kChunkSlots)) {
-                o.rot_doc = g;
-                break;
-            }
-            uint32_t cur = d.start;
-            const uint32_t end = d.start + d.len, send = S(end);
-            uint32_t base = S(cur);
-            while ((uint32_t)used + (send - base) > (uint32_t)kPoolBlocks) {
-                const uint32_t k = pool_search(P, cur, end, base, (uint32_t)(kPoolBlocks - used));
-                const uint32_t sk = S(k);
-                int32_t u = used + (int32_t)(sk - base);
-                const bool split = P[k] - sk == 16u;
-                const int32_t ch[4] = {kNodeBlocks, split ? kNodeBlocks : kEdgeBlocks, kEdgeBlocks, kEdgeBlocks};
-                for (int i = 0; i < (split ? 4 : 2); ++i) {
-                    if (u + ch[i] > kPoolBlocks) {
-                        ++pools;
-                        u = ch[i];
-                    } else {
-                        u += ch[i];
-                    }
+        uint32_t cur = start, base = S(start);
+        const uint32_t send = S(endp);
+        uint32_t cw = kNone, cv = 0;  // coarse window: blocks [cw, cw + 64)
+        uint32_t k_last = kNone;
+        while (pools < kRotatePools && (uint32_t)used + (send - base) > (uint32_t)kPoolBlocks) {
+            const uint32_t cap = (uint32_t)(kPoolBlocks - used);
+            // the block holding the boundary: first b >= cur / 64 with C[b] - base > cap
+            uint32_t b = cur >> 6;
+            for (;;) {
+                if (cw == kNone || b < cw || b >= cw + 64) {
+                    cw = b;
+                    const uint32_t bi = cw + lane;
+                    cv = (uint64_t)bi * 64 < N ? C[bi] : 0xffffffffu;
                 }
-                used = u;
-                cur = k + 1;
-                base = P[k];
+                const uint64_t m = __ballot(cw + lane >= b && ((uint64_t)(cw + lane) * 64 >= N || cv - base > cap));
+                if (m) {
+                    b = cw + (uint32_t)__ffsll((long long)m) - 1u;
+                    break;
+                }
+                b = cw + 64;
             }
+            const uint32_t x = b * 64 + lane;
+            const uint64_t mk = __ballot(x >= cur && x < endp && P[x] - base > cap);
+            const uint32_t k = mk ? b * 64 + (uint32_t)__ffsll((long long)mk) - 1u : endp - 1u;  // (mk != 0)
+            const uint32_t sk = S(k);
+            int32_t u = used + (int32_t)(sk - base);
+            const bool split = P[k] - sk == 16u;
+            const int32_t ch[4] = {kNodeBlocks, split ? kNodeBlocks : kEdgeBlocks, kEdgeBlocks, kEdgeBlocks};
+            for (int i = 0; i < (split ? 4 : 2); ++i) {
+                if (u + ch[i] > kPoolBlocks) {
+                    ++pools;
+                    u = ch[i];
+                } else {
+                    u += ch[i];
+                }
+            }
+            used = u;
+            cur = k + 1;
+            base = P[k];
+            k_last = k;
+        }
+        if (pools >= kRotatePools) {
+            // the doc holding the 2,048th pool's first charge: rotation before the next one
+            uint32_t lo = sh.doc0, hi = sh.doc0 + sh.ndocs;  // docs[lo].start <= k_last < docs[hi].start
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (docs[mid].start <= k_last) lo = mid;
+                else hi = mid;
+            }
+            o.rot_doc = lo + 1;
+        } else {
             used += (int32_t)(send - base);
         }
         o.pools = pools;
         o.used = used;
     }
-    if (lane_id() == 0) out[s] = o;
+    if (lane == 0) out[s] = o;
 }
 
 struct Max {
@@ -1170,7 +1187,10 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
             PSA_CHECK(hipStreamSynchronize(s));
             fprintf(stderr, "psa pools: blocks scanned\n");
         }
-        k_pool_scan<<<nshards, 64, 0, s>>>(nshards, shards, docs, P, pool_out);
+        auto *C = (uint32_t *)get(n64 / 64 * 4 + 256);
+        k_pool_coarse<<<blocks((N + 63) / 64), tb, 0, s>>>(N, P, C);
+        k_pool_scan<<<nshards, 64, 0, s>>>(nshards, shards, docs, P, C, N, pool_out);
+        put(C, n64 / 64 * 4 + 256);
         PSA_CHECK(hipGetLastError());
         put(tmp2, tsz + 256);  // (stream-ordered reuse, as above)
         put(tab, cap * sizeof(PoolSlot));
