@@ -527,7 +527,14 @@ __global__ void __launch_bounds__(256) k_psa_links_text(uint32_t N, const uint32
 }
 
 // ---------------------------------------------------------------- lcp with those neighbours
-constexpr uint32_t kLceSpan = 256;  // text positions per thread (Kasai-style amortisation)
+// text positions per thread (Kasai-style amortisation): 256, or fewer (a multiple of 8)
+// when that leaves fewer than 2^18 threads -- a one-chunk window of the single instance
+constexpr uint32_t kLceSpan = 256;
+inline uint32_t lce_span(uint64_t n) {
+    uint64_t sp = kLceSpan;
+    while (sp > 16 && n / sp < (1u << 18)) sp /= 2;
+    return (uint32_t)sp;
+}
 
 // 8 text bytes from any offset: two aligned 8-byte loads and a funnel shift
 PSA_DEV uint64_t ld8(const uint64_t *G8, uint32_t off) {
@@ -548,18 +555,18 @@ PSA_DEV uint32_t lce(const uint64_t *G8, uint32_t p, uint32_t q, uint32_t k, uin
     return lim;
 }
 
-// One thread per kLceSpan consecutive positions.  The per-position arrays are read and
+// One thread per `span` consecutive positions.  The per-position arrays are read and
 // written 8 positions at a time with 16-byte accesses: a wave's 64 threads sit 256
 // positions apart, so per-position 2- and 4-byte accesses would each touch a different
 // cache line (and 64 threads x 5 arrays of such lines do not stay cached between the
 // thread's consecutive positions).
 __global__ void __launch_bounds__(256) k_psa_lce(uint32_t N, const uint64_t *G8, const uint16_t *dist,
                                                  const uint32_t *psvp, const uint32_t *nsvp, uint16_t *lcp_p,
-                                                 uint16_t *lcp_n) {
+                                                 uint16_t *lcp_n, uint32_t span) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t p0 = t * kLceSpan;
+    const uint32_t p0 = t * span;
     if (p0 >= N) return;
-    const uint32_t p1 = min(N, p0 + kLceSpan);
+    const uint32_t p1 = min(N, p0 + span);
     uint32_t kp = 0, kn = 0, qprev = kNoPos - 1, sprev = kNoPos - 1;
     for (uint32_t b = p0; b < p1; b += 8) {
         const uint32_t nb = min(8u, p1 - b);
@@ -1130,8 +1137,8 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     }
     auto *lcp_p = (uint16_t *)rank;  // ranks are no longer needed: two u16 arrays in their place
     auto *lcp_n = (uint16_t *)get(n64 * 2);
-    k_psa_lce<<<blocks((n64 + kLceSpan - 1) / kLceSpan), tb, 0, s>>>(N, (const uint64_t *)G, dist, psvp, nsvp, lcp_p,
-                                                                     lcp_n);
+    const uint32_t lsp = lce_span(n64);
+    k_psa_lce<<<blocks((n64 + lsp - 1) / lsp), tb, 0, s>>>(N, (const uint64_t *)G, dist, psvp, nsvp, lcp_p, lcp_n, lsp);
     PSA_CHECK(hipEventRecord(e2, s));
     if (verbose) {
         PSA_CHECK(hipStreamSynchronize(s));
