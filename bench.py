@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--no-exact", action="store_true",
                     help="skip the exact-mode getitem (profiling runs: one compat batch per step only)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process group for N > 1 (nccl = RCCL over xGMI; gloo: CPU transport, for tests)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r02.json"),
                     help="per-kernel PMC summary (tools/pmc_summary.py); used only if its workload matches")
     return ap.parse_args()
@@ -272,6 +274,7 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
     out_cap = int(2 * raw_bytes + 256 * n + (1 << 20))
     out = torch.empty(out_cap, dtype=torch.uint8, device=dev)
     gather_buf = [None]
+    gathered = [None]
     st = px.Store(records_per_shard=rps, device=local)
 
     def step():
@@ -297,7 +300,10 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
             if gather_buf[0] is None or gather_buf[0].numel() < nb:
                 gather_buf[0] = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
             st.save_device(gather_buf[0].data_ptr(), nb)
-            gather_blobs(gather_buf[0][:nb], dst=0)
+            blob = gather_buf[0][:nb]
+            if a.backend == "gloo":  # (gloo moves CPU tensors)
+                blob = blob.cpu()
+            gathered[0] = gather_blobs(blob, dst=0)
             torch.cuda.synchronize()
             g_ms = (time.perf_counter() - tg) * 1e3
         if rc != px.PX_OK or int(res["status"].max()) != 0:
@@ -321,7 +327,7 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
         dist.barrier()
     T1 = time.perf_counter()
     r = {"corpus": corpus, "st": st, "runs": runs, "elapsed": T1 - T0, "n": n, "raw": raw_bytes,
-         "out": out, "out_cap": out_cap, "keys_host": keys_host}
+         "out": out, "out_cap": out_cap, "keys_host": keys_host, "gathered": gathered[0]}
     # exact-mode getitem (one timed call, outside the step loop) and parity counts
     last = runs[-1]
     if a.no_exact:
@@ -348,13 +354,52 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
     return r
 
 
+def check_gathered(cfg, r, rps, world, records, sample=300):
+    """Rank 0, outside the timed region: load every rank's gathered chunk blob (the last
+    step's) into a fresh store and read back a sample of each rank's keys.  EXACT getitem
+    must equal the record's escaped doc (regenerated from that rank's corpus part), and
+    the compat getitem of rank 0's own records must equal its live store's."""
+    import numpy as np
+    import pixiu_amd as px
+    from pixiu_amd import synth
+    blobs = r["gathered"]
+    with px.Store(records_per_shard=rps) as st:
+        for b in blobs:
+            if b.is_cuda:
+                st.load(b.data_ptr(), on_device=True, length=b.numel())
+            else:
+                st.load(np.ascontiguousarray(b.numpy()).tobytes())
+        checked = exact_eq = 0
+        gathered_q = 0
+        for rk in range(world):
+            cp = r["corpus"] if rk == 0 else synth.make(cfg, records, part=rk)
+            rows = np.linspace(0, cp.n - 1, min(sample, cp.n)).astype(int).tolist()
+            keys = [cp.key(i) for i in rows]
+            got = st.get_batch(keys, px.EXACT)
+            for i, g in zip(rows, got):
+                v = cp.val(i)
+                d = cp.key(i).replace(b"\xfb", b"\xfb\xfb") + b"\xfb\x00"
+                if v:
+                    d += v.replace(b"\xfb", b"\xfb\xfb") + b"\xfb\x02"
+                exact_eq += g == d
+                checked += 1
+            if rk == 0:
+                comp_loaded = st.get_batch(keys, px.COMPAT)
+                gathered_q = int(st.stats()["last_gather_queries"])
+                comp_live = r["st"].get_batch(keys, px.COMPAT)
+                own_compat_eq = sum(x == y for x, y in zip(comp_loaded, comp_live))
+        return {"ranks": world, "blob_bytes": [int(b.numel()) for b in blobs], "records_checked": checked,
+                "exact_equal": exact_eq, "rank0_compat_equal_live": own_compat_eq,
+                "rank0_gather_served": gathered_q, "records_per_rank_sampled": min(sample, r["n"])}
+
+
 def summarize(cfg, r, rps, world, a, pmc_path):
     """Aggregate one config's runs (whole-job volumes over ranks) into its report."""
     import torch
     import torch.distributed as dist
     runs = r["runs"]
     steps = len(runs)
-    dev = r["out"].device
+    dev = r["out"].device if a.backend == "nccl" else torch.device("cpu")
     set_s = sum(x["set_s"] for x in runs)
     get_s = sum(x["get_s"] for x in runs)
     tot = torch.tensor([r["elapsed"], set_s, get_s, r["exact_s"]], dtype=torch.float64, device=dev)
@@ -459,9 +504,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
+    ndev = torch.cuda.device_count()
+    local = local % max(ndev, 1)  # (ranks beyond the visible GPUs share them: tests on one GPU)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     import pixiu_amd as px
 
     rps = a.rps if a.rps is not None else DEFAULT_RPS[a.config]
@@ -484,6 +534,7 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
+    gather_check = check_gathered(a.config, r, rps, world, a.records) if world > 1 else None
 
     st, corpus, runs = r["st"], r["corpus"], r["runs"]
     n, raw_bytes = r["n"], r["raw"]
@@ -514,6 +565,9 @@ def main():
         if k in main_sum:
             line[k] = main_sum[k]
     line["getitem_split_ms"] = {k: round(v, 3) for k, v in get_split.items()}
+    if gather_check:
+        line["gather_check"] = gather_check
+        line["config"]["backend"] = a.backend
     line["ub_reads"] = int(st.stats()["ub_reads"])
     if per_config:
         line["per_config"] = per_config

@@ -13,9 +13,12 @@
 //
 // including the CLI's `ctrl.st.cbt_chunk->getitem(ctrl.st.local_chunk.used_num - 1)->len`
 // (main.cpp:67).  Semantics are the reference's single instance (one shard);
-// getitem and iter stream the compat expansion (PXSGen byte-for-byte).  Difference:
-// reinsert compaction runs inside setitem/delitem; calling
-// `reinsert` directly does nothing.
+// getitem and iter stream the compat expansion (PXSGen byte-for-byte).  Generators are
+// lazy: getitem only looks the record up and expands it (<= 64 KiB) at the first pull;
+// iter expands its records kIterWindow at a time as the caller advances, so host memory
+// stays bounded whatever the prefix matches.  reinsert(PiXiuChunk *&) compacts a closed
+// slot-full chunk (PiXiuCtrl.cpp:88-114); chunk_at(seq) names one (an extension: the
+// reference reaches its chunks only through its internals).
 #ifndef PIXIU_CTRL_FACADE_H
 #define PIXIU_CTRL_FACADE_H
 
@@ -23,6 +26,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <map>
+#include <memory>
 #include <vector>
 
 #include "pixiu_amd.h"
@@ -37,12 +43,17 @@ struct PiXiuStr {  // compressed record as the reference lays it out (PiXiuStr.h
     uint8_t data[1];
 };
 
-// A generator over an already-expanded buffer (the GPU expands the whole record).
+// PiXiuStr::parse(0, PXSG_MAX_TO)'s generator: the record is addressed at getitem time and
+// expanded on the GPU at the first pull (or handed over already expanded by CBTGen).
 struct PXSGen {
+    px_ctx *ctx = nullptr;
+    px_rec rec{};
+    bool ready = false;
     std::vector<uint8_t> buf;
     size_t cur = 0;
 
     bool operator()(uint8_t &rv) {
+        if (!ready) expand();
         if (cur >= buf.size()) return false;
         rv = buf[cur++];
         return true;
@@ -50,19 +61,70 @@ struct PXSGen {
 
     // PiXiuStr.h:200-211: drain, keep visible bytes 33..126, NUL-terminate, free the gen
     char *consume_repr(void);
+
+  private:
+    void expand() {
+        ready = true;
+        // a compat expansion is at most PXSG_MAX_TO + 1 bytes (the over-yield of a range
+        // ending inside a 251 pair); the call reports the exact need if it is short
+        buf.resize(PXSG_MAX_TO + 1024);
+        uint64_t off = 0, need = 0;
+        uint32_t len = 0, status = 0;
+        int rc = px_parse_batch(ctx, 1, &rec, PX_COMPAT, buf.data(), buf.size(), 0, &off, &len, &status, &need);
+        if (rc == PX_ESPACE) {
+            buf.resize(need);
+            rc = px_parse_batch(ctx, 1, &rec, PX_COMPAT, buf.data(), buf.size(), 0, &off, &len, &status, &need);
+        }
+        if (rc != PX_OK || status != PX_OK) {
+            buf.clear();
+            return;
+        }
+        buf.erase(buf.begin(), buf.begin() + (long)off);
+        buf.resize(len);
+        buf.shrink_to_fit();
+    }
 };
 
-// PiXiuCtrl::iter's generator (CritBitTree.h:134-157): yields one PXSGen per record,
-// expanded up front on the GPU.
+// PiXiuCtrl::iter's generator (CritBitTree.h:134-157): the matching records in yield order,
+// expanded kIterWindow at a time, one batch per window, as the caller advances.
 struct CBTGen {
-    std::vector<std::vector<uint8_t>> docs;
-    size_t cur = 0;
+    static constexpr uint32_t kIterWindow = 64;
+    px_ctx *ctx = nullptr;
+    std::vector<px_rec> recs;
+    std::vector<std::vector<uint8_t>> win;  // expansions of recs[base .. base + win.size())
+    size_t cur = 0, base = 0;
 
     bool operator()(PXSGen *&rv) {
-        if (cur >= docs.size()) return false;
+        if (cur >= recs.size()) return false;
+        if (cur >= base + win.size()) fill(cur);
         rv = new PXSGen();
-        rv->buf = std::move(docs[cur++]);
+        rv->ctx = ctx;
+        rv->rec = recs[cur];
+        rv->ready = true;
+        rv->buf = std::move(win[cur - base]);
+        ++cur;
         return true;
+    }
+
+  private:
+    void fill(size_t at) {
+        const uint32_t n = (uint32_t)std::min<size_t>(kIterWindow, recs.size() - at);
+        std::vector<uint8_t> out((size_t)n * (PXSG_MAX_TO + 1024));
+        std::vector<uint64_t> off(n);
+        std::vector<uint32_t> len(n), status(n);
+        uint64_t need = 0;
+        int rc = px_parse_batch(ctx, n, recs.data() + at, PX_COMPAT, out.data(), out.size(), 0, off.data(), len.data(),
+                                status.data(), &need);
+        if (rc == PX_ESPACE) {
+            out.resize(need);
+            rc = px_parse_batch(ctx, n, recs.data() + at, PX_COMPAT, out.data(), out.size(), 0, off.data(), len.data(),
+                                status.data(), &need);
+        }
+        base = at;
+        win.assign(n, std::vector<uint8_t>());
+        for (uint32_t i = 0; i < n; ++i)
+            if (status[i] == PX_OK)
+                win[i].assign(out.begin() + (long)off[i], out.begin() + (long)(off[i] + len[i]));
     }
 };
 
@@ -129,19 +191,16 @@ struct PiXiuCtrl {
         return px_contains_batch(ctx, 1, k, off, &res) == PX_OK && res;
     }
 
+    // PiXiuCtrl::getitem (PiXiuCtrl.cpp:59-61): NULL for a missing key; the record is
+    // expanded when the generator is first pulled
     PXSGen *getitem(uint8_t k[], int k_len) {
         uint64_t koff[2] = {0, (uint64_t)k_len};
-        std::vector<uint8_t> out(4 * PXSG_MAX_TO + 1024);
-        uint64_t off = 0, need = 0;
-        uint32_t len = 0, status = 0;
-        int rc = px_get_batch(ctx, 1, k, koff, PX_COMPAT, out.data(), out.size(), 0, &off, &len, &status, &need);
-        if (rc == PX_ESPACE) {
-            out.resize(need);
-            rc = px_get_batch(ctx, 1, k, koff, PX_COMPAT, out.data(), out.size(), 0, &off, &len, &status, &need);
-        }
-        if (rc != PX_OK || status != PX_OK) return nullptr;
+        px_rec r;
+        uint32_t status = 0;
+        if (px_locate_batch(ctx, 1, k, koff, &r, &status) != PX_OK || status != PX_OK) return nullptr;
         PXSGen *g = new PXSGen();
-        g->buf.assign(out.begin() + (long)off, out.begin() + (long)(off + len));
+        g->ctx = ctx;
+        g->rec = r;
         return g;
     }
 
@@ -156,20 +215,9 @@ struct PiXiuCtrl {
         }
         if (rc != PX_OK) return nullptr;
         CBTGen *g = new CBTGen();
-        if (!n) return g;
-        std::vector<uint8_t> out((size_t)n * (4 * PXSG_MAX_TO + 1024));
-        std::vector<uint64_t> off(n);
-        std::vector<uint32_t> len(n), status(n);
-        uint64_t need = 0;
-        rc = px_parse_batch(ctx, n, recs.data(), PX_COMPAT, out.data(), out.size(), 0, off.data(), len.data(),
-                            status.data(), &need);
-        if (rc == PX_ESPACE) {
-            out.resize(need);
-            rc = px_parse_batch(ctx, n, recs.data(), PX_COMPAT, out.data(), out.size(), 0, off.data(), len.data(),
-                                status.data(), &need);
-        }
-        for (uint32_t i = 0; i < n; ++i)
-            g->docs.emplace_back(out.begin() + (long)off[i], out.begin() + (long)(off[i] + (status[i] == PX_OK ? len[i] : 0)));
+        g->ctx = ctx;
+        recs.resize(n);
+        g->recs = std::move(recs);
         return g;
     }
 
@@ -192,6 +240,7 @@ struct PiXiuCtrl {
         }
         chunk_view = PiXiuChunk();
         chunk_view.owner = this;
+        closed.clear();
         st.cbt_chunk = &chunk_view;
         st.local_chunk.used_num = 0;
     }
@@ -200,9 +249,34 @@ struct PiXiuCtrl {
         if (ctx) px_close(ctx);
         ctx = nullptr;
         st.cbt_chunk = nullptr;
+        closed.clear();
     }
 
-    void reinsert(PiXiuChunk *&) {}
+    // PiXiuCtrl::reinsert (PiXiuCtrl.cpp:88-114): compacts a closed slot-full chunk and, as
+    // the reference, clears the caller's pointer.  Other chunks (the live one, or one closed
+    // by the pool count, on which the reference dereferences NULL) are left as they are.
+    void reinsert(PiXiuChunk *&chunk) {
+        if (!chunk || !ctx) return;
+        if (px_reinsert(ctx, 0, chunk->chunk) == PX_OK) {
+            closed.erase(chunk->chunk);
+            chunk = nullptr;
+        }
+    }
+
+    // extension: the chunk with sequence number `seq` (0 = the first), for reinsert
+    PiXiuChunk *chunk_at(uint32_t seq) {
+        if (seq == chunk_view.chunk) return &chunk_view;
+        auto &p = closed[seq];
+        if (!p) {
+            p.reset(new PiXiuChunk());
+            p->owner = this;
+            p->chunk = seq;
+        }
+        return p.get();
+    }
+
+  private:
+    std::map<uint32_t, std::unique_ptr<PiXiuChunk>> closed;
 };
 
 inline PiXiuStr *PiXiuChunk::getitem(int idx) {

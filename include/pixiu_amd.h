@@ -21,6 +21,8 @@
  *   px_iter ................... PiXiuCtrl::iter -> CBTGen           (PiXiuCtrl.cpp:71-75, CritBitTree.h:55-157)
  *   px_parse_batch ............ PiXiuStr::parse(from,to,chunk)      (PiXiuStr.cpp:166-176)
  *   px_export ................. cbt_chunk->getitem(idx) bytes       (PiXiuStr.cpp:202-206, main.cpp:67)
+ *   px_locate_batch ........... CritBitTree::getitem's lookup       (CritBitTree.cpp:180-196, before the parse)
+ *   px_reinsert ............... PiXiuCtrl::reinsert(PiXiuChunk *&)  (PiXiuCtrl.cpp:88-114)
  *   px_save / px_load ......... (none: the reference has no persistence; chunk blob v1)
  *
  * All calls are synchronous on the context's HIP stream.  A context is not
@@ -147,6 +149,20 @@ int px_del_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *k
  * empty (the reference returns a NULL generator).  PX_ESPACE: *n_out = records needed. */
 int px_iter(px_ctx *ctx, const uint8_t *prefix, uint64_t prefix_len, px_rec *recs, uint32_t cap,
             uint32_t *n_out);
+
+/* The lookup half of getitem (CritBitTree.cpp:180-196): the record each key resolves to,
+ * recs[i] = {shard, chunk, idx, 0, 65535}, status[i] = PX_OK or PX_ENOTFOUND.  A caller
+ * expands it later with px_parse_batch (a lazily drained PXSGen). */
+int px_locate_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff, px_rec *recs,
+                    uint32_t *status);
+
+/* PiXiuCtrl::reinsert(PiXiuChunk *&) called directly (PiXiuCtrl.cpp:88-114): chunk `chunk`
+ * (sequence number) of shard `shard` is compacted -- every live record, compat-expanded,
+ * is set again as a ready doc (rotation trigger only) and the chunk's records are gone.
+ * Defined for a closed slot-full chunk: the reference visits all 65,535 slots and
+ * dereferences NULL otherwise.  PX_EINVAL for the live chunk, a chunk with empty slots,
+ * or an unknown one. */
+int px_reinsert(px_ctx *ctx, uint32_t shard, uint32_t chunk);
 
 /* Compressed bytes of stored records, copied to host CSR (out_off has n+1 entries). */
 int px_export(px_ctx *ctx, uint32_t n, const px_rec *recs, uint8_t *out, uint64_t out_cap,

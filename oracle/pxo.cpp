@@ -969,6 +969,18 @@ int pxo_set(pxo_shard *s, const uint8_t *k, int klen, const uint8_t *v, int vlen
     }
 }
 
+// PiXiuCtrl::reinsert(PiXiuChunk *&) called directly (PiXiuCtrl.cpp:88-114) on closed chunk c:
+// PXO_EINVAL for the live chunk or an unknown one
+int pxo_reinsert(pxo_shard *s, uint32_t c) {
+    if ((size_t)c + 1 >= s->chunks.size()) return PXO_EINVAL;
+    try {
+        s->reinsert_chunk((int)c, false);
+    } catch (const Fail &f) {
+        return f.code;
+    }
+    return 0;
+}
+
 int pxo_contains(pxo_shard *s, const uint8_t *k, int klen) {
     try {
         Bytes key;

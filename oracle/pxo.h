@@ -54,6 +54,8 @@ int pxo_locate(pxo_shard *s, const uint8_t *k, int klen, uint32_t *chunk, uint32
 
 /* PiXiuCtrl::contains (1/0) and ::delitem (0 deleted, 1 not found) */
 int pxo_contains(pxo_shard *s, const uint8_t *k, int klen);
+/* PiXiuCtrl::reinsert on closed chunk c (PiXiuCtrl.cpp:88-114) */
+int pxo_reinsert(pxo_shard *s, uint32_t c);
 int pxo_delete(pxo_shard *s, const uint8_t *k, int klen);
 /* PiXiuCtrl::iter: (chunk, idx) of the yielded records in order; count, PXO_NOTFOUND
    for an empty tree, PXO_ESPACE if cap is too small. */

@@ -13,10 +13,13 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <vector>
+
 static PiXiuCtrl g_ctrl;
 static PiXiuChunk *g_last_chunk = nullptr;
 static uint32_t g_chunk_serial = 0;
 static bool g_live = false;
+static std::vector<PiXiuChunk *> g_chunks;  // chunk by serial (nullptr once reinserted)
 
 extern "C" {
 
@@ -25,6 +28,7 @@ void refx_init(void) {
     g_ctrl.init_prop();                      // PiXiuCtrl.cpp:77-81
     g_last_chunk = g_ctrl.st.cbt_chunk;
     g_chunk_serial = 0;
+    g_chunks.assign(1, g_last_chunk);
     g_live = true;
 }
 
@@ -41,6 +45,7 @@ int refx_setitem(const uint8_t *k, int klen, const uint8_t *v, int vlen,
     if (g_ctrl.st.cbt_chunk != g_last_chunk) {
         g_last_chunk = g_ctrl.st.cbt_chunk;
         g_chunk_serial++;
+        g_chunks.push_back(g_last_chunk);
     }
     if (chunk_no) *chunk_no = g_chunk_serial;
     if (idx) *idx = (uint32_t)(g_ctrl.st.local_chunk.used_num - 1);
@@ -73,6 +78,19 @@ int refx_getitem(const uint8_t *k, int klen, uint8_t *out, int cap) {
     PXSGen *gen = g_ctrl.getitem((uint8_t *)k, klen);
     if (gen == nullptr) return -1;
     return drain(gen, out, cap);
+}
+
+// PiXiuCtrl::reinsert(PiXiuChunk *&) (PiXiuCtrl.cpp:88-114) called directly on the chunk
+// with the given serial; -1 for the live chunk or one already freed
+int refx_reinsert(uint32_t serial) {
+    if (serial >= g_chunks.size() || !g_chunks[serial] || g_chunks[serial] == g_ctrl.st.cbt_chunk) return -1;
+    g_ctrl.reinsert(g_chunks[serial]);  // (sets the entry to NULL, as the reference's reference argument)
+    if (g_ctrl.st.cbt_chunk != g_last_chunk) {  // the re-sets rotated the live chunk
+        g_last_chunk = g_ctrl.st.cbt_chunk;
+        g_chunk_serial++;
+        g_chunks.push_back(g_last_chunk);
+    }
+    return 0;
 }
 
 int refx_contains(const uint8_t *k, int klen) {

@@ -79,7 +79,7 @@ REC_DTYPE = np.dtype([("shard", "<u4"), ("chunk", "<u4"), ("idx", "<u4"), ("from
 # every symbol include/pixiu_amd.h declares
 EXPORTS = ["px_open", "px_close", "px_strerror", "px_set_batch", "px_get_batch", "px_parse_batch",
            "px_contains_batch", "px_del_batch", "px_export", "px_stats_get", "px_stream", "px_reset",
-           "px_last_store", "px_import_chunk", "px_iter", "px_save", "px_load"]
+           "px_last_store", "px_import_chunk", "px_iter", "px_save", "px_load", "px_locate_batch", "px_reinsert"]
 
 _LIB = None
 
@@ -114,6 +114,8 @@ def load_library() -> C.CDLL:
     lib.px_iter.argtypes = [vp, vp, u64, vp, u32, vp]
     lib.px_save.argtypes = [vp, vp, u64, i32, vp]
     lib.px_load.argtypes = [vp, vp, u64, i32, vp]
+    lib.px_locate_batch.argtypes = [vp, u32, vp, vp, vp, vp]
+    lib.px_reinsert.argtypes = [vp, u32, u32]
     _LIB = lib
     return lib
 
@@ -273,6 +275,24 @@ class Store:
         if rc != PX_OK:
             raise PxError(rc, "px_del_batch")
         return r[:n]
+
+    def locate(self, keys):
+        """The record each key resolves to (REC_DTYPE, parse range [0, 65535)) and its status
+        (PX_OK / PX_ENOTFOUND): getitem's lookup without the expansion."""
+        kb, ko = keys if isinstance(keys, tuple) else csr(keys)
+        n = len(ko) - 1
+        recs = np.zeros(max(n, 1), REC_DTYPE)
+        st = np.zeros(max(n, 1), np.uint32)
+        rc = self._lib.px_locate_batch(self._h, n, _ptr(kb), _ptr(ko), _ptr(recs), _ptr(st))
+        if rc != PX_OK:
+            raise PxError(rc, "px_locate_batch")
+        return recs[:n], st[:n]
+
+    def reinsert(self, shard: int, chunk: int):
+        """PiXiuCtrl::reinsert(PiXiuChunk *&) on a closed slot-full chunk (PiXiuCtrl.cpp:88-114)."""
+        rc = self._lib.px_reinsert(self._h, shard, chunk)
+        if rc != PX_OK:
+            raise PxError(rc, "px_reinsert")
 
     def iter(self, prefix: bytes):
         """PiXiuCtrl::iter: the yielded records (REC_DTYPE, yield order), or None when every

@@ -104,7 +104,9 @@ struct PsaAlloc {
     void *(*alloc)(void *self, uint64_t n);
     void (*release)(void *self, void *p, uint64_t n);
     void *self;
+    uint32_t *pin;  // >= kPsaPinWords pinned host words (counts come back through them)
 };
+constexpr uint32_t kPsaPinWords = 512;
 struct PsaStats {
     uint32_t iterations;  // prefix-doubling steps after the first sort
     uint32_t active[24];  // unsorted suffixes entering each doubling step
@@ -116,6 +118,13 @@ struct PsaStats {
 // leaf per byte, a closed pool holds >= 65,531 blocks, and rotation needs 2,048 pools
 // (PiXiuCtrl.cpp:13; MemPool.cpp:7-37): (2047 * 65531 - 5) / 16
 constexpr uint32_t kPsaMaxText = (uint32_t)((2047ull * 65531ull - 5ull) / 16ull);
+// device scratch per text position of one suffix-array round at its peak (px_psa.hip:
+// text, doc ids, distances, ranks, suffix array, sort keys and values, flags, links, lcp,
+// and the MemPool emulation's link records and candidate table), rounded up
+constexpr uint64_t kPsaBytesPerPos = 96;
+// shards per round: the first sort key holds the shard id in its top bits
+constexpr uint32_t kPsaShardBits = 19;
+constexpr uint32_t kPsaMaxShards = 1u << kPsaShardBits;
 
 // segment index entry (k_tokenize fills it, k_link sets a record token's target)
 struct alignas(16) SegEnt {

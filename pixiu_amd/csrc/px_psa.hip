@@ -35,12 +35,13 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
+#include <vector>
 
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
-#include <rocprim/device/device_select.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/reverse_iterator.hpp>
 
 #include "px_common.h"
 
@@ -90,309 +91,535 @@ __global__ void __launch_bounds__(256) k_psa_key0(uint32_t N, const uint8_t *G, 
 }
 
 // group heads of the first sort: a new group at a key change, and every suffix shorter
-// than 5 symbols (its key holds its whole string: equal ones are equal strings, kept
-// in position order by the stable sort and resolved as they are)
-__global__ void __launch_bounds__(256) k_psa_head0(uint32_t N, const uint64_t *keys, const uint32_t *sa,
-                                                   const uint16_t *dist, uint32_t syms, uint32_t *hflag) {
+// than `syms` symbols (its key holds its whole string, so its last symbol is 0: equal ones
+// are equal strings, kept in position order by the stable sort and resolved as they are)
+__global__ void __launch_bounds__(256) k_psa_head0(uint32_t N, const uint64_t *keys, uint32_t *hflag) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= N) return;
-    const uint32_t p = sa[r];
-    const bool complete = dist[p] < syms;
-    hflag[r] = (r == 0 || keys[r] != keys[r - 1] || complete) ? r : 0u;
+    const uint64_t k = keys[r];
+    const bool complete = (k & 511u) == 0;
+    hflag[r] = (r == 0 || k != keys[r - 1] || complete) ? r : 0u;
 }
 
-// rank = group head index; active = not a singleton group
-__global__ void __launch_bounds__(256) k_psa_rank0(uint32_t N, const uint32_t *sa, const uint32_t *head,
-                                                   uint32_t *rank, uint8_t *active) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= N) return;
-    rank[sa[r]] = head[r];
-    const bool h = head[r] == r;
-    const bool hn = r + 1 == N || head[r + 1] == r + 1;
-    active[r] = (h && hn) ? 0 : 1;
+// ---------------------------------------------------------------- unsorted groups
+// Prefix doubling keeps the suffixes that still share their first h symbols with another
+// suffix in GROUPS: a group is a range [start, start + size) of the suffix array, and
+// rank[p] = the group's start for each of its suffixes.  A step sorts every group by the
+// rank of the suffix h further on (0 past the doc end), rewriting sa inside the group, and
+// its subgroups (equal keys) become the next step's groups.  State per suffix-array slot:
+//   act[slot] = 1   the slot's suffix is in a group (still unsorted)
+//   gsz[slot]       at a group's first slot: size | tag << 31, where tag = the parity of the
+//                   step that sorts it (groups a step creates are invisible to that step)
+//   key[slot]       this step's key, gathered by k_dbl_key before any group is sorted, so
+//                   the sorters can write the new ranks directly
+// Sorting by group size: <= 64 where they lie (k_dbl_win: one wave per 64-slot window sorts
+// the groups starting in it), 65..kRegMax by one wave in registers, up to kMedMax by one
+// workgroup in LDS, larger ones by a gathered radix sort (host-driven: only early steps).
+constexpr uint32_t kWinMax = 64, kRegMax = 512, kMedMax = 4096;
+constexpr uint32_t kTag = 1u << 31, kSizeMask = kTag - 1u;
+constexpr int kLongClasses = 5;  // E = 2, 4, 8 (registers), LDS, big
+struct LongLists {
+    uint64_t *lst[kLongClasses];  // entry: start | size << 32
+    uint32_t *cnt;                // [0..4] entries, [5] overflow flag
+    uint32_t cap[kLongClasses];
+};
+PSA_DEV uint32_t long_class(uint32_t size) {
+    return size <= 128 ? 0u : size <= 256 ? 1u : size <= kRegMax ? 2u : size <= kMedMax ? 3u : 4u;
 }
-
-// doubling step h: key (group, rank of the suffix h further, 0 past the doc end)
-__global__ void __launch_bounds__(256) k_psa_key2(uint32_t m, const uint32_t *act, const uint32_t *rank,
-                                                  const uint16_t *dist, uint32_t h, uint64_t *keys, uint32_t *vals) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= m) return;
-    const uint32_t p = act[t];
-    const uint64_t hi = rank[p];
-    const uint64_t lo = h < dist[p] ? (uint64_t)rank[p + h] + 1 : 0;
-    keys[t] = hi << 32 | lo;
-    vals[t] = p;
+// per-step counters: suffixes sorted, slots still in groups after the step, largest group
+// left.  Kept in kStatShards shards on lines of their own (one line per shard and counter
+// set: a single address taking one atomic per wave serialises the whole launch), summed by
+// k_stat_sum into the cnt words the host reads
+constexpr uint32_t kStatShards = 64, kStatStride = 32;
+struct StepStat {
+    uint32_t *sh;  // [kStatShards][kStatStride]: sorted, active, maxsz
+};
+PSA_DEV void stat_put(const StepStat &ss, uint32_t slot, uint32_t sorted, uint32_t active, uint32_t mx) {
+    uint32_t *c = ss.sh + (slot & (kStatShards - 1)) * kStatStride;
+    if (sorted) atomicAdd(c, sorted);
+    if (active) atomicAdd(c + 1, active);
+    if (mx) atomicMax(c + 2, mx);
 }
-
-__global__ void __launch_bounds__(256) k_psa_head2(uint32_t m, const uint64_t *keys, uint32_t *gflag, uint32_t *sflag) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= m) return;
-    const uint64_t k = keys[t];
-    const bool first = t == 0;
-    gflag[t] = (first || (k >> 32) != (keys[t - 1] >> 32)) ? t : 0u;
-    // a suffix whose string ended (lo == 0) is complete: its own group
-    sflag[t] = (first || k != keys[t - 1] || (uint32_t)k == 0) ? t : 0u;
-}
-
-__global__ void __launch_bounds__(256) k_psa_rank2(uint32_t m, const uint64_t *keys, const uint32_t *pos,
-                                                   const uint32_t *gfirst, const uint32_t *sfirst, uint32_t *sa,
-                                                   uint32_t *rank, uint8_t *active) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= m) return;
-    const uint64_t k = keys[t];
-    const uint32_t g = (uint32_t)(k >> 32);
-    const uint32_t p = pos[t];
-    sa[g + (t - gfirst[t])] = p;
-    rank[p] = g + (sfirst[t] - gfirst[t]);
-    const bool h = sfirst[t] == t;
-    const bool hn = t + 1 == m || keys[t + 1] != k || (uint32_t)keys[t + 1] == 0;
-    active[t] = (h && hn) ? 0 : 1;
-}
-
-// ---------------------------------------------------------------- segmented doubling sort
-// A doubling step's keys arrive in suffix-array order, so each group (equal high word) is
-// a contiguous range and only needs sorting by the low word inside it.  From the third
-// step on almost every group is small (config 3: every group <= 113 suffixes from h = 24
-// on, 90 % of suffixes in groups <= 1,024 at h = 12), so groups are sorted where they lie:
-// <= 64 by one wave (bitonic over lanes), <= kSegBlock by one workgroup (bitonic in LDS),
-// and only the rest go through the global radix sort.  Ties (equal low words: identical
-// complete strings) keep their input order, as the stable radix sort keeps them.
-constexpr uint32_t kSegBlock = 1024;
-
-__global__ void __launch_bounds__(256) k_seg_flag(uint32_t m, const uint64_t *keys, uint8_t *fl) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= m) return;
-    fl[t] = (t == 0 || (keys[t] >> 32) != (keys[t - 1] >> 32)) ? 1 : 0;
-}
-
-// group sizes -> size classes: c < 6: size <= 2^(c+1) (sorted 64 / 2^(c+1) groups per
-// wave), 6: <= kSegBlock (one workgroup), 7: larger (radix).  The class lists are one
-// array partitioned class-major: per-block class counts, one exclusive scan over them
-// (class-major), then every block writes its groups at its offsets.
-constexpr int kSegClasses = 8;
-PSA_DEV uint32_t seg_class_of(uint32_t g, uint32_t ng, const uint32_t *gs, uint32_t m) {
-    const uint32_t sz = (g + 1 < ng ? gs[g + 1] : m) - gs[g];
-    uint32_t c = sz <= kSegBlock ? 6 : 7;
-    for (int k = 5; k >= 0; --k)
-        if (sz <= (2u << k)) c = (uint32_t)k;
-    return c;
-}
-__global__ void __launch_bounds__(256) k_seg_hist(uint32_t ng, const uint32_t *gs, uint32_t m, uint32_t nb,
-                                                  uint32_t *hist) {
-    __shared__ uint32_t h[kSegClasses];
-    if (threadIdx.x < kSegClasses) h[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g < ng) atomicAdd(&h[seg_class_of(g, ng, gs, m)], 1u);
-    __syncthreads();
-    if (threadIdx.x < kSegClasses) hist[threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
-}
-__global__ void __launch_bounds__(256) k_seg_part(uint32_t ng, const uint32_t *gs, uint32_t m, uint32_t nb,
-                                                  const uint32_t *offs, uint32_t *lists) {
-    __shared__ uint32_t h[kSegClasses];
-    if (threadIdx.x < kSegClasses) h[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g < ng) {
-        const uint32_t c = seg_class_of(g, ng, gs, m);
-        lists[offs[c * nb + blockIdx.x] + atomicAdd(&h[c], 1u)] = g;  // order inside a class is free
+__global__ void k_stat_sum(const uint32_t *sh, uint32_t *sorted, uint32_t *active, uint32_t *maxsz) {
+    const uint32_t l = threadIdx.x;  // one wave
+    uint32_t a = sh[l * kStatStride], b = sh[l * kStatStride + 1], c = sh[l * kStatStride + 2];
+    for (int o = 32; o > 0; o >>= 1) {
+        a += (uint32_t)__shfl_xor((int)a, o);
+        b += (uint32_t)__shfl_xor((int)b, o);
+        c = max(c, (uint32_t)__shfl_xor((int)c, o));
     }
-}
-// class start offsets -> out[0..8] (out[8] = ng)
-__global__ void k_seg_bounds(uint32_t nb, const uint32_t *offs, uint32_t ng, uint32_t *out) {
-    const uint32_t c = threadIdx.x;
-    if (c < kSegClasses) out[c] = offs[c * nb];
-    if (c == kSegClasses) out[c] = ng;
-}
-
-PSA_DEV void cas_shfl(uint64_t &k, uint32_t &v, uint32_t lane, uint32_t j, bool up) {
-    const uint64_t ok = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(k >> 32), (int)j) << 32) |
-                        (uint32_t)__shfl_xor((int)(uint32_t)k, (int)j);
-    const uint32_t ov = (uint32_t)__shfl_xor((int)v, (int)j);
-    const bool lower = (lane & j) == 0;
-    const bool take = up == lower ? ok < k : ok > k;
-    if (take) {
-        k = ok;
-        v = ov;
+    if (l == 0) {
+        *sorted = a;
+        *active = b;
+        *maxsz = c;
     }
 }
 
-// groups of <= S suffixes, 64 / S per wave: bitonic over S-lane segments, sort key
-// (low word << 6 | input index)
-template <uint32_t S>
-__global__ void __launch_bounds__(256) k_seg_sortS(uint32_t n, const uint32_t *list, const uint32_t *gs, uint32_t ng,
-                                                   uint32_t m, const uint64_t *keys, const uint32_t *vals,
-                                                   uint64_t *keys_out, uint32_t *vals_out) {
-    // grid-stride: a dispatch holds fewer than 2^32 work-items, and there can be ~10^8 groups
-    constexpr uint32_t G = 64 / S;
-    const uint32_t lane = lane_id(), i = lane & (S - 1);
+PSA_DEV uint32_t wave_incl_sum(uint32_t x) {
+    const uint32_t lane = lane_id();
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+        if (lane >= o) x += y;
+    }
+    return x;
+}
+PSA_DEV uint32_t wave_sum(uint32_t x) {
+    for (int o = 32; o > 0; o >>= 1) x += (uint32_t)__shfl_xor((int)x, o);
+    return x;
+}
+PSA_DEV uint32_t wave_max(uint32_t x) {
+    for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o));
+    return x;
+}
+// one stat_put per workgroup (every thread of the block calls it)
+PSA_DEV void block_stat(const StepStat &ss, uint32_t sorted, uint32_t active, uint32_t mx) {
+    __shared__ uint32_t red[3][4];
+    sorted = wave_sum(sorted);
+    active = wave_sum(active);
+    mx = wave_max(mx);
+    const uint32_t wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        red[0][wv] = sorted;
+        red[1][wv] = active;
+        red[2][wv] = mx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t nw = blockDim.x >> 6;
+        uint32_t a = 0, b = 0, c = 0;
+        for (uint32_t w = 0; w < nw; ++w) {
+            a += red[0][w];
+            b += red[1][w];
+            c = max(c, red[2][w]);
+        }
+        stat_put(ss, blockIdx.x, a, b, c);
+    }
+}
+PSA_DEV uint64_t shfl64(uint64_t x, uint32_t src) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)x, (int)src), hi = (uint32_t)__shfl((int)(uint32_t)(x >> 32), (int)src);
+    return (uint64_t)hi << 32 | lo;
+}
+PSA_DEV uint64_t mask_le(uint32_t j) { return j >= 63 ? ~0ull : (2ull << j) - 1ull; }
+PSA_DEV uint64_t mask_gt(uint32_t j) { return ~mask_le(j); }
+PSA_DEV uint32_t hibit(uint64_t m) { return 63u - (uint32_t)__clzll((long long)m); }  // (m != 0)
+PSA_DEV uint32_t lobit(uint64_t m) { return (uint32_t)__ffsll((long long)m) - 1u; }  // (m != 0)
+
+// append long groups (wave-wide: every lane calls it; `valid` lanes hold one entry each)
+PSA_DEV void push_long(const LongLists &L, bool valid, uint64_t ent) {
+    const uint32_t cls = valid ? long_class((uint32_t)(ent >> 32)) : 255u;
+    const uint32_t lane = lane_id();
+    for (uint32_t c = 0; c < (uint32_t)kLongClasses; ++c) {
+        const uint64_t m = __ballot(cls == c);
+        if (!m) continue;
+        const uint32_t leader = lobit(m);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&L.cnt[c], (uint32_t)__popcll(m));
+        base = (uint32_t)__shfl((int)base, (int)leader);
+        if (cls == c) {
+            const uint32_t at = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            if (at < L.cap[c]) L.lst[c][at] = ent;
+            else atomicOr(&L.cnt[kLongClasses], 1u);  // (cannot happen: lists hold N / (class min) groups)
+        }
+    }
+}
+
+// rank = group head index, sd = doc distance in suffix-array order, act / gsz of the first
+// groups (tag 0: step 0 sorts them).  A group's size is written at its start by its last
+// element; every other slot writes its own gsz (0)
+__global__ void __launch_bounds__(256) k_psa_groups0(uint32_t N, const uint32_t *sa, const uint32_t *head,
+                                                     const uint16_t *dist, uint32_t *rank, uint16_t *sd, uint8_t *act,
+                                                     uint32_t *gsz, StepStat ss) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t a = 0, mx = 0;
+    if (r < N) {
+        const uint32_t p = sa[r], hd = head[r];
+        rank[p] = hd;
+        sd[r] = dist[p];
+        const bool hn = r + 1 == N || head[r + 1] == r + 1;  // r + 1 starts the next group
+        a = (hd != r || !hn) ? 1u : 0u;                       // in a group of >= 2
+        act[r] = (uint8_t)a;
+        if (!(hd == r && !hn)) gsz[r] = 0;  // (not the start of a group of >= 2)
+        if (hn && hd != r) {                // the last element of a group of >= 2
+            gsz[hd] = r - hd + 1;
+            mx = r - hd + 1;
+        }
+    }
+    block_stat(ss, 0, a, mx);
+}
+
+// this step's keys: rank of the suffix h further on (+1), 0 past the doc end.  Flat over the
+// suffix array, 16 slots per thread: every scattered rank read of the step in flight at once
+__global__ void __launch_bounds__(256) k_dbl_key(uint32_t N, uint32_t h, const uint8_t *act, const uint32_t *sa,
+                                                 const uint16_t *sd, const uint32_t *rank, uint32_t *key) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t s0 = t * 16;
+    if (s0 >= N) return;
+    if (s0 + 16 <= N) {
+        const uint4 av = *(const uint4 *)(act + s0);
+        if ((av.x | av.y | av.z | av.w) == 0) return;
+        uint32_t p[16], k[16];
+        uint16_t d[16];
+        for (int q = 0; q < 4; ++q) *(uint4 *)(p + 4 * q) = *(const uint4 *)(sa + s0 + 4 * q);
+        for (int q = 0; q < 2; ++q) *(uint4 *)(d + 8 * q) = *(const uint4 *)(sd + s0 + 8 * q);
+        const uint32_t aw[4] = {av.x, av.y, av.z, av.w};
+#pragma unroll
+        for (int i = 0; i < 16; ++i)  // (slots outside groups get a key nobody reads)
+            k[i] = ((aw[i >> 2] >> (8 * (i & 3))) & 0xffu) && h < d[i] ? rank[p[i] + h] + 1u : 0u;
+        for (int q = 0; q < 4; ++q) *(uint4 *)(key + s0 + 4 * q) = *(const uint4 *)(k + 4 * q);
+    } else {
+        for (uint32_t s = s0; s < N; ++s)
+            if (act[s]) key[s] = h < sd[s] ? rank[sa[s] + h] + 1u : 0u;
+    }
+}
+
+// One wave per 64-slot window: the groups of <= 64 that start in it (and so end within
+// the next window) are sorted where they lie, 128 slots over 64 lanes (A: slot b + lane,
+// B: slot b + 64 + lane); a longer group starting in it goes to its class list.  Each
+// member ranks itself against its group's keys (staged in LDS): its sorted position
+// (key, then index -- stable), the members before it with an equal key (0: it heads a
+// subgroup) and the members with its key (the subgroup size).  So it writes its own
+// destination, its new rank (only where it changes) and act / gsz of the next step's
+// groups without any sorting network.
+struct WinElem {
+    bool mem;
+    uint32_t c, z, i, key, p, d;  // group start lane, size, index in the group, key, payload
+};
+PSA_DEV void win_rank(const WinElem &e, const uint32_t *lk, uint32_t smax, uint32_t &lt, uint32_t &eqb, uint32_t &eqt) {
+    lt = eqb = eqt = 0;
+    for (uint32_t t = 0; t < smax; ++t) {  // (smax is wave-uniform)
+        const uint32_t kt = lk[(e.c + t) & 127u];
+        if (e.mem && t < e.z && t != e.i) {
+            lt += (kt < e.key || (kt == e.key && t < e.i)) ? 1u : 0u;
+            eqb += (kt == e.key && t < e.i) ? 1u : 0u;
+            eqt += kt == e.key ? 1u : 0u;
+        }
+    }
+}
+PSA_DEV void win_put(const WinElem &e, uint32_t b, uint32_t lt, uint32_t eqb, uint32_t eqt, uint32_t tag, uint32_t *sa,
+                     uint16_t *sd, uint8_t *act, uint32_t *gsz, uint32_t *rank, uint32_t &ac, uint32_t &mx) {
+    const uint32_t dst = b + e.c + lt;
+    // key 0: a complete suffix, a subgroup of its own (equal complete strings stay in index order)
+    const bool head = e.key == 0 || eqb == 0;
+    const uint32_t hd = e.key == 0 ? lt : lt - eqb, size = e.key == 0 ? 1u : eqt + 1u;
+    const bool grp = e.key != 0 && size >= 2;
+    sa[dst] = e.p;
+    sd[dst] = (uint16_t)e.d;
+    act[dst] = grp ? 1 : 0;
+    gsz[dst] = head && grp ? (size | (tag ^ kTag)) : 0u;
+    if (hd != 0) rank[e.p] = b + e.c + hd;
+    ac += grp;
+    if (head && grp) mx = max(mx, size);
+}
+__global__ void __launch_bounds__(256) k_dbl_win(uint32_t N, uint32_t tag, uint32_t *sa, uint16_t *sd, uint8_t *act,
+                                                 uint32_t *gsz, const uint32_t *key, uint32_t *rank, LongLists L,
+                                                 StepStat ss) {
+    __shared__ uint32_t lks[4][128];
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    uint32_t *lk = lks[wv];
+    const uint32_t nwin = (N + 63) / 64;
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);
-    for (uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); w * G < n; w += waves) {
-        const uint32_t slot = w * G + lane / S;
-        uint32_t a = 0, sz = 0;
-        if (slot < n) {
-            const uint32_t g = list[slot];
-            a = gs[g];
-            sz = (g + 1 < ng ? gs[g + 1] : m) - a;
+    uint32_t sorted = 0, active = 0, mx = 0;
+    uint64_t pend = 0;  // pending long groups, lane i holds entry i
+    uint32_t npend = 0;
+    for (uint32_t w = blockIdx.x * (blockDim.x >> 6) + wv; w < nwin; w += waves) {
+        const uint32_t b = w * 64, sA = b + lane, sB = b + 64 + lane;
+        const bool inA = sA < N;
+        if (!__ballot(inA && act[sA])) continue;
+        const uint32_t g = inA ? gsz[sA] : 0u;
+        const bool start = (g & kTag) == tag && (g & kSizeMask) >= 2;
+        const uint32_t gs = g & kSizeMask;
+        const uint64_t S = __ballot(start && gs <= kWinMax);
+        const uint64_t Lg = __ballot(start && gs > kWinMax);
+        if (Lg) {  // (at most one: it runs past the window)
+            const uint32_t l = lobit(Lg);
+            const uint32_t sz = (uint32_t)__shfl((int)gs, (int)l);
+            if (lane == npend) pend = (uint64_t)(b + l) | (uint64_t)sz << 32;
+            if (++npend == 64) {
+                push_long(L, true, pend);
+                npend = 0;
+            }
         }
-        uint64_t k = ~0ull, hi = 0;
-        uint32_t v = 0;
-        if (i < sz) {
-            const uint64_t key = keys[a + i];
-            hi = key >> 32;
-            k = (key & 0xffffffffull) << 6 | i;
-            v = vals[a + i];
+        if (!S) continue;
+        // membership: the last small start at or before the slot, if the slot lies inside it
+        const uint32_t cA = (S & mask_le(lane)) ? hibit(S & mask_le(lane)) : 64u;
+        const uint32_t cB = hibit(S);
+        const uint32_t zA = (uint32_t)__shfl((int)gs, (int)(cA & 63u)), zB = (uint32_t)__shfl((int)gs, (int)cB);
+        WinElem A{cA < 64 && lane < cA + zA, cA & 63u, zA, lane - cA, 0, 0, 0};
+        WinElem B{64 + lane < cB + zB, cB, zB, 64 + lane - cB, 0, 0, 0};
+        if (A.mem) {
+            A.key = key[sA];
+            A.p = sa[sA];
+            A.d = sd[sA];
         }
-        for (uint32_t kk = 2; kk <= S; kk <<= 1)
-            for (uint32_t j = kk >> 1; j > 0; j >>= 1) cas_shfl(k, v, lane, j, (i & kk) == 0);
-        if (i < sz) {
-            keys_out[a + i] = hi << 32 | (k >> 6);
-            vals_out[a + i] = v;
+        if (B.mem) {
+            B.key = key[sB];
+            B.p = sa[sB];
+            B.d = sd[sB];
         }
+        lk[lane] = A.key;
+        lk[64 + lane] = B.key;
+        const uint32_t smax = wave_max((S >> lane) & 1ull ? gs : 0u);
+        uint32_t lA, eA, tA, lB, eB, tB;
+        win_rank(A, lk, smax, lA, eA, tA);
+        win_rank(B, lk, smax, lB, eB, tB);
+        uint32_t ac = 0;
+        if (A.mem) win_put(A, b, lA, eA, tA, tag, sa, sd, act, gsz, rank, ac, mx);
+        if (B.mem) win_put(B, b, lB, eB, tB, tag, sa, sd, act, gsz, rank, ac, mx);
+        sorted += (uint32_t)__popcll(__ballot(A.mem)) + (uint32_t)__popcll(__ballot(B.mem));
+        active += ac;
     }
+    push_long(L, lane < npend, pend);
+    active = wave_sum(active);
+    mx = wave_max(mx);
+    if (lane == 0) stat_put(ss, blockIdx.x * 4 + wv, sorted, active, mx);
 }
 
-// one workgroup per group of 65..kSegBlock: bitonic sort in LDS
-__global__ void __launch_bounds__(256) k_seg_sortblk(const uint32_t *list, const uint32_t *gs, uint32_t ng, uint32_t m,
-                                                     const uint64_t *keys, const uint32_t *vals, uint64_t *keys_out,
-                                                     uint32_t *vals_out) {
-    __shared__ uint64_t sk[kSegBlock];
-    __shared__ uint32_t sv[kSegBlock];
-    const uint32_t g = list[blockIdx.x];
-    const uint32_t a = gs[g], sz = (g + 1 < ng ? gs[g + 1] : m) - a;
-    uint32_t P = 128;
-    while (P < sz) P <<= 1;
-    const uint64_t hi = keys[a] >> 32;
-    for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
-        if (i < sz) {
-            sk[i] = (keys[a + i] & 0xffffffffull) << 10 | i;
-            sv[i] = vals[a + i];
-        } else {
-            sk[i] = ~0ull;
-            sv[i] = 0;
+// The subgroups of one sorted group (positions q = 0..size-1 in sorted order, any layout):
+// writes element q's slot and reports whether it opens / continues a group.  Shared by the
+// register and LDS sorters through a per-position view.
+PSA_DEV void put_sorted(uint32_t start, uint32_t q, uint32_t p, uint32_t d, uint32_t key, bool head, uint32_t hd,
+                        uint32_t nxt, uint32_t tag, uint32_t *sa, uint16_t *sd, uint8_t *act, uint32_t *gsz, uint32_t *rank,
+                        uint32_t &ac, uint32_t &mx) {
+    const uint32_t dst = start + q, szn = nxt - q;
+#ifdef PX_PSA_DEBUG
+    if (szn > 0x10000000u) printf("put_sorted: start %u q %u nxt %u head %d hd %u key %u\n", start, q, nxt, (int)head, hd, key);
+#endif
+    sa[dst] = p;
+    sd[dst] = (uint16_t)d;
+    const bool grp = key != 0 && !(head && szn == 1);
+    act[dst] = grp ? 1 : 0;
+    gsz[dst] = head && grp ? (szn | (tag ^ kTag)) : 0u;
+    if (hd != 0) rank[p] = start + hd;
+    ac += grp;
+    if (head && grp) mx = max(mx, szn);
+}
+
+// One wave per group of 65..64*E suffixes: E elements per lane (lane l holds positions
+// l*E .. l*E+E-1), bitonic sort in registers; payloads through LDS.
+template <uint32_t E>
+__global__ void __launch_bounds__(256) k_dbl_reg(const uint64_t *list, const uint32_t *cnt_p, uint32_t tag, uint32_t *sa,
+                                                 uint16_t *sd, uint8_t *act, uint32_t *gsz, const uint32_t *key,
+                                                 uint32_t *rank, StepStat ss) {
+    __shared__ uint32_t lp[4][64 * E];
+    __shared__ uint16_t ld[4][64 * E];
+    const uint32_t cnt = __hip_atomic_load(cnt_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    uint32_t sorted = 0, active = 0, mx = 0;
+    for (uint32_t gi = blockIdx.x * (blockDim.x >> 6) + wv; gi < cnt; gi += waves) {
+        const uint64_t ent = list[gi];
+        const uint32_t start = (uint32_t)ent, size = (uint32_t)(ent >> 32);
+        uint64_t x[E];
+#pragma unroll
+        for (uint32_t r = 0; r < E; ++r) {
+            const uint32_t i = lane * E + r;
+            if (i < size) {
+                x[r] = (uint64_t)key[start + i] << 11 | i;
+                lp[wv][i] = sa[start + i];
+                ld[wv][i] = sd[start + i];
+            } else {
+                x[r] = ~0ull;
+            }
         }
-    }
-    __syncthreads();
-    for (uint32_t kk = 2; kk <= P; kk <<= 1)
-        for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
-                const uint32_t l = i ^ j;
-                if (l > i) {
-                    const bool up = (i & kk) == 0;
-                    const uint64_t x = sk[i], y = sk[l];
-                    if (up ? x > y : x < y) {
-                        sk[i] = y;
-                        sk[l] = x;
-                        const uint32_t t = sv[i];
-                        sv[i] = sv[l];
-                        sv[l] = t;
+#pragma unroll
+        for (uint32_t k = 2; k <= 64 * E; k <<= 1)
+#pragma unroll
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                if (j < E) {
+#pragma unroll
+                    for (uint32_t r = 0; r < E; ++r) {
+                        if (r & j) continue;
+                        const uint32_t i = lane * E + r;
+                        const bool up = (i & k) == 0;
+                        const uint64_t a = x[r], c = x[r | j];
+                        if (up ? a > c : a < c) {
+                            x[r] = c;
+                            x[r | j] = a;
+                        }
+                    }
+                } else {
+                    const uint32_t lj = j / E;
+                    const bool lower = (lane & lj) == 0;
+#pragma unroll
+                    for (uint32_t r = 0; r < E; ++r) {
+                        const uint64_t o = shfl64(x[r], lane ^ lj);
+                        const bool up = ((lane * E + r) & k) == 0;
+                        x[r] = up == lower ? (o < x[r] ? o : x[r]) : (o > x[r] ? o : x[r]);
                     }
                 }
             }
+        // subgroup heads as a lane mask over the lane's E positions; the head at or before a
+        // position and the next one after it come from the mask and two cross-lane scans
+        const uint32_t prevk = (uint32_t)__shfl_up((int)(uint32_t)(x[E - 1] >> 11), 1);
+        uint32_t hm = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < E; ++r) {
+            const uint32_t i = lane * E + r;
+            const uint32_t kr = (uint32_t)(x[r] >> 11), pk = r ? (uint32_t)(x[r - 1] >> 11) : prevk;
+            if (i < size && (i == 0 || kr != pk || kr == 0)) hm |= 1u << r;
+        }
+        uint32_t lmax = hm ? lane * E + (31u - (uint32_t)__clz(hm)) + 1u : 0u;  // last head + 1 (0: none)
+        uint32_t lmin = hm ? lane * E + (uint32_t)__ffs(hm) - 1u : 0xffffffffu;  // first head
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)lmax, o), z = (uint32_t)__shfl_down((int)lmin, o);
+            if (lane >= o) lmax = max(lmax, y);
+            if (lane + o < 64) lmin = min(lmin, z);
+        }
+        // (shuffles outside the selects: a lane that reads an inactive lane gets 0)
+        const uint32_t up1 = (uint32_t)__shfl_up((int)lmax, 1), dn1 = (uint32_t)__shfl_down((int)lmin, 1);
+        const uint32_t before = lane ? up1 - 1u : 0u;         // head before the lane
+        const uint32_t after = lane < 63 ? dn1 : 0xffffffffu;  // head after it
+        uint32_t ac = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < E; ++r) {
+            const uint32_t i = lane * E + r;
+            if (i >= size) continue;
+            const uint32_t le = hm & ((2u << r) - 1u), gt = hm & ~((2u << r) - 1u);
+            const uint32_t hd = le ? lane * E + (31u - (uint32_t)__clz(le)) : before;
+            const uint32_t nx = min(gt ? lane * E + (uint32_t)__ffs(gt) - 1u : after, size);
+            const uint32_t o = (uint32_t)(x[r] & 2047u);
+            put_sorted(start, i, lp[wv][o], ld[wv][o], (uint32_t)(x[r] >> 11), (hm >> r) & 1u, hd, nx, tag, sa, sd, act,
+                       gsz, rank, ac, mx);
+        }
+        sorted += size;
+        active += wave_sum(ac);
+    }
+    mx = wave_max(mx);
+    if (lane == 0) stat_put(ss, blockIdx.x * 4 + wv, sorted, active, mx);
+}
+
+// one workgroup per group of kRegMax+1 .. kMedMax: bitonic sort of the keys in LDS; then
+// each thread takes C = P / 256 consecutive positions: their heads as a mask, their payloads
+// gathered before any slot of the group is rewritten, and the subgroup bounds across threads
+// from two block scans
+__global__ void __launch_bounds__(256) k_dbl_blk(const uint64_t *list, const uint32_t *cnt_p, uint32_t tag, uint32_t *sa,
+                                                 uint16_t *sd, uint8_t *act, uint32_t *gsz, const uint32_t *key,
+                                                 uint32_t *rank, StepStat ss) {
+    __shared__ uint64_t sk[kMedMax];
+    __shared__ uint32_t sl[256], sf[256];
+    constexpr uint32_t kC = kMedMax / 256;
+    const uint32_t cnt = __hip_atomic_load(cnt_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t tid = threadIdx.x;
+    uint32_t sorted = 0, active = 0, mx = 0;
+    for (uint32_t gi = blockIdx.x; gi < cnt; gi += gridDim.x) {
+        const uint64_t ent = list[gi];
+        const uint32_t start = (uint32_t)ent, size = (uint32_t)(ent >> 32);
+        uint32_t P = 256;
+        while (P < size) P <<= 1;
+        for (uint32_t i = tid; i < P; i += 256) sk[i] = i < size ? (uint64_t)key[start + i] << 12 | i : ~0ull;
+        __syncthreads();
+        for (uint32_t kk = 2; kk <= P; kk <<= 1)
+            for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+                for (uint32_t i = tid; i < P; i += 256) {
+                    const uint32_t l = i ^ j;
+                    if (l > i) {
+                        const bool up = (i & kk) == 0;
+                        const uint64_t x = sk[i], y = sk[l];
+                        if (up ? x > y : x < y) {
+                            sk[i] = y;
+                            sk[l] = x;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        const uint32_t C = P / 256, i0 = tid * C;
+        uint32_t hm = 0, pv[kC], dv[kC];
+#pragma unroll
+        for (uint32_t c = 0; c < kC; ++c) {
+            const uint32_t i = i0 + c;
+            if (c < C && i < size) {
+                const uint64_t x = sk[i];
+                const uint32_t k = (uint32_t)(x >> 12);
+                if (i == 0 || k != (uint32_t)(sk[i - 1] >> 12) || k == 0) hm |= 1u << c;
+                const uint32_t o = (uint32_t)(x & 4095u);
+                pv[c] = sa[start + o];
+                dv[c] = sd[start + o];
+            }
+        }
+        sl[tid] = hm ? i0 + (31u - (uint32_t)__clz(hm)) + 1u : 0u;
+        sf[tid] = hm ? i0 + (uint32_t)__ffs(hm) - 1u : 0xffffffffu;
+        __syncthreads();  // (every payload of the group is read: its slots may be rewritten)
+        for (uint32_t o = 1; o < 256; o <<= 1) {
+            const uint32_t a = tid >= o ? max(sl[tid], sl[tid - o]) : sl[tid];
+            const uint32_t b = tid + o < 256 ? min(sf[tid], sf[tid + o]) : sf[tid];
+            __syncthreads();
+            sl[tid] = a;
+            sf[tid] = b;
             __syncthreads();
         }
-    for (uint32_t i = threadIdx.x; i < sz; i += blockDim.x) {
-        keys_out[a + i] = hi << 32 | (sk[i] >> 10);
-        vals_out[a + i] = sv[i];
-    }
-}
-
-// big groups: mark their elements, then gather / radix sort / scatter back
-__global__ void __launch_bounds__(256) k_seg_mark(const uint32_t *list, const uint32_t *gs, uint32_t ng, uint32_t m,
-                                                  uint8_t *fl) {
-    const uint32_t g = list[blockIdx.x];
-    const uint32_t a = gs[g], sz = (g + 1 < ng ? gs[g + 1] : m) - a;
-    for (uint32_t i = threadIdx.x; i < sz; i += blockDim.x) fl[a + i] = 1;
-}
-__global__ void __launch_bounds__(256) k_seg_gather(uint32_t n, const uint32_t *idx, const uint64_t *keys,
-                                                    const uint32_t *vals, uint64_t *ck, uint32_t *cv) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    ck[i] = keys[idx[i]];
-    cv[i] = vals[idx[i]];
-}
-__global__ void __launch_bounds__(256) k_seg_scatter(uint32_t n, const uint32_t *idx, const uint64_t *ck,
-                                                     const uint32_t *cv, uint64_t *keys_out, uint32_t *vals_out) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    keys_out[idx[i]] = ck[i];
-    vals_out[idx[i]] = cv[i];
-}
-
-// ---------------------------------------------------------------- stream compaction
-// out = values[i] (or i itself when values is null) for every i < n with flags[i] != 0, in
-// order.  Three passes: per-tile counts, a scan over the tiles, per-tile writes.  A
-// tile is 4,096 elements (16 per thread, read as one 16-byte flag vector).
-constexpr uint32_t kCmpTile = 4096;
-PSA_DEV uint32_t nflags16(const uint8_t *f, uint32_t i, uint32_t n, uint32_t &bits) {
-    bits = 0;
-    if (i + 16 <= n) {
-        const uint4 v = *(const uint4 *)(f + i);
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-        for (int q = 0; q < 4; ++q)
-            for (int b = 0; b < 4; ++b)
-                if ((w[q] >> (8 * b)) & 0xffu) bits |= 1u << (4 * q + b);
-    } else {
-        for (uint32_t k = 0; k < 16 && i + k < n; ++k)
-            if (f[i + k]) bits |= 1u << k;
-    }
-    return (uint32_t)__popc(bits);
-}
-__global__ void __launch_bounds__(256) k_cmp_count(uint32_t n, const uint8_t *flags, uint32_t *tile_cnt) {
-    __shared__ uint32_t red[4];
-    const uint32_t i = blockIdx.x * kCmpTile + threadIdx.x * 16;
-    uint32_t bits;
-    uint32_t c = i < n ? nflags16(flags, i, n, bits) : 0;
-    for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
-}
-__global__ void __launch_bounds__(256) k_cmp_write(uint32_t n, const uint8_t *flags, const uint32_t *values,
-                                                   const uint32_t *tile_off, uint32_t *out) {
-    __shared__ uint32_t wsum[4];
-    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-    const uint32_t i = blockIdx.x * kCmpTile + threadIdx.x * 16;
-    uint32_t bits = 0;
-    const uint32_t c = i < n ? nflags16(flags, i, n, bits) : 0;
-    // exclusive prefix of c over the block
-    uint32_t x = c;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
-        if ((int)lane >= o) x += y;
-    }
-    if (lane == 63) wsum[wv] = x;
-    __syncthreads();
-    uint32_t base = tile_off[blockIdx.x] + x - c;
-    for (uint32_t k = 0; k < wv; ++k) base += wsum[k];
-    if (!bits) return;
-    if (values && i + 16 <= n) {
-        uint32_t v[16];
-        for (int q = 0; q < 4; ++q) *(uint4 *)(v + 4 * q) = *(const uint4 *)(values + i + 4 * q);
-        for (uint32_t k = 0; k < 16; ++k)
-            if (bits >> k & 1u) out[base++] = v[k];
-    } else {
-        for (uint32_t k = 0; k < 16; ++k)
-            if (bits >> k & 1u) out[base++] = values ? values[i + k] : i + k;
-    }
-}
-
-__global__ void k_cmp_total(uint32_t nt, const uint32_t *tile_cnt, const uint32_t *tile_off, uint32_t *total) {
-    *total = nt ? tile_off[nt - 1] + tile_cnt[nt - 1] : 0;
-}
-
-// debug (PX_PSA_SEGCHECK=1): compare the segmented sort with the radix sort
-__global__ void k_seg_cmp(uint32_t m, const uint64_t *k1, const uint32_t *v1, const uint64_t *k2, const uint32_t *v2,
-                          uint32_t *out) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= m) return;
-    if (k1[t] != k2[t] || v1[t] != v2[t]) {
-        const uint32_t c = atomicAdd(&out[0], 1u);
-        if (c == 0) {
-            out[1] = t;
+        const uint32_t before = tid ? sl[tid - 1] - 1u : 0u, after = tid < 255 ? sf[tid + 1] : 0xffffffffu;
+        uint32_t ac = 0;
+#pragma unroll
+        for (uint32_t c = 0; c < kC; ++c) {
+            const uint32_t i = i0 + c;
+            if (c < C && i < size) {
+                const uint32_t le = hm & ((2u << c) - 1u), gt = hm & ~((2u << c) - 1u);
+                const uint32_t hd = le ? i0 + (31u - (uint32_t)__clz(le)) : before;
+                const uint32_t nx = min(gt ? i0 + (uint32_t)__ffs(gt) - 1u : after, size);
+                put_sorted(start, i, pv[c], dv[c], (uint32_t)(sk[i] >> 12), (hm >> c) & 1u, hd, nx, tag, sa, sd, act, gsz,
+                           rank, ac, mx);
+            }
         }
+        active += ac;
+        sorted += size;
+        __syncthreads();  // (sk is refilled by the next group)
+    }
+    block_stat(ss, tid == 0 ? sorted : 0u, active, mx);
+}
+
+// big groups (host-driven steps): gather every member with key (group << 32 | key), radix
+// sort (stable: ties keep suffix-array order), place back, heads by a max-scan, then ranks
+// and subgroups.  boff = exclusive prefix of the groups' sizes (host-computed).
+__global__ void __launch_bounds__(256) k_big_gather(uint32_t nb, const uint64_t *list, const uint32_t *boff,
+                                                    const uint32_t *sa, const uint16_t *sd, const uint32_t *key,
+                                                    uint64_t *ck, uint32_t *cv, uint32_t *gp, uint16_t *gd, StepStat ss) {
+    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        const uint64_t ent = list[b];
+        const uint32_t start = (uint32_t)ent, size = (uint32_t)(ent >> 32), o = boff[b];
+        for (uint32_t i = threadIdx.x; i < size; i += blockDim.x) {
+            ck[o + i] = (uint64_t)b << 32 | key[start + i];
+            cv[o + i] = o + i;
+            gp[o + i] = sa[start + i];
+            gd[o + i] = sd[start + i];
+        }
+        if (threadIdx.x == 0) stat_put(ss, b, size, 0, 0);
     }
 }
+__global__ void __launch_bounds__(256) k_big_head(uint32_t T, const uint32_t *boff, const uint64_t *ck2, uint32_t *hf) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= T) return;
+    const uint64_t c = ck2[k];
+    const uint32_t b = (uint32_t)(c >> 32), key = (uint32_t)c;
+    hf[k] = (k == boff[b] || key != (uint32_t)ck2[k - 1] || key == 0) ? k : 0u;
+}
+__global__ void __launch_bounds__(256) k_big_put(uint32_t T, const uint64_t *list, const uint32_t *boff, const uint64_t *ck2,
+                                                 const uint32_t *cv2, const uint32_t *gp, const uint16_t *gd,
+                                                 const uint32_t *hf, const uint32_t *hk, const uint32_t *nk, uint32_t tag,
+                                                 uint32_t *sa, uint16_t *sd, uint8_t *act, uint32_t *gsz, uint32_t *rank,
+                                                 StepStat ss) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t ac = 0, mx = 0;
+    if (k < T) {
+        const uint64_t c = ck2[k];
+        const uint32_t b = (uint32_t)(c >> 32), key = (uint32_t)c, o = boff[b];
+        const uint32_t size = (uint32_t)(list[b] >> 32), q = k - o, src = cv2[k];
+        const uint32_t nxt = min(nk[k] - o, size);
+        put_sorted((uint32_t)list[b], q, gp[src], gd[src], key, hf[k] == k, hk[k] - o, nxt, tag, sa, sd, act, gsz, rank,
+                   ac, mx);
+    }
+    block_stat(ss, 0, ac, mx);
+}
+// nk[k] = the next head position after k (T past the last), from the head flags
+__global__ void __launch_bounds__(256) k_big_next(uint32_t T, const uint32_t *hf, uint32_t *nf) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= T) return;
+    nf[k] = k + 1 == T ? T : (hf[k + 1] == k + 1 ? k + 1 : 0xffffffffu);
+}
+
+struct Min {
+    PSA_DEV uint32_t operator()(uint32_t a, uint32_t b) const { return a < b ? a : b; }
+};
 
 // ---------------------------------------------------------------- nearest smaller positions
 // 64-ary min tree over the suffix array's values (text positions)
@@ -892,11 +1119,71 @@ struct Max {
 
 }  // namespace
 
+
 #define PSA_CHECK(x)                         \
     do {                                     \
         hipError_t e_ = (x);                 \
         if (e_ != hipSuccess) return e_;     \
     } while (0)
+
+namespace {
+// Device scratch borrowed from the runtime's heap and released on every exit, errors and
+// exceptions (PxFail from the heap) included.  The heap hands a released block out again
+// only to later work on the same stream, so releasing while kernels still use it is safe.
+class Scratch {
+  public:
+    explicit Scratch(const PsaAlloc &A) : A_(A) {}
+    Scratch(const Scratch &) = delete;
+    ~Scratch() {
+        for (auto &b : live_) A_.release(A_.self, b.first, b.second);
+    }
+    template <class T>
+    T *get(uint64_t bytes) {
+        void *p = A_.alloc(A_.self, bytes);
+        live_.emplace_back(p, bytes);
+        return static_cast<T *>(p);
+    }
+    void put(const void *p) {
+        for (size_t i = 0; i < live_.size(); ++i)
+            if (live_[i].first == p) {
+                A_.release(A_.self, live_[i].first, live_[i].second);
+                live_[i] = live_.back();
+                live_.pop_back();
+                return;
+            }
+    }
+
+  private:
+    const PsaAlloc &A_;
+    std::vector<std::pair<void *, uint64_t>> live_;
+};
+struct EventSet {
+    std::vector<hipEvent_t> e;
+    ~EventSet() {
+        for (auto x : e) (void)hipEventDestroy(x);
+    }
+    hipError_t make(size_t n, unsigned flags) {
+        while (e.size() < n) {
+            hipEvent_t x;
+            const hipError_t r = hipEventCreateWithFlags(&x, flags);
+            if (r != hipSuccess) return r;
+            e.push_back(x);
+        }
+        return hipSuccess;
+    }
+};
+bool env_on(const char *name) {
+    const char *v = std::getenv(name);
+    return v && *v == '1';
+}
+constexpr uint32_t kMaxSteps = 20;  // h doubles from >= 5 past 65,535 (the longest doc) in 15
+// persistent grids of the doubling kernels (grid-stride over windows, and over lists whose
+// sizes only the device knows)
+constexpr uint32_t kGridWin = 16384, kGridReg = 2048, kGridBlk = 1024;
+// the cnt words of psa_run
+constexpr uint32_t kCntLong = 0, kCntSorted = 16, kCntActive = 48, kCntMax = 96, kCntCand = 200, kCntWords = 256;
+static_assert(kCntSorted + kMaxSteps < kCntActive && kCntActive + kMaxSteps + 1 < kCntMax && kCntMax + kMaxSteps + 1 < kCntCand, "cnt layout");
+}  // namespace
 
 // Runs the pipeline; messages land in every new doc's msg array, the new records' chunk /
 // slot / status in rec_*, and shard_flag[k] (device, zeroed by the caller) is set for shards
@@ -907,216 +1194,202 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
                    const PsaShard *shards, uint32_t N, uint32_t *rec_chunk, uint32_t *rec_idx, uint32_t *rec_status,
                    uint32_t *shard_flag, bool any_pools, PsaPoolOut *pool_out, PsaStats *st) {
     if (!N || !ndocs) return hipSuccess;
-    auto get = [&](uint64_t n) { return A.alloc(A.self, n); };
-    auto put = [&](void *p, uint64_t n) { A.release(A.self, p, n); };
-    hipEvent_t e0, e1, e2, e3, e4;
-    PSA_CHECK(hipEventCreate(&e4));
-    PSA_CHECK(hipEventCreate(&e0));
-    PSA_CHECK(hipEventCreate(&e1));
-    PSA_CHECK(hipEventCreate(&e2));
-    PSA_CHECK(hipEventCreate(&e3));
+    if (nshards > kPsaMaxShards) return hipErrorInvalidValue;  // (the caller splits rounds below this)
+    Scratch S(A);
+    EventSet ev, sev;
+    PSA_CHECK(ev.make(5, hipEventDefault));
+    hipEvent_t e0 = ev.e[0], e1 = ev.e[1], e2 = ev.e[2], e3 = ev.e[3], e4 = ev.e[4];
+    const bool verbose = env_on("PX_PSA_VERBOSE");
     PSA_CHECK(hipEventRecord(e0, s));
     const uint64_t n64 = N;
-    auto *G = (uint8_t *)get(n64 + 64);
-    auto *pdoc = (uint32_t *)get(n64 * 4);
-    auto *dist = (uint16_t *)get(n64 * 2);
-    auto *rank = (uint32_t *)get(n64 * 4);
-    auto *sa = (uint32_t *)get(n64 * 4);
-    auto *keys = (uint64_t *)get(n64 * 8);
-    auto *keys2 = (uint64_t *)get(n64 * 8);
-    auto *vals = (uint32_t *)get(n64 * 4);
-    auto *vals2 = (uint32_t *)get(n64 * 4);
-    auto *f1 = (uint32_t *)get(n64 * 4);
-    auto *f2 = (uint32_t *)get(n64 * 4);
-    auto *act = (uint8_t *)get(n64);
-    auto *cnt = (uint32_t *)get(64);
-    PSA_CHECK(hipMemsetAsync(G + N, 0, 64, s));  // (ld8 reads up to 15 bytes past the text)
     const uint32_t tb = 256;
     auto blocks = [&](uint64_t n) { return (uint32_t)((n + tb - 1) / tb); };
+    auto *G = S.get<uint8_t>(n64 + 64);
+    auto *pdoc = S.get<uint32_t>(n64 * 4);
+    auto *dist = S.get<uint16_t>(n64 * 2);
+    auto *rank = S.get<uint32_t>(n64 * 4);
+    auto *sa = S.get<uint32_t>(n64 * 4);
+    // cnt: counters read back by the host (kCnt* offsets)
+    auto *cnt = S.get<uint32_t>(kCntWords * 4);
+    uint32_t *ncand = cnt + kCntCand;
+    PSA_CHECK(hipMemsetAsync(G + N, 0, 64, s));  // (ld8 reads up to 15 bytes past the text)
+    PSA_CHECK(hipMemsetAsync(cnt, 0, kCntWords * 4, s));
+
+    // ---- first sort: shard | `syms` symbols of 9 bits
     int shard_bits = 1;
-    while ((1u << shard_bits) <= nshards && shard_bits < 19) ++shard_bits;
+    while ((1u << shard_bits) < nshards) ++shard_bits;
     const uint32_t syms = std::min<uint32_t>(6, (64 - shard_bits) / 9);  // 5 or 6 symbols
     k_psa_gather<<<std::min<uint32_t>((ndocs + 3) / 4, 65535u), 256, 0, s>>>(ndocs, docs, G, pdoc, dist);
+    auto *keys = S.get<uint64_t>(n64 * 8);
+    auto *keys2 = S.get<uint64_t>(n64 * 8);
+    auto *vals = S.get<uint32_t>(n64 * 4);
     k_psa_key0<<<blocks(N), tb, 0, s>>>(N, G, pdoc, docs, dist, syms, keys, vals);
-    // temp storage: the largest of sort / scan / select over N elements
-    size_t t_sort = 0, t_scan = 0, t_sel = 0;
-    PSA_CHECK(rocprim::radix_sort_pairs(nullptr, t_sort, keys, keys2, vals, sa, (size_t)N, 0, 64, s));
-    PSA_CHECK(rocprim::inclusive_scan(nullptr, t_scan, f1, f1, (size_t)N, Max(), s));
-    PSA_CHECK(rocprim::select(nullptr, t_sel, sa, act, vals, cnt, (size_t)N, s));
-    size_t t_sel2 = 0, t_sel3 = 0;
-    PSA_CHECK(rocprim::select(nullptr, t_sel2, rocprim::counting_iterator<uint32_t>(0), act, vals, cnt, (size_t)N, s));
-    PSA_CHECK(rocprim::exclusive_scan(nullptr, t_sel3, f1, f2, 0u, (size_t)N, rocprim::plus<uint32_t>(), s));
-    t_sel = std::max({t_sel, t_sel2, t_sel3});
-    const size_t t_bytes = std::max({t_sort, t_scan, t_sel}) + 256;
-    void *tmp = get(t_bytes);
-    // stream compaction (k_cmp_*): out = the flagged values (or indices), count -> cnt[0]
-    const uint64_t n_tiles = (n64 + kCmpTile - 1) / kCmpTile + 1;
-    auto *tcnt = (uint32_t *)get(n_tiles * 8);
-    uint32_t *toff = tcnt + n_tiles;
-    auto compact = [&](const uint8_t *fl, const uint32_t *vin, uint32_t *out, uint32_t n) -> hipError_t {
-        const uint32_t nt = (n + kCmpTile - 1) / kCmpTile;
-        if (!nt) return hipMemsetAsync(cnt, 0, 4, s);
-        k_cmp_count<<<nt, 256, 0, s>>>(n, fl, tcnt);
-        size_t b = t_bytes;
-        const hipError_t e = rocprim::exclusive_scan(tmp, b, tcnt, toff, 0u, (size_t)nt, rocprim::plus<uint32_t>(), s);
+    {
+        size_t t_sort = 0, t_scan = 0;
+        PSA_CHECK(rocprim::radix_sort_pairs(nullptr, t_sort, keys, keys2, vals, sa, (size_t)N, 0, 9 * syms + shard_bits, s));
+        PSA_CHECK(rocprim::inclusive_scan(nullptr, t_scan, vals, vals, (size_t)N, Max(), s));
+        size_t t_bytes = std::max(t_sort, t_scan) + 256;
+        void *tmp = S.get<void>(t_bytes);
+        PSA_CHECK(rocprim::radix_sort_pairs(tmp, t_bytes, keys, keys2, vals, sa, (size_t)N, 0, 9 * syms + shard_bits, s));
+        uint32_t *hflag = (uint32_t *)keys, *head = (uint32_t *)keys + N;  // (the unsorted keys are spent)
+        k_psa_head0<<<blocks(N), tb, 0, s>>>(N, keys2, hflag);
+        t_bytes = std::max(t_sort, t_scan) + 256;
+        PSA_CHECK(rocprim::inclusive_scan(tmp, t_bytes, hflag, head, (size_t)N, Max(), s));
+        S.put(tmp);
+        S.put(keys2);
+        S.put(vals);
+    }
+    // ---- the first groups, then prefix doubling over them
+    auto *sd = S.get<uint16_t>(n64 * 2);
+    auto *act = S.get<uint8_t>(n64 + 64);
+    auto *gsz = S.get<uint32_t>(n64 * 4 + 64);
+    // step k's counters: suffixes sorted, slots still in groups after it, largest group left
+    // (index 0 of active / maxsz: after the first grouping)
+    // (region 0: the first grouping, region k + 1: step k)
+    auto *stat_sh = S.get<uint32_t>((uint64_t)(kMaxSteps + 1) * kStatShards * kStatStride * 4);
+    PSA_CHECK(hipMemsetAsync(stat_sh, 0, (size_t)(kMaxSteps + 1) * kStatShards * kStatStride * 4, s));
+    auto region = [&](uint32_t k) { return StepStat{stat_sh + (uint64_t)k * kStatShards * kStatStride}; };
+    auto stats_of = [&](uint32_t k) { return region(k + 1); };
+    k_psa_groups0<<<blocks(N), tb, 0, s>>>(N, sa, (const uint32_t *)keys + N, dist, rank, sd, act, gsz, region(0));
+    k_stat_sum<<<1, 64, 0, s>>>(region(0).sh, cnt + kCntSorted + kMaxSteps, cnt + kCntActive, cnt + kCntMax);
+    S.put(keys);
+    auto *key = S.get<uint32_t>(n64 * 4 + 64);
+    LongLists LL;
+    {
+        const uint32_t lo[kLongClasses] = {kWinMax + 1, 129, 257, kRegMax + 1, kMedMax + 1};
+        for (int c = 0; c < kLongClasses; ++c) {
+            LL.cap[c] = (uint32_t)(n64 / lo[c] + 64);
+            LL.lst[c] = S.get<uint64_t>((uint64_t)LL.cap[c] * 8);
+        }
+        LL.cnt = cnt + kCntLong;
+    }
+    uint32_t *pin = A.pin;  // pinned host words: counts come back through them
+    auto read_words = [&](uint32_t at, uint32_t n) -> hipError_t {  // -> pin[at .. at + n)
+        hipError_t e = hipMemcpyAsync(pin + at, cnt + at, n * 4, hipMemcpyDeviceToHost, s);
+        return e == hipSuccess ? hipStreamSynchronize(s) : e;
+    };
+    PSA_CHECK(read_words(0, kCntWords));
+    uint32_t active = pin[kCntActive], maxsz = pin[kCntMax];
+    uint32_t h = syms, it = 0;
+    const uint32_t gwin = std::min<uint32_t>((uint32_t)((n64 + 255) / 256), kGridWin);
+    // one step: every group's keys (flat), then every group sorted by them (windows, then
+    // the long-group lists the window kernel filled); big groups need their count on the host
+    auto step = [&](bool big) -> hipError_t {
+        const uint32_t tag = (it & 1u) ? kTag : 0u;
+        const StepStat ss = stats_of(it);
+        hipError_t e = hipMemsetAsync(cnt + kCntLong, 0, 8 * 4, s);
         if (e != hipSuccess) return e;
-        k_cmp_write<<<nt, 256, 0, s>>>(n, fl, vin, toff, out);
-        k_cmp_total<<<1, 1, 0, s>>>(nt, tcnt, toff, cnt);
+        k_dbl_key<<<blocks((n64 + 15) / 16), tb, 0, s>>>(N, h, act, sa, sd, rank, key);
+        k_dbl_win<<<gwin, 256, 0, s>>>(N, tag, sa, sd, act, gsz, key, rank, LL, ss);
+        k_dbl_reg<2><<<kGridReg, 256, 0, s>>>(LL.lst[0], LL.cnt + 0, tag, sa, sd, act, gsz, key, rank, ss);
+        k_dbl_reg<4><<<kGridReg, 256, 0, s>>>(LL.lst[1], LL.cnt + 1, tag, sa, sd, act, gsz, key, rank, ss);
+        k_dbl_reg<8><<<kGridReg, 256, 0, s>>>(LL.lst[2], LL.cnt + 2, tag, sa, sd, act, gsz, key, rank, ss);
+        k_dbl_blk<<<kGridBlk, 256, 0, s>>>(LL.lst[3], LL.cnt + 3, tag, sa, sd, act, gsz, key, rank, ss);
+        auto sum = [&]() {
+            k_stat_sum<<<1, 64, 0, s>>>(ss.sh, cnt + kCntSorted + it, cnt + kCntActive + 1 + it, cnt + kCntMax + 1 + it);
+        };
+        if (big) {
+            e = read_words(kCntLong, 8);
+            if (e != hipSuccess) return e;
+            const uint32_t nbig = pin[kCntLong + 4];
+            if (pin[kCntLong + kLongClasses]) return hipErrorUnknown;  // (list overflow: cannot happen)
+            if (nbig) {
+                std::vector<uint64_t> bl(nbig);
+                e = hipMemcpy(bl.data(), LL.lst[4], (size_t)nbig * 8, hipMemcpyDeviceToHost);  // (synchronous)
+                if (e != hipSuccess) return e;
+                std::vector<uint32_t> boff(nbig);
+                uint64_t T = 0;
+                for (uint32_t b = 0; b < nbig; ++b) {
+                    boff[b] = (uint32_t)T;
+                    T += bl[b] >> 32;
+                }
+                auto *d_boff = S.get<uint32_t>((uint64_t)nbig * 4 + 64);
+                e = hipMemcpy(d_boff, boff.data(), (size_t)nbig * 4, hipMemcpyHostToDevice);
+                if (e != hipSuccess) return e;
+                auto *ck = S.get<uint64_t>(T * 8), *ck2 = S.get<uint64_t>(T * 8);
+                auto *cv = S.get<uint32_t>(T * 4), *cv2 = S.get<uint32_t>(T * 4);
+                auto *gp = S.get<uint32_t>(T * 4), *hf = S.get<uint32_t>(T * 4), *hk = S.get<uint32_t>(T * 4);
+                auto *nf = S.get<uint32_t>(T * 4), *nk = S.get<uint32_t>(T * 4);
+                auto *gd = S.get<uint16_t>(T * 2 + 64);
+                k_big_gather<<<std::min<uint32_t>(nbig, 65535u), 256, 0, s>>>(nbig, LL.lst[4], d_boff, sa, sd, key, ck, cv,
+                                                                               gp, gd, ss);
+                int bbits = 1;
+                while ((1ull << bbits) < nbig) ++bbits;
+                size_t t1 = 0, t2 = 0, t3 = 0;
+                auto rev_in = rocprim::make_reverse_iterator(nf + T);
+                auto rev_out = rocprim::make_reverse_iterator(nk + T);
+                e = rocprim::radix_sort_pairs(nullptr, t1, ck, ck2, cv, cv2, (size_t)T, 0, 32 + bbits, s);
+                if (e == hipSuccess) e = rocprim::inclusive_scan(nullptr, t2, hf, hk, (size_t)T, Max(), s);
+                if (e == hipSuccess) e = rocprim::inclusive_scan(nullptr, t3, rev_in, rev_out, (size_t)T, Min(), s);
+                if (e != hipSuccess) return e;
+                const size_t tt0 = std::max({t1, t2, t3}) + 256;
+                void *tmp = S.get<void>(tt0);
+                size_t tt = tt0;
+                e = rocprim::radix_sort_pairs(tmp, tt, ck, ck2, cv, cv2, (size_t)T, 0, 32 + bbits, s);
+                if (e != hipSuccess) return e;
+                k_big_head<<<blocks(T), tb, 0, s>>>((uint32_t)T, d_boff, ck2, hf);
+                k_big_next<<<blocks(T), tb, 0, s>>>((uint32_t)T, hf, nf);
+                tt = tt0;
+                e = rocprim::inclusive_scan(tmp, tt, hf, hk, (size_t)T, Max(), s);
+                if (e != hipSuccess) return e;
+                tt = tt0;
+                e = rocprim::inclusive_scan(tmp, tt, rev_in, rev_out, (size_t)T, Min(), s);
+                if (e != hipSuccess) return e;
+                k_big_put<<<blocks(T), tb, 0, s>>>((uint32_t)T, LL.lst[4], d_boff, ck2, cv2, gp, gd, hf, hk, nk, tag, sa, sd,
+                                                   act, gsz, rank, ss);
+                for (const void *q : {(const void *)d_boff, (const void *)ck, (const void *)ck2, (const void *)cv,
+                                      (const void *)cv2, (const void *)gp, (const void *)hf, (const void *)hk,
+                                      (const void *)nf, (const void *)nk, (const void *)gd, (const void *)tmp})
+                    S.put(q);
+            }
+        }
+        sum();
+        ++it;
+        h *= 2;
         return hipGetLastError();
     };
-    size_t tb_ = t_bytes;
-    PSA_CHECK(rocprim::radix_sort_pairs(tmp, tb_, keys, keys2, vals, sa, (size_t)N, 0, 9 * syms + shard_bits, s));
-    k_psa_head0<<<blocks(N), tb, 0, s>>>(N, keys2, sa, dist, syms, f1);
-    tb_ = t_bytes;
-    PSA_CHECK(rocprim::inclusive_scan(tmp, tb_, f1, vals2, (size_t)N, Max(), s));
-    k_psa_rank0<<<blocks(N), tb, 0, s>>>(N, sa, vals2, rank, act);
-    tb_ = t_bytes;
-    uint32_t *alist = vals;  // active suffixes, in suffix-array order
-    PSA_CHECK(compact(act, sa, alist, N));
-    uint32_t m = 0;
-    // (counts come back through a synchronous copy after the stream drained: no async
-    // copy into pageable memory, see px_runtime.cpp d2h)
-    PSA_CHECK(hipStreamSynchronize(s));
-    PSA_CHECK(hipMemcpy(&m, cnt, 4, hipMemcpyDeviceToHost));
-    int rank_bits = 1;
-    while (rank_bits < 32 && (1ull << rank_bits) <= n64) ++rank_bits;
-    const bool verbose = [] {
-        const char *v = std::getenv("PX_PSA_VERBOSE");
-        return v && *v == '1';
-    }();
-    const bool segcheck = [] {
-        const char *v = std::getenv("PX_PSA_SEGCHECK");
-        return v && *v == '1';
-    }();
-    const bool segsort = [] {  // PX_PSA_SEGSORT=0: every doubling step through the radix sort
-        const char *e = std::getenv("PX_PSA_SEGSORT");
-        return !(e && e[0] == '0');
-    }();
-    // group starts and the three group lists (an active group has >= 2 suffixes: <= m/2 groups)
-    const uint64_t half = n64 / 2 + 64;
-    auto *gsl = segsort ? (uint32_t *)get(half * 12) : nullptr;
-    uint32_t it = 0;
-    for (uint32_t h = syms; m > 0; h *= 2, ++it) {
-        if (st && it < 24) st->active[it] = m;
-        if (it >= 20) return hipErrorUnknown;  // cannot happen: docs are <= 65,535 bytes
-        k_psa_key2<<<blocks(m), tb, 0, s>>>(m, alist, rank, dist, h, keys, vals2);
-        if (segsort) {
-            // groups are ranges of the (suffix-array ordered) keys: sort each where it lies
-            k_seg_flag<<<blocks(m), tb, 0, s>>>(m, keys, act);
-            tb_ = t_bytes;
-            PSA_CHECK(compact(act, nullptr, gsl, m));
-            PSA_CHECK(hipStreamSynchronize(s));
-            uint32_t ng = 0;
-            PSA_CHECK(hipMemcpy(&ng, cnt, 4, hipMemcpyDeviceToHost));
-            uint32_t *lists = gsl + half;
-            const uint32_t nbk = blocks(ng);
-            uint32_t *hist = gsl + 2 * half, *offs = hist + (uint64_t)kSegClasses * nbk;
-            k_seg_hist<<<nbk, tb, 0, s>>>(ng, gsl, m, nbk, hist);
-            tb_ = t_bytes;
-            PSA_CHECK(rocprim::exclusive_scan(tmp, tb_, hist, offs, 0u, (size_t)kSegClasses * nbk, rocprim::plus<uint32_t>(), s));
-            k_seg_part<<<nbk, tb, 0, s>>>(ng, gsl, m, nbk, offs, lists);
-            k_seg_bounds<<<1, 64, 0, s>>>(nbk, offs, ng, cnt + 1);
-            PSA_CHECK(hipStreamSynchronize(s));
-            uint32_t cb[kSegClasses + 1] = {};
-            PSA_CHECK(hipMemcpy(cb, cnt + 1, sizeof cb, hipMemcpyDeviceToHost));
-            uint32_t c8[kSegClasses];
-            uint32_t *lc[kSegClasses];
-            for (int c = 0; c < kSegClasses; ++c) {
-                c8[c] = cb[c + 1] - cb[c];
-                lc[c] = lists + cb[c];
-            }
-            if (verbose)
-                fprintf(stderr, "psa: step %u h=%u m=%u groups=%u (<=2..64: %u %u %u %u %u %u, <=%u: %u, larger: %u)\n",
-                        it, h, m, ng, c8[0], c8[1], c8[2], c8[3], c8[4], c8[5], kSegBlock, c8[6], c8[7]);
-            auto grid = [&](uint32_t n, uint32_t per_wave) {
-                return std::min<uint32_t>((n + 4 * per_wave - 1) / (4 * per_wave), 1u << 16);
-            };
-            if (c8[0]) k_seg_sortS<2><<<grid(c8[0], 32), 256, 0, s>>>(c8[0], lc[0], gsl, ng, m, keys, vals2, keys2, f2);
-            if (c8[1]) k_seg_sortS<4><<<grid(c8[1], 16), 256, 0, s>>>(c8[1], lc[1], gsl, ng, m, keys, vals2, keys2, f2);
-            if (c8[2]) k_seg_sortS<8><<<grid(c8[2], 8), 256, 0, s>>>(c8[2], lc[2], gsl, ng, m, keys, vals2, keys2, f2);
-            if (c8[3]) k_seg_sortS<16><<<grid(c8[3], 4), 256, 0, s>>>(c8[3], lc[3], gsl, ng, m, keys, vals2, keys2, f2);
-            if (c8[4]) k_seg_sortS<32><<<grid(c8[4], 2), 256, 0, s>>>(c8[4], lc[4], gsl, ng, m, keys, vals2, keys2, f2);
-            if (c8[5]) k_seg_sortS<64><<<grid(c8[5], 1), 256, 0, s>>>(c8[5], lc[5], gsl, ng, m, keys, vals2, keys2, f2);
-            if (c8[6]) k_seg_sortblk<<<c8[6], 256, 0, s>>>(lc[6], gsl, ng, m, keys, vals2, keys2, f2);
-            PSA_CHECK(hipGetLastError());
-            uint32_t c3[3] = {0, 0, c8[7]};
-            uint32_t *lbig = lc[7];
-            if (c3[2]) {
-                PSA_CHECK(hipMemsetAsync(act, 0, m, s));
-                k_seg_mark<<<c3[2], 256, 0, s>>>(lbig, gsl, ng, m, act);
-                uint32_t *tl = f1;  // free until the group-head scan below
-                tb_ = t_bytes;
-                PSA_CHECK(compact(act, nullptr, tl, m));
-                PSA_CHECK(hipStreamSynchronize(s));
-                uint32_t ml = 0;
-                PSA_CHECK(hipMemcpy(&ml, cnt, 4, hipMemcpyDeviceToHost));
-                auto *ck = (uint64_t *)get((uint64_t)ml * 24 + 64);
-                uint64_t *ck2 = ck + ml;
-                auto *cv = (uint32_t *)(ck2 + ml), *cv2 = cv + ml;
-                k_seg_gather<<<blocks(ml), tb, 0, s>>>(ml, tl, keys, vals2, ck, cv);
-                tb_ = t_bytes;
-                PSA_CHECK(rocprim::radix_sort_pairs(tmp, tb_, ck, ck2, cv, cv2, (size_t)ml, 0, 32 + rank_bits, s));
-                k_seg_scatter<<<blocks(ml), tb, 0, s>>>(ml, tl, ck2, cv2, keys2, f2);
-                PSA_CHECK(hipStreamSynchronize(s));
-                put(ck, (uint64_t)ml * 24 + 64);
-            }
-            if (segcheck) {
-                auto *k3 = (uint64_t *)get((uint64_t)m * 12 + 64);
-                auto *v3 = (uint32_t *)(k3 + m);
-                tb_ = t_bytes;
-                PSA_CHECK(rocprim::radix_sort_pairs(tmp, tb_, keys, k3, vals2, v3, (size_t)m, 0, 32 + rank_bits, s));
-                PSA_CHECK(hipMemsetAsync(cnt + 12, 0, 8, s));
-                k_seg_cmp<<<blocks(m), tb, 0, s>>>(m, keys2, f2, k3, v3, cnt + 12);
-                PSA_CHECK(hipStreamSynchronize(s));
-                uint32_t r2[2];
-                PSA_CHECK(hipMemcpy(r2, cnt + 12, 8, hipMemcpyDeviceToHost));
-                if (r2[0]) {
-                    uint64_t a[4], b[4];
-                    uint32_t va[4], vb[4];
-                    const uint32_t t0 = r2[1] > 1 ? r2[1] - 1 : 0;
-                    PSA_CHECK(hipMemcpy(a, keys2 + t0, 32, hipMemcpyDeviceToHost));
-                    PSA_CHECK(hipMemcpy(b, k3 + t0, 32, hipMemcpyDeviceToHost));
-                    PSA_CHECK(hipMemcpy(va, f2 + t0, 16, hipMemcpyDeviceToHost));
-                    PSA_CHECK(hipMemcpy(vb, v3 + t0, 16, hipMemcpyDeviceToHost));
-                    fprintf(stderr, "psa segcheck step %u: %u mismatches, first at t=%u\n", it, r2[0], r2[1]);
-                    for (int q = 0; q < 4; ++q)
-                        fprintf(stderr, "  t=%u seg %016llx/%u radix %016llx/%u\n", t0 + q, (unsigned long long)a[q], va[q],
-                                (unsigned long long)b[q], vb[q]);
-                }
-                put(k3, (uint64_t)m * 12 + 64);
-            }
-        } else {
-            tb_ = t_bytes;
-            PSA_CHECK(rocprim::radix_sort_pairs(tmp, tb_, keys, keys2, vals2, f2, (size_t)m, 0, 32 + rank_bits, s));
-        }
-        // f2 = positions in the new order; group heads f1 -> vals2, subgroup heads in the
-        // (now free) unsorted key buffer: flags in its first half, scan in its second
-        uint32_t *sfl = (uint32_t *)keys, *sfirst = (uint32_t *)keys + N;
-        k_psa_head2<<<blocks(m), tb, 0, s>>>(m, keys2, f1, sfl);
-        tb_ = t_bytes;
-        PSA_CHECK(rocprim::inclusive_scan(tmp, tb_, f1, vals2, (size_t)m, Max(), s));
-        tb_ = t_bytes;
-        PSA_CHECK(rocprim::inclusive_scan(tmp, tb_, sfl, sfirst, (size_t)m, Max(), s));
-        k_psa_rank2<<<blocks(m), tb, 0, s>>>(m, keys2, f2, vals2, sfirst, sa, rank, act);
-        tb_ = t_bytes;
-        PSA_CHECK(compact(act, f2, alist, m));
-        PSA_CHECK(hipStreamSynchronize(s));
-        PSA_CHECK(hipMemcpy(&m, cnt, 4, hipMemcpyDeviceToHost));
+    // host-driven while a group may exceed kMedMax (its radix sort needs the host); groups
+    // only split, so afterwards the steps run without host round trips: the host stays one
+    // step ahead and stops one (empty, cheap) step after the last group
+    while (active > 0 && maxsz > kMedMax) {
+        if (it >= kMaxSteps) return hipErrorUnknown;  // cannot happen: docs are <= 65,535 bytes
+        PSA_CHECK(step(true));
+        PSA_CHECK(read_words(0, kCntWords));
+        active = pin[kCntActive + it];
+        maxsz = pin[kCntMax + it];
+        if (verbose)
+            fprintf(stderr, "psa: step %u (host) sorted %u (long groups %u %u %u %u %u) -> %u in groups, largest %u\n",
+                    it - 1, pin[kCntSorted + it - 1], pin[kCntLong], pin[kCntLong + 1], pin[kCntLong + 2],
+                    pin[kCntLong + 3], pin[kCntLong + 4], active, maxsz);
     }
-    if (st) st->iterations = it;
-    put(keys2, n64 * 8);
-    put(vals2, n64 * 4);
-    put(act, n64);
-    if (gsl) put(gsl, half * 12);
-    put(tcnt, n_tiles * 8);
-    put(tmp, t_bytes);
+    if (active > 0) {
+        PSA_CHECK(sev.make(kMaxSteps, hipEventDisableTiming));
+        const uint32_t it0 = it;
+        bool done = false;
+        while (!done) {
+            if (it >= kMaxSteps) return hipErrorUnknown;
+            PSA_CHECK(step(false));
+            const uint32_t k = it - 1;
+            PSA_CHECK(hipMemcpyAsync(pin + 256 + k, cnt + kCntActive + 1 + k, 4, hipMemcpyDeviceToHost, s));
+            PSA_CHECK(hipEventRecord(sev.e[k], s));
+            if (k >= it0 + 1) {
+                PSA_CHECK(hipEventSynchronize(sev.e[k - 1]));
+                done = pin[256 + k - 1] == 0;
+            }
+        }
+    }
+    PSA_CHECK(read_words(0, kCntWords));
+    if (pin[kCntActive + it] != 0 || pin[kCntLong + kLongClasses]) return hipErrorUnknown;
+    for (const void *q : {(const void *)sd, (const void *)act, (const void *)gsz, (const void *)key}) S.put(q);
+    for (int c = 0; c < kLongClasses; ++c) S.put(LL.lst[c]);
     PSA_CHECK(hipEventRecord(e1, s));
+
     // ---- nearest smaller positions in suffix-array order (min tree over sa)
     MinTree t{};
     t.lvl[0] = sa;
     t.n[0] = N;
     t.levels = 1;
-    uint32_t *lv_buf = (uint32_t *)keys;  // the key buffer is free now: tree levels live in it
+    auto *lv_buf = S.get<uint32_t>(n64 / 64 * 4 * 2 + 1024);
     uint64_t lv_off = 0;
     while (t.n[t.levels - 1] > 1 && t.levels < 8) {
         const uint32_t nin = t.n[t.levels - 1];
@@ -1128,112 +1401,79 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         t.n[t.levels] = nout;
         ++t.levels;
     }
-    uint32_t *psvp = f1, *nsvp = f2;
+    auto *psvp = S.get<uint32_t>(n64 * 4), *nsvp = S.get<uint32_t>(n64 * 4);
     {
-        auto *links = (uint2 *)get(n64 * 8);
+        auto *links = S.get<uint2>(n64 * 8);
         k_psa_ansv<<<(uint32_t)((n64 + 255) / 256), 256, 0, s>>>(N, t, shards, nshards, links);
         k_psa_links_text<<<blocks(N), tb, 0, s>>>(N, rank, links, psvp, nsvp);
-        put(links, n64 * 8);  // (stream-ordered reuse)
+        S.put(links);
     }
+    S.put(lv_buf);
+    S.put(sa);
     auto *lcp_p = (uint16_t *)rank;  // ranks are no longer needed: two u16 arrays in their place
-    auto *lcp_n = (uint16_t *)get(n64 * 2);
+    auto *lcp_n = S.get<uint16_t>(n64 * 2);
     const uint32_t lsp = lce_span(n64);
     k_psa_lce<<<blocks((n64 + lsp - 1) / lsp), tb, 0, s>>>(N, (const uint64_t *)G, dist, psvp, nsvp, lcp_p, lcp_n, lsp);
     PSA_CHECK(hipEventRecord(e2, s));
-    if (verbose) {
-        PSA_CHECK(hipStreamSynchronize(s));
-        fprintf(stderr, "psa: links + lcp done\n");
-    }
     // ---- messages
     k_psa_msg0<<<blocks(N), tb, 0, s>>>(N, pdoc, docs, lcp_p, lcp_n);
     k_psa_runs<<<blocks(N), tb, 0, s>>>(N, G, pdoc, docs, dist, psvp, nsvp, lcp_p, lcp_n, shard_flag);
     k_psa_place<<<blocks(ndocs), tb, 0, s>>>(ndocs, docs, shards, rec_chunk, rec_idx, rec_status);
     PSA_CHECK(hipEventRecord(e3, s));
-    if (verbose) {
-        PSA_CHECK(hipStreamSynchronize(s));
-        fprintf(stderr, "psa: messages done\n");
-    }
     if (any_pools) {  // ---- MemPool emulation (rotation points)
-        auto *code = (uint8_t *)get(n64 + 64);
-        auto *E = (uint32_t *)keys, *blk = (uint32_t *)keys + N;  // the key buffer is free
-        uint32_t *P = vals;
-        PSA_CHECK(hipMemsetAsync(cnt + 14, 0, 4, s));
-        auto *rec = (LinkRec *)get(n64 * sizeof(LinkRec));
-        k_pool_pack<<<blocks(N), tb, 0, s>>>(N, psvp, nsvp, lcp_p, lcp_n, dist, rec);
-        k_pool_leaf<<<blocks(N), tb, 0, s>>>(N, G, pdoc, docs, shards, rec, code, E, cnt + 14);
-        put(rec, n64 * sizeof(LinkRec));  // (stream-ordered: the heap hands it out again only later)
+        auto *code = S.get<uint8_t>(n64 + 64);
+        auto *E = S.get<uint32_t>(n64 * 4), *blk = S.get<uint32_t>(n64 * 4), *P = S.get<uint32_t>(n64 * 4);
+        {
+            auto *rec = S.get<LinkRec>(n64 * sizeof(LinkRec));
+            k_pool_pack<<<blocks(N), tb, 0, s>>>(N, psvp, nsvp, lcp_p, lcp_n, dist, rec);
+            k_pool_leaf<<<blocks(N), tb, 0, s>>>(N, G, pdoc, docs, shards, rec, code, E, ncand);
+            S.put(rec);
+        }
         // the candidate table: 2x the candidates, read back for big windows; a small window
         // (one chunk, the single instance's rounds) sizes it from N and skips the round trip
         uint32_t nc = 0;
         uint64_t cap = 1024;
         const bool small_n = N <= (1u << 26);
-        const bool pv = [] {
-            const char *v = std::getenv("PX_PSA_VERBOSE");
-            return v && *v == '1';
-        }();
-        if (!small_n || pv) {
+        if (!small_n || verbose) {
+            PSA_CHECK(hipMemcpyAsync(pin, ncand, 4, hipMemcpyDeviceToHost, s));
             PSA_CHECK(hipStreamSynchronize(s));
-            PSA_CHECK(hipMemcpy(&nc, cnt + 14, 4, hipMemcpyDeviceToHost));
-            if (pv) fprintf(stderr, "psa pools: %u split candidates\n", nc);
+            nc = pin[0];
+            if (verbose) fprintf(stderr, "psa pools: %u split candidates\n", nc);
         }
         while (cap < 2ull * (small_n ? N : nc)) cap <<= 1;
-        auto *tab = (PoolSlot *)get(cap * sizeof(PoolSlot));
+        auto *tab = S.get<PoolSlot>(cap * sizeof(PoolSlot));
         PSA_CHECK(hipMemsetAsync(tab, 0xff, cap * sizeof(PoolSlot), s));
         const uint32_t mask = (uint32_t)(cap - 1);
         k_pool_insert<<<blocks(N), tb, 0, s>>>(N, code, E, lcp_p, lcp_n, tab, mask);
-        if (pv) {
-            PSA_CHECK(hipStreamSynchronize(s));
-            fprintf(stderr, "psa pools: inserted (table %llu slots)\n", (unsigned long long)cap);
-        }
         k_pool_blocks<<<blocks(N), tb, 0, s>>>(N, code, E, lcp_p, lcp_n, tab, mask, blk);
         size_t tsz = 0;
         PSA_CHECK(rocprim::inclusive_scan(nullptr, tsz, blk, P, (size_t)N, rocprim::plus<uint32_t>(), s));
-        void *tmp2 = get(tsz + 256);
+        void *tmp2 = S.get<void>(tsz + 256);
         PSA_CHECK(rocprim::inclusive_scan(tmp2, tsz, blk, P, (size_t)N, rocprim::plus<uint32_t>(), s));
-        if (pv) {
-            PSA_CHECK(hipStreamSynchronize(s));
-            fprintf(stderr, "psa pools: blocks scanned\n");
-        }
-        auto *C = (uint32_t *)get(n64 / 64 * 4 + 256);
+        auto *C = S.get<uint32_t>(n64 / 64 * 4 + 256);
         k_pool_coarse<<<blocks((N + 63) / 64), tb, 0, s>>>(N, P, C);
         k_pool_scan<<<nshards, 64, 0, s>>>(nshards, shards, docs, P, C, N, pool_out);
-        put(C, n64 / 64 * 4 + 256);
         PSA_CHECK(hipGetLastError());
-        put(tmp2, tsz + 256);  // (stream-ordered reuse, as above)
-        put(tab, cap * sizeof(PoolSlot));
-        put(code, n64 + 64);
     }
     PSA_CHECK(hipEventRecord(e4, s));
+    PSA_CHECK(hipMemcpyAsync(pin, cnt, kCntWords * 4, hipMemcpyDeviceToHost, s));
     PSA_CHECK(hipEventSynchronize(e4));
-    if (any_pools && st) PSA_CHECK(hipMemcpy(&st->candidates, cnt + 14, 4, hipMemcpyDeviceToHost));
+    PSA_CHECK(hipStreamSynchronize(s));
     if (st) {
+        st->iterations = it;
+        for (uint32_t k = 0; k < 24; ++k) st->active[k] = k < kMaxSteps ? pin[kCntSorted + k] : 0;
+        st->candidates = any_pools ? pin[kCntCand] : 0;
         PSA_CHECK(hipEventElapsedTime(&st->ms_pool, e3, e4));
         PSA_CHECK(hipEventElapsedTime(&st->ms_sort, e0, e1));
         PSA_CHECK(hipEventElapsedTime(&st->ms_lcp, e1, e2));
         PSA_CHECK(hipEventElapsedTime(&st->ms_msg, e2, e3));
-        if (const char *v = std::getenv("PX_PSA_VERBOSE"); v && *v == '1') {
-            fprintf(stderr, "psa: N=%u docs=%u shards=%u syms=%u sort %.2f ms, links+lcp %.2f ms, msgs %.2f ms; active:",
+        if (verbose) {
+            fprintf(stderr, "psa: N=%u docs=%u shards=%u syms=%u sort %.2f ms, links+lcp %.2f ms, msgs %.2f ms; sorted:",
                     N, ndocs, nshards, syms, st->ms_sort, st->ms_lcp, st->ms_msg);
             for (uint32_t k = 0; k < it && k < 24; ++k) fprintf(stderr, " %u", st->active[k]);
             fprintf(stderr, "\n");
         }
     }
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    (void)hipEventDestroy(e2);
-    (void)hipEventDestroy(e3);
-    (void)hipEventDestroy(e4);
-    put(lcp_n, n64 * 2);
-    put(dist, n64 * 2);
-    put(G, n64 + 64);
-    put(pdoc, n64 * 4);
-    put(rank, n64 * 4);
-    put(sa, n64 * 4);
-    put(keys, n64 * 8);
-    put(vals, n64 * 4);
-    put(f1, n64 * 4);
-    put(f2, n64 * 4);
-    put(cnt, 64);
     return hipGetLastError();
 }
 

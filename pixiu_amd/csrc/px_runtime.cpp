@@ -25,6 +25,7 @@
 
 #include "../../include/pixiu_amd.h"
 #include "px_common.h"
+#include "px_host.h"
 
 namespace px {
 hipError_t launch_doc_len(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, const uint8_t *,
@@ -105,86 +106,23 @@ inline uint64_t pow2_at_least(uint64_t v) {
 }
 
 // ---------------------------------------------------------------- device heap
-// Best-fit allocator over 1 GiB slabs: a free block is split on allocation and merged
-// with its free neighbours (inside its slab) on release, so batches of varying sizes
-// reuse the same memory instead of growing the footprint.  No hipMalloc per shard.
-class DevHeap {
-  public:
-    ~DevHeap() {
-        for (auto &s : slabs_) (void)hipFree(s.first);
+// px_host.h's best-fit block heap over 1 GiB hipMalloc slabs: batches of varying sizes
+// reuse the same memory instead of growing the footprint; no hipMalloc per shard.
+struct HipRaw {
+    static void *get(uint64_t n) {
+        void *v = nullptr;
+        return hipMalloc(&v, n) == hipSuccess ? v : nullptr;
     }
+    static void put(void *p) { (void)hipFree(p); }
+};
+class DevHeap : public pxh::BlockHeap<HipRaw> {
+  public:
     void *alloc(uint64_t n) {
-        n = round_up(std::max<uint64_t>(n, 256), 256);
-        auto it = by_size_.lower_bound(n);
-        if (it == by_size_.end()) {
-            const uint64_t sz = std::max<uint64_t>(n, kSlab);
-            void *v = nullptr;
-            if (hipMalloc(&v, sz) != hipSuccess) throw PxFail{PX_ENOMEM};
-            char *s = static_cast<char *>(v);
-            slabs_.emplace(s, s + sz);
-            held_ += sz;
-            add_free(s, sz);
-            it = by_size_.lower_bound(n);
-        }
-        char *p = it->second;
-        uint64_t sz = it->first;
-        by_size_.erase(it);
-        by_addr_.erase(p);
-        if (sz - n >= 256) {  // split: the tail stays free
-            add_free(p + n, sz - n);
-            sz = n;
-        }
-        live_[p] = sz;
+        void *p = BlockHeap::alloc(n);
+        if (!p) throw PxFail{PX_ENOMEM};
         return p;
     }
-    void release(void *v, uint64_t) {
-        if (!v) return;
-        char *p = static_cast<char *>(v);
-        auto lv = live_.find(p);
-        if (lv == live_.end()) return;
-        uint64_t sz = lv->second;
-        live_.erase(lv);
-        auto slab = std::prev(slabs_.upper_bound(p));  // the slab holding p
-        // merge with the free block right after and right before, inside the slab
-        auto nx = by_addr_.find(p + sz);
-        if (nx != by_addr_.end() && nx->first < slab->second) {
-            sz += nx->second;
-            erase_free(nx->first, nx->second);
-        }
-        auto pv = by_addr_.lower_bound(p);
-        if (pv != by_addr_.begin()) {
-            --pv;
-            if (pv->first >= slab->first && pv->first + pv->second == p) {
-                char *q = pv->first;
-                const uint64_t qs = pv->second;
-                erase_free(q, qs);
-                p = q;
-                sz += qs;
-            }
-        }
-        add_free(p, sz);
-    }
-    uint64_t held() const { return held_; }
-
-  private:
-    void add_free(char *p, uint64_t sz) {
-        by_addr_[p] = sz;
-        by_size_.emplace(sz, p);
-    }
-    void erase_free(char *p, uint64_t sz) {
-        by_addr_.erase(p);
-        for (auto r = by_size_.equal_range(sz); r.first != r.second; ++r.first)
-            if (r.first->second == p) {
-                by_size_.erase(r.first);
-                break;
-            }
-    }
-    static constexpr uint64_t kSlab = 1ull << 30;
-    std::map<char *, char *> slabs_;  // start -> end
-    std::map<char *, uint64_t> by_addr_;
-    std::multimap<uint64_t, char *> by_size_;
-    std::unordered_map<void *, uint64_t> live_;
-    uint64_t held_ = 0;
+    void release(void *v, uint64_t) { BlockHeap::release(v); }
 };
 
 // pinned-free scratch buffer that only grows
@@ -230,277 +168,20 @@ struct HostBuf {
     }
 };
 
-// raw key -> shard for multi-shard stores.  Open addressing over 64-bit key hashes
-// with the key bytes in one arena: a lookup touches one slot and the key's bytes,
-// with no per-key heap node and no std::string built for the probe.
-class KeyMap {
-    struct Slot {
-        uint64_t h, off;
-        uint32_t len, shard;  // len == kFree: empty
-        uint32_t chunk, idx;  // the record last stored under the key (a hint: verified on use)
-    };
-    static constexpr uint32_t kFree = ~0u;
-    std::vector<Slot> tab_;
-    std::vector<uint8_t> bytes_;
-    size_t n_ = 0;
-
-    static uint64_t mix(uint64_t h) {
-        h ^= h >> 32;
-        h *= 0xD6E8FEB86659FD93ull;
-        h ^= h >> 32;
-        return h;
-    }
-    size_t probe(uint64_t h, const uint8_t *k, size_t n) const {  // slot of k, or the free slot it goes in
-        const size_t m = tab_.size() - 1;
-        for (size_t i = h & m;; i = (i + 1) & m) {
-            const Slot &e = tab_[i];
-            if (e.len == kFree) return i;
-            if (e.h == h && e.len == n && (n == 0 || std::memcmp(bytes_.data() + e.off, k, n) == 0)) return i;
-        }
-    }
-    void grow() {
-        std::vector<Slot> old(std::max<size_t>(tab_.size() * 2, 1024), Slot{0, 0, kFree, 0, ~0u, 0});
-        old.swap(tab_);
-        const size_t m = tab_.size() - 1;
-        for (const Slot &e : old)
-            if (e.len != kFree) {
-                size_t i = e.h & m;
-                while (tab_[i].len != kFree) i = (i + 1) & m;
-                tab_[i] = e;
-            }
-    }
-
-  public:
-    static uint64_t hash(const uint8_t *k, size_t n) {
-        uint64_t h = 0x9E3779B97F4A7C15ull ^ n;
-        size_t i = 0;
-        for (; i + 8 <= n; i += 8) {
-            uint64_t w;
-            std::memcpy(&w, k + i, 8);
-            h = mix(h ^ w) * 0x9E3779B97F4A7C15ull;
-        }
-        uint64_t w = 0;
-        std::memcpy(&w, k + i, n - i);
-        return mix(mix(h ^ w) + n);
-    }
-    // shard of k, or -1
-    int64_t find(const uint8_t *k, size_t n) const {
-        if (tab_.empty()) return -1;
-        const Slot &e = tab_[probe(hash(k, n), k, n)];
-        return e.len == kFree ? -1 : (int64_t)e.shard;
-    }
-    // shard and record hint of k; false when k was never stored
-    bool find_hint(const uint8_t *k, size_t n, uint32_t *shard, uint32_t *chunk, uint32_t *idx) const {
-        if (tab_.empty()) return false;
-        const Slot &e = tab_[probe(hash(k, n), k, n)];
-        if (e.len == kFree) return false;
-        *shard = e.shard;
-        *chunk = e.chunk;
-        *idx = e.idx;
-        return true;
-    }
-    // room for `more` keys without rehashing on the way
-    void reserve(size_t more) {
-        while ((n_ + more) * 2 > tab_.size()) grow();
-    }
-    // put, returning the shard k was stored under before (-1: new key)
-    int64_t upsert(const uint8_t *k, size_t n, uint32_t shard, uint32_t chunk, uint32_t idx) {
-        if ((n_ + 1) * 2 > tab_.size()) grow();
-        const uint64_t h = hash(k, n);
-        Slot &e = tab_[probe(h, k, n)];
-        if (e.len == kFree) {
-            e = Slot{h, bytes_.size(), (uint32_t)n, shard, chunk, idx};
-            bytes_.insert(bytes_.end(), k, k + n);
-            ++n_;
-            return -1;
-        }
-        const int64_t prev = e.shard;
-        e.shard = shard;
-        e.chunk = chunk;
-        e.idx = idx;
-        return prev;
-    }
-    void put(const uint8_t *k, size_t n, uint32_t shard, uint32_t chunk = ~0u, uint32_t idx = 0) {
-        if ((n_ + 1) * 2 > tab_.size()) grow();
-        const uint64_t h = hash(k, n);
-        Slot &e = tab_[probe(h, k, n)];
-        if (e.len == kFree) {
-            e = Slot{h, bytes_.size(), (uint32_t)n, shard, chunk, idx};
-            bytes_.insert(bytes_.end(), k, k + n);
-            ++n_;
-        } else {
-            e.shard = shard;
-            e.chunk = chunk;
-            e.idx = idx;
-        }
-    }
-    void clear() {
-        tab_.clear();
-        bytes_.clear();
-        n_ = 0;
-    }
-};
-
-// KeyMap split into 16 partitions by key hash: a batch's upserts run one partition per
-// host thread, each seeing its keys in record order
-class PartKeyMap {
-  public:
-    static constexpr uint32_t kParts = 16;
-    static uint32_t part_of(const uint8_t *k, size_t n) { return (uint32_t)(KeyMap::hash(k, n) >> 60); }
-    int64_t find(const uint8_t *k, size_t n) const { return p_[part_of(k, n)].find(k, n); }
-    bool find_hint(const uint8_t *k, size_t n, uint32_t *shard, uint32_t *chunk, uint32_t *idx) const {
-        return p_[part_of(k, n)].find_hint(k, n, shard, chunk, idx);
-    }
-    void put(const uint8_t *k, size_t n, uint32_t shard, uint32_t chunk = ~0u, uint32_t idx = 0) {
-        p_[part_of(k, n)].put(k, n, shard, chunk, idx);
-    }
-    KeyMap &part(uint32_t i) { return p_[i]; }
-    void clear() {
-        for (auto &m : p_) m.clear();
-    }
-
-  private:
-    KeyMap p_[kParts];
-};
-
-// host wall time per phase of one call, printed on stderr when `env` is 1
-struct PhaseClock {
-    bool on = false;
-    const char *name;
-    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), t = t0;
-    std::string out;
-    const char *cur = "setup";
-    PhaseClock(const char *nm, const char *env) : name(nm) {
-        const char *v = std::getenv(env);
-        on = v && *v == '1';
-    }
-    void mark(const char *next) {  // closes the running phase, starts `next`
-        if (!on) return;
-        const auto now = std::chrono::steady_clock::now();
-        char b[128];
-        snprintf(b, sizeof b, "\n  %8.2f ms  %s", std::chrono::duration<double, std::milli>(now - t).count(), cur);
-        out += b;
-        t = now;
-        cur = next;
-    }
-    ~PhaseClock() {
-        if (!on) return;
-        mark("");
-        fprintf(stderr, "%s:%s\n  %8.2f ms  total\n", name, out.c_str(),
-                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
-    }
-};
-
-// Persistent host workers (created once per process): spawning threads per call cost
-// more than a 10k-key lookup batch itself.  run(n, f) calls f(0..n-1) on the workers
-// and the caller, and returns when every call has returned.
-class WorkerPool {
-  public:
-    static WorkerPool &get() {
-        static WorkerPool pool(std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1);
-        return pool;
-    }
-    uint32_t size() const { return (uint32_t)workers_.size() + 1; }
-    void run(uint32_t ntask, const std::function<void(uint32_t)> &f) {
-        std::lock_guard<std::mutex> one(run_mu_);  // one job at a time (callers from several threads)
-        std::unique_lock<std::mutex> lk(m_);
-        busy_.wait(lk, [&] { return active_ == 0; });  // no worker still holds the last job
-        fn_ = &f;
-        ntask_ = ntask;
-        next_.store(0);
-        done_ = 0;
-        ++gen_;
-        lk.unlock();
-        work_.notify_all();
-        uint32_t mine = 0;
-        for (uint32_t t; (t = next_.fetch_add(1)) < ntask;) {
-            f(t);
-            ++mine;
-        }
-        lk.lock();
-        done_ += mine;
-        busy_.wait(lk, [&] { return done_ == ntask_ && active_ == 0; });
-    }
-    ~WorkerPool() {
-        {
-            std::lock_guard<std::mutex> lk(m_);
-            quit_ = true;
-        }
-        work_.notify_all();
-        for (auto &t : workers_) t.join();
-    }
-
-  private:
-    explicit WorkerPool(uint32_t n) {
-        for (uint32_t i = 0; i < n; ++i) workers_.emplace_back([this] { loop(); });
-    }
-    void loop() {
-        uint64_t seen = 0;
-        for (;;) {
-            std::unique_lock<std::mutex> lk(m_);
-            work_.wait(lk, [&] { return quit_ || gen_ != seen; });
-            if (quit_) return;
-            seen = gen_;
-            ++active_;
-            const std::function<void(uint32_t)> *f = fn_;
-            const uint32_t nt = ntask_;
-            lk.unlock();
-            uint32_t mine = 0;
-            for (uint32_t t; (t = next_.fetch_add(1)) < nt;) {
-                (*f)(t);
-                ++mine;
-            }
-            lk.lock();
-            done_ += mine;
-            --active_;
-            busy_.notify_all();
-        }
-    }
-    std::vector<std::thread> workers_;
-    std::mutex m_, run_mu_;
-    std::condition_variable work_, busy_;
-    const std::function<void(uint32_t)> *fn_ = nullptr;
-    uint32_t ntask_ = 0, done_ = 0, active_ = 0;
-    std::atomic<uint32_t> next_{0};
-    uint64_t gen_ = 0;
-    bool quit_ = false;
-};
-
-// fn(lo, hi) over [0, n) on up to `threads` host threads (inline for small n)
-template <class F>
-void parallel_ranges(uint32_t n, uint32_t threads, F fn) {
-    if (threads <= 1 || n < 2048) {
-        fn(0u, n);
-        return;
-    }
-    threads = std::min<uint32_t>({threads, WorkerPool::get().size(), n / 512});
-    const uint32_t tasks = threads * 4;  // a few ranges per thread: uneven keys balance out
-    const uint32_t per = (n + tasks - 1) / tasks;
-    const std::function<void(uint32_t)> job = [&](uint32_t t) {
-        const uint32_t lo = t * per, hi = std::min(n, lo + per);
-        if (lo < hi) fn(lo, hi);
-    };
-    WorkerPool::get().run(tasks, job);
-}
+using pxh::KeyMap;
+using pxh::parallel_ranges;
+using pxh::PartKeyMap;
+using pxh::PhaseClock;
+using pxh::WorkerPool;
 
 // ---------------------------------------------------------------- crit-bit index
-// Restates CritBitTree.cpp:13-269 over the COMPAT-decoded key prefix of each stored
-// record (computed on the GPU at setitem time).  Walk bytes past a key's end read 0
-// (as getitem does); crit-bit trees are canonical, so this equals the reference's
-// tree whenever the decoded key prefixes equal the true keys.
-struct Leaf {
-    uint32_t chunk, idx;  // global chunk id, slot
-};
-struct CbtRef {
-    int32_t inner = -1;
-    Leaf leaf{0, 0};
-};
-struct CbtInner {
-    CbtRef kid[2];
-    uint16_t diff_at;
-    uint8_t mask;
-};
-inline int crit_dir(uint8_t mask, uint8_t byte) { return (1 + (mask | byte)) >> 8; }
+// px_host.h's CritBit (CritBitTree.cpp:13-269 restated over the compat-decoded key
+// prefixes of the stored records); one tree per shard.
+using pxh::CbtInner;
+using pxh::CbtRef;
+using pxh::crit_dir;
+using pxh::Leaf;
+static_assert(pxh::kEscByte == kEsc && pxh::kKeyEndByte == kKeyEnd, "escape bytes");
 
 struct Chunk {
     uint32_t shard = 0;
@@ -526,7 +207,7 @@ struct Chunk {
     std::vector<Span> span;
 };
 
-struct Shard {
+struct Shard : pxh::CritBit {
     uint32_t id = 0;
     // device arena
     void *arena = nullptr;
@@ -550,11 +231,6 @@ struct Shard {
     int64_t closed = -1;  // slot-full live chunk whose rotation trigger has run
     uint32_t records = 0;
     std::vector<uint32_t> chunks;  // global chunk ids by chunk_seq
-    // CritBit
-    std::vector<CbtInner> cbt;
-    std::vector<int32_t> cbt_free;
-    bool has_root = false;
-    CbtRef root;
 };
 
 }  // namespace
@@ -585,12 +261,24 @@ struct px_ctx {
     DevBuf scratch_frames, dq_buf, dstat_buf, dlen_buf, in_buf, tmp_buf, link_buf, iter_buf, init_buf, stout_buf,
         slotput_buf;
     HostBuf hq_buf, hres_buf;  // pinned: decode queries up, lengths + statuses down
+    HostBuf psa_pin;           // pinned: px_psa.hip's count read-backs
     DevBuf sink_buf;           // k_gst_encode's message sink for replayed docs
     PsaStats psa_stats{};      // the last set batch's suffix-array pass
     // PX_PSA=0 sends every shard through k_gst_encode (A/B comparisons, tests)
     static bool psa_enabled() {
         const char *e = std::getenv("PX_PSA");
         return !(e && *e == '0');
+    }
+    // text positions one suffix-array round may take: its scratch (kPsaBytesPerPos per
+    // position, px_psa.hip) must fit the free device memory, and positions are 32-bit.
+    // PX_PSA_ROUND_MAX (positions) lowers it (tests of the multi-round path).
+    uint64_t psa_round_cap() {
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 0;
+        uint64_t cap = (uint64_t)(0.85 * (double)(fr + heap.cached_free())) / kPsaBytesPerPos;
+        cap = std::min<uint64_t>(cap, 0x7ff00000ull);  // (group sizes carry a tag bit: < 2^31)
+        if (const char *e = std::getenv("PX_PSA_ROUND_MAX")) cap = std::min<uint64_t>(cap, std::strtoull(e, nullptr, 10));
+        return std::max<uint64_t>(cap, 1);
     }
     uint32_t host_threads() const {
         const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
@@ -904,98 +592,14 @@ struct px_ctx {
     }
 
     // ------------------------------------------------------------ crit-bit ops
-    struct Best {
-        int32_t grand = -1, pa = -1;
-        int dir = 3;
-        Leaf crit{0, 0};
-    };
-    static Best best_match(const Shard &s, const std::string &q) {
-        Best b;
-        CbtRef p = s.root;
-        while (p.inner >= 0) {
-            const CbtInner &n = s.cbt[(size_t)p.inner];
-            uint8_t byte = q.size() > n.diff_at ? (uint8_t)q[n.diff_at] : 0;
-            b.dir = crit_dir(n.mask, byte);
-            b.grand = b.pa;
-            b.pa = p.inner;
-            p = n.kid[b.dir];
-        }
-        b.crit = p.leaf;
-        return b;
+    // (the tree is px_host.h's CritBit; here: the stored key prefixes and what a replace /
+    // delete does to the record)
+    auto kp_fn() const {
+        return [this](const Leaf &l, uint32_t *len) { return kp_of(l, len); };
     }
-
     // CritBitTree::setitem; q = escaped key incl. 251,0.  Returns 1 on replace.
     int cbt_insert(Shard &s, const std::string &q, Leaf nl) {
-        CbtRef nref;
-        nref.leaf = nl;
-        if (!s.has_root) {
-            s.has_root = true;
-            s.root = nref;
-            return 0;
-        }
-        Best b = best_match(s, q);
-        uint32_t clen;
-        const uint8_t *crit = kp_of(b.crit, &clen);
-        size_t k = 0;
-        uint16_t diff_at = 0;
-        uint8_t crit_rv = 0, src_rv = 0;
-        bool spec = false;
-        for (;;) {
-            if (k >= clen) break;
-            crit_rv = crit[k];
-            if (k >= q.size()) break;
-            src_rv = (uint8_t)q[k];
-            ++k;
-            if (crit_rv != src_rv) break;
-            if (!spec && crit_rv == kEsc) {
-                spec = true;
-            } else if (spec) {
-                if (crit_rv == kKeyEnd) {
-                    chunk_delitem(s, b.crit);
-                    if (b.pa < 0) s.root = nref;
-                    else s.cbt[(size_t)b.pa].kid[b.dir] = nref;
-                    return 1;
-                }
-                spec = false;
-            }
-            ++diff_at;
-        }
-        if (spec) return 0;
-        uint8_t mask = crit_rv ^ src_rv;
-        mask |= mask >> 1;
-        mask |= mask >> 2;
-        mask |= mask >> 4;
-        mask = (uint8_t)((mask & ~(mask >> 1)) ^ 0xff);
-        uint8_t at = diff_at < q.size() ? (uint8_t)q[diff_at] : 0;
-        int dir = crit_dir(mask, at);
-        int32_t in;
-        if (!s.cbt_free.empty()) {
-            in = s.cbt_free.back();
-            s.cbt_free.pop_back();
-        } else {
-            s.cbt.emplace_back();
-            in = (int32_t)s.cbt.size() - 1;
-        }
-        s.cbt[(size_t)in].diff_at = diff_at;
-        s.cbt[(size_t)in].mask = mask;
-        s.cbt[(size_t)in].kid[dir] = nref;
-        int32_t parent = -1;
-        int pdir = 0;
-        CbtRef p = s.root;
-        while (p.inner >= 0) {
-            const CbtInner &n = s.cbt[(size_t)p.inner];
-            if (n.diff_at > diff_at || (n.diff_at == diff_at && n.mask > mask)) break;
-            uint8_t byte = q.size() > n.diff_at ? (uint8_t)q[n.diff_at] : 0;
-            pdir = crit_dir(n.mask, byte);
-            parent = p.inner;
-            p = n.kid[pdir];
-        }
-        CbtRef iref;
-        iref.inner = in;
-        if (parent < 0) s.root = iref;
-        else s.cbt[(size_t)parent].kid[pdir] = iref;
-        s.cbt[(size_t)in].kid[1 - dir] = p;
-        return 0;
+        return s.insert(q, nl, kp_fn(), [&](const Leaf &l) { chunk_delitem(s, l); });
     }
 
     // PiXiuChunk::delitem (PiXiuStr.cpp:178-187): dead mark, live count, Glob
@@ -1008,84 +612,18 @@ struct px_ctx {
         if (ch.used < 0.8 * kChunkSlots) s.glob = l.chunk;
     }
 
-    // CritBitTree::getitem's key_eq (PiXiuStr.cpp:129-143)
-    // PXSGen_key_eq on the stored compat key prefix: equal through the key terminator
+    // CritBitTree::getitem's key_eq (PiXiuStr.cpp:129-143) on the stored compat key prefix
     bool kp_matches(const Leaf &l, const std::string &q) const {
         uint32_t clen;
         const uint8_t *crit = kp_of(l, &clen);
-        bool spec = false;
-        for (size_t k = 0; k < clen && k < q.size() && crit[k] == (uint8_t)q[k]; ++k) {
-            uint8_t v = crit[k];
-            if (!spec && v == kEsc) {
-                spec = true;
-            } else if (spec) {
-                if (v == kKeyEnd) return true;
-                spec = false;
-            }
-        }
-        return false;
+        return pxh::CritBit::key_eq(crit, clen, q);
     }
-    bool cbt_lookup(const Shard &s, const std::string &q, Leaf *out) const {
-        if (!s.has_root) return false;
-        Best b = best_match(s, q);
-        if (!kp_matches(b.crit, q)) return false;
-        *out = b.crit;
-        return true;
-    }
-
+    bool cbt_lookup(const Shard &s, const std::string &q, Leaf *out) const { return s.lookup(q, kp_fn(), out); }
     // CritBitTree::contains (CritBitTree.cpp:154-178): crit stream vs the escaped key bytes
-    bool cbt_contains(const Shard &s, const std::string &q) const {
-        if (!s.has_root) return false;
-        Best b = best_match(s, q);
-        uint32_t clen;
-        const uint8_t *crit = kp_of(b.crit, &clen);
-        bool spec = false;
-        for (size_t k = 0; k < clen && k < q.size() && crit[k] == (uint8_t)q[k]; ++k) {
-            uint8_t v = crit[k];
-            if (!spec && v == kEsc) {
-                spec = true;
-            } else if (spec) {
-                if (v == kKeyEnd) return true;
-                spec = false;
-            }
-        }
-        return false;
-    }
-
+    bool cbt_contains(const Shard &s, const std::string &q) const { return s.lookup(q, kp_fn(), nullptr); }
     // CritBitTree::delitem (CritBitTree.cpp:107-152)
     int cbt_delete(Shard &s, const std::string &q) {
-        if (!s.has_root) return 1;
-        Best b = best_match(s, q);
-        uint32_t clen;
-        const uint8_t *crit = kp_of(b.crit, &clen);
-        bool spec = false;
-        for (size_t k = 0; k < clen && k < q.size() && crit[k] == (uint8_t)q[k]; ++k) {
-            uint8_t v = crit[k];
-            if (!spec && v == kEsc) {
-                spec = true;
-            } else if (spec) {
-                if (v == kKeyEnd) {
-                    if (b.pa < 0) {
-                        s.has_root = false;
-                        s.root = CbtRef{};
-                    } else {
-                        const CbtRef other = s.cbt[(size_t)b.pa].kid[1 - b.dir];
-                        if (b.grand < 0) {
-                            s.root = other;
-                        } else {
-                            CbtInner &g = s.cbt[(size_t)b.grand];
-                            int gd = (g.kid[0].inner == b.pa) ? 0 : 1;
-                            g.kid[gd] = other;
-                        }
-                        s.cbt_free.push_back(b.pa);
-                    }
-                    chunk_delitem(s, b.crit);
-                    return 0;
-                }
-                spec = false;
-            }
-        }
-        return 1;
+        return s.remove(q, kp_fn(), [&](const Leaf &l) { chunk_delitem(s, l); });
     }
 
     // PiXiuStr::startswith (PiXiuStr.cpp:145-164) on a stored record: its stored compat
@@ -1105,35 +643,10 @@ struct px_ctx {
         return got == p;
     }
 
-    // CritBitTree::iter (CBTGHelper / CBTGen, CritBitTree.h:55-157): follow the
-    // prefix's crit bits; from the first node whose diff_at is past the prefix take
-    // the whole subtree (kid 0 first).  The first leaf reached must start with the
-    // prefix, else the generator yields NULL and stops; later leaves are unchecked.
+    // CritBitTree::iter (CBTGHelper / CBTGen, CritBitTree.h:55-157); the first leaf
+    // reached must start with the prefix (rec_startswith)
     bool cbt_iter(const Shard &s, const std::string &p, std::vector<Leaf> &out) {
-        if (!s.has_root) return false;
-        bool harvest = false;
-        std::vector<std::pair<CbtRef, bool>> stack{{s.root, false}};
-        while (!stack.empty()) {
-            auto [ref, include_all] = stack.back();
-            stack.pop_back();
-            if (ref.inner < 0) {
-                if (!harvest && !rec_startswith(ref.leaf, p)) break;
-                harvest = true;
-                out.push_back(ref.leaf);
-                continue;
-            }
-            const CbtInner &n = s.cbt[(size_t)ref.inner];
-            uint8_t crit = p.size() > n.diff_at ? (uint8_t)p[n.diff_at] : 0;
-            int direct = crit_dir(n.mask, crit);
-            if (!include_all && n.diff_at >= p.size()) include_all = true;
-            if (include_all) {
-                stack.push_back({n.kid[1], true});
-                stack.push_back({n.kid[0], true});
-            } else {
-                stack.push_back({n.kid[direct], false});
-            }
-        }
-        return true;
+        return s.iter(p, [&](const Leaf &l) { return rec_startswith(l, p); }, out);
     }
 
     // the escaped key the CritBit stores (raw bytes, 251 doubled, then 251,0), built
@@ -1334,7 +847,7 @@ struct px_ctx {
         uint32_t chunk, idx;
         const uint8_t *doc;
     };
-    void build_spans(const std::vector<SpanReq> &reqs, uint32_t mode = 0) {
+    void build_spans(const std::vector<SpanReq> &reqs, uint32_t mode = 0, bool exact_too = true) {
         if (reqs.empty() || !spans_enabled()) return;
         std::vector<DecodeQuery> q;
         q.reserve(reqs.size());
@@ -1406,7 +919,7 @@ struct px_ctx {
             heap.release(dcnt, nj * 4 + 64);
         }
         heap.release(addr, tot * 4 + 64);
-        if (mode == 0) {  // exact tables for the records whose compat expansion is not the doc
+        if (mode == 0 && exact_too) {  // exact tables for the records whose compat expansion is not the doc
             std::vector<SpanReq> x;
             for (const SpanReq &r : reqs) {
                 const Chunk &ch = chunks[r.chunk];
@@ -2010,9 +1523,14 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             std::vector<uint32_t> pcount;  // new docs in the window
             uint64_t gpos = 0;
             bool any_pools = false;
+            // a round holds at most round_cap positions (device scratch, 32-bit positions)
+            // and kPsaMaxShards shards (the first sort key's shard bits); the shards that do
+            // not fit wait for the next round
+            const uint64_t round_cap = psa_round_cap();
             for (size_t ri = 0; ri < runs.size(); ++ri) {
                 Run &u = runs[ri];
                 if (u.done) continue;
+                if (ps.size() >= kPsaMaxShards) break;
                 Shard &sh = *work[u.k].s;
                 if (u.live.size() == (size_t)kChunkSlots) {  // slot-full: rotation before the next doc
                     ++u.seq;
@@ -2040,7 +1558,11 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
                 // (new bytes: up to the window, and at least half a window once the live
                 // chunk alone has outgrown it without rotating)
                 const uint64_t win = std::max<uint64_t>(u.window, kPsaMaxText);
-                const uint64_t budget = std::max<uint64_t>(win > u.live_bytes ? win - u.live_bytes : 0, win / 2);
+                // (and no more than the round's position cap leaves: a chunk that does not
+                // rotate inside a shorter window simply continues in the next round)
+                const uint64_t room = round_cap > gpos + u.live_bytes ? round_cap - gpos - u.live_bytes : 0;
+                const uint64_t budget =
+                    std::min(std::max<uint64_t>(win > u.live_bytes ? win - u.live_bytes : 0, win / 2), room);
                 uint32_t cnt = 0;
                 uint64_t nb = 0;
                 for (size_t i = u.next; i < u.recs.size() && u.live.size() + cnt < (size_t)kChunkSlots; ++i) {
@@ -2051,6 +1573,10 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
                     off += doc_len[r];
                     nb += doc_len[r];
                     ++cnt;
+                }
+                if (!ps.empty() && gpos + off > round_cap) {  // (a round takes at least one shard)
+                    pd.resize(psh.doc0);
+                    break;
                 }
                 psh.len = (uint32_t)off;
                 psh.ndocs = (uint32_t)(pd.size() - psh.doc0);
@@ -2071,7 +1597,8 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             h2d(d_ps, ps.data(), ps.size() * sizeof(PsaShard));
             hcheck(hipMemsetAsync(d_flag, 0, ps.size() * 4, stream));
             PsaAlloc A{[](void *self, uint64_t b) { return static_cast<px_ctx *>(self)->heap.alloc(b); },
-                       [](void *self, void *p, uint64_t b) { static_cast<px_ctx *>(self)->heap.release(p, b); }, this};
+                       [](void *self, void *p, uint64_t b) { static_cast<px_ctx *>(self)->heap.release(p, b); }, this,
+                       static_cast<uint32_t *>(psa_pin.get(kPsaPinWords * 4))};
             PsaStats rst{};
             hcheck(psa_run(stream, A, (uint32_t)pd.size(), d_pd, (uint32_t)ps.size(), d_ps, (uint32_t)gpos, d_chunk,
                            d_idx, d_status, d_flag, any_pools, d_pool, &rst));
@@ -2897,7 +2424,7 @@ int px_ctx::load(const uint8_t *src, uint64_t len, int src_on_device, uint32_t *
     if (opts.records_per_shard == 0 && !shards.empty() && shards[0]->records) return PX_EINVAL;
     const uint32_t n = h.n_records;
     if (!n) {
-        if (first_shard) *first_shard = (uint32_t)shards.size();
+        if (first_shard) *first_shard = opts.records_per_shard == 0 ? 0u : (uint32_t)shards.size();
         return PX_OK;
     }
     // ---- bytes to the device (one store allocation: data, then lane entries)
@@ -2956,8 +2483,8 @@ int px_ctx::load(const uint8_t *src, uint64_t len, int src_on_device, uint32_t *
     heap.release(data, data_cap);
     heap.release(d_slots, (uint64_t)n * sizeof(RecSlot));
     heap.release(d_tmp, (uint64_t)n * 8);
-    // ---- shards and chunks
-    const uint32_t first = (uint32_t)shards.size();
+    // ---- shards and chunks (a single-shard store takes them into shard 0, empty or new)
+    const uint32_t first = opts.records_per_shard == 0 ? 0u : (uint32_t)shards.size();
     std::map<uint32_t, Shard *> target;  // source shard -> shard here
     std::vector<uint32_t> rchunk(n);
     std::vector<Shard *> rshard(n);
@@ -3046,6 +2573,15 @@ int px_ctx::load(const uint8_t *src, uint64_t len, int src_on_device, uint32_t *
         if (cbt_insert(s, q, Leaf{jobs[j].chunk, k})) {
             // a duplicate key inside the blob: the later record replaced the earlier
         }
+    }
+    // span tables for the loaded records (compat only: without their docs compat == exact is
+    // unknown, so exact getitems of loaded records keep the segment walk)
+    {
+        std::vector<SpanReq> reqs;
+        for (const BlobChunk &c : bc)
+            for (uint32_t k = 0; k < c.n; ++k)
+                if (!chunks[rchunk[c.first + k]].dead[k]) reqs.push_back(SpanReq{rchunk[c.first + k], k, nullptr});
+        build_spans(reqs, 0, false);
     }
     stats.chunks = chunks.size();
     if (first_shard) *first_shard = first;
@@ -3185,6 +2721,44 @@ int px_parse_batch(px_ctx *ctx, uint32_t n, const px_rec *recs, int mode, uint8_
             q[i].out_cap = (uint32_t)round_up(span + 64, 16);
         }
         return ctx->expand(q, out, out_cap, out_on_device, out_off, out_len, status, needed, pre);
+    })
+}
+
+int px_locate_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff, px_rec *recs,
+                    uint32_t *status) {
+    if (!ctx || (n && (!keys || !koff || !recs || !status))) return PX_EINVAL;
+    PX_GUARD({
+        std::string ek;
+        for (uint32_t i = 0; i < n; ++i) {
+            DecodeQuery q;
+            uint32_t pre = PX_OK;
+            ctx->resolve_key(keys + koff[i], koff[i + 1] - koff[i], PX_COMPAT, ek, q, pre);
+            status[i] = pre;
+            recs[i] = px_rec{0, 0, 0, 0, kMaxDoc};
+            if (pre != PX_OK) continue;
+            const uint32_t sh = ctx->chunks[q.chunk].shard;
+            const auto &cs = ctx->shards[sh]->chunks;
+            recs[i].shard = sh;
+            recs[i].chunk = (uint32_t)(std::find(cs.begin(), cs.end(), q.chunk) - cs.begin());
+            recs[i].idx = q.idx;
+        }
+        return PX_OK;
+    })
+}
+
+int px_reinsert(px_ctx *ctx, uint32_t shard, uint32_t chunk) {
+    if (!ctx || shard >= ctx->shards.size()) return PX_EINVAL;
+    PX_GUARD({
+        Shard &s = *ctx->shards[shard];
+        if (chunk >= s.chunks.size()) return PX_EINVAL;
+        const uint32_t c = s.chunks[chunk];
+        const Chunk &ch = ctx->chunks[c];
+        // closed (PiXiuChunk::total_num set at rotation) and slot-full; the live chunk is the
+        // shard's last one
+        if (chunk + 1 == s.chunks.size() || ch.total == 0 || ch.n != (uint32_t)kChunkSlots) return PX_EINVAL;
+        ctx->reinsert_chunk(s, c, false);
+        if (s.glob == (int64_t)c) s.glob = -1;  // (the reference would keep a dangling Glob_Reinsert_Chunk)
+        return PX_OK;
     })
 }
 

@@ -12,8 +12,11 @@ def record_range(n: int, world: int, rank: int) -> tuple:
 
 
 def gather_blobs(blob, dst: int = 0):
-    """Gather variable-size 1-D uint8 tensors to `dst`.  Returns the list of
-    per-rank blobs on dst (trimmed to their true sizes), None elsewhere."""
+    """Gather variable-size 1-D uint8 tensors to `dst`: the sizes by one all_gather, then
+    every blob at its exact size, point to point (one batched group of sends / receives:
+    grouped ncclSend / ncclRecv over xGMI with RCCL; plain isend / irecv with gloo, whose
+    tensors live on the CPU).  Returns the list of per-rank blobs on dst (its own is the
+    tensor passed in), None elsewhere."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size()
@@ -23,13 +26,17 @@ def gather_blobs(blob, dst: int = 0):
     sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
     dist.all_gather(sizes, size)
     sizes = [int(s.item()) for s in sizes]
-    mx = max(sizes) if sizes else 0
-    padded = blob
-    if blob.numel() < mx:
-        padded = torch.zeros(mx, dtype=blob.dtype, device=dev)
-        padded[:blob.numel()] = blob
-    recv = [torch.empty(mx, dtype=blob.dtype, device=dev) for _ in range(world)] if rank == dst else None
-    dist.gather(padded, recv, dst=dst)
-    if rank != dst:
-        return None
-    return [r[:s] for r, s in zip(recv, sizes)]
+    out = None
+    if rank == dst:
+        out = [blob if r == dst else torch.empty(sizes[r], dtype=blob.dtype, device=dev) for r in range(world)]
+        ops = [(dist.irecv, out[r], r) for r in range(world) if r != dst and sizes[r]]
+    else:
+        ops = [(dist.isend, blob, dst)] if blob.numel() else []
+    if ops:
+        if dist.get_backend() == "nccl":
+            reqs = dist.batch_isend_irecv([dist.P2POp(f, t, peer) for f, t, peer in ops])
+        else:
+            reqs = [f(t, peer) for f, t, peer in ops]
+        for q in reqs:
+            q.wait()
+    return out

@@ -13,7 +13,8 @@ import subprocess
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ORACLE_SO = os.path.join(ROOT, "oracle", "_build", "libpxo.so")
+# PXO_LIB: another build of the same restatement (the sanitizer build, oracle/Makefile asan)
+ORACLE_SO = os.environ.get("PXO_LIB") or os.path.join(ROOT, "oracle", "_build", "libpxo.so")
 REF_SO = os.path.join(ROOT, "oracle", "_ref", "libpxref.so")
 
 COMPAT, EXACT = 0, 1
@@ -184,6 +185,10 @@ class _Shard:
     def delete(self, k: bytes) -> int:
         return self.lib.pxo_delete(self.h, k, len(k))
 
+    def reinsert(self, chunk: int) -> int:
+        """PiXiuCtrl::reinsert(PiXiuChunk *&) on closed chunk `chunk` (PiXiuCtrl.cpp:88-114)"""
+        return self.lib.pxo_reinsert(self.h, chunk)
+
     def locate(self, k: bytes):
         """(chunk, idx) of the key's record, or None."""
         cn, ix = C.c_uint32(), C.c_uint32()
@@ -224,6 +229,9 @@ class Reference(_Runner):
 
     def delete(self, k: bytes) -> int:
         return self.lib.refx_delitem(k, len(k))
+
+    def reinsert(self, chunk: int) -> int:
+        return self.lib.refx_reinsert(chunk)
 
     def contains(self, k: bytes) -> int:
         return self.lib.refx_contains(k, len(k))

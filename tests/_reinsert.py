@@ -10,7 +10,10 @@ reference's reinsert is well defined (PiXiuStr.cpp:189-193), then trigger it:
                  re-inserts it through Glob_Reinsert_Chunk (PiXiuCtrl.cpp:64-67);
 * glob_replace — setitems replacing keys of a closed chunk do the same through the
                  CritBit replace (CritBitTree.cpp:32-38) and the setitem trigger
-                 (PiXiuCtrl.cpp:26-29), inside one batch, followed by more deletes.
+                 (PiXiuCtrl.cpp:26-29), inside one batch, followed by more deletes;
+* direct       — PiXiuCtrl::reinsert(PiXiuChunk *&) called by the client on a closed chunk
+                 that is 85 % live (no trigger would fire: need_reinsert is false, and
+                 Glob_Reinsert_Chunk never points at it, which keeps the reference defined).
 
 ``run_scalar`` drives one record at a time through the oracle or the reference;
 ``state`` / ``digest`` reduce the end state to what both can report: every touched key's
@@ -71,13 +74,26 @@ def scenarios() -> dict:
         ("del", [ks[i] for i in range(40000, 41000)]),
         ("set", ks[nxt:nxt + 10], vs[nxt:nxt + 10]),
     ]
+    rng = random.Random(13)
+    n = FULL + 10
+    ks = [key(i) for i in range(n + 40)]
+    vs = [_val(rng, i) for i in range(n + 40)]
+    out["direct"] = [
+        ("set", ks[:n], vs[:n]),
+        ("del", [ks[i] for i in range(0, FULL, 7)]),
+        ("reinsert", 0),
+        ("set", ks[n:n + 20], vs[n:n + 20]),
+        ("del", [ks[i] for i in range(FULL, FULL + 6)]),
+        ("set", ks[n + 20:], vs[n + 20:]),
+    ]
     return out
 
 
 def touched(ops) -> list:
     seen = set()
     for op in ops:
-        seen.update(op[1])
+        if op[0] != "reinsert":
+            seen.update(op[1])
     return sorted(seen)
 
 
@@ -89,6 +105,8 @@ def run_scalar(impl, ops) -> list:
             for k, v in zip(op[1], op[2]):
                 r = impl.set(k, v)
                 rets.append(int(r[0] if isinstance(r, tuple) else r))
+        elif op[0] == "reinsert":
+            rets.append(int(impl.reinsert(op[1])))
         else:
             for k in op[1]:
                 rets.append(int(impl.delete(k)))
@@ -115,6 +133,9 @@ def ops_sha256(ops) -> str:
     h = hashlib.sha256()
     for op in ops:
         h.update(op[0].encode())
+        if op[0] == "reinsert":
+            h.update(b"%d" % op[1])
+            continue
         for k in op[1]:
             h.update(b"%d:" % len(k) + k)
         if op[0] == "set":

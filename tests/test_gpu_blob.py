@@ -78,6 +78,23 @@ def test_load_rejects(store_factory):
         a.load(good)
 
 
+def test_load_into_empty_single_shard(store_factory):
+    """px_load into a single-shard store reports shard 0, the shard the chunks went into
+    (include/pixiu_amd.h: *first_shard), whether the store is new or was reset."""
+    cp = _cp(300)
+    keys, vals = [cp.key(i) for i in range(cp.n)], [cp.val(i) for i in range(cp.n)]
+    a = store_factory(records_per_shard=0)
+    a.set_batch(keys, vals)
+    blob_ = a.save()
+    b = store_factory(records_per_shard=0)
+    b.set_batch([b"tmp"], [b"x"])
+    b.reset()
+    assert b.load(blob_) == 0
+    assert b.get_batch(keys) == a.get_batch(keys)
+    c = store_factory(records_per_shard=0)
+    assert c.load(blob_) == 0
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

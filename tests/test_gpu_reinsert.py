@@ -21,6 +21,9 @@ def _split(ops, batch):
         return ops
     out = []
     for op in ops:
+        if op[0] == "reinsert":
+            out.append(op)
+            continue
         for a in range(0, len(op[1]), batch):
             out.append((op[0],) + tuple(x[a:a + batch] for x in op[1:]))
     return out
@@ -53,6 +56,9 @@ def test_gpu_reinsert_matches_reference(name, batch, store_factory, oracle):
             r = st.set_batch(list(op[1]), list(op[2]))
             assert int(r["status"].max()) == 0
             rets += r["replaced"].tolist()
+        elif op[0] == "reinsert":
+            st.reinsert(0, op[1])
+            rets.append(0)
         else:
             rets += st.delete(list(op[1])).tolist()
     keys = R.touched(ops)

@@ -225,6 +225,41 @@ def rotation():
     return out
 
 
+def chunk_digest(r):
+    """per-chunk (first record, records, sha256 of the chunk's compressed bytes in slot
+    order, compressed bytes) of one instance's run"""
+    chunks = {}
+    for i, c in enumerate(r["chunk"]):
+        chunks.setdefault(c, []).append(i)
+    per = []
+    for c in sorted(chunks):
+        rows = chunks[c]
+        assert [r["idx"][i] for i in rows] == list(range(len(rows)))
+        per.append({"chunk": c, "first": rows[0], "records": len(rows),
+                    "sha256": hashlib.sha256(b"".join(r["comp"][i] for i in rows)).hexdigest(),
+                    "comp_bytes": sum(len(r["comp"][i]) for i in rows)})
+    return per
+
+
+def c3_single(runner=None, n=10000):
+    """config 3 (the README shape, 10k x 60 KB) as ONE PiXiuCtrl over every page, the
+    reference's own configuration (PiXiuCtrl.cpp:12-25): one row per chunk."""
+    import time
+    cp = synth.make(3, n)
+    keys = [cp.key(i) for i in range(n)]
+    vals = [cp.val(i) for i in range(n)]
+    t = time.time()
+    r = (runner or REF).run(keys, vals, do_get=False)
+    dt = time.time() - t
+    per = chunk_digest(r)
+    out = {"config": 3, "n": n, "raw_bytes": cp.raw_bytes, "chunks": per,
+           "comp_bytes": sum(p["comp_bytes"] for p in per),
+           "input_sha256": hashlib.sha256(cp.keys.tobytes() + cp.vals.tobytes()).hexdigest(),
+           "generator": type(runner or REF).__name__, "seconds": round(dt, 1)}
+    print(f"c3_single: {len(per)} chunks, ratio {out['comp_bytes'] / cp.raw_bytes:.4f}, {dt:.0f} s")
+    return out
+
+
 def reinsert():
     """tests/_reinsert.py scenarios through the reference, one record at a time: digests
     of every record's return and of the end state (presence, compat getitem, slot,
@@ -257,6 +292,8 @@ def main():
         json.dump(rotation(), open(os.path.join(OUT, "rotation.json"), "w"), indent=1)
     if "reinsert" in what:
         json.dump(reinsert(), open(os.path.join(OUT, "reinsert.json"), "w"), indent=1)
+    if "c3_single" in what:  # (not in the default set: ~13 minutes of reference time)
+        json.dump(c3_single(), open(os.path.join(OUT, "c3_single.json"), "w"), indent=1)
 
 
 if __name__ == "__main__":
