@@ -16,3 +16,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_psa.py tests/test_gpu_pools
 R=$PWD
 cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace -d $O/${TAG}_prof -o prof -- python3 $R/bench.py --no-cpu \
   --no-single --no-pcie --no-exact --no-checks --configs "" --steps 1 --warmup 0 > $O/${TAG}_prof.log 2>&1
+if [ "$SPROF" = 1 ]; then
+  timeout -k 10 200 rocprofv3 --kernel-trace -d $O/${TAG}_sprof -o prof -- python3 $R/bench.py --rps 0 --no-cpu \
+    --no-single --no-pcie --no-exact --no-checks --configs "" --steps 1 --warmup 0 > $O/${TAG}_sprof.log 2>&1
+fi
