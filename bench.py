@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--no-single", action="store_true",
                     help="skip the single-instance leg (config 3 as one shard, GPU and CPU)")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) leg")
+    ap.add_argument("--no-cliff", action="store_true", help="skip the walk-fallback leg (one forced-flag shard)")
     ap.add_argument("--no-exact", action="store_true",
                     help="skip the exact-mode getitem (profiling runs: one compat batch per step only)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
@@ -95,6 +96,69 @@ def cpu_baseline(corpus, rps, budget_s):
         s += rps
     return {"set_MBps": raw / t_set / 1e6, "get_MBps": exp / t_get / 1e6, "records": nrec, "raw": raw,
             "shards": shards, "seconds": t_set + t_get}
+
+
+def walk_cliff(local, corpus, records=8):
+    """The walk fallback's cost: the first `records` records as one shard, once through
+    the suffix-array path and once with the stale-pair check forced to fire
+    (PX_DEBUG_PSA_FLAG_ROUND=1: the shard is re-walked by k_gst_encode).
+    Both must give the same bytes (the configs hold no stale state)."""
+    import pixiu_amd as px
+    kv = ((np.ascontiguousarray(corpus.keys[:corpus.koff[records]]), corpus.koff[:records + 1].astype(np.uint64)),
+          (np.ascontiguousarray(corpus.vals[:corpus.voff[records]]), corpus.voff[:records + 1].astype(np.uint64)))
+    raw = int(corpus.koff[records] + corpus.voff[records])
+    out = {}
+    for name, flag in (("psa", None), ("psa", None), ("walk", "1")):
+        if flag:
+            os.environ["PX_DEBUG_PSA_FLAG_ROUND"] = flag
+        try:
+            with px.Store(records_per_shard=records, device=local) as st:
+                t0 = time.perf_counter()
+                r = st.set_batch(*kv)
+                dt = time.perf_counter() - t0
+                s = st.stats()
+                out[name] = {"s": dt, "walk_shards": int(s["last_walk_shards"]),
+                             "comp": st.export(px.records_of(r))}
+        finally:
+            os.environ.pop("PX_DEBUG_PSA_FLAG_ROUND", None)
+    return {"records": records, "raw_bytes": raw, "psa_MBps": round(raw / out["psa"]["s"] / 1e6, 3),
+            "walk_MBps": round(raw / out["walk"]["s"] / 1e6, 3),
+            "walk_over_psa_time": round(out["walk"]["s"] / out["psa"]["s"], 1),
+            "walked_shards": out["walk"]["walk_shards"], "bytes_equal": out["walk"]["comp"] == out["psa"]["comp"],
+            "note": "one shard forced to the walk fallback (PX_DEBUG_PSA_FLAG_ROUND=1), host buffers, one call"}
+
+
+def small_batches(local, calls=300):
+    """Facade-shaped setitem: one record per call (PiXiuCtrl::setitem through px_set_batch,
+    n = 1) into one store at records_per_shard = 0, config-4 records (256 B).  Every call
+    re-encodes its shard's live chunk on the suffix-array path, so the time per call grows
+    with the chunk: reported for the first and the last 50 calls."""
+    import pixiu_amd as px
+    from pixiu_amd import synth
+    cp = synth.make(4, calls)
+    ts = []
+    with px.Store(records_per_shard=0, device=local) as st:
+        for i in range(calls):
+            k, v = cp.key(i), cp.val(i)
+            t0 = time.perf_counter()
+            st.set_batch([k], [v])
+            ts.append(time.perf_counter() - t0)
+        live = int(st.stats()["chunks"])
+    raw = int(cp.raw_bytes)
+    return {"calls": calls, "record_bytes": raw // calls, "chunks": live,
+            "ms_per_call_first50": round(float(np.mean(ts[:50])) * 1e3, 3),
+            "ms_per_call_last50": round(float(np.mean(ts[-50:])) * 1e3, 3),
+            "MBps": round(raw / sum(ts) / 1e6, 4)}
+
+
+def cpu_calibration():
+    """The oracle-vs-reference speed factors measured in the build container (the GPU box
+    has no reference): profiles/cpu_calibration_r03.json, or None."""
+    path = os.path.join(ROOT, "profiles", "cpu_calibration_r03.json")
+    try:
+        return json.load(open(path))
+    except (OSError, ValueError):
+        return None
 
 
 def cpu_single_instance(corpus, budget_s):
@@ -393,6 +457,32 @@ def check_gathered(cfg, r, rps, world, records, sample=300):
                 "rank0_gather_served": gathered_q, "records_per_rank_sampled": min(sample, r["n"])}
 
 
+def check_single(r0):
+    """The single-instance leg against the reference (outside the timed region): every
+    chunk's first record, record count and sha256 of its compressed bytes must equal
+    tests/golden/c3_single.json, which the reference produced over the same corpus
+    (tools/make_golden.py c3_single)."""
+    import hashlib
+    import pixiu_amd as px
+    path = os.path.join(ROOT, "tests", "golden", "c3_single.json")
+    if not os.path.exists(path):
+        return None
+    g = json.load(open(path))
+    cp = r0["corpus"]
+    if cp.n != g["n"]:
+        return {"skipped": f"{cp.n} records, the golden holds {g['n']}"}
+    res = r0["runs"][-1]["res"]
+    comp = r0["st"].export(px.records_of(res))
+    rows = {}
+    for i, c in enumerate(res["chunk"].tolist()):
+        rows.setdefault(c, []).append(i)
+    got = [(v[0], len(v), hashlib.sha256(b"".join(comp[i] for i in v)).hexdigest()) for _, v in sorted(rows.items())]
+    want = [(c["first"], c["records"], c["sha256"]) for c in g["chunks"]]
+    return {"golden": "tests/golden/c3_single.json", "chunks": len(got), "golden_chunks": len(want),
+            "chunks_equal": sum(x == y for x, y in zip(got, want)),
+            "comp_bytes_equal": sum(map(len, comp)) == g["comp_bytes"]}
+
+
 def summarize(cfg, r, rps, world, a, pmc_path):
     """Aggregate one config's runs (whole-job volumes over ranks) into its report."""
     import torch
@@ -590,6 +680,14 @@ def main():
                                 "sample": f"first {cb['records']} records ({cb['raw'] / 1e6:.1f} MB) of the same "
                                           f"corpus, same {rps}-record shards, oracle/pxo.cpp single-threaded, "
                                           f"{cb['seconds']:.1f} s"}
+        cal = cpu_calibration()
+        if cal:  # the reference's own speed relative to the port, timed on one shared host
+            line["cpu_baseline"]["calibration"] = {
+                "ref_over_port_set": round(cal["ref_over_port_set"], 4),
+                "ref_over_port_get": round(cal["ref_over_port_get"], 4),
+                "reference_equivalent_value": round(cb["set_MBps"] * cal["ref_over_port_set"]
+                                                    + cb["get_MBps"] * cal["ref_over_port_get"], 4),
+                "source": "profiles/cpu_calibration_r03.json (tools/calibrate_cpu.py: " + cal["workload"] + ")"}
         line["parity_sample"] = {"records": tot_c, "compressed_equal": eq_c, "getitem_equal": eq_g}
         mt = cpu_baseline_mt(corpus, rps, cb["set_MBps"], a.cpu_seconds / 2)
         line["cpu_baseline_mt"] = {"value": round(mt["set_MBps"] + mt["get_MBps"], 4), "unit": "MB/s",
@@ -600,6 +698,9 @@ def main():
                                              f"{mt['seconds']:.1f} s"}
     if not a.no_pcie and world == 1:
         line["pcie_inclusive"] = pcie_leg(st, px, corpus, r["keys_host"], r["out_cap"])
+    if not a.no_cliff and world == 1:
+        line["walk_fallback"] = walk_cliff(local, corpus)
+        line["one_record_per_call"] = small_batches(local)
     st.close()
     if not a.no_single and world == 1 and a.config == 3 and rps != 0:
         # the same corpus as ONE shard (records_per_shard = 0): the reference's single
@@ -614,7 +715,7 @@ def main():
             "ms_per_step": s0.get("ms_per_step"), "chunks": s0["encode_stage"].get("chunks"),
             "psa_rounds": s0["encode_stage"].get("psa_rounds"),
             "encode_stage_ms": s0["kernel_ms"]["encode_stage"],
-            "psa_split_ms": s0["encode_stage"].get("psa_split_ms")}
+            "psa_split_ms": s0["encode_stage"].get("psa_split_ms"), "reference_check": check_single(r0)}
         if not a.no_cpu:
             c0 = cpu_single_instance(corpus, a.cpu_seconds)
             line["single_instance"]["cpu_baseline"] = {
@@ -622,6 +723,10 @@ def main():
                 "set_MBps": round(c0["set_MBps"], 4), "get_MBps": round(c0["get_MBps"], 4), "cores": 1,
                 "kind": "port", "sample": f"first {c0['records']} records ({c0['raw'] / 1e6:.2f} MB) into one "
                                           f"oracle instance, {c0['seconds']:.1f} s"}
+            cal = cpu_calibration()
+            if cal:
+                line["single_instance"]["cpu_baseline"]["reference_equivalent_value"] = round(
+                    c0["set_MBps"] * cal["ref_over_port_set"] + c0["get_MBps"] * cal["ref_over_port_get"], 4)
         r0["st"].close()
     print(json.dumps(line), flush=True)
     if world > 1:

@@ -161,7 +161,7 @@ int px_locate_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t
  * is set again as a ready doc (rotation trigger only) and the chunk's records are gone.
  * Defined for a closed slot-full chunk: the reference visits all 65,535 slots and
  * dereferences NULL otherwise.  PX_EINVAL for the live chunk, a chunk with empty slots,
- * or an unknown one. */
+ * one with no live record left (compacted already), or an unknown one. */
 int px_reinsert(px_ctx *ctx, uint32_t shard, uint32_t chunk);
 
 /* Compressed bytes of stored records, copied to host CSR (out_off has n+1 entries). */

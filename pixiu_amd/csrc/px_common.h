@@ -219,8 +219,11 @@ struct SpanJob {
     uint32_t len;         // output bytes (k_decode_addr's length)
     uint32_t doc_len;
     uint32_t *count;      // count pass: spans | kSpanBad, eq flag in bit 30
-    uint32_t pad;
+    uint32_t *tix;        // write pass: tile index (kGatherTile bytes per tile), or null
 };
+// the gather's tile: one lane assembles kGatherTile output bytes; tix[t] = the span
+// holding output byte t * kGatherTile
+constexpr uint32_t kGatherTile = 64;
 constexpr uint32_t kSpanBad = 1u << 31, kSpanEq = 1u << 30;
 
 // gather query: one full-range getitem served from a span table
@@ -229,7 +232,10 @@ struct GatherQuery {
     const uint8_t *base;
     uint64_t out_off;
     uint32_t nspan, len, cap;
-    uint32_t slot;  // result index (out_len / status)
+    uint32_t slot;    // result index (out_len / status)
+    const uint32_t *tix;  // tile index of the span table
+    uint32_t tile0;   // the launch's global tile number of this query's first tile
+    uint32_t pad;
 };
 
 // decode frame (scratch, one stack per wave)

@@ -2210,6 +2210,9 @@ __global__ void __launch_bounds__(256) k_span_build(uint32_t n, const SpanJob *j
                     e[0] = (uint32_t)v;
                     e[1] = k;
                 }
+                // tile index: the span holding byte k, at every tile start
+                if (jb.tix && in && (k % kGatherTile) == 0)
+                    ((PX_GAS uint32_t *)jb.tix)[k / kGatherTile] = cnt + rank + (start ? 1u : 0u) - 1u;
             }
             cnt += (uint32_t)__popcll(m);
             prev_last = __shfl(v, 63);
@@ -2223,57 +2226,53 @@ __global__ void __launch_bounds__(256) k_span_build(uint32_t n, const SpanJob *j
     }
 }
 
-// Gather: one wave per task.  A task is one query (lane l takes span k0 + l, 64 spans a
-// step), or several consecutive queries whose spans total <= 64 (small records: one
-// span per lane, each lane finds its query from the queries' span offsets).  Spans up
-// to kLaneCopyMax bytes are copied by their lane, longer ones by the whole wave.
-// Output stops at each query's cap.
-PX_DEV void gather_one(const GatherQuery &q0, uint32_t k_lo, uint32_t k_hi, uint8_t *out_, uint32_t *out_len,
-                       uint32_t *status) {
-    const uint32_t lane = lane_id();
-    const PX_GAS SpanEnt *sp = (const PX_GAS SpanEnt *)uni64((uint64_t)q0.span);
-    const PX_GAS uint8_t *base = (const PX_GAS uint8_t *)uni64((uint64_t)q0.base);
-    PX_GAS uint8_t *o = (PX_GAS uint8_t *)out_ + uni64(q0.out_off);
-    const uint32_t nspan = min(uni(q0.nspan), k_hi), cap = uni(q0.cap), len = uni(q0.len);
-    // the next step's entries are loaded before this step's copies (one round trip per
-    // step instead of two)
-    auto load_ent = [&](uint32_t k, int32_t &rel, uint32_t &st, uint32_t &en) {
-        rel = 0;
-        st = en = 0;
-        if (k < nspan) {  // this entry and the next one's start (the table ends with a sentinel)
-            const u32x4 e = *(const PX_GAS u32x4_u *)(sp + k);
-            rel = (int32_t)e.x;
-            st = e.y;
-            en = e.w;
-        }
-    };
-    int32_t nrel;
-    uint32_t nst, nen;
-    load_ent(k_lo + lane, nrel, nst, nen);
-    for (uint32_t k0 = k_lo; k0 < nspan; k0 += 64) {
-        const int32_t rel = nrel;
-        const uint32_t st = nst;
-        uint32_t en = nen;
-        if (k0 + 64 < nspan) load_ent(k0 + 64 + lane, nrel, nst, nen);
-        if (uni(st) >= cap) break;  // spans are in output order: lane 0's start is the lowest
-        en = min(en, cap);
-        const uint32_t nb = en > st ? en - st : 0;
-        const bool lng = nb > kLaneCopyMax;
-        if (nb && !lng) span_copy(o + st, base + rel, nb);
-        uint64_t lm = ballot(lng);
-        while (lm) {
-            const uint32_t j = ffs64(lm);
-            lm &= lm - 1;
-            wave_copy(o + readlane(st, j), base + (int32_t)readlane((uint32_t)rel, j), readlane(nb, j));
-        }
+// Gather: a full-range getitem served from its span table.  One wave per task of 64
+// consecutive tiles of the launch; lane j assembles tile g0 + j: kGatherTile output bytes
+// of one query.  Its first span comes from the tile index, the spans come in two at a time
+// as 16-byte entry pairs, and each piece of a span that falls in the tile is read with
+// unaligned 16-byte loads and merged into four 16-byte registers at its byte offset; the
+// tile then leaves with four aligned 16-byte stores.  Queries are 16-byte aligned in the
+// output and own >= 64 bytes past their expansion (out_cap = doc + 64, rounded to 16), so
+// whole 16-byte blocks are stored; sources have >= 64 bytes of slack behind them.
+PX_DEV u32x4 shl_bytes(u32x4 w, uint32_t b) {  // byte i of the result = byte i - b of w (0 below)
+    const uint32_t ds = b >> 2, bs = b & 3u;
+    uint32_t t[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int k = i - (int)ds;
+        t[i] = k == 0 ? w.x : k == 1 ? w.y : k == 2 ? w.z : k == 3 ? w.w : 0u;
     }
-    if (lane == 0 && k_lo == 0) {  // result slot: the query's position in the k_decode launch
-        out_len[q0.slot] = min(len, cap);
-        status[q0.slot] = len > cap ? (uint32_t)kErrSpace : (uint32_t)kOk;
-    }
+    if (bs == 0) return u32x4{t[0], t[1], t[2], t[3]};
+    const uint32_t sh = 4u - bs;
+    return u32x4{__builtin_amdgcn_alignbyte(t[0], 0u, sh), __builtin_amdgcn_alignbyte(t[1], t[0], sh),
+                 __builtin_amdgcn_alignbyte(t[2], t[1], sh), __builtin_amdgcn_alignbyte(t[3], t[2], sh)};
+}
+PX_DEV uint32_t byte_mask(int lo, int hi) {  // bytes [lo, hi) of a dword (clamped to 0..4)
+    lo = max(lo, 0);
+    hi = min(hi, 4);
+    if (hi <= lo) return 0u;
+    const uint32_t m = hi - lo == 4 ? 0xffffffffu : ((1u << (8 * (hi - lo))) - 1u);
+    return m << (8 * lo);
+}
+// output bytes [lo, hi) of 16-byte block r (0 <= lo < hi <= 16) from src (src = byte lo)
+PX_DEV void put_piece(u32x4 &r, uint32_t lo, uint32_t hi, const PX_GAS uint8_t *src) {
+    const u32x4 v = shl_bytes(ld16(src), lo);
+    r.x |= v.x & byte_mask((int)lo, (int)hi);
+    r.y |= v.y & byte_mask((int)lo - 4, (int)hi - 4);
+    r.z |= v.z & byte_mask((int)lo - 8, (int)hi - 8);
+    r.w |= v.w & byte_mask((int)lo - 12, (int)hi - 12);
 }
 
-__global__ void __launch_bounds__(256) k_gather(uint32_t ntask, const uint4 *tasks, const GatherQuery *qs,
+// the first query of every 64-tile wave: the query holding tile 64 t
+__global__ void __launch_bounds__(256) k_gather_tasks(uint32_t nq, const GatherQuery *qs, uint32_t *task_q) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    const GatherQuery q = qs[i];
+    const uint32_t nt = max(1u, (min(q.len, q.cap) + kGatherTile - 1) / kGatherTile);
+    for (uint32_t t = (q.tile0 + 63) & ~63u; t < q.tile0 + nt; t += 64) task_q[t >> 6] = i;
+}
+
+__global__ void __launch_bounds__(256) k_gather(uint32_t ntask, const uint32_t *task_q, const GatherQuery *qs, uint32_t nq,
                                                 uint8_t *out_, uint32_t *out_len, uint32_t *status, uint32_t remap) {
     const uint32_t lane = lane_id();
     uint32_t lb = blockIdx.x;
@@ -2283,46 +2282,66 @@ __global__ void __launch_bounds__(256) k_gather(uint32_t ntask, const uint4 *tas
     }
     const uint32_t ti = lb * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (ti >= ntask) return;
-    const uint4 task = tasks[ti];
-    const uint32_t first = uni(task.x), count = uni(task.y);
-    if (count == 1) {  // one query, or the span range [z, w) of a long one
-        gather_one(qs[first], uni(task.z), uni(task.w), out_, out_len, status);
-        return;
+    const uint32_t q0 = uni(task_q[ti]), g0 = ti * 64;
+    // which query each lane's tile belongs to: the queries starting inside the task set
+    // their bit (q0 holds tile g0)
+    const uint32_t t0n = q0 + 1 + lane < nq ? qs[q0 + 1 + lane].tile0 : 0xffffffffu;
+    uint64_t M = 0;
+    {
+        const uint64_t bit = t0n - g0 < 64u ? 1ull << (t0n - g0) : 0ull;
+        M = bit;
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)M, o), hi = (uint32_t)__shfl_xor((int)(uint32_t)(M >> 32), o);
+            M |= (uint64_t)hi << 32 | lo;
+        }
     }
-    // several small queries (each >= 1 span, <= 64 spans in all): lane i holds query i
-    GatherQuery q{};
-    if (lane < count) q = qs[first + lane];
-    const uint32_t ns = lane < count ? q.nspan : 0;
-    const uint32_t st0 = wave_excl_scan((int32_t)ns);  // this query's first lane
-    uint64_t starts = lane < count ? (1ull << st0) : 0;
-    for (int o = 32; o >= 1; o >>= 1) {
-        const uint64_t y = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(starts >> 32), o) << 32) |
-                           (uint32_t)__shfl_xor((int)(uint32_t)starts, o);
-        starts |= y;
-    }
-    const uint32_t total = uni(readlane(st0 + ns, count - 1));
-    const uint32_t qi = (uint32_t)__popcll(starts & (lane == 63 ? ~0ull : ((2ull << lane) - 1))) - 1u;
-    const int src = (int)min(qi, 63u);
-    const uint64_t spp = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uint64_t)q.span >> 32), src) << 32) |
-                         (uint32_t)__shfl((int)(uint32_t)(uint64_t)q.span, src);
-    const uint64_t bp = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uint64_t)q.base >> 32), src) << 32) |
-                        (uint32_t)__shfl((int)(uint32_t)(uint64_t)q.base, src);
-    const uint64_t oo = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(q.out_off >> 32), src) << 32) |
-                        (uint32_t)__shfl((int)(uint32_t)q.out_off, src);
-    const uint32_t qcap = (uint32_t)__shfl((int)q.cap, src), qst = (uint32_t)__shfl((int)st0, src);
-    if (lane < total) {
-        const PX_GAS SpanEnt *sp = (const PX_GAS SpanEnt *)spp;
-        const uint32_t k = lane - qst;
-        const u32x4 e = *(const PX_GAS u32x4_u *)(sp + k);
-        const int32_t rel = (int32_t)e.x;
-        const uint32_t s0 = e.y;
-        const uint32_t en = min(e.w, qcap);
-        if (en > s0) span_copy((PX_GAS uint8_t *)out_ + oo + s0, (const PX_GAS uint8_t *)bp + rel, en - s0);
-    }
-    if (lane < count) {
-        out_len[q.slot] = min(q.len, q.cap);
+    const uint32_t qi = q0 + (uint32_t)__popcll(M & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull)));
+    if (qi >= nq) return;
+    const GatherQuery q = qs[qi];
+    const uint32_t t = g0 + lane - q.tile0;
+    const uint32_t lim = min(q.len, q.cap), a = t * kGatherTile;
+    if (t == 0) {
+        out_len[q.slot] = lim;
         status[q.slot] = q.len > q.cap ? (uint32_t)kErrSpace : (uint32_t)kOk;
     }
+    if (a >= lim) return;
+    const uint32_t e = min(a + kGatherTile, lim);
+    const PX_GAS uint8_t *base = (const PX_GAS uint8_t *)q.base;
+    const PX_GAS uint32_t *sp = (const PX_GAS uint32_t *)q.span;  // {rel, start} pairs, then the sentinel
+    uint32_t k = ((const PX_GAS uint32_t *)q.tix)[t];
+    u32x4 r[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+    // spans come in 8 entries (64 bytes, four independent loads) at a time: 7 spans and the
+    // start that ends the 7th (a tile holds ~7 spans on average: usually one round trip)
+    for (bool more = true; more;) {
+        uint32_t en[16];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) *(u32x4 *)(en + 4 * v) = *(const PX_GAS u32x4_u *)(sp + 2 * k + 4 * v);
+#pragma unroll
+        for (int h = 0; h < 7; ++h) {
+            const int32_t rel = (int32_t)en[2 * h];
+            const uint32_t st = en[2 * h + 1], nx = en[2 * h + 3];
+            if (st >= e) {  // (also at the sentinel: its start is the doc length)
+                more = false;
+                break;
+            }
+            const uint32_t x0 = max(st, a), x1 = min(nx, e);
+            if (x0 < x1) {
+                const PX_GAS uint8_t *src = base + rel + (int32_t)(x0 - st);  // source of output byte x0
+                const uint32_t d0 = x0 - a, d1 = x1 - a;
+#pragma unroll
+                for (uint32_t b = 0; b < 4; ++b) {
+                    const uint32_t lo = max(d0, 16 * b), hi = min(d1, 16 * b + 16);
+                    if (lo < hi) put_piece(r[b], lo - 16 * b, hi - 16 * b, src + (lo - d0));
+                }
+            }
+        }
+        if (en[15] >= e) break;  // span k + 7 starts past the tile (entries k .. k + 7 are real)
+        k += 7;
+    }
+    PX_GAS uint8_t *o = (PX_GAS uint8_t *)out_ + q.out_off + a;
+#pragma unroll
+    for (uint32_t b = 0; b < 4; ++b)
+        if (16 * b < e - a) *(PX_GAS u32x4 *)(o + 16 * b) = r[b];
 }
 
 // ====================================================================== migrate
@@ -2463,10 +2482,11 @@ hipError_t launch_span_build(hipStream_t s, uint32_t n, const SpanJob *jobs) {
     return hipGetLastError();
 }
 
-hipError_t launch_gather(hipStream_t s, uint32_t ntask, const uint4 *tasks, const GatherQuery *qs, uint8_t *out,
-                         uint32_t *out_len, uint32_t *status, bool remap) {
+hipError_t launch_gather(hipStream_t s, uint32_t ntask, uint32_t *task_q, const GatherQuery *qs, uint32_t nq,
+                         uint8_t *out, uint32_t *out_len, uint32_t *status, bool remap) {
     if (!ntask) return hipSuccess;
-    k_gather<<<(ntask + 3) / 4, 256, 0, s>>>(ntask, tasks, qs, out, out_len, status, remap ? 1u : 0u);
+    k_gather_tasks<<<(nq + 255) / 256, 256, 0, s>>>(nq, qs, task_q);
+    k_gather<<<(ntask + 3) / 4, 256, 0, s>>>(ntask, task_q, qs, nq, out, out_len, status, remap ? 1u : 0u);
     return hipGetLastError();
 }
 

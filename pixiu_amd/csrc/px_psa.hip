@@ -250,8 +250,10 @@ __global__ void __launch_bounds__(256) k_psa_groups0(uint32_t N, const uint32_t 
 // this step's keys: rank of the suffix h further on (+1), 0 past the doc end.  Flat over the
 // suffix array, 16 slots per thread: every scattered rank read of the step in flight at once
 __global__ void __launch_bounds__(256) k_dbl_key(uint32_t N, uint32_t h, const uint8_t *act, const uint32_t *sa,
-                                                 const uint16_t *sd, const uint32_t *rank, uint32_t *key) {
+                                                 const uint16_t *sd, const uint32_t *rank, uint32_t *key,
+                                                 uint32_t *long_cnt) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < 8) long_cnt[t] = 0;  // (the step's long-group lists start empty: k_dbl_win fills them)
     const uint32_t s0 = t * 16;
     if (s0 >= N) return;
     if (s0 + 16 <= N) {
@@ -346,13 +348,30 @@ __global__ void __launch_bounds__(256) k_dbl_win(uint32_t N, uint32_t tag, uint3
         const uint32_t zA = (uint32_t)__shfl((int)gs, (int)(cA & 63u)), zB = (uint32_t)__shfl((int)gs, (int)cB);
         WinElem A{cA < 64 && lane < cA + zA, cA & 63u, zA, lane - cA, 0, 0, 0};
         WinElem B{64 + lane < cB + zB, cB, zB, 64 + lane - cB, 0, 0, 0};
+        if (A.mem) A.key = key[sA];
+        if (B.mem) B.key = key[sB];
+        {
+            // every group keeps one key (a repeat longer than 2h): the groups stay as they are,
+            // only their sizes move to the next step's tag
+            const uint32_t k0A = (uint32_t)__shfl((int)A.key, (int)A.c), k0B = (uint32_t)__shfl((int)A.key, (int)cB);
+            const uint64_t split = __ballot(A.mem && (A.key != k0A || A.key == 0)) |
+                                   __ballot(B.mem && (B.key != k0B || B.key == 0));
+            if (!split) {
+                if ((S >> lane) & 1ull) {
+                    gsz[sA] = gs | (tag ^ kTag);
+                    mx = max(mx, gs);
+                }
+                const uint32_t m = (uint32_t)__popcll(__ballot(A.mem)) + (uint32_t)__popcll(__ballot(B.mem));
+                sorted += m;
+                active += lane == 0 ? m : 0u;
+                continue;
+            }
+        }
         if (A.mem) {
-            A.key = key[sA];
             A.p = sa[sA];
             A.d = sd[sA];
         }
         if (B.mem) {
-            B.key = key[sB];
             B.p = sa[sB];
             B.d = sd[sB];
         }
@@ -410,15 +429,28 @@ __global__ void __launch_bounds__(256) k_dbl_reg(const uint64_t *list, const uin
         const uint64_t ent = list[gi];
         const uint32_t start = (uint32_t)ent, size = (uint32_t)(ent >> 32);
         uint64_t x[E];
+        const uint32_t key0 = key[start];
+        bool split = false;
+#pragma unroll
+        for (uint32_t r = 0; r < E; ++r) {
+            const uint32_t i = lane * E + r;
+            const uint32_t k = i < size ? key[start + i] : key0;
+            x[r] = i < size ? (uint64_t)k << 11 | i : ~0ull;
+            split = split || k != key0 || k == 0;
+        }
+        if (!__ballot(split)) {  // one key: the group stays as it is (see k_dbl_win)
+            if (lane == 0) gsz[start] = size | (tag ^ kTag);
+            mx = max(mx, size);
+            sorted += size;
+            active += size;
+            continue;
+        }
 #pragma unroll
         for (uint32_t r = 0; r < E; ++r) {
             const uint32_t i = lane * E + r;
             if (i < size) {
-                x[r] = (uint64_t)key[start + i] << 11 | i;
                 lp[wv][i] = sa[start + i];
                 ld[wv][i] = sd[start + i];
-            } else {
-                x[r] = ~0ull;
             }
         }
 #pragma unroll
@@ -506,8 +538,22 @@ __global__ void __launch_bounds__(256) k_dbl_blk(const uint64_t *list, const uin
         const uint32_t start = (uint32_t)ent, size = (uint32_t)(ent >> 32);
         uint32_t P = 256;
         while (P < size) P <<= 1;
-        for (uint32_t i = tid; i < P; i += 256) sk[i] = i < size ? (uint64_t)key[start + i] << 12 | i : ~0ull;
-        __syncthreads();
+        const uint32_t key0 = key[start];
+        bool split = false;
+        for (uint32_t i = tid; i < P; i += 256) {
+            const uint32_t k = i < size ? key[start + i] : key0;
+            split = split || k != key0 || k == 0;
+            sk[i] = i < size ? (uint64_t)k << 12 | i : ~0ull;
+        }
+        if (!__syncthreads_or(split)) {  // one key: the group stays as it is (see k_dbl_win)
+            if (tid == 0) {
+                gsz[start] = size | (tag ^ kTag);
+                active += size;
+            }
+            mx = max(mx, size);
+            sorted += size;
+            continue;  // (the barrier above: nobody reads sk any more)
+        }
         for (uint32_t kk = 2; kk <= P; kk <<= 1)
             for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
                 for (uint32_t i = tid; i < P; i += 256) {
@@ -758,6 +804,7 @@ __global__ void __launch_bounds__(256) k_psa_links_text(uint32_t N, const uint32
 // when that leaves fewer than 2^18 threads -- a one-chunk window of the single instance
 constexpr uint32_t kLceSpan = 256;
 inline uint32_t lce_span(uint64_t n) {
+    if (const char *e = std::getenv("PX_LCE_SPAN")) return (uint32_t)std::max(8, std::atoi(e) / 8 * 8);  // (experiments)
     uint64_t sp = kLceSpan;
     while (sp > 16 && n / sp < (1u << 18)) sp /= 2;
     return (uint32_t)sp;
@@ -950,17 +997,16 @@ __global__ void __launch_bounds__(256) k_pool_pack(uint32_t N, const uint32_t *p
     if (p >= N) return;
     rec[p] = LinkRec{psvp[p], nsvp[p], lp[p], ln[p], dist[p], 0};
 }
-__global__ void __launch_bounds__(256) k_pool_leaf(uint32_t N, const uint8_t *G, const uint32_t *pdoc, const PsaDoc *docs,
-                                                   const PsaShard *shards, const LinkRec *R, uint8_t *code, uint32_t *E,
-                                                   uint32_t *ncand) {
+__global__ void __launch_bounds__(256) k_pool_leaf(uint32_t N, const uint8_t *G, const PsaShard *shards, uint32_t nshards,
+                                                   const LinkRec *R, uint8_t *code, uint32_t *E, uint32_t *ncand) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t c = 0;
     if (p < N) {
-        const PsaDoc &d = docs[pdoc[p]];
-        if (shards[d.shard].pools) {
+        // (shards are contiguous in position space as in rank space: the same search)
+        if (shards[shard_of_rank(shards, nshards, p)].pools) {
             const LinkRec me = R[p];
             const uint32_t l = max(me.lp, me.ln);
-            if (p + l < d.start + d.len) {
+            if (l < me.dist) {  // p + l before the doc's end
                 c = 1;
                 if (l) {
                     uint32_t q = kNoPos;
@@ -1029,72 +1075,168 @@ __global__ void __launch_bounds__(256) k_pool_blocks(uint32_t N, uint8_t *code, 
     blk[p] = c == 1 ? 8u : c == 3 ? 16u : 0u;
 }
 
-// C[b] = the blocks before the end of the b-th 64-position block (P at 64b + 63)
+// C[b] = the blocks before the end of the b-th kPoolCoarse-position block
+constexpr uint32_t kPoolCoarse = 1024;
 __global__ void __launch_bounds__(256) k_pool_coarse(uint32_t N, const uint32_t *P, uint32_t *C) {
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if ((uint64_t)b * 64 >= N) return;
-    C[b] = P[min(b * 64 + 63, N - 1)];
+    if ((uint64_t)b * kPoolCoarse >= N) return;
+    C[b] = P[min(b * kPoolCoarse + kPoolCoarse - 1, N - 1)];
 }
 
-// One wave per emulating shard: the pool state from the chunk's root node on, boundary by
-// boundary.  A pool boundary is the first leaf whose pattern does not fit the open pool:
-// the wave keeps 64 coarse prefix values (4,096 positions) in registers, finds the block
-// holding the boundary by one ballot, then its leaf with one 64-position load, and
-// resolves the leaf's [5, 3] / [5, 5, 3, 3] charges.  The 2,048th pool opened inside doc g
-// rotates the chunk before doc g + 1 (PiXiuCtrl.cpp:13); the window's doc count never
-// reaches 65,535 (the host rotates slot-full chunks between rounds).
-__global__ void __launch_bounds__(64) k_pool_scan(uint32_t nshards, const PsaShard *shards, const PsaDoc *docs,
-                                                  const uint32_t *P, const uint32_t *C, uint32_t N, PsaPoolOut *out) {
+// One block per emulating shard: the pool state from the chunk's root node on, boundary by
+// boundary.  A pool boundary is the first leaf whose pattern does not fit the open pool;
+// boundaries form one dependent chain (~2,000 per chunk, ~5,500 positions apart), so the
+// scan is latency-bound and built to keep HBM off that chain.  The prefix values P are
+// staged into LDS in kScanWin-position windows; wave 0 resolves every boundary inside a
+// window from LDS (a ballot over 64-position maxima, then one over the 64 positions) and
+// charges the leaf's [5, 3] / [5, 5, 3, 3] blocks one by one, while the other 15 waves stage
+// the following window into the second buffer.  A boundary further on than that (a long
+// stretch of positions without leaves) is found through the 1,024-position coarse values C
+// and its window staged by all waves.  The 2,048th pool opened inside doc g rotates the chunk
+// before doc g + 1 (PiXiuCtrl.cpp:13); the window's doc count never reaches 65,535 (the host
+// rotates slot-full chunks between rounds).
+constexpr uint32_t kScanWin = 16384, kScanThreads = 1024;
+PSA_DEV void scan_stage(uint32_t *Pw, uint32_t *Cw, const uint32_t *P, uint32_t N, uint32_t wb, uint32_t t0,
+                        uint32_t nt) {
+    for (uint32_t i = t0 * 4; i < kScanWin; i += nt * 4) {
+        uint4 v;
+        if (wb + i + 4 <= N) {
+            v = *(const uint4 *)(P + wb + i);
+        } else {  // (0xffffffff past N: "exceeds")
+            v.x = wb + i < N ? P[wb + i] : 0xffffffffu;
+            v.y = wb + i + 1 < N ? P[wb + i + 1] : 0xffffffffu;
+            v.z = wb + i + 2 < N ? P[wb + i + 2] : 0xffffffffu;
+            v.w = wb + i + 3 < N ? P[wb + i + 3] : 0xffffffffu;
+        }
+        *(uint4 *)(Pw + i) = v;
+        if ((i & 63) == 60) Cw[i >> 6] = v.w;  // the 64-position group's last value
+    }
+}
+__global__ void __launch_bounds__(kScanThreads) k_pool_scan(uint32_t nshards, const PsaShard *shards, const PsaDoc *docs,
+                                                            const uint32_t *P, const uint32_t *C, uint32_t N,
+                                                            PsaPoolOut *out) {
+    __shared__ uint32_t Pw[2][kScanWin];       // P[wb + i]
+    __shared__ uint32_t Cw[2][kScanWin / 64];  // P[wb + 64 j + 63]
+    __shared__ uint32_t sh_wb, sh_go, sh_restage;
     const uint32_t s = blockIdx.x;
     if (s >= nshards) return;
-    const uint32_t lane = lane_id();
+    const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
     const PsaShard sh = shards[s];
-    PsaPoolOut o{kNone, 0, 0, 0};
-    if (sh.pools && sh.ndocs) {
-        auto S = [&](uint32_t x) { return x ? P[x - 1] : 0u; };  // blocks before position x
-        const uint32_t start = docs[sh.doc0].start, endp = sh.base + sh.len;
-        int32_t pools = 1, used = kNodeBlocks;  // the root (SuffixTree::init_prop)
-        uint32_t cur = start, base = S(start);
-        const uint32_t send = S(endp);
-        uint32_t cw = kNone, cv = 0;  // coarse window: blocks [cw, cw + 64)
-        uint32_t k_last = kNone;
-        while (pools < kRotatePools && (uint32_t)used + (send - base) > (uint32_t)kPoolBlocks) {
-            const uint32_t cap = (uint32_t)(kPoolBlocks - used);
-            // the block holding the boundary: first b >= cur / 64 with C[b] - base > cap
-            uint32_t b = cur >> 6;
-            for (;;) {
-                if (cw == kNone || b < cw || b >= cw + 64) {
-                    cw = b;
-                    const uint32_t bi = cw + lane;
-                    cv = (uint64_t)bi * 64 < N ? C[bi] : 0xffffffffu;
-                }
-                const uint64_t m = __ballot(cw + lane >= b && ((uint64_t)(cw + lane) * 64 >= N || cv - base > cap));
-                if (m) {
-                    b = cw + (uint32_t)__ffsll((long long)m) - 1u;
-                    break;
-                }
-                b = cw + 64;
+    if (!sh.pools || !sh.ndocs) {
+        if (threadIdx.x == 0) out[s] = PsaPoolOut{kNone, 0, 0, 0};
+        return;
+    }
+    const uint32_t nblk = (N + kPoolCoarse - 1) / kPoolCoarse;
+    auto S = [&](uint32_t x) { return x ? P[x - 1] : 0u; };  // blocks before position x
+    const uint32_t start = docs[sh.doc0].start, endp = sh.base + sh.len;
+    // wave 0's state (uniform across its lanes)
+    int32_t pools = 1, used = kNodeBlocks;  // the root (SuffixTree::init_prop)
+    uint32_t cur = start, base = S(start);
+    const uint32_t send = S(endp);
+    uint32_t cw = kNone, cv = 0;  // coarse window: blocks [cw, cw + 64)
+    uint32_t k_last = kNone;
+    auto more = [&]() { return pools < kRotatePools && (uint32_t)used + (send - base) > (uint32_t)kPoolBlocks; };
+    // the window holding the next boundary (wave 0): from the coarse values
+    auto locate = [&]() {
+        const uint32_t cap = (uint32_t)(kPoolBlocks - used);
+        uint32_t b = cur / kPoolCoarse;  // first b >= cur / kPoolCoarse with C[b] - base > cap
+        for (;;) {
+            if (cw == kNone || b < cw || b >= cw + 64) {
+                cw = b;
+                cv = cw + lane < nblk ? C[cw + lane] : 0xffffffffu;
             }
-            const uint32_t x = b * 64 + lane;
-            const uint64_t mk = __ballot(x >= cur && x < endp && P[x] - base > cap);
-            const uint32_t k = mk ? b * 64 + (uint32_t)__ffsll((long long)mk) - 1u : endp - 1u;  // (mk != 0)
-            const uint32_t sk = S(k);
-            int32_t u = used + (int32_t)(sk - base);
-            const bool split = P[k] - sk == 16u;
-            const int32_t ch[4] = {kNodeBlocks, split ? kNodeBlocks : kEdgeBlocks, kEdgeBlocks, kEdgeBlocks};
-            for (int i = 0; i < (split ? 4 : 2); ++i) {
-                if (u + ch[i] > kPoolBlocks) {
-                    ++pools;
-                    u = ch[i];
-                } else {
-                    u += ch[i];
-                }
-            }
-            used = u;
-            cur = k + 1;
-            base = P[k];
-            k_last = k;
+            const uint64_t m = __ballot(cw + lane >= b && (cw + lane >= nblk || cv - base > cap));
+            if (m) return cw + (uint32_t)__ffsll((long long)m) - 1u;
+            b = cw + 64;
         }
+    };
+    uint32_t buf = 0, wb = 0;
+    if (wave == 0) {
+        const uint32_t go = more() ? 1u : 0u;
+        if (go) wb = max(locate() * kPoolCoarse, cur & ~63u);
+        if (lane == 0) {
+            sh_go = go;
+            sh_wb = wb;
+        }
+    }
+    __syncthreads();
+    if (sh_go) scan_stage(Pw[0], Cw[0], P, N, sh_wb, threadIdx.x, kScanThreads);
+    __syncthreads();
+    uint32_t last_cur = kNone;  // (every window resolves >= 1 boundary or moves on; a stall ends the scan)
+    while (sh_go) {
+        wb = sh_wb;
+        const uint32_t wend = wb + kScanWin;
+        if (wave == 0) {
+            const uint32_t *pw = Pw[buf], *cwin = Cw[buf];
+            const uint32_t before = wb ? P[wb - 1] : 0u;  // P at wb - 1
+            while (more()) {
+                const uint32_t cap = (uint32_t)(kPoolBlocks - used);
+                // the 64-position group holding the boundary, within the window
+                uint32_t j = cur > wb ? (cur - wb) >> 6 : 0u, jg = kNone;
+                while (j < kScanWin / 64) {
+                    const uint32_t jj = j + lane;
+                    const uint64_t m = __ballot(jj < kScanWin / 64 && cwin[jj < kScanWin / 64 ? jj : 0] - base > cap);
+                    if (m) {
+                        jg = j + (uint32_t)__ffsll((long long)m) - 1u;
+                        break;
+                    }
+                    j += 64;
+                }
+                if (jg == kNone) break;  // past the window
+                const uint32_t x = wb + 64 * jg + lane;
+                const uint32_t v = pw[64 * jg + lane];
+                const uint64_t mk = __ballot(x >= cur && x < endp && v - base > cap);
+                if (!mk) break;  // (only past endp: cannot happen while more())
+                const uint32_t L = (uint32_t)__ffsll((long long)mk) - 1u;
+                const uint32_t k = wb + 64 * jg + L;
+                const uint32_t Pk = (uint32_t)__shfl((int)v, (int)L);
+                const uint32_t sk = k == start ? base : (k == wb ? before : pw[k - wb - 1]);
+                int32_t u = used + (int32_t)(sk - base);
+                const bool split = Pk - sk == 16u;
+                const int32_t ch[4] = {kNodeBlocks, split ? kNodeBlocks : kEdgeBlocks, kEdgeBlocks, kEdgeBlocks};
+                for (int i = 0; i < (split ? 4 : 2); ++i) {
+                    if (u + ch[i] > kPoolBlocks) {
+                        ++pools;
+                        u = ch[i];
+                    } else {
+                        u += ch[i];
+                    }
+                }
+                used = u;
+                cur = k + 1;
+                base = Pk;
+                k_last = k;
+                if (cur >= wend) break;
+            }
+        } else {  // the next window, speculatively: the one right after this
+            scan_stage(Pw[buf ^ 1], Cw[buf ^ 1], P, N, wend, threadIdx.x - 64, kScanThreads - 64);
+        }
+        __syncthreads();
+        if (wave == 0) {
+            uint32_t go = more() && cur != last_cur ? 1u : 0u, nwb = wend, re = 0;
+            last_cur = cur;
+            if (go) {
+                const uint32_t b = locate();
+                if (b * kPoolCoarse + kPoolCoarse > wend + kScanWin) {  // beyond the staged window
+                    nwb = max(b * kPoolCoarse, cur & ~63u);
+                    re = 1;
+                }
+            }
+            if (lane == 0) {
+                sh_go = go;
+                sh_wb = nwb;
+                sh_restage = re;
+            }
+        }
+        __syncthreads();
+        buf ^= 1;
+        if (sh_go && sh_restage) {
+            scan_stage(Pw[buf], Cw[buf], P, N, sh_wb, threadIdx.x, kScanThreads);
+            __syncthreads();
+        }
+    }
+    if (threadIdx.x == 0) {
+        PsaPoolOut o{kNone, 0, 0, 0};
         if (pools >= kRotatePools) {
             // the doc holding the 2,048th pool's first charge: rotation before the next one
             uint32_t lo = sh.doc0, hi = sh.doc0 + sh.ndocs;  // docs[lo].start <= k_last < docs[hi].start
@@ -1109,8 +1251,8 @@ __global__ void __launch_bounds__(64) k_pool_scan(uint32_t nshards, const PsaSha
         }
         o.pools = pools;
         o.used = used;
+        out[s] = o;
     }
-    if (lane == 0) out[s] = o;
 }
 
 struct Max {
@@ -1277,9 +1419,8 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     auto step = [&](bool big) -> hipError_t {
         const uint32_t tag = (it & 1u) ? kTag : 0u;
         const StepStat ss = stats_of(it);
-        hipError_t e = hipMemsetAsync(cnt + kCntLong, 0, 8 * 4, s);
-        if (e != hipSuccess) return e;
-        k_dbl_key<<<blocks((n64 + 15) / 16), tb, 0, s>>>(N, h, act, sa, sd, rank, key);
+        hipError_t e = hipSuccess;
+        k_dbl_key<<<blocks((n64 + 15) / 16), tb, 0, s>>>(N, h, act, sa, sd, rank, key, cnt + kCntLong);
         k_dbl_win<<<gwin, 256, 0, s>>>(N, tag, sa, sd, act, gsz, key, rank, LL, ss);
         k_dbl_reg<2><<<kGridReg, 256, 0, s>>>(LL.lst[0], LL.cnt + 0, tag, sa, sd, act, gsz, key, rank, ss);
         k_dbl_reg<4><<<kGridReg, 256, 0, s>>>(LL.lst[1], LL.cnt + 1, tag, sa, sd, act, gsz, key, rank, ss);
@@ -1426,7 +1567,7 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         {
             auto *rec = S.get<LinkRec>(n64 * sizeof(LinkRec));
             k_pool_pack<<<blocks(N), tb, 0, s>>>(N, psvp, nsvp, lcp_p, lcp_n, dist, rec);
-            k_pool_leaf<<<blocks(N), tb, 0, s>>>(N, G, pdoc, docs, shards, rec, code, E, ncand);
+            k_pool_leaf<<<blocks(N), tb, 0, s>>>(N, G, shards, nshards, rec, code, E, ncand);
             S.put(rec);
         }
         // the candidate table: 2x the candidates, read back for big windows; a small window
@@ -1450,9 +1591,9 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         PSA_CHECK(rocprim::inclusive_scan(nullptr, tsz, blk, P, (size_t)N, rocprim::plus<uint32_t>(), s));
         void *tmp2 = S.get<void>(tsz + 256);
         PSA_CHECK(rocprim::inclusive_scan(tmp2, tsz, blk, P, (size_t)N, rocprim::plus<uint32_t>(), s));
-        auto *C = S.get<uint32_t>(n64 / 64 * 4 + 256);
-        k_pool_coarse<<<blocks((N + 63) / 64), tb, 0, s>>>(N, P, C);
-        k_pool_scan<<<nshards, 64, 0, s>>>(nshards, shards, docs, P, C, N, pool_out);
+        auto *C = S.get<uint32_t>(n64 / kPoolCoarse * 4 + 256);
+        k_pool_coarse<<<blocks((N + kPoolCoarse - 1) / kPoolCoarse), tb, 0, s>>>(N, P, C);
+        k_pool_scan<<<nshards, kScanThreads, 0, s>>>(nshards, shards, docs, P, C, N, pool_out);
         PSA_CHECK(hipGetLastError());
     }
     PSA_CHECK(hipEventRecord(e4, s));

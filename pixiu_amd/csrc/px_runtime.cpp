@@ -51,8 +51,8 @@ hipError_t launch_rehash(hipStream_t, const uint4 *, uint32_t, uint32_t, uint4 *
 hipError_t launch_decode_addr(hipStream_t, const DecodeQuery *, uint32_t, const RecSlot *const *, int32_t *,
                               uint32_t *, uint32_t *, Frame *, uint32_t, uint32_t);
 hipError_t launch_span_build(hipStream_t, uint32_t, const SpanJob *);
-hipError_t launch_gather(hipStream_t, uint32_t, const uint4 *, const GatherQuery *, uint8_t *, uint32_t *, uint32_t *,
-                         bool);
+hipError_t launch_gather(hipStream_t, uint32_t, uint32_t *, const GatherQuery *, uint32_t, uint8_t *, uint32_t *,
+                         uint32_t *, bool);
 int debug_trace_take(int32_t *, uint32_t);
 int debug_prof_take(unsigned long long *, uint32_t);
 }  // namespace px
@@ -199,9 +199,11 @@ struct Chunk {
     // span tables (full-range getitem as a gather); sized lazily
     struct Span {
         const SpanEnt *p = nullptr;  // device; null: decode through the segment walk
+        const uint32_t *t = nullptr;  // its tile index (the span at every kGatherTile-th byte)
         uint32_t n = 0, len = 0;     // spans, compat expansion length
         bool eq = false;             // the compat expansion equals the doc (== exact)
         const SpanEnt *xp = nullptr;  // exact expansion's table when it differs (!eq)
+        const uint32_t *xt = nullptr;
         uint32_t xn = 0, xlen = 0;
     };
     std::vector<Span> span;
@@ -261,6 +263,7 @@ struct px_ctx {
     DevBuf scratch_frames, dq_buf, dstat_buf, dlen_buf, in_buf, tmp_buf, link_buf, iter_buf, init_buf, stout_buf,
         slotput_buf;
     HostBuf hq_buf, hres_buf;  // pinned: decode queries up, lengths + statuses down
+    HostBuf hg_buf[2];         // pinned: gather queries up (a head and a tail launch)
     HostBuf psa_pin;           // pinned: px_psa.hip's count read-backs
     DevBuf sink_buf;           // k_gst_encode's message sink for replayed docs
     PsaStats psa_stats{};      // the last set batch's suffix-array pass
@@ -687,16 +690,17 @@ struct px_ctx {
     // the table serving query q: {entries, count, expansion length}, or entries == null
     struct SpanView {
         const SpanEnt *p;
+        const uint32_t *t;
         uint32_t n, len;
     };
     SpanView span_view(const DecodeQuery &q) const {
-        if (q.chunk == kNone || q.from != 0 || q.to < kMaxDoc) return SpanView{nullptr, 0, 0};
+        if (q.chunk == kNone || q.from != 0 || q.to < kMaxDoc) return SpanView{nullptr, nullptr, 0, 0};
         const Chunk &ch = chunks[q.chunk];
-        if (q.idx >= ch.span.size()) return SpanView{nullptr, 0, 0};
+        if (q.idx >= ch.span.size()) return SpanView{nullptr, nullptr, 0, 0};
         const Chunk::Span &sp = ch.span[q.idx];
-        if (!sp.p) return SpanView{nullptr, 0, 0};
-        if (q.mode == 0 || sp.eq) return SpanView{sp.p, sp.n, sp.len};
-        return SpanView{sp.xp, sp.xn, sp.xlen};
+        if (!sp.p) return SpanView{nullptr, nullptr, 0, 0};
+        if (q.mode == 0 || sp.eq) return SpanView{sp.p, sp.t, sp.n, sp.len};
+        return SpanView{sp.xp, sp.xt, sp.xn, sp.xlen};
     }
 
     // Full-range getitem queries on records with span tables go to k_gather: they are
@@ -709,48 +713,34 @@ struct px_ctx {
             const SpanView sp = span_view(qn[j]);
             if (!sp.p) continue;
             g.push_back(GatherQuery{sp.p, chunks[qn[j].chunk].slots[qn[j].idx].comp, qn[j].out_off, sp.n, sp.len,
-                                    qn[j].out_cap, j - lo + slot0});
+                                    qn[j].out_cap, j - lo + slot0, sp.t, 0, 0});
             qn[j].chunk = kNone;
             qn[j].nrec = 0;
         }
         return g;
     }
-    // after the k_decode launch on the same stream (its skipped-query results are overwritten)
-    // tasks: one query, or consecutive queries of 1..64 spans each with <= 64 spans in all
-    // (one wave serves them together: small records leave most lanes idle otherwise)
-    void launch_gathers(hipStream_t st, const std::vector<GatherQuery> &g, uint8_t *out, uint32_t *dl, uint32_t *ds,
-                        GatherQuery *&dbuf) {
+    // after the k_decode launch on the same stream (its skipped-query results are overwritten).
+    // The launch's tiles (a tile = kGatherTile output bytes of one query; a query's tiles
+    // are consecutive) go 64 to a wave, across queries when they are small; the queries go
+    // up from pinned memory (`which`: the launch's own staging buffer) and k_gather_tasks
+    // finds each wave's first query on the device.
+    void launch_gathers(hipStream_t st, std::vector<GatherQuery> &g, uint8_t *out, uint32_t *dl, uint32_t *ds,
+                        GatherQuery *&dbuf, int which) {
         if (g.empty()) return;
-        // a long record is split into pieces of kPiece spans (one wave each: more waves in
-        // flight to hide the entry -> bytes round trips)
-        static const uint32_t kPiece = [] {
-            const char *e = std::getenv("PX_GATHER_PIECE");
-            const int v = e ? std::atoi(e) : 0;
-            return v >= 64 ? (uint32_t)v : 1024u;
-        }();
-        std::vector<uint4> tasks;
-        tasks.reserve(g.size());
-        for (uint32_t i = 0; i < (uint32_t)g.size();) {
-            uint32_t j = i, tot = 0;
-            // (small records only: a packed span is copied by one lane, however long)
-            while (j < g.size() && j - i < 64 && g[j].nspan >= 1 && g[j].len <= 4096 && tot + g[j].nspan <= 64)
-                tot += g[j++].nspan;
-            if (j > i + 1) {
-                tasks.push_back(make_uint4(i, j - i, 0, 0));
-            } else {  // one query alone, in pieces
-                j = i + 1;
-                const uint32_t ns = g[i].nspan;
-                for (uint32_t k = 0; k == 0 || k < ns; k += kPiece) tasks.push_back(make_uint4(i, 1, k, k + kPiece));
-            }
-            i = j;
+        uint32_t tiles = 0;
+        for (auto &q : g) {
+            q.tile0 = tiles;
+            tiles += std::max<uint32_t>(1, (std::min(q.len, q.cap) + kGatherTile - 1) / kGatherTile);  // (>= 1: the status)
         }
+        const uint32_t ntask = (tiles + 63) / 64;
         const uint64_t qb = round_up(g.size() * sizeof(GatherQuery), 64);
-        dbuf = (GatherQuery *)heap.alloc(qb + tasks.size() * sizeof(uint4));
-        auto *dt = (uint4 *)((uint8_t *)dbuf + qb);
-        hcheck(hipMemcpyAsync(dbuf, g.data(), g.size() * sizeof(GatherQuery), hipMemcpyHostToDevice, st));
-        hcheck(hipMemcpyAsync(dt, tasks.data(), tasks.size() * sizeof(uint4), hipMemcpyHostToDevice, st));
-        hcheck(launch_gather(st, (uint32_t)tasks.size(), dt, dbuf, out, dl, ds, true));
-        gather_bytes[dbuf] = qb + tasks.size() * sizeof(uint4);
+        auto *hg = (GatherQuery *)hg_buf[which].get(g.size() * sizeof(GatherQuery));
+        std::memcpy(hg, g.data(), g.size() * sizeof(GatherQuery));
+        dbuf = (GatherQuery *)heap.alloc(qb + (uint64_t)ntask * 4);
+        auto *task_q = (uint32_t *)((uint8_t *)dbuf + qb);
+        hcheck(hipMemcpyAsync(dbuf, hg, g.size() * sizeof(GatherQuery), hipMemcpyHostToDevice, st));
+        hcheck(launch_gather(st, ntask, task_q, dbuf, (uint32_t)g.size(), out, dl, ds, true));
+        gather_bytes[dbuf] = qb + (uint64_t)ntask * 4;
     }
     std::map<void *, uint64_t> gather_bytes;  // launch_gathers' device buffers -> their sizes
     void release_gathers(GatherQuery *d) {
@@ -817,7 +807,7 @@ struct px_ctx {
                                  waves | (xcd ? 0x80000000u : 0u), !timed));
         }
         GatherQuery *dgq = nullptr;
-        launch_gathers(stream, gq, out_dev, dl, ds, dgq);
+        launch_gathers(stream, gq, out_dev, dl, ds, dgq, 0);
         if (timed) hcheck(hipEventRecord(ev1, stream));
         auto *hr = (uint32_t *)hres_buf.get((uint64_t)nq * 8);
         hcheck(hipMemcpyAsync(hr, dl, (size_t)nq * 8, hipMemcpyDeviceToHost, stream));  // lengths, then statuses
@@ -866,7 +856,7 @@ struct px_ctx {
             if (st[k] != kOk) continue;
             const Chunk &ch = chunks[reqs[k].chunk];
             jobs.push_back(SpanJob{addr + q[k].out_off, ch.slots[reqs[k].idx].comp, reqs[k].doc, nullptr, len[k],
-                                   ch.doc_len[reqs[k].idx], nullptr, 0});
+                                   ch.doc_len[reqs[k].idx], nullptr, nullptr});
             ji.push_back((uint32_t)k);
         }
         if (!jobs.empty()) {
@@ -879,36 +869,47 @@ struct px_ctx {
             std::vector<uint32_t> cnt(nj);
             d2h(cnt.data(), dcnt, nj * 4);
             sync();
-            uint64_t ents = 0;
+            uint64_t ents = 0, tiles = 0;
             for (size_t j = 0; j < nj; ++j)
-                if (!(cnt[j] & kSpanBad)) ents += (cnt[j] & ~(kSpanBad | kSpanEq)) + 1;
+                if (!(cnt[j] & kSpanBad)) {
+                    ents += (cnt[j] & ~(kSpanBad | kSpanEq)) + 1;
+                    tiles += (len[ji[j]] + kGatherTile - 1) / kGatherTile;
+                }
             if (ents) {
-                auto *tab = (SpanEnt *)heap.alloc(ents * sizeof(SpanEnt) + 64);
-                store_blocks.emplace_back(tab, ents * sizeof(SpanEnt) + 64);
-                uint64_t o = 0;
+                // entries, then every record's tile index (4 B per kGatherTile output bytes)
+                const uint64_t tab_bytes = round_up(ents * sizeof(SpanEnt), 64) + tiles * 4 + 64;
+                auto *tab = (SpanEnt *)heap.alloc(tab_bytes);
+                store_blocks.emplace_back(tab, tab_bytes);
+                auto *tixb = (uint32_t *)((uint8_t *)tab + round_up(ents * sizeof(SpanEnt), 64));
+                uint64_t o = 0, to = 0;
                 for (size_t j = 0; j < nj; ++j) {
                     const uint32_t k = ji[j];
                     Chunk &ch = chunks[reqs[k].chunk];
                     if (ch.span.size() < ch.n) ch.span.resize(ch.n);
                     if (cnt[j] & kSpanBad) {
                         jobs[j].out = nullptr;
+                        jobs[j].tix = nullptr;
                         jobs[j].len = 0;
                         continue;
                     }
                     const uint32_t ns = cnt[j] & ~(kSpanBad | kSpanEq);
                     jobs[j].out = tab + o;
+                    jobs[j].tix = tixb + to;
                     Chunk::Span &sp = ch.span[reqs[k].idx];
                     if (mode == 0) {
                         sp.p = tab + o;
+                        sp.t = tixb + to;
                         sp.n = ns;
                         sp.len = len[k];
                         sp.eq = (cnt[j] & kSpanEq) != 0;
                     } else {
                         sp.xp = tab + o;
+                        sp.xt = tixb + to;
                         sp.xn = ns;
                         sp.xlen = len[k];
                     }
                     o += ns + 1;
+                    to += (len[k] + kGatherTile - 1) / kGatherTile;
                     stats.span_entries += ns + 1;
                 }
                 h2d(djobs, jobs.data(), nj * sizeof(SpanJob));
@@ -1019,7 +1020,7 @@ struct px_ctx {
         auto *hr = (uint32_t *)hres_buf.get((uint64_t)n * 8);
         std::memcpy(qn, q.data(), (size_t)head * sizeof(DecodeQuery));
         phase.mark("head gathers + launch");
-        const std::vector<GatherQuery> g1 = take_gathers(qn, 0, head, 0);
+        std::vector<GatherQuery> g1 = take_gathers(qn, 0, head, 0);
         auto any_walk = [&](uint32_t lo, uint32_t hi) {
             for (uint32_t j = lo; j < hi; ++j)
                 if (qn[j].chunk != kNone) return true;
@@ -1033,7 +1034,7 @@ struct px_ctx {
             hcheck(launch_decode(stream, dq, head, (const RecSlot *const *)chunk_tab, out, dl, ds, frames, depth,
                                  w1 | 0x80000000u, false));
         GatherQuery *dg1 = nullptr, *dg2 = nullptr;
-        launch_gathers(stream, g1, out, dl, ds, dg1);
+        launch_gathers(stream, g1, out, dl, ds, dg1, 0);
         // the tail: resolved while the head decodes
         phase.mark("tail lookups");
         auto t1 = clk::now();
@@ -1048,7 +1049,7 @@ struct px_ctx {
         }
         phase.mark("tail gathers + launch");
         std::memcpy(qn + head, q.data() + head, (size_t)(n - head) * sizeof(DecodeQuery));
-        const std::vector<GatherQuery> g2 = take_gathers(qn, head, n, 0);
+        std::vector<GatherQuery> g2 = take_gathers(qn, head, n, 0);
         stats.last_gather_queries = (uint32_t)(g1.size() + g2.size());
         hcheck(hipStreamWaitEvent(stream2, ev0, 0));  // chunk table and head queries uploaded
         if (any_walk(head, n)) {
@@ -1057,7 +1058,7 @@ struct px_ctx {
             hcheck(launch_decode(stream2, dq + head, n - head, (const RecSlot *const *)chunk_tab, out, dl + head,
                                  ds + head, frames + (uint64_t)w1 * depth, depth, w2 | 0x80000000u, false));
         }
-        launch_gathers(stream2, g2, out, dl + head, ds + head, dg2);
+        launch_gathers(stream2, g2, out, dl + head, ds + head, dg2, 1);
         hcheck(hipEventRecord(ev_join, stream2));
         hcheck(hipStreamWaitEvent(stream, ev_join, 0));
         hcheck(hipEventRecord(ev1, stream));
@@ -2755,7 +2756,8 @@ int px_reinsert(px_ctx *ctx, uint32_t shard, uint32_t chunk) {
         const Chunk &ch = ctx->chunks[c];
         // closed (PiXiuChunk::total_num set at rotation) and slot-full; the live chunk is the
         // shard's last one
-        if (chunk + 1 == s.chunks.size() || ch.total == 0 || ch.n != (uint32_t)kChunkSlots) return PX_EINVAL;
+        if (chunk + 1 == s.chunks.size() || ch.total == 0 || ch.n != (uint32_t)kChunkSlots || ch.used == 0)
+            return PX_EINVAL;  // (used 0: compacted already -- the reference's pointer is NULL by then)
         ctx->reinsert_chunk(s, c, false);
         if (s.glob == (int64_t)c) s.glob = -1;  // (the reference would keep a dangling Glob_Reinsert_Chunk)
         return PX_OK;

@@ -133,9 +133,12 @@ int main() {
         PiXiuChunk *c0 = ctrl.chunk_at(0);
         ctrl.reinsert(c0);
         CHECK(c0 == NULL);
-        PiXiuChunk *live_chunk = ctrl.st.cbt_chunk;
-        ctrl.reinsert(live_chunk);  // the live chunk is not compacted
+        PiXiuChunk *live_chunk = ctrl.chunk_at(1);  // (the records went in through the C ABI)
+        ctrl.reinsert(live_chunk);                  // the live chunk is not compacted
         CHECK(live_chunk != NULL);
+        PiXiuChunk *again = ctrl.chunk_at(0);  // nor a chunk with nothing live left
+        ctrl.reinsert(again);
+        CHECK(again != NULL);
         for (int i = 0; i < n; i += 13) {
             PXSGen *gi = ctrl.getitem((uint8_t *)ks[i].c_str(), (int)ks[i].size());
             CHECK((gi != NULL) == live[i]);

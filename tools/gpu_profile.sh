@@ -22,7 +22,7 @@ if [ "${SKIP_BENCH:-0}" != 1 ]; then
   timeout -k 10 600 python -u bench.py $BENCH_ARGS > $O/${TAG}_bench.log 2>&1 || { echo "BENCH FAILED"; tail -20 $O/${TAG}_bench.log; exit 1; }
   tail -1 $O/${TAG}_bench.log
 fi
-PROF="bench.py --steps 1 --warmup 0 --no-cpu --no-pcie --no-checks --no-exact --no-single --configs= --config $CFG ${RPS:+--rps $RPS}"
+PROF="bench.py --steps 1 --warmup 0 --no-cpu --no-pcie --no-cliff --no-checks --no-exact --no-single --configs= --config $CFG ${RPS:+--rps $RPS}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/${TAG}_ks -o ks --output-format csv \
   -- python3 $PROF > $O/${TAG}_ks.log 2>&1 || { echo "KTRACE FAILED"; tail -20 $O/${TAG}_ks.log; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $O/${TAG}_pmc_f -o f --output-format csv \
