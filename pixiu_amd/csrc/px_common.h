@@ -223,7 +223,7 @@ struct SpanJob {
 };
 // the gather's tile: one lane assembles kGatherTile output bytes; tix[t] = the span
 // holding output byte t * kGatherTile
-constexpr uint32_t kGatherTile = 64;
+constexpr uint32_t kGatherTile = 32;
 constexpr uint32_t kSpanBad = 1u << 31, kSpanEq = 1u << 30;
 
 // gather query: one full-range getitem served from a span table

@@ -2227,13 +2227,18 @@ __global__ void __launch_bounds__(256) k_span_build(uint32_t n, const SpanJob *j
 }
 
 // Gather: a full-range getitem served from its span table.  One wave per task of 64
-// consecutive tiles of the launch; lane j assembles tile g0 + j: kGatherTile output bytes
-// of one query.  Its first span comes from the tile index, the spans come in two at a time
-// as 16-byte entry pairs, and each piece of a span that falls in the tile is read with
-// unaligned 16-byte loads and merged into four 16-byte registers at its byte offset; the
-// tile then leaves with four aligned 16-byte stores.  Queries are 16-byte aligned in the
-// output and own >= 64 bytes past their expansion (out_cap = doc + 64, rounded to 16), so
-// whole 16-byte blocks are stored; sources have >= 64 bytes of slack behind them.
+// consecutive tiles of the launch; lane j assembles tile g0 + j: kGatherTile (32) output
+// bytes of one query, two 16-byte blocks.  Its first span comes from the tile index; spans
+// come in seven at a time (eight 8-byte entries: the eighth start ends the seventh span).
+// Every load of a batch is issued before any is used -- the pieces' source loads do not sit
+// behind one another's latency: the seven spans' first pieces (each up to its 16-byte block's
+// end) and the continuation of the span that crosses the block boundary.  Each piece is read
+// with one unaligned 16-byte load, shifted to its byte offset and merged into its block; the
+// tile leaves with two aligned 16-byte stores.  Queries are 16-byte aligned in the output
+// and own >= 64 bytes past their expansion (out_cap = doc + 64, rounded to 16), so whole
+// 16-byte blocks are stored; sources have >= 64 bytes of slack behind them; reads of entries
+// past a table's sentinel stay inside the table allocation (its tile index and 64-byte tail
+// follow) and are never used.
 PX_DEV u32x4 shl_bytes(u32x4 w, uint32_t b) {  // byte i of the result = byte i - b of w (0 below)
     const uint32_t ds = b >> 2, bs = b & 3u;
     uint32_t t[4];
@@ -2254,25 +2259,25 @@ PX_DEV uint32_t byte_mask(int lo, int hi) {  // bytes [lo, hi) of a dword (clamp
     const uint32_t m = hi - lo == 4 ? 0xffffffffu : ((1u << (8 * (hi - lo))) - 1u);
     return m << (8 * lo);
 }
-// output bytes [lo, hi) of 16-byte block r (0 <= lo < hi <= 16) from src (src = byte lo)
-PX_DEV void put_piece(u32x4 &r, uint32_t lo, uint32_t hi, const PX_GAS uint8_t *src) {
-    const u32x4 v = shl_bytes(ld16(src), lo);
-    r.x |= v.x & byte_mask((int)lo, (int)hi);
-    r.y |= v.y & byte_mask((int)lo - 4, (int)hi - 4);
-    r.z |= v.z & byte_mask((int)lo - 8, (int)hi - 8);
-    r.w |= v.w & byte_mask((int)lo - 12, (int)hi - 12);
+// v (output-aligned) masked to bytes [lo, hi) of a 16-byte block (empty when hi <= lo)
+PX_DEV u32x4 mask_piece(u32x4 v, int lo, int hi) {
+    return u32x4{v.x & byte_mask(lo, hi), v.y & byte_mask(lo - 4, hi - 4), v.z & byte_mask(lo - 8, hi - 8),
+                 v.w & byte_mask(lo - 12, hi - 12)};
 }
 
-// the first query of every 64-tile wave: the query holding tile 64 t
-__global__ void __launch_bounds__(256) k_gather_tasks(uint32_t nq, const GatherQuery *qs, uint32_t *task_q) {
+// the task table: per 64-tile task, its first query and the tiles (bits) where later queries
+// start.  The caller zeroes it.
+__global__ void __launch_bounds__(256) k_gather_tasks(uint32_t nq, const GatherQuery *qs, uint4 *task) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nq) return;
     const GatherQuery q = qs[i];
     const uint32_t nt = max(1u, (min(q.len, q.cap) + kGatherTile - 1) / kGatherTile);
-    for (uint32_t t = (q.tile0 + 63) & ~63u; t < q.tile0 + nt; t += 64) task_q[t >> 6] = i;
+    for (uint32_t t = (q.tile0 + 63) & ~63u; t < q.tile0 + nt; t += 64) task[t >> 6].x = i;
+    const uint32_t b = q.tile0 & 63u;
+    if (b) atomicOr(b < 32 ? &task[q.tile0 >> 6].z : &task[q.tile0 >> 6].w, 1u << (b & 31));
 }
 
-__global__ void __launch_bounds__(256) k_gather(uint32_t ntask, const uint32_t *task_q, const GatherQuery *qs, uint32_t nq,
+__global__ void __launch_bounds__(256) k_gather(uint32_t ntask, const uint4 *task, const GatherQuery *qs, uint32_t nq,
                                                 uint8_t *out_, uint32_t *out_len, uint32_t *status, uint32_t remap) {
     const uint32_t lane = lane_id();
     uint32_t lb = blockIdx.x;
@@ -2282,20 +2287,10 @@ __global__ void __launch_bounds__(256) k_gather(uint32_t ntask, const uint32_t *
     }
     const uint32_t ti = lb * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (ti >= ntask) return;
-    const uint32_t q0 = uni(task_q[ti]), g0 = ti * 64;
-    // which query each lane's tile belongs to: the queries starting inside the task set
-    // their bit (q0 holds tile g0)
-    const uint32_t t0n = q0 + 1 + lane < nq ? qs[q0 + 1 + lane].tile0 : 0xffffffffu;
-    uint64_t M = 0;
-    {
-        const uint64_t bit = t0n - g0 < 64u ? 1ull << (t0n - g0) : 0ull;
-        M = bit;
-        for (int o = 32; o > 0; o >>= 1) {
-            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)M, o), hi = (uint32_t)__shfl_xor((int)(uint32_t)(M >> 32), o);
-            M |= (uint64_t)hi << 32 | lo;
-        }
-    }
-    const uint32_t qi = q0 + (uint32_t)__popcll(M & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull)));
+    const uint4 td = task[ti];
+    const uint32_t g0 = ti * 64;
+    const uint64_t M = (uint64_t)uni(td.w) << 32 | uni(td.z);
+    const uint32_t qi = uni(td.x) + (uint32_t)__popcll(M & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull)));
     if (qi >= nq) return;
     const GatherQuery q = qs[qi];
     const uint32_t t = g0 + lane - q.tile0;
@@ -2305,43 +2300,62 @@ __global__ void __launch_bounds__(256) k_gather(uint32_t ntask, const uint32_t *
         status[q.slot] = q.len > q.cap ? (uint32_t)kErrSpace : (uint32_t)kOk;
     }
     if (a >= lim) return;
-    const uint32_t e = min(a + kGatherTile, lim);
+    const uint32_t e = min(a + kGatherTile, lim), B = a + 16;  // B: the second block's first byte
     const PX_GAS uint8_t *base = (const PX_GAS uint8_t *)q.base;
     const PX_GAS uint32_t *sp = (const PX_GAS uint32_t *)q.span;  // {rel, start} pairs, then the sentinel
     uint32_t k = ((const PX_GAS uint32_t *)q.tix)[t];
-    u32x4 r[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
-    // spans come in 8 entries (64 bytes, four independent loads) at a time: 7 spans and the
-    // start that ends the 7th (a tile holds ~7 spans on average: usually one round trip)
-    for (bool more = true; more;) {
+    u32x4 r0 = {0, 0, 0, 0}, r1 = {0, 0, 0, 0};
+    for (;;) {
         uint32_t en[16];
 #pragma unroll
         for (int v = 0; v < 4; ++v) *(u32x4 *)(en + 4 * v) = *(const PX_GAS u32x4_u *)(sp + 2 * k + 4 * v);
+        // span h covers output [st_h, st_{h+1}); alive while no earlier start reached e (the
+        // sentinel's start is the length: entries past it are never used).  Loads go out
+        // from 32-bit offsets off base (0: a dummy read of the record's first bytes).
+        uint32_t live = 0;  // bit h: span h has a piece in the tile (an unbroken run from bit 0)
+        bool alive = true;
+        int32_t off[7];
+        int32_t coff = 0;   // the span crossing into block 1: source of byte B
+        uint32_t cend = 0;  // its end in the tile (0: none)
 #pragma unroll
         for (int h = 0; h < 7; ++h) {
-            const int32_t rel = (int32_t)en[2 * h];
             const uint32_t st = en[2 * h + 1], nx = en[2 * h + 3];
-            if (st >= e) {  // (also at the sentinel: its start is the doc length)
-                more = false;
-                break;
-            }
             const uint32_t x0 = max(st, a), x1 = min(nx, e);
-            if (x0 < x1) {
-                const PX_GAS uint8_t *src = base + rel + (int32_t)(x0 - st);  // source of output byte x0
-                const uint32_t d0 = x0 - a, d1 = x1 - a;
-#pragma unroll
-                for (uint32_t b = 0; b < 4; ++b) {
-                    const uint32_t lo = max(d0, 16 * b), hi = min(d1, 16 * b + 16);
-                    if (lo < hi) put_piece(r[b], lo - 16 * b, hi - 16 * b, src + (lo - d0));
-                }
+            alive = alive && st < e;  // (then x0 < x1: span 0 holds byte a, later ones start past it)
+            const bool ok = alive;
+            off[h] = ok ? (int32_t)en[2 * h] + (int32_t)(x0 - st) : 0;
+            live |= ok ? 1u << h : 0u;
+            if (ok && x0 < B && x1 > B) {
+                coff = off[h] + (int32_t)(B - x0);
+                cend = x1;
             }
         }
-        if (en[15] >= e) break;  // span k + 7 starts past the tile (entries k .. k + 7 are real)
+        u32x4 v[7];
+#pragma unroll
+        for (int h = 0; h < 7; ++h) v[h] = ld16(base + off[h]);
+        const u32x4 vc = ld16(base + coff);
+#pragma unroll
+        for (int h = 0; h < 7; ++h) {
+            if (!((live >> h) & 1u)) continue;
+            const uint32_t st = en[2 * h + 1], nx = en[2 * h + 3];
+            const uint32_t d0 = max(st, a) - a, d1 = min(nx, e) - a;
+            const uint32_t blk = d0 >> 4, lo = d0 & 15u;
+            const uint32_t hi = min(d1, 16u * blk + 16u) - 16u * blk;
+            const u32x4 w = mask_piece(shl_bytes(v[h], lo), (int)lo, (int)hi);
+            if (blk == 0) {
+                r0 |= w;
+            } else {
+                r1 |= w;
+            }
+        }
+        if (cend) r1 |= mask_piece(vc, 0, (int)(cend - B));
+        // done once span k + 7 starts past the tile, or the sentinel came
+        if (live != 0x7fu || en[15] >= e) break;
         k += 7;
     }
     PX_GAS uint8_t *o = (PX_GAS uint8_t *)out_ + q.out_off + a;
-#pragma unroll
-    for (uint32_t b = 0; b < 4; ++b)
-        if (16 * b < e - a) *(PX_GAS u32x4 *)(o + 16 * b) = r[b];
+    *(PX_GAS u32x4 *)o = r0;
+    if (B < e) *(PX_GAS u32x4 *)(o + 16) = r1;
 }
 
 // ====================================================================== migrate
@@ -2482,11 +2496,14 @@ hipError_t launch_span_build(hipStream_t s, uint32_t n, const SpanJob *jobs) {
     return hipGetLastError();
 }
 
-hipError_t launch_gather(hipStream_t s, uint32_t ntask, uint32_t *task_q, const GatherQuery *qs, uint32_t nq,
+hipError_t launch_gather(hipStream_t s, uint32_t ntask, void *task_buf, const GatherQuery *qs, uint32_t nq,
                          uint8_t *out, uint32_t *out_len, uint32_t *status, bool remap) {
     if (!ntask) return hipSuccess;
-    k_gather_tasks<<<(nq + 255) / 256, 256, 0, s>>>(nq, qs, task_q);
-    k_gather<<<(ntask + 3) / 4, 256, 0, s>>>(ntask, task_q, qs, nq, out, out_len, status, remap ? 1u : 0u);
+    uint4 *task = (uint4 *)task_buf;  // ntask x 16 B
+    hipError_t e = hipMemsetAsync(task, 0, (size_t)ntask * 16, s);
+    if (e != hipSuccess) return e;
+    k_gather_tasks<<<(nq + 255) / 256, 256, 0, s>>>(nq, qs, task);
+    k_gather<<<(ntask + 3) / 4, 256, 0, s>>>(ntask, task, qs, nq, out, out_len, status, remap ? 1u : 0u);
     return hipGetLastError();
 }
 

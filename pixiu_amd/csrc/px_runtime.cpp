@@ -51,7 +51,7 @@ hipError_t launch_rehash(hipStream_t, const uint4 *, uint32_t, uint32_t, uint4 *
 hipError_t launch_decode_addr(hipStream_t, const DecodeQuery *, uint32_t, const RecSlot *const *, int32_t *,
                               uint32_t *, uint32_t *, Frame *, uint32_t, uint32_t);
 hipError_t launch_span_build(hipStream_t, uint32_t, const SpanJob *);
-hipError_t launch_gather(hipStream_t, uint32_t, uint32_t *, const GatherQuery *, uint32_t, uint8_t *, uint32_t *,
+hipError_t launch_gather(hipStream_t, uint32_t, void *, const GatherQuery *, uint32_t, uint8_t *, uint32_t *,
                          uint32_t *, bool);
 int debug_trace_take(int32_t *, uint32_t);
 int debug_prof_take(unsigned long long *, uint32_t);
@@ -736,11 +736,11 @@ struct px_ctx {
         const uint64_t qb = round_up(g.size() * sizeof(GatherQuery), 64);
         auto *hg = (GatherQuery *)hg_buf[which].get(g.size() * sizeof(GatherQuery));
         std::memcpy(hg, g.data(), g.size() * sizeof(GatherQuery));
-        dbuf = (GatherQuery *)heap.alloc(qb + (uint64_t)ntask * 4);
-        auto *task_q = (uint32_t *)((uint8_t *)dbuf + qb);
+        dbuf = (GatherQuery *)heap.alloc(qb + (uint64_t)ntask * 16);
+        void *task = (uint8_t *)dbuf + qb;  // per task: first query, query-start bits (16 B)
         hcheck(hipMemcpyAsync(dbuf, hg, g.size() * sizeof(GatherQuery), hipMemcpyHostToDevice, st));
-        hcheck(launch_gather(st, ntask, task_q, dbuf, (uint32_t)g.size(), out, dl, ds, true));
-        gather_bytes[dbuf] = qb + (uint64_t)ntask * 4;
+        hcheck(launch_gather(st, ntask, task, dbuf, (uint32_t)g.size(), out, dl, ds, true));
+        gather_bytes[dbuf] = qb + (uint64_t)ntask * 16;
     }
     std::map<void *, uint64_t> gather_bytes;  // launch_gathers' device buffers -> their sizes
     void release_gathers(GatherQuery *d) {
