@@ -1098,20 +1098,49 @@ __global__ void __launch_bounds__(256) k_pool_coarse(uint32_t N, const uint32_t 
 constexpr uint32_t kScanWin = 16384, kScanThreads = 1024;
 PSA_DEV void scan_stage(uint32_t *Pw, uint32_t *Cw, const uint32_t *P, uint32_t N, uint32_t wb, uint32_t t0,
                         uint32_t nt) {
-    for (uint32_t i = t0 * 4; i < kScanWin; i += nt * 4) {
-        uint4 v;
+    // every load of the window goes out before any LDS store (up to kStageRegs 16-byte
+    // loads per thread): one HBM round trip per window, not one per loop step
+    constexpr uint32_t kStageRegs = 5;  // (16,384 positions over >= 960 threads)
+    uint4 v[kStageRegs];
+#pragma unroll
+    for (uint32_t r = 0; r < kStageRegs; ++r) {
+        const uint32_t i = (t0 + r * nt) * 4;
+        if (i >= kScanWin) continue;
         if (wb + i + 4 <= N) {
-            v = *(const uint4 *)(P + wb + i);
+            v[r] = *(const uint4 *)(P + wb + i);
         } else {  // (0xffffffff past N: "exceeds")
-            v.x = wb + i < N ? P[wb + i] : 0xffffffffu;
-            v.y = wb + i + 1 < N ? P[wb + i + 1] : 0xffffffffu;
-            v.z = wb + i + 2 < N ? P[wb + i + 2] : 0xffffffffu;
-            v.w = wb + i + 3 < N ? P[wb + i + 3] : 0xffffffffu;
+            v[r].x = wb + i < N ? P[wb + i] : 0xffffffffu;
+            v[r].y = wb + i + 1 < N ? P[wb + i + 1] : 0xffffffffu;
+            v[r].z = wb + i + 2 < N ? P[wb + i + 2] : 0xffffffffu;
+            v[r].w = wb + i + 3 < N ? P[wb + i + 3] : 0xffffffffu;
         }
-        *(uint4 *)(Pw + i) = v;
-        if ((i & 63) == 60) Cw[i >> 6] = v.w;  // the 64-position group's last value
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kStageRegs; ++r) {
+        const uint32_t i = (t0 + r * nt) * 4;
+        if (i >= kScanWin) continue;
+        *(uint4 *)(Pw + i) = v[r];
+        if ((i & 63) == 60) Cw[i >> 6] = v[r].w;  // the 64-position group's last value
     }
 }
+// first i in [lo, hi) with key(i) > t (key non-decreasing), hi if none: one wave, 64-ary
+// narrowing (one dependent load per 64x), every lane calls it
+template <class Key>
+PSA_DEV uint32_t wave_first_gt(uint32_t lo, uint32_t hi, uint32_t t, Key key) {
+    const uint32_t lane = lane_id();
+    while (hi - lo > 64) {
+        const uint32_t step = (hi - lo + 63) / 64;
+        const uint32_t last = min(lo + (lane + 1) * step, hi) - 1;
+        const uint64_t m = __ballot(lo + lane * step < hi && key(last) > t);
+        if (!m) return hi;
+        const uint32_t L = lobit(m);
+        hi = min(lo + (L + 1) * step, hi);
+        lo = lo + L * step;
+    }
+    const uint64_t m = __ballot(lo + lane < hi && key(lo + lane) > t);
+    return m ? lo + lobit(m) : hi;
+}
+
 __global__ void __launch_bounds__(kScanThreads) k_pool_scan(uint32_t nshards, const PsaShard *shards, const PsaDoc *docs,
                                                             const uint32_t *P, const uint32_t *C, uint32_t N,
                                                             PsaPoolOut *out) {
@@ -1136,6 +1165,44 @@ __global__ void __launch_bounds__(kScanThreads) k_pool_scan(uint32_t nshards, co
     uint32_t cw = kNone, cv = 0;  // coarse window: blocks [cw, cw + 64)
     uint32_t k_last = kNone;
     auto more = [&]() { return pools < kRotatePools && (uint32_t)used + (send - base) > (uint32_t)kPoolBlocks; };
+    // The bound test.  A pool closes when the next charge (<= 5 blocks) does
+    // not fit, so pools 1 .. 2,047 each close holding kPoolBlocks - 4 .. kPoolBlocks blocks, and
+    // the charge that opens pool 2,048 starts at a running count in [2047 (kPoolBlocks - 4),
+    // 2047 kPoolBlocks].  The leaf holding it lies between the first leaf whose running count
+    // (root included) passes the low end and the first that passes the high end: if those are
+    // in one doc, the chunk rotates before the next doc; if none passes the low end, it does
+    // not rotate.  Only the other cases need the boundary chain below.
+    if (wave == 0) {
+        constexpr uint32_t kLo = (uint32_t)(kRotatePools - 1) * (uint32_t)(kPoolBlocks - 4);
+        constexpr uint32_t kHi = (uint32_t)(kRotatePools - 1) * (uint32_t)kPoolBlocks;
+        // running count through x = kNodeBlocks + (P[x] - base) (P is a modular prefix sum: its
+        // differences inside the shard are exact and non-decreasing)
+        auto Pk = [&](uint32_t x) { return P[x] - base; };
+        const uint32_t klo = wave_first_gt(start, endp, kLo - (uint32_t)kNodeBlocks, Pk);
+        uint32_t verdict = 0;  // 0: chain needed, 1: no rotation, 2: rotation before doc rd
+        uint32_t rd = kNone;
+        if (klo == endp) {
+            verdict = 1;
+        } else {
+            const uint32_t khi = wave_first_gt(klo, endp, kHi - (uint32_t)kNodeBlocks, Pk);
+            if (khi != endp) {
+                auto Dk = [&](uint32_t g) { return docs[g].start; };
+                const uint32_t d0 = sh.doc0, d1 = sh.doc0 + sh.ndocs;
+                const uint32_t glo = wave_first_gt(d0, d1, klo, Dk) - 1, ghi = wave_first_gt(d0, d1, khi, Dk) - 1;
+                if (glo == ghi) {
+                    verdict = 2;
+                    rd = glo + 1;
+                }
+            }
+        }
+        if (lane == 0) {
+            sh_go = verdict;
+            if (verdict) out[s] = PsaPoolOut{verdict == 2 ? rd : kNone, verdict == 2 ? kRotatePools : 0, 0, 0};
+        }
+    }
+    __syncthreads();
+    if (sh_go) return;  // (uniform: the whole block leaves)
+    __syncthreads();
     // the window holding the next boundary (wave 0): from the coarse values
     auto locate = [&]() {
         const uint32_t cap = (uint32_t)(kPoolBlocks - used);
