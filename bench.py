@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group for N > 1 (nccl = RCCL over xGMI; gloo: CPU transport, for tests)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r02.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r03.json"),
                     help="per-kernel PMC summary (tools/pmc_summary.py); used only if its workload matches")
     return ap.parse_args()
 
@@ -535,7 +535,7 @@ def summarize(cfg, r, rps, world, a, pmc_path):
                     for k, v in pmc.items():
                         # (tools/pmc_summary.py names rocPRIM's sort / scan kernels by their
                         # k_id_wrapper / k_scan_determinism template pieces)
-                        if isinstance(v, dict) and (k.startswith(("k_psa", "k_seg", "k_cmp", "k_pool")) or "rocprim" in k
+                        if isinstance(v, dict) and (k.startswith(("k_psa", "k_seg", "k_cmp", "k_pool", "k_dbl", "k_big", "k_stat")) or "rocprim" in k
                                                     or k in ("k_gst_encode", "k_id_wrapper", "k_scan_determinism")):
                             tot_b += v["hbm_bytes_per_launch"] * v["dispatches"]
                     traffic = tot_b or None
