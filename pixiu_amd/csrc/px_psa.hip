@@ -617,20 +617,33 @@ __global__ void __launch_bounds__(256) k_dbl_blk(const uint64_t *list, const uin
 // big groups (host-driven steps): gather every member with key (group << 32 | key), radix
 // sort (stable: ties keep suffix-array order), place back, heads by a max-scan, then ranks
 // and subgroups.  boff = exclusive prefix of the groups' sizes (host-computed).
-__global__ void __launch_bounds__(256) k_big_gather(uint32_t nb, const uint64_t *list, const uint32_t *boff,
+// flat over the T gathered members: a block's 256 members span at most two groups (every
+// big group has > 4,096 members), found by one search of boff per block
+__global__ void __launch_bounds__(256) k_big_gather(uint32_t T, uint32_t nb, const uint64_t *list, const uint32_t *boff,
                                                     const uint32_t *sa, const uint16_t *sd, const uint32_t *key,
                                                     uint64_t *ck, uint32_t *cv, uint32_t *gp, uint16_t *gd, StepStat ss) {
-    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
-        const uint64_t ent = list[b];
-        const uint32_t start = (uint32_t)ent, size = (uint32_t)(ent >> 32), o = boff[b];
-        for (uint32_t i = threadIdx.x; i < size; i += blockDim.x) {
-            ck[o + i] = (uint64_t)b << 32 | key[start + i];
-            cv[o + i] = o + i;
-            gp[o + i] = sa[start + i];
-            gd[o + i] = sd[start + i];
+    __shared__ uint32_t sb;
+    const uint32_t k0 = blockIdx.x * blockDim.x, k = k0 + threadIdx.x;
+    if (threadIdx.x == 0) {  // the group holding k0: last b with boff[b] <= k0
+        uint32_t lo = 0, hi = nb;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (boff[mid] <= k0) lo = mid;
+            else hi = mid;
         }
-        if (threadIdx.x == 0) stat_put(ss, b, size, 0, 0);
+        sb = lo;
     }
+    __syncthreads();
+    if (k >= T) return;
+    uint32_t b = sb;
+    if (b + 1 < nb && boff[b + 1] <= k) ++b;
+    const uint64_t ent = list[b];
+    const uint32_t start = (uint32_t)ent, o = boff[b], i = k - o;
+    ck[k] = (uint64_t)b << 32 | key[start + i];
+    cv[k] = k;
+    gp[k] = sa[start + i];
+    gd[k] = sd[start + i];
+    if (i == 0) stat_put(ss, b, (uint32_t)(ent >> 32), 0, 0);
 }
 __global__ void __launch_bounds__(256) k_big_head(uint32_t T, const uint32_t *boff, const uint64_t *ck2, uint32_t *hf) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -829,6 +842,44 @@ PSA_DEV uint32_t lce(const uint64_t *G8, uint32_t p, uint32_t q, uint32_t k, uin
     return lim;
 }
 
+// The lcp values at every span's first position, where k_psa_lce would start from zero: a
+// span that begins inside a long repeat (the 8 KB templates) would otherwise compare it 8
+// bytes per step alone.  Here 8 lanes share a comparison, 64 bytes per step; a wave runs
+// 8 comparisons (4 span starts, each with both neighbours).  seed[2 t] / seed[2 t + 1] =
+// lcp with the previous / next smaller neighbour of span t's first position.
+__global__ void __launch_bounds__(256) k_psa_lce_seed(uint32_t N, uint32_t nspan, const uint64_t *G8,
+                                                      const uint16_t *dist, const uint32_t *psvp,
+                                                      const uint32_t *nsvp, uint32_t span, uint16_t *seed) {
+    const uint32_t lane = lane_id(), grp = lane >> 3, sub = lane & 7u;
+    const uint32_t c = (blockIdx.x * blockDim.x + threadIdx.x) >> 3;  // comparison index
+    const uint32_t t = c >> 1;
+    bool live = t < nspan;
+    uint32_t p = 0, q = kNoPos, lim = 0;
+    if (live) {
+        p = t * span;
+        q = (c & 1u) ? nsvp[p] : psvp[p];
+        if (q != kNoPos) lim = min((uint32_t)dist[p], (uint32_t)dist[q]);
+    }
+    uint32_t res = lim;  // (kNoPos: 0)
+    bool done = !live || q == kNoPos;
+    for (uint32_t k = 0;; k += 64) {
+        done = done || k >= lim;
+        if (!__ballot(!done)) break;
+        const uint32_t off = k + 8 * sub;
+        uint64_t x = 0;
+        if (!done && off < lim) x = ld8(G8, p + off) ^ ld8(G8, q + off);
+        const uint64_t m = __ballot(x != 0);
+        const uint32_t gm = (uint32_t)(m >> (8 * grp)) & 0xffu;
+        if (!done && gm) {
+            const uint32_t first = (uint32_t)__ffs(gm) - 1u;  // the group's first mismatching lane
+            const uint64_t xf = shfl64(x, grp * 8 + first);
+            res = min(lim, k + 8 * first + (uint32_t)(__builtin_ctzll(xf) >> 3));
+            done = true;
+        }
+    }
+    if (live && sub == 0) seed[c] = (uint16_t)(q == kNoPos ? 0u : res);
+}
+
 // One thread per `span` consecutive positions.  The per-position arrays are read and
 // written 8 positions at a time with 16-byte accesses: a wave's 64 threads sit 256
 // positions apart, so per-position 2- and 4-byte accesses would each touch a different
@@ -836,10 +887,11 @@ PSA_DEV uint32_t lce(const uint64_t *G8, uint32_t p, uint32_t q, uint32_t k, uin
 // thread's consecutive positions).
 __global__ void __launch_bounds__(256) k_psa_lce(uint32_t N, const uint64_t *G8, const uint16_t *dist,
                                                  const uint32_t *psvp, const uint32_t *nsvp, uint16_t *lcp_p,
-                                                 uint16_t *lcp_n, uint32_t span) {
+                                                 uint16_t *lcp_n, uint32_t span, const uint16_t *seed) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t p0 = t * span;
     if (p0 >= N) return;
+    const uint32_t seed_p = seed[2 * t], seed_n = seed[2 * t + 1];
     const uint32_t p1 = min(N, p0 + span);
     uint32_t kp = 0, kn = 0, qprev = kNoPos - 1, sprev = kNoPos - 1;
     for (uint32_t b = p0; b < p1; b += 8) {
@@ -870,13 +922,17 @@ __global__ void __launch_bounds__(256) k_psa_lce(uint32_t N, const uint64_t *G8,
             const bool shn = sn != kNoPos && sn == sprev + 1 && kn >= 2;
             kp = kp ? kp - 1 : 0;
             kn = kn ? kn - 1 : 0;
-            if (q == kNoPos) {
+            if (p == p0) {  // (k_psa_lce_seed)
+                kp = seed_p;
+                kn = seed_n;
+            } else if (q == kNoPos) {
                 kp = 0;
             } else if (!shp) {
                 const uint32_t lim = min(dp, (uint32_t)dist[q]);
                 kp = lce(G8, p, q, min(kp, lim), lim);
             }
-            if (sn == kNoPos) {
+            if (p == p0) {
+            } else if (sn == kNoPos) {
                 kn = 0;
             } else if (!shn) {
                 const uint32_t lim = min(dp, (uint32_t)dist[sn]);
@@ -1519,8 +1575,7 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
                 auto *gp = S.get<uint32_t>(T * 4), *hf = S.get<uint32_t>(T * 4), *hk = S.get<uint32_t>(T * 4);
                 auto *nf = S.get<uint32_t>(T * 4), *nk = S.get<uint32_t>(T * 4);
                 auto *gd = S.get<uint16_t>(T * 2 + 64);
-                k_big_gather<<<std::min<uint32_t>(nbig, 65535u), 256, 0, s>>>(nbig, LL.lst[4], d_boff, sa, sd, key, ck, cv,
-                                                                               gp, gd, ss);
+                k_big_gather<<<blocks(T), tb, 0, s>>>((uint32_t)T, nbig, LL.lst[4], d_boff, sa, sd, key, ck, cv, gp, gd, ss);
                 int bbits = 1;
                 while ((1ull << bbits) < nbig) ++bbits;
                 size_t t1 = 0, t2 = 0, t3 = 0;
@@ -1621,7 +1676,14 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     auto *lcp_p = (uint16_t *)rank;  // ranks are no longer needed: two u16 arrays in their place
     auto *lcp_n = S.get<uint16_t>(n64 * 2);
     const uint32_t lsp = lce_span(n64);
-    k_psa_lce<<<blocks((n64 + lsp - 1) / lsp), tb, 0, s>>>(N, (const uint64_t *)G, dist, psvp, nsvp, lcp_p, lcp_n, lsp);
+    {
+        const uint32_t nspan = (uint32_t)((n64 + lsp - 1) / lsp);
+        auto *seed = S.get<uint16_t>((uint64_t)nspan * 4 + 64);
+        k_psa_lce_seed<<<(uint32_t)(((uint64_t)nspan * 16 + 255) / 256), 256, 0, s>>>(N, nspan, (const uint64_t *)G, dist,
+                                                                                       psvp, nsvp, lsp, seed);
+        k_psa_lce<<<blocks(nspan), tb, 0, s>>>(N, (const uint64_t *)G, dist, psvp, nsvp, lcp_p, lcp_n, lsp, seed);
+        S.put(seed);
+    }
     PSA_CHECK(hipEventRecord(e2, s));
     // ---- messages
     k_psa_msg0<<<blocks(N), tb, 0, s>>>(N, pdoc, docs, lcp_p, lcp_n);
