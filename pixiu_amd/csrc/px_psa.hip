@@ -57,15 +57,20 @@ constexpr uint32_t kPass = 0xffffffffu;
 PSA_DEV uint32_t lane_id() { return threadIdx.x & 63u; }
 
 // ---------------------------------------------------------------- text
-// G = the text, pdoc = doc id and dist = bytes to the doc's end, per position
-__global__ void __launch_bounds__(256) k_psa_gather(uint32_t ndocs, const PsaDoc *docs, uint8_t *G, uint32_t *pdoc,
-                                                    uint16_t *dist) {
+// G = the text, pdoc = doc id and dist = bytes to the doc's end, per position.  One wave per
+// slice of a doc (`slices` per doc, so that a window of a few long docs -- a single-instance
+// round holds ~210 -- still spreads over the chip)
+__global__ void __launch_bounds__(256) k_psa_gather(uint32_t ndocs, const PsaDoc *docs, uint32_t slices, uint8_t *G,
+                                                    uint32_t *pdoc, uint16_t *dist) {
     const uint32_t lane = lane_id();
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);
-    for (uint32_t g = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); g < ndocs; g += waves) {
+    const uint64_t nw = (uint64_t)ndocs * slices;
+    for (uint64_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); w < nw; w += waves) {
+        const uint32_t g = (uint32_t)(w / slices), sl = (uint32_t)(w % slices);
         const PsaDoc d = docs[g];
+        const uint32_t lo = (uint32_t)((uint64_t)d.len * sl / slices), hi = (uint32_t)((uint64_t)d.len * (sl + 1) / slices);
         const PX_GAS uint8_t *src = (const PX_GAS uint8_t *)d.src;
-        for (uint32_t o = lane; o < d.len; o += 64) {
+        for (uint32_t o = lo + lane; o < hi; o += 64) {
             G[d.start + o] = src[o];
             pdoc[d.start + o] = g;
             dist[d.start + o] = (uint16_t)(d.len - o);  // 1..65,535
@@ -1054,7 +1059,7 @@ __global__ void __launch_bounds__(256) k_pool_pack(uint32_t N, const uint32_t *p
     rec[p] = LinkRec{psvp[p], nsvp[p], lp[p], ln[p], dist[p], 0};
 }
 __global__ void __launch_bounds__(256) k_pool_leaf(uint32_t N, const uint8_t *G, const PsaShard *shards, uint32_t nshards,
-                                                   const LinkRec *R, uint8_t *code, uint32_t *E, uint32_t *ncand) {
+                                                   const LinkRec *R, uint8_t *code, uint32_t *E, StepStat cs) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t c = 0;
     if (p < N) {
@@ -1071,14 +1076,25 @@ __global__ void __launch_bounds__(256) k_pool_leaf(uint32_t N, const uint8_t *G,
                     if (q != kNoPos) {
                         // climb to E = the earliest occurrence of T[q .. q+l), keeping q's record
                         LinkRec rq = R[q], r = rq;
-                        uint32_t e = q;
+                        uint32_t e = q, steps = 0, hop = 0;
                         for (;;) {
-                            if (r.lp >= l) e = r.psv;
-                            else if (r.ln >= l) e = r.nsv;
-                            else break;
+                            if (r.lp >= l) {
+                                hop = r.lp;
+                                e = r.psv;
+                            } else if (r.ln >= l) {
+                                hop = r.ln;
+                                e = r.nsv;
+                            } else {
+                                break;
+                            }
+                            ++steps;
                             r = R[e];
                         }
-                        if (r.dist > l && rq.dist > l && G[q + l] == G[e + l]) {
+                        // T[q + l] == T[e + l]: trivially when q is E; after one hop its lcp is
+                        // lcp(q, E) itself (both suffixes go on past l: bytes equal iff > l);
+                        // after more hops the text decides
+                        const bool same = steps == 0 ? true : steps == 1 ? hop > l : G[q + l] == G[e + l];
+                        if (r.dist > l && rq.dist > l && same) {
                             c = 2;
                             E[p] = e;
                         }
@@ -1088,8 +1104,9 @@ __global__ void __launch_bounds__(256) k_pool_leaf(uint32_t N, const uint8_t *G,
         }
         code[p] = (uint8_t)c;
     }
-    const uint64_t m = __ballot(c == 2);
-    if (lane_id() == 0 && m) atomicAdd(ncand, (uint32_t)__popcll(m));
+    // the candidate count: one sharded atomic per workgroup (a single counter taking one
+    // atomic per wave serialised the launch)
+    block_stat(cs, c == 2 ? 1u : 0u, 0, 0);
 }
 
 struct PoolSlot {
@@ -1484,7 +1501,11 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     int shard_bits = 1;
     while ((1u << shard_bits) < nshards) ++shard_bits;
     const uint32_t syms = std::min<uint32_t>(6, (64 - shard_bits) / 9);  // 5 or 6 symbols
-    k_psa_gather<<<std::min<uint32_t>((ndocs + 3) / 4, 65535u), 256, 0, s>>>(ndocs, docs, G, pdoc, dist);
+    {
+        const uint32_t slices = std::max<uint32_t>(1, std::min<uint32_t>(64, 16384 / ndocs));
+        const uint64_t nw = (uint64_t)ndocs * slices;
+        k_psa_gather<<<(uint32_t)std::min<uint64_t>((nw + 3) / 4, 65535u), 256, 0, s>>>(ndocs, docs, slices, G, pdoc, dist);
+    }
     auto *keys = S.get<uint64_t>(n64 * 8);
     auto *keys2 = S.get<uint64_t>(n64 * 8);
     auto *vals = S.get<uint32_t>(n64 * 4);
@@ -1696,21 +1717,23 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         {
             auto *rec = S.get<LinkRec>(n64 * sizeof(LinkRec));
             k_pool_pack<<<blocks(N), tb, 0, s>>>(N, psvp, nsvp, lcp_p, lcp_n, dist, rec);
-            k_pool_leaf<<<blocks(N), tb, 0, s>>>(N, G, shards, nshards, rec, code, E, ncand);
+            auto *csh = S.get<uint32_t>(kStatShards * kStatStride * 4);
+            PSA_CHECK(hipMemsetAsync(csh, 0, kStatShards * kStatStride * 4, s));
+            k_pool_leaf<<<blocks(N), tb, 0, s>>>(N, G, shards, nshards, rec, code, E, StepStat{csh});
+            k_stat_sum<<<1, 64, 0, s>>>(csh, ncand, cnt + kCntCand + 1, cnt + kCntCand + 2);
             S.put(rec);
         }
         // the candidate table: 2x the candidates, read back for big windows; a small window
         // (one chunk, the single instance's rounds) sizes it from N and skips the round trip
+        // (sized from the candidate count: one read-back, against a table twice the window
+        // that costs a 2x larger clear and spreads the inserts over twice the lines)
         uint32_t nc = 0;
         uint64_t cap = 1024;
-        const bool small_n = N <= (1u << 26);
-        if (!small_n || verbose) {
-            PSA_CHECK(hipMemcpyAsync(pin, ncand, 4, hipMemcpyDeviceToHost, s));
-            PSA_CHECK(hipStreamSynchronize(s));
-            nc = pin[0];
-            if (verbose) fprintf(stderr, "psa pools: %u split candidates\n", nc);
-        }
-        while (cap < 2ull * (small_n ? N : nc)) cap <<= 1;
+        PSA_CHECK(hipMemcpyAsync(pin, ncand, 4, hipMemcpyDeviceToHost, s));
+        PSA_CHECK(hipStreamSynchronize(s));
+        nc = pin[0];
+        if (verbose) fprintf(stderr, "psa pools: %u split candidates\n", nc);
+        while (cap < 2ull * nc) cap <<= 1;
         auto *tab = S.get<PoolSlot>(cap * sizeof(PoolSlot));
         PSA_CHECK(hipMemsetAsync(tab, 0xff, cap * sizeof(PoolSlot), s));
         const uint32_t mask = (uint32_t)(cap - 1);

@@ -1662,8 +1662,10 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
                 u.live_bytes += took;
                 u.next += take;
                 if (rot) {
-                    // the window for the next chunk: a little more than this one held
-                    u.window = std::max<uint64_t>(kPsaMaxText, u.live_bytes + u.live_bytes / 12);
+                    // the window for the next chunk: a little more than this one held (chunks of
+                    // one corpus hold nearly the same bytes: config 3's 51 full chunks are
+                    // 194-196 docs; a window that misses costs one more round for that chunk)
+                    u.window = std::max<uint64_t>(kPsaMaxText, u.live_bytes + u.live_bytes / 40);
                     ++u.seq;
                     ++psa_rotations;
                     u.live.clear();
