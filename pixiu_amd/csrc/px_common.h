@@ -238,6 +238,13 @@ struct GatherQuery {
     uint32_t pad;
 };
 
+// gather task (64 tiles): the first query, the span holding the task's first tile in its
+// table, and a bit per tile where a later query starts
+struct alignas(16) GatherTask {
+    uint32_t q0, k0;
+    unsigned long long M;
+};
+
 // decode frame (scratch, one stack per wave)
 struct alignas(16) Frame {
     uint32_t rec;     // chunk-local idx of the record being parsed ("self")

@@ -2265,34 +2265,82 @@ PX_DEV u32x4 mask_piece(u32x4 v, int lo, int hi) {
                  v.w & byte_mask(lo - 12, hi - 12)};
 }
 
-// the task table: per 64-tile task, its first query and the tiles (bits) where later queries
-// start.  The caller zeroes it.
-__global__ void __launch_bounds__(256) k_gather_tasks(uint32_t nq, const GatherQuery *qs, uint4 *task) {
+// the task table: per 64-tile task, its first query, the span holding the task's first tile
+// in that query's table, and the tiles (bits) where later queries start.  The caller zeroes it.
+__global__ void __launch_bounds__(256) k_gather_tasks(uint32_t nq, const GatherQuery *qs, GatherTask *task) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nq) return;
     const GatherQuery q = qs[i];
     const uint32_t nt = max(1u, (min(q.len, q.cap) + kGatherTile - 1) / kGatherTile);
-    for (uint32_t t = (q.tile0 + 63) & ~63u; t < q.tile0 + nt; t += 64) task[t >> 6].x = i;
+    const uint32_t ntix = (q.len + kGatherTile - 1) / kGatherTile;  // (the tile index's length)
+    for (uint32_t t = (q.tile0 + 63) & ~63u; t < q.tile0 + nt; t += 64) {
+        GatherTask &d = task[t >> 6];
+        d.q0 = i;
+        d.k0 = t - q.tile0 < ntix ? q.tix[t - q.tile0] : 0u;
+    }
     const uint32_t b = q.tile0 & 63u;
-    if (b) atomicOr(b < 32 ? &task[q.tile0 >> 6].z : &task[q.tile0 >> 6].w, 1u << (b & 31));
+    if (b) atomicOr(&task[q.tile0 >> 6].M, 1ull << b);
 }
 
-__global__ void __launch_bounds__(256) k_gather(uint32_t ntask, const uint4 *task, const GatherQuery *qs, uint32_t nq,
+// Gather (see the comment above shl_bytes): one wave per task of 64 tiles.  The TA (the
+// per-CU address unit) bounds this kernel -- every lane of a scattered 16-byte load is an
+// address of its own (rocprofv3: TA_BUSY ~70 % of the launch, r03w) -- so the wave keeps
+// vector loads to the ones that carry bytes: its first query comes in by scalar loads
+// (every lane of a wave that lies in one query), the span entries of that query from the
+// task's first tile on are staged in LDS by two coalesced loads per lane and each lane finds
+// its own span there, and a source load is issued only by the lanes whose span has a piece.
+constexpr uint32_t kGatherStage = 256;
+__global__ void __launch_bounds__(256) k_gather(uint32_t ntask, const GatherTask *task, const GatherQuery *qs, uint32_t nq,
                                                 uint8_t *out_, uint32_t *out_len, uint32_t *status, uint32_t remap) {
+    __shared__ uint2 stage_all[4][kGatherStage];
+    __shared__ u32x4 tile_all[4][64 * 3];  // per lane: its 32-byte tile and a 16-byte pad
     const uint32_t lane = lane_id();
     uint32_t lb = blockIdx.x;
     if (remap) {  // XCD-aware order, as k_decode
         const uint32_t nb = gridDim.x, x = blockIdx.x & 7u, per = nb >> 3, rem = nb & 7u;
         lb = x * per + min(x, rem) + (blockIdx.x >> 3);
     }
-    const uint32_t ti = lb * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint32_t ti = uni(lb * (blockDim.x >> 6) + (threadIdx.x >> 6));
     if (ti >= ntask) return;
-    const uint4 td = task[ti];
-    const uint32_t g0 = ti * 64;
-    const uint64_t M = (uint64_t)uni(td.w) << 32 | uni(td.z);
-    const uint32_t qi = uni(td.x) + (uint32_t)__popcll(M & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull)));
+    uint2 *stage = stage_all[threadIdx.x >> 6];
+    const uint32_t g0 = ti * 64, q0 = uni(task[ti].q0), k0 = uni(task[ti].k0);
+    const uint64_t M = ((uint64_t)uni((uint32_t)(task[ti].M >> 32)) << 32) | uni((uint32_t)task[ti].M);
+    const uint32_t qi = q0 + (uint32_t)__popcll(M & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull)));
+    // the first query, by scalar loads (uniform address)
+    const GatherQuery &Q0 = qs[q0];
+    const PX_GAS uint2 *sp0 = (const PX_GAS uint2 *)Q0.span;
+    const uint32_t nent0 = uni(Q0.nspan) + 1u;  // (the sentinel included)
+    const uint32_t nst = min(kGatherStage, nent0 > k0 ? nent0 - k0 : 0u);
+    // its entries [k0, k0 + nst): coalesced, two entries per lane per load
+    {
+        u32x4 sv[kGatherStage / 128];
+#pragma unroll
+        for (uint32_t r = 0; r < kGatherStage / 128; ++r) {  // (both loads out before either is stored)
+            const uint32_t j = r * 128 + 2 * lane;
+            if (j + 1 < nst) {
+                sv[r] = *(const PX_GAS u32x4_u *)(sp0 + k0 + j);
+            } else if (j < nst) {
+                sv[r] = u32x4{sp0[k0 + j].x, sp0[k0 + j].y, 0u, 0u};
+            }
+        }
+#pragma unroll
+        for (uint32_t r = 0; r < kGatherStage / 128; ++r) {
+            const uint32_t j = r * 128 + 2 * lane;
+            if (j < nst) stage[j] = uint2{sv[r].x, sv[r].y};
+            if (j + 1 < nst) stage[j + 1] = uint2{sv[r].z, sv[r].w};
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (qi >= nq) return;
-    const GatherQuery q = qs[qi];
+    const bool fast = qi == q0;
+    GatherQuery q;
+    if (M == 0) {  // (uniform) every lane in the first query
+        q = Q0;
+    } else {
+        q = qs[qi];
+    }
     const uint32_t t = g0 + lane - q.tile0;
     const uint32_t lim = min(q.len, q.cap), a = t * kGatherTile;
     if (t == 0) {
@@ -2303,55 +2351,80 @@ __global__ void __launch_bounds__(256) k_gather(uint32_t ntask, const uint4 *tas
     const uint32_t e = min(a + kGatherTile, lim), B = a + 16;  // B: the second block's first byte
     const PX_GAS uint8_t *base = (const PX_GAS uint8_t *)q.base;
     const PX_GAS uint32_t *sp = (const PX_GAS uint32_t *)q.span;  // {rel, start} pairs, then the sentinel
-    uint32_t k = ((const PX_GAS uint32_t *)q.tix)[t];
-    u32x4 r0 = {0, 0, 0, 0}, r1 = {0, 0, 0, 0};
+    // the span holding byte a: the last staged entry starting at or before a (the staged
+    // range starts with the span holding the task's first tile); the tile index otherwise
+    uint32_t k;
+    if (fast && nst && stage[nst - 1].y > a) {
+        uint32_t lo = 0, hi = nst - 1;  // stage[lo].y <= a < stage[hi].y
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (stage[mid].y <= a) lo = mid;
+            else hi = mid;
+        }
+        k = k0 + lo;
+    } else {
+        k = ((const PX_GAS uint32_t *)q.tix)[t];
+    }
+    // the tile is assembled in LDS: each span piece is written whole (16 unaligned bytes from
+    // its first source byte, at its output offset), in output order, so the bytes a write puts
+    // past its piece are overwritten by the pieces after it (the last one's land in the pad)
+    uint8_t *tl = (uint8_t *)&tile_all[threadIdx.x >> 6][lane * 3];
     for (;;) {
         uint32_t en[16];
+        if (fast && k - k0 + 8 <= nst) {  // (staged)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) *(u32x4 *)(en + 4 * v) = *(const PX_GAS u32x4_u *)(sp + 2 * k + 4 * v);
+            for (int v = 0; v < 8; ++v) {
+                const uint2 x = stage[k - k0 + v];
+                en[2 * v] = x.x;
+                en[2 * v + 1] = x.y;
+            }
+        } else {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) *(u32x4 *)(en + 4 * v) = *(const PX_GAS u32x4_u *)(sp + 2 * k + 4 * v);
+        }
         // span h covers output [st_h, st_{h+1}); alive while no earlier start reached e (the
-        // sentinel's start is the length: entries past it are never used).  Loads go out
-        // from 32-bit offsets off base (0: a dummy read of the record's first bytes).
+        // sentinel's start is the length: entries past it are never used).  A piece is at most
+        // 32 bytes, and at most one piece of a 32-byte tile is longer than 16 (its second half
+        // is one more load).
         uint32_t live = 0;  // bit h: span h has a piece in the tile (an unbroken run from bit 0)
         bool alive = true;
         int32_t off[7];
-        int32_t coff = 0;   // the span crossing into block 1: source of byte B
-        uint32_t cend = 0;  // its end in the tile (0: none)
+        uint32_t d0[7];
+        uint32_t lh = 7;  // the piece longer than 16 bytes (7: none)
 #pragma unroll
         for (int h = 0; h < 7; ++h) {
             const uint32_t st = en[2 * h + 1], nx = en[2 * h + 3];
             const uint32_t x0 = max(st, a), x1 = min(nx, e);
             alive = alive && st < e;  // (then x0 < x1: span 0 holds byte a, later ones start past it)
-            const bool ok = alive;
-            off[h] = ok ? (int32_t)en[2 * h] + (int32_t)(x0 - st) : 0;
-            live |= ok ? 1u << h : 0u;
-            if (ok && x0 < B && x1 > B) {
-                coff = off[h] + (int32_t)(B - x0);
-                cend = x1;
-            }
+            off[h] = alive ? (int32_t)en[2 * h] + (int32_t)(x0 - st) : 0;
+            d0[h] = x0 - a;
+            live |= alive ? 1u << h : 0u;
+            if (alive && x1 - x0 > 16) lh = h;
         }
+        // every load of the batch goes out before any is used, each from the lanes that need it
         u32x4 v[7];
+        u32x4 vl = {0, 0, 0, 0};
 #pragma unroll
-        for (int h = 0; h < 7; ++h) v[h] = ld16(base + off[h]);
-        const u32x4 vc = ld16(base + coff);
+        for (int h = 0; h < 7; ++h) {
+            v[h] = u32x4{0, 0, 0, 0};
+            if ((live >> h) & 1u) v[h] = ld16(base + off[h]);
+        }
+        const int32_t loff = lh < 7 ? off[lh < 7 ? lh : 0] + 16 : 0;
+        if (lh < 7) vl = ld16(base + loff);
 #pragma unroll
         for (int h = 0; h < 7; ++h) {
             if (!((live >> h) & 1u)) continue;
-            const uint32_t st = en[2 * h + 1], nx = en[2 * h + 3];
-            const uint32_t d0 = max(st, a) - a, d1 = min(nx, e) - a;
-            const uint32_t blk = d0 >> 4, lo = d0 & 15u;
-            const uint32_t hi = min(d1, 16u * blk + 16u) - 16u * blk;
-            const u32x4 w = mask_piece(shl_bytes(v[h], lo), (int)lo, (int)hi);
-            if (blk == 0) {
-                r0 |= w;
-            } else {
-                r1 |= w;
-            }
+            *(u32x4_u *)(tl + d0[h]) = v[h];
+            if (lh == (uint32_t)h) *(u32x4_u *)(tl + d0[h] + 16) = vl;
         }
-        if (cend) r1 |= mask_piece(vc, 0, (int)(cend - B));
         // done once span k + 7 starts past the tile, or the sentinel came
         if (live != 0x7fu || en[15] >= e) break;
         k += 7;
+    }
+    u32x4 r0 = *(const u32x4 *)tl, r1 = *(const u32x4 *)(tl + 16);
+    if (e - a < kGatherTile) {  // the record's last tile: zeros past its end, as before
+        r0 = mask_piece(r0, 0, (int)(e - a));
+        r1 = mask_piece(r1, 0, (int)(e - a) - 16);
     }
     PX_GAS uint8_t *o = (PX_GAS uint8_t *)out_ + q.out_off + a;
     *(PX_GAS u32x4 *)o = r0;
@@ -2499,8 +2572,8 @@ hipError_t launch_span_build(hipStream_t s, uint32_t n, const SpanJob *jobs) {
 hipError_t launch_gather(hipStream_t s, uint32_t ntask, void *task_buf, const GatherQuery *qs, uint32_t nq,
                          uint8_t *out, uint32_t *out_len, uint32_t *status, bool remap) {
     if (!ntask) return hipSuccess;
-    uint4 *task = (uint4 *)task_buf;  // ntask x 16 B
-    hipError_t e = hipMemsetAsync(task, 0, (size_t)ntask * 16, s);
+    GatherTask *task = (GatherTask *)task_buf;
+    hipError_t e = hipMemsetAsync(task, 0, (size_t)ntask * sizeof(GatherTask), s);
     if (e != hipSuccess) return e;
     k_gather_tasks<<<(nq + 255) / 256, 256, 0, s>>>(nq, qs, task);
     k_gather<<<(ntask + 3) / 4, 256, 0, s>>>(ntask, task, qs, nq, out, out_len, status, remap ? 1u : 0u);

@@ -736,11 +736,11 @@ struct px_ctx {
         const uint64_t qb = round_up(g.size() * sizeof(GatherQuery), 64);
         auto *hg = (GatherQuery *)hg_buf[which].get(g.size() * sizeof(GatherQuery));
         std::memcpy(hg, g.data(), g.size() * sizeof(GatherQuery));
-        dbuf = (GatherQuery *)heap.alloc(qb + (uint64_t)ntask * 16);
-        void *task = (uint8_t *)dbuf + qb;  // per task: first query, query-start bits (16 B)
+        dbuf = (GatherQuery *)heap.alloc(qb + (uint64_t)ntask * sizeof(GatherTask));
+        void *task = (uint8_t *)dbuf + qb;  // per task: GatherTask
         hcheck(hipMemcpyAsync(dbuf, hg, g.size() * sizeof(GatherQuery), hipMemcpyHostToDevice, st));
         hcheck(launch_gather(st, ntask, task, dbuf, (uint32_t)g.size(), out, dl, ds, true));
-        gather_bytes[dbuf] = qb + (uint64_t)ntask * 16;
+        gather_bytes[dbuf] = qb + (uint64_t)ntask * sizeof(GatherTask);
     }
     std::map<void *, uint64_t> gather_bytes;  // launch_gathers' device buffers -> their sizes
     void release_gathers(GatherQuery *d) {
