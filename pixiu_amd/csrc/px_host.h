@@ -179,6 +179,18 @@ class KeyMap {
         return mix(mix(h ^ w) + n);
     }
     size_t size() const { return n_; }
+    // batched lookups: the slot a hash starts probing at, to prefetch ahead of find_hint_h
+    const void *slot_addr(uint64_t h) const { return tab_.empty() ? nullptr : &tab_[h & (tab_.size() - 1)]; }
+    // find_hint with the hash already computed
+    bool find_hint_h(uint64_t h, const uint8_t *k, size_t n, uint32_t *shard, uint32_t *chunk, uint32_t *idx) const {
+        if (tab_.empty()) return false;
+        const Slot &e = tab_[probe(h, k, n)];
+        if (e.len == kFree) return false;
+        *shard = e.shard;
+        *chunk = e.chunk;
+        *idx = e.idx;
+        return true;
+    }
     // shard of k, or -1
     int64_t find(const uint8_t *k, size_t n) const {
         if (tab_.empty()) return -1;
@@ -240,6 +252,11 @@ class PartKeyMap {
         p_[part_of(k, n)].put(k, n, shard, chunk, idx);
     }
     KeyMap &part(uint32_t i) { return p_[i]; }
+    // batched lookups with the hash computed once (KeyMap::hash(k, n))
+    const void *slot_addr(uint64_t h) const { return p_[h >> 60].slot_addr(h); }
+    bool find_hint_h(uint64_t h, const uint8_t *k, size_t n, uint32_t *shard, uint32_t *chunk, uint32_t *idx) const {
+        return p_[h >> 60].find_hint_h(h, k, n, shard, chunk, idx);
+    }
     size_t size() const {
         size_t n = 0;
         for (const auto &m : p_) n += m.size();

@@ -964,6 +964,44 @@ struct px_ctx {
         q.out_cap = (uint32_t)round_up(chunks[l.chunk].doc_len[l.idx] + 64, 16);
     }
 
+    // resolve_key over keys [lo, hi) with the key map's cache misses overlapped: the hashes
+    // of the next kAhead keys are computed and their first probe slots prefetched, then the
+    // hinted record's chunk metadata and key prefix, so each key's lookup finds its lines in
+    // cache (a lone lookup is a chain of ~6 dependent misses)
+    void resolve_range(uint32_t lo, uint32_t hi, const uint8_t *keys, const uint64_t *koff, int mode,
+                       DecodeQuery *q, uint32_t *pre) {
+        std::string ek;
+        if (opts.records_per_shard == 0 || hi - lo < 64) {
+            for (uint32_t i = lo; i < hi; ++i) resolve_key(keys + koff[i], koff[i + 1] - koff[i], mode, ek, q[i], pre[i]);
+            return;
+        }
+        constexpr uint32_t kAhead = 16;
+        uint64_t hs[2 * kAhead];
+        auto stage1 = [&](uint32_t i) {  // hash, prefetch the probe slot
+            const uint64_t h = pxh::KeyMap::hash(keys + koff[i], koff[i + 1] - koff[i]);
+            hs[i % (2 * kAhead)] = h;
+            if (const void *a = keymap.slot_addr(h)) __builtin_prefetch(a);
+        };
+        auto stage2 = [&](uint32_t i) {  // the hinted record's metadata and key prefix
+            uint32_t sh, c, x;
+            if (keymap.find_hint_h(hs[i % (2 * kAhead)], keys + koff[i], koff[i + 1] - koff[i], &sh, &c, &x) &&
+                c < chunks.size() && x < chunks[c].n) {
+                const Chunk &ch = chunks[c];
+                __builtin_prefetch(&ch.dead[x]);
+                __builtin_prefetch(&ch.doc_len[x]);
+                __builtin_prefetch(&ch.kp_off[x]);
+                __builtin_prefetch(&ch.kp_len[x]);
+            }
+        };
+        const uint32_t pro = std::min(hi, lo + kAhead);
+        for (uint32_t i = lo; i < pro; ++i) stage1(i);
+        for (uint32_t i = lo; i < hi; ++i) {
+            if (i + kAhead < hi) stage1(i + kAhead);
+            if (i + kAhead / 2 < hi) stage2(i + kAhead / 2);
+            resolve_key(keys + koff[i], koff[i + 1] - koff[i], mode, ek, q[i], pre[i]);
+        }
+    }
+
     // share of a get batch (in 64ths) resolved before the first decode launch
     static uint32_t opts_head_frac() {
         static const uint32_t f = [] {
@@ -985,10 +1023,7 @@ struct px_ctx {
         using clk = std::chrono::steady_clock;
         std::vector<DecodeQuery> q(n);
         std::vector<uint32_t> pre(n, PX_OK);
-        auto resolve = [&](uint32_t lo, uint32_t hi) {
-            std::string ek;
-            for (uint32_t i = lo; i < hi; ++i) resolve_key(keys + koff[i], koff[i + 1] - koff[i], mode, ek, q[i], pre[i]);
-        };
+        auto resolve = [&](uint32_t lo, uint32_t hi) { resolve_range(lo, hi, keys, koff, mode, q.data(), pre.data()); };
         uint64_t total = 0;
         auto place = [&](uint32_t lo, uint32_t hi) {  // output offsets, in key order
             for (uint32_t i = lo; i < hi; ++i) {

@@ -133,6 +133,10 @@ static void test_keymaps() {
         if (i % 5 == 0) {
             uint32_t a, b, c;
             CHECK(pm.find_hint(kb, k.size(), &a, &b, &c) && a == sh && b == sh + 1 && c == sh + 2);
+            // the batched form (hash computed by the caller) agrees
+            const uint64_t h = pxh::KeyMap::hash(kb, k.size());
+            CHECK(pm.slot_addr(h) != nullptr);
+            CHECK(pm.find_hint_h(h, kb, k.size(), &a, &b, &c) && a == sh && b == sh + 1 && c == sh + 2);
             std::string miss = k + "\x01\x02\x03";
             CHECK(pm.find((const uint8_t *)miss.data(), miss.size()) == (ref.count(miss) ? (int64_t)ref[miss] : -1));
         }
