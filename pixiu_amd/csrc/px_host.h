@@ -328,7 +328,9 @@ class WorkerPool {
         }
         lk.lock();
         done_ += mine;
-        busy_.wait(lk, [&] { return done_ == ntask_ && active_ == 0; });
+        // back as soon as every task ran: a worker that woke late finds none left and never
+        // calls f (the next run waits for it to leave before it publishes a new job)
+        busy_.wait(lk, [&] { return done_ == ntask_; });
     }
     ~WorkerPool() {
         {
