@@ -96,8 +96,8 @@ static_assert(sizeof(PsaShard) == 32, "PsaShard layout");
 // next chunk (kNone: every doc stays), and the pool state after the last doc that stays
 struct PsaPoolOut {
     uint32_t rot_doc;
-    int32_t pools, used;
-    uint32_t splits;  // split leaves (inner nodes) in the docs that stay
+    int32_t pools, used;  // (after the docs that stay; the bound test leaves them 0 / 2,048)
+    uint32_t how;         // 0: the boundary chain ran, 1: the bound test (no rotation), 2: (rotation)
 };
 // device scratch for px_psa.hip, borrowed from the runtime's heap
 struct PsaAlloc {

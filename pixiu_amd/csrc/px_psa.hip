@@ -1216,7 +1216,7 @@ PSA_DEV uint32_t wave_first_gt(uint32_t lo, uint32_t hi, uint32_t t, Key key) {
 
 __global__ void __launch_bounds__(kScanThreads) k_pool_scan(uint32_t nshards, const PsaShard *shards, const PsaDoc *docs,
                                                             const uint32_t *P, const uint32_t *C, uint32_t N,
-                                                            PsaPoolOut *out) {
+                                                            PsaPoolOut *out, uint32_t chain_only) {
     __shared__ uint32_t Pw[2][kScanWin];       // P[wb + i]
     __shared__ uint32_t Cw[2][kScanWin / 64];  // P[wb + 64 j + 63]
     __shared__ uint32_t sh_wb, sh_go, sh_restage;
@@ -1245,7 +1245,7 @@ __global__ void __launch_bounds__(kScanThreads) k_pool_scan(uint32_t nshards, co
     // (root included) passes the low end and the first that passes the high end: if those are
     // in one doc, the chunk rotates before the next doc; if none passes the low end, it does
     // not rotate.  Only the other cases need the boundary chain below.
-    if (wave == 0) {
+    if (wave == 0 && !chain_only) {  // (chain_only: PX_DEBUG_POOL_CHAIN, tests of the chain)
         constexpr uint32_t kLo = (uint32_t)(kRotatePools - 1) * (uint32_t)(kPoolBlocks - 4);
         constexpr uint32_t kHi = (uint32_t)(kRotatePools - 1) * (uint32_t)kPoolBlocks;
         // running count through x = kNodeBlocks + (P[x] - base) (P is a modular prefix sum: its
@@ -1270,9 +1270,10 @@ __global__ void __launch_bounds__(kScanThreads) k_pool_scan(uint32_t nshards, co
         }
         if (lane == 0) {
             sh_go = verdict;
-            if (verdict) out[s] = PsaPoolOut{verdict == 2 ? rd : kNone, verdict == 2 ? kRotatePools : 0, 0, 0};
+            if (verdict) out[s] = PsaPoolOut{verdict == 2 ? rd : kNone, verdict == 2 ? kRotatePools : 0, 0, verdict};
         }
     }
+    if (threadIdx.x == 0 && chain_only) sh_go = 0;
     __syncthreads();
     if (sh_go) return;  // (uniform: the whole block leaves)
     __syncthreads();
@@ -1745,7 +1746,8 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         PSA_CHECK(rocprim::inclusive_scan(tmp2, tsz, blk, P, (size_t)N, rocprim::plus<uint32_t>(), s));
         auto *C = S.get<uint32_t>(n64 / kPoolCoarse * 4 + 256);
         k_pool_coarse<<<blocks((N + kPoolCoarse - 1) / kPoolCoarse), tb, 0, s>>>(N, P, C);
-        k_pool_scan<<<nshards, kScanThreads, 0, s>>>(nshards, shards, docs, P, C, N, pool_out);
+        k_pool_scan<<<nshards, kScanThreads, 0, s>>>(nshards, shards, docs, P, C, N, pool_out,
+                                                     env_on("PX_DEBUG_POOL_CHAIN") ? 1u : 0u);
         PSA_CHECK(hipGetLastError());
     }
     PSA_CHECK(hipEventRecord(e4, s));

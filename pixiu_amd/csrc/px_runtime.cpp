@@ -1657,15 +1657,16 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
                 pst.iterations = std::max(pst.iterations, rst.iterations);
             }
             if (const char *v = std::getenv("PX_PSA_VERBOSE"); v && *v == '1') {
-                uint32_t nf = 0, nr = 0;
+                uint32_t nf = 0, nr = 0, nb = 0;
                 for (size_t i = 0; i < ps.size(); ++i) {
                     nf += flag[i] != 0;
                     nr += ps[i].pools && pout[i].rot_doc != kNone;
+                    nb += ps[i].pools && pout[i].how != 0;
                 }
-                fprintf(stderr, "psa round %u: %zu shards, %zu docs, N=%llu, pools %d (%u candidates, %.2f ms), "
-                                "%u rotations, %u flagged, sort %.2f lcp %.2f msg %.2f ms\n",
+                fprintf(stderr, "psa round %u: %zu shards, %zu docs, N=%llu, pools %d (%u candidates, %.2f ms, "
+                                "%u decided by the bound), %u rotations, %u flagged, sort %.2f lcp %.2f msg %.2f ms\n",
                         psa_rounds, ps.size(), pd.size(), (unsigned long long)gpos, (int)any_pools, rst.candidates,
-                        rst.ms_pool, nr, nf, rst.ms_sort, rst.ms_lcp, rst.ms_msg);
+                        rst.ms_pool, nb, nr, nf, rst.ms_sort, rst.ms_lcp, rst.ms_msg);
             }
             heap.release(d_pd, pd.size() * sizeof(PsaDoc));
             heap.release(d_ps, ps.size() * sizeof(PsaShard) + ps.size() * 4 + 64);

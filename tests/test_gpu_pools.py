@@ -46,9 +46,14 @@ def _set(st, cp, pieces):
     return np.concatenate(res)
 
 
-def test_single_instance_rotates_like_the_oracle(store_factory):
-    """config 3, 420 records (25 MB) in one batch at rps = 0: two rotations by pool count"""
+@pytest.mark.parametrize("chain", [False, True])
+def test_single_instance_rotates_like_the_oracle(chain, store_factory, monkeypatch):
+    """config 3, 420 records (25 MB) in one batch at rps = 0: two rotations by pool count.
+    chain: PX_DEBUG_POOL_CHAIN=1 skips the bound test, so every window runs the boundary
+    chain; both must place every record where the reference does"""
     from pixiu_amd import synth
+    if chain:
+        monkeypatch.setenv("PX_DEBUG_POOL_CHAIN", "1")
     cp = synth.make(3, 420)
     st = store_factory(records_per_shard=0)
     r = _set(st, cp, [(0, cp.n)])
@@ -93,10 +98,14 @@ def _oracle_get(cp, rps, rows):
     return [out[i] for i in rows]
 
 
-@pytest.mark.parametrize("cfg,n,rps", [(2, 20000, 0), (4, 60000, 0), (5, 400, 200)])
-def test_pool_emulation_matches_oracle(cfg, n, rps, store_factory):
-    """configs 2 / 4 (byte-251 stress) / 5: every record's chunk, slot and bytes"""
+@pytest.mark.parametrize("cfg,n,rps,chain", [(2, 20000, 0, False), (4, 60000, 0, False), (5, 400, 200, False),
+                                             (4, 60000, 0, True)])
+def test_pool_emulation_matches_oracle(cfg, n, rps, chain, store_factory, monkeypatch):
+    """configs 2 / 4 (byte-251 stress) / 5: every record's chunk, slot and bytes (chain: the
+    boundary chain in every window, as above)"""
     from pixiu_amd import synth
+    if chain:
+        monkeypatch.setenv("PX_DEBUG_POOL_CHAIN", "1")
     cp = synth.make(cfg, n)
     st = store_factory(records_per_shard=rps)
     r = st.set_batch((cp.keys, cp.koff.astype(np.uint64)), (cp.vals, cp.voff.astype(np.uint64)))
