@@ -1177,8 +1177,10 @@ struct px_ctx {
             auto *kbuf = (uint8_t *)heap.alloc(qo + 64);
             std::vector<uint32_t> ql, qs;
             run_decode(q, kbuf, ql, qs, false);
-            std::vector<uint8_t> hk(qo);
-            d2h(hk.data(), kbuf, qo);
+            // (uninitialised: 1 M key prefixes are ~80 MB, which a zero fill would write twice)
+            std::unique_ptr<uint8_t[]> hk_store(new uint8_t[qo + 1]);
+            uint8_t *hk = hk_store.get();
+            d2h(hk, kbuf, qo);
             sync();
             heap.release(kbuf, qo + 64);
             std::vector<DecodeQuery> again;
@@ -1193,7 +1195,7 @@ struct px_ctx {
                     redo[i] = 2;
                     continue;
                 }
-                if (pass == 0 && qs[i] == kErrSpace && key_end(hk.data() + q[i].out_off, ql[i]) == 0) {
+                if (pass == 0 && qs[i] == kErrSpace && key_end(hk + q[i].out_off, ql[i]) == 0) {
                     DecodeQuery d = q[i];
                     d.out_off = ao;
                     d.out_cap = jobs[qj[i]].doc_len + 256;
@@ -1211,7 +1213,7 @@ struct px_ctx {
                 for (uint32_t i = runs[k]; i < runs[k + 1]; ++i) {
                     if (redo[i]) continue;
                     const KpJob &j = jobs[qj[i]];
-                    const uint8_t *p = hk.data() + q[i].out_off;
+                    const uint8_t *p = hk + q[i].out_off;
                     const uint32_t ke = key_end(p, ql[i]);
                     const uint32_t keep = ke ? ke : ql[i];
                     Chunk &ch = chunks[j.chunk];
@@ -1915,18 +1917,27 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     }
     // push new slot entries to the device tables (one copy per touched chunk range)
     {
-        std::map<uint32_t, std::pair<uint32_t, uint32_t>> touched;  // chunk -> [lo, hi)
+        // chunk -> [lo, hi) of its new slots (a flat table over chunk ids: a batch of 1 M
+        // records paid a std::map lookup per record here)
+        std::vector<std::pair<uint32_t, uint32_t>> span_of(chunks.size(), {kNone, 0});
+        std::vector<uint32_t> touched;
         for (uint32_t r = 0; r < n; ++r) {
             if (rgchunk[r] == kNone) continue;
-            auto it = touched.find(rgchunk[r]);
-            if (it == touched.end()) touched[rgchunk[r]] = {ridx[r], ridx[r] + 1};
-            else it->second.second = ridx[r] + 1;
+            auto &t = span_of[rgchunk[r]];
+            if (t.first == kNone) {
+                t = {ridx[r], ridx[r] + 1};
+                touched.push_back(rgchunk[r]);
+            } else {
+                t.second = ridx[r] + 1;
+            }
         }
+        std::sort(touched.begin(), touched.end());
         std::vector<SlotPut> puts;
-        for (auto &t : touched) {
-            chunk_reserve(t.first, chunks[t.first].n);
-            Chunk &ch = chunks[t.first];
-            for (uint32_t i = t.second.first; i < t.second.second; ++i) puts.push_back(SlotPut{ch.dev + i, ch.slots[i]});
+        puts.reserve(n);
+        for (uint32_t c : touched) {
+            chunk_reserve(c, chunks[c].n);
+            Chunk &ch = chunks[c];
+            for (uint32_t i = span_of[c].first; i < span_of[c].second; ++i) puts.push_back(SlotPut{ch.dev + i, ch.slots[i]});
         }
         if (!puts.empty()) {
             auto *d = (SlotPut *)slotput_buf.get(puts.size() * sizeof(SlotPut));
