@@ -26,7 +26,7 @@
 //   k_psa_key0     5-symbol keys (shard in the top bits) -> radix sort (rocPRIM)
 //   prefix doubling: keys (group, rank[p+h]) of unsorted suffixes only, stable radix
 //                  sort, group heads by max-scans, ranks and SA written back
-//   k_psa_minlvl / k_psa_ansv   nearest smaller position left/right in SA order
+//   k_psa_minlvl / k_psa_ansv_blk   nearest smaller position left/right in SA order
 //                  (a 64-ary min tree; one wave per 64 ranks, ballot descents)
 //   k_psa_lce      lcp with those two neighbours, Kasai-style in text order
 //                  (lcp(p) >= lcp(p-1) - 1 for both neighbours)
@@ -743,71 +743,154 @@ PSA_DEV uint32_t shard_of_rank(const PsaShard *shards, uint32_t nshards, uint32_
     return a;
 }
 
-__global__ void __launch_bounds__(256) k_psa_ansv(uint32_t N, MinTree t, const PsaShard *shards, uint32_t nshards,
-                                                  uint2 *links) {
-    const uint32_t lane = lane_id();
-    const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (w * 64 >= N) return;
+// Block-level ANSV: one workgroup per kAnsvBlock ranks.  Each wave first resolves its
+// 64-rank sub-blocks by binary lifting; an element with no smaller value on a side
+// inside its sub-block then looks for the nearest sub-block of the workgroup whose minimum is
+// smaller (one ballot over the 64 sub-block minima in LDS) and, inside it, for the nearest
+// smaller element (one ballot over its 64 values in LDS).  Each wave computes the sub-block
+// links with binary lifting over window minima: ml[k] / mr[k] = the minimum of the 2^k lanes
+// ending / starting at this lane, and (pl, lane) extends while its minimum stays >= v.  Only the workgroup's own prefix /
+// suffix minima (≈ 2 ln 4096 ≈ 17 of 4,096) go to the global min tree: 64× fewer dependent
+// global searches than one wave per 64 ranks.
+constexpr uint32_t kAnsvBlock = 4096, kAnsvSub = kAnsvBlock / 64;
+constexpr uint16_t kNone16 = 0xffffu;    // (block-local indices are < 4,096)
+constexpr uint16_t kQueued16 = 0xc000u;  // | queue slot: resolved through the global min tree
+constexpr uint32_t kAnsvQCap = 512;      // (a random block has ≈ 2 ln 4096 ≈ 17 such sides)
+__global__ void __launch_bounds__(512) k_psa_ansv_blk(uint32_t N, MinTree t, const PsaShard *shards, uint32_t nshards,
+                                                      uint2 *links) {
+    __shared__ uint32_t V[kAnsvBlock];        // the block's suffix-array values
+    __shared__ uint16_t PS[kAnsvBlock], NS[kAnsvBlock];  // block-local index of the nearest smaller, or kNone16
+    __shared__ uint32_t M[kAnsvSub];          // sub-block minima
+    __shared__ uint16_t Q[kAnsvQCap];         // queued sides: block-local index | dir << 15
+    __shared__ uint32_t QR[kAnsvQCap], qn;    // their nearest smaller rank (or kNoPos)
+    const uint32_t lane = lane_id(), wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const uint32_t b0 = blockIdx.x * kAnsvBlock;
+    if (b0 >= N) return;
     const uint32_t *sa = t.lvl[0];
-    const uint32_t r = w * 64 + lane;
-    const bool live = r < N;
-    const uint32_t v = live ? sa[r] : kNoPos;
-    // this block of 64 ranks lies in one shard unless it straddles a boundary
-    const uint32_t r0 = w * 64, r1 = min(N, r0 + 64) - 1;
-    const uint32_t s0 = shard_of_rank(shards, nshards, __builtin_amdgcn_readfirstlane(r0));
-    const PsaShard sh0 = shards[s0];
-    uint32_t lo = sh0.base, hi = sh0.base + sh0.len;
-    if (r1 >= hi && live && r >= hi) {
-        const PsaShard sh = shards[shard_of_rank(shards, nshards, r)];
-        lo = sh.base;
-        hi = sh.base + sh.len;
+    if (threadIdx.x == 0) qn = 0;
+    // phase 1: sub-blocks by lifting
+    for (uint32_t sb = wave; sb < kAnsvSub; sb += nw) {
+        const uint32_t li = sb * 64 + lane, r = b0 + li;
+        const uint32_t v = r < N ? sa[r] : kNoPos;
+        uint32_t ml[6], mr[6];
+        ml[0] = mr[0] = v;
+        for (int k = 1; k < 6; ++k) {
+            const uint32_t w = 1u << (k - 1);
+            const uint32_t a = (uint32_t)__shfl((int)ml[k - 1], (int)((lane - w) & 63u));
+            const uint32_t b = (uint32_t)__shfl((int)mr[k - 1], (int)((lane + w) & 63u));
+            ml[k] = lane >= w ? min(ml[k - 1], a) : ml[k - 1];
+            mr[k] = lane + w < 64 ? min(mr[k - 1], b) : mr[k - 1];
+        }
+        int pl = (int)lane - 1, pr = (int)lane + 1;
+        for (int k = 5; k >= 0; --k) {
+            const int w = 1 << k;
+            const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute(max(pl, 0) << 2, (int)ml[k]);
+            if (pl - w + 1 >= 0 && a >= v) pl -= w;
+            const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(min(pr, 63) << 2, (int)mr[k]);
+            if (pr + w - 1 <= 63 && b >= v) pr += w;
+        }
+        V[li] = v;
+        PS[li] = pl >= 0 ? (uint16_t)(sb * 64 + (uint32_t)pl) : kNone16;
+        NS[li] = pr <= 63 ? (uint16_t)(sb * 64 + (uint32_t)pr) : kNone16;
+        // the sub-block's minimum: lanes 0..31 (lane 0's mr[5]) and 32..63 (lane 63's ml[5])
+        const uint32_t m63 = (uint32_t)__shfl((int)ml[5], 63);
+        if (lane == 0) M[sb] = min(mr[5], m63);
     }
-    // inside the 64-rank block: binary lifting over window minima.  ml[k] = min of the
-    // 2^k lanes ending at this lane, mr[k] = of the 2^k lanes starting at it
-    uint32_t ml[6], mr[6];
-    ml[0] = mr[0] = v;
-    for (int k = 1; k < 6; ++k) {
-        const uint32_t w = 1u << (k - 1);
-        const uint32_t a = (uint32_t)__shfl((int)ml[k - 1], (int)((lane - w) & 63u));
-        const uint32_t b = (uint32_t)__shfl((int)mr[k - 1], (int)((lane + w) & 63u));
-        ml[k] = lane >= w ? min(ml[k - 1], a) : ml[k - 1];
-        mr[k] = lane + w < 64 ? min(mr[k - 1], b) : mr[k - 1];
-    }
-    // nearest smaller to the left: extend (pl, lane) while its minimum stays >= v
-    int pl = (int)lane - 1, pr = (int)lane + 1;
-    for (int k = 5; k >= 0; --k) {
-        const int w = 1 << k;
-        const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute(max(pl, 0) << 2, (int)ml[k]);
-        if (pl - w + 1 >= 0 && a >= v) pl -= w;
-        const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(min(pr, 63) << 2, (int)mr[k]);
-        if (pr + w - 1 <= 63 && b >= v) pr += w;
-    }
-    uint32_t ps = pl >= 0 ? r - (lane - (uint32_t)pl) : kNoPos;
-    uint32_t ns = pr <= 63 ? r + ((uint32_t)pr - lane) : kNoPos;
-    if (ns != kNoPos && ns >= N) ns = kNoPos;
-    // the rest through the min tree, one element at a time (few per block: the block's
-    // prefix / suffix minima)
-    uint64_t need = __ballot(live && (ps == kNoPos || ns == kNoPos));
-    while (need) {
-        const uint32_t l = (uint32_t)__ffsll((long long)need) - 1u;
-        need &= need - 1;
-        const uint32_t ri = w * 64 + l;
-        const uint32_t vi = (uint32_t)__shfl((int)v, (int)l);
-        const uint32_t pi = (uint32_t)__shfl((int)ps, (int)l);
-        const uint32_t ni = (uint32_t)__shfl((int)ns, (int)l);
-        const uint32_t fp = pi == kNoPos ? tree_find(t, ri, vi, 0) : pi;
-        const uint32_t fn = ni == kNoPos ? tree_find(t, ri, vi, 1) : ni;
-        if (lane == l) {
-            ps = fp;
-            ns = fn;
+    __syncthreads();
+    // phase 2: across sub-blocks, inside the workgroup (LDS only)
+    for (uint32_t sb = wave; sb < kAnsvSub; sb += nw) {
+        const uint32_t li = sb * 64 + lane;
+        const uint32_t v = V[li];
+        uint64_t need = __ballot(b0 + li < N && (PS[li] == kNone16 || NS[li] == kNone16));
+        const uint32_t mlane = M[lane];  // (kAnsvSub == 64: one sub-block minimum per lane)
+        while (need) {
+            const uint32_t l = (uint32_t)__ffsll((long long)need) - 1u;
+            need &= need - 1;
+            const uint32_t vi = (uint32_t)__shfl((int)v, (int)l);
+            const uint32_t e = sb * 64 + l;
+            if (PS[e] == kNone16) {  // (uniform: every lane reads the same word)
+                const uint64_t ms = __ballot(lane < sb && mlane < vi);
+                if (ms) {
+                    const uint32_t j = 63u - (uint32_t)__clzll((long long)ms);
+                    const uint64_t mv = __ballot(V[j * 64 + lane] < vi);
+                    if (lane == 0) PS[e] = (uint16_t)(j * 64 + 63u - (uint32_t)__clzll((long long)mv));
+                }
+            }
+            if (NS[e] == kNone16) {
+                const uint64_t ms = __ballot(lane > sb && mlane < vi);
+                if (ms) {
+                    const uint32_t j = (uint32_t)__ffsll((long long)ms) - 1u;
+                    const uint64_t mv = __ballot(V[j * 64 + lane] < vi);
+                    if (lane == 0) NS[e] = (uint16_t)(j * 64 + (uint32_t)__ffsll((long long)mv) - 1u);
+                }
+            }
         }
     }
-    if (live)  // in rank order (coalesced); k_psa_links_text moves them to text order
-        links[r] = make_uint2((ps != kNoPos && ps >= lo) ? sa[ps] : kNoPos, (ns != kNoPos && ns < hi) ? sa[ns] : kNoPos);
+    __syncthreads();
+    // phase 3: the workgroup's own prefix / suffix minima (a side unresolved inside the
+    // workgroup has no smaller value there) go to a queue, shared out over all waves, and
+    // each searches the global min tree from the workgroup's edge outward; a queue overflow
+    // (adversarial input) is searched by the owning wave in phase 4
+    for (uint32_t sb = wave; sb < kAnsvSub; sb += nw) {
+        const uint32_t li = sb * 64 + lane;
+        const bool live = b0 + li < N;
+        for (uint32_t dir = 0; dir < 2; ++dir) {
+            uint16_t *X = dir == 0 ? PS : NS;
+            const bool q = live && X[li] == kNone16;
+            const uint64_t m = __ballot(q);
+            if (!m) continue;
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(&qn, (uint32_t)__popcll(m));
+            base = (uint32_t)__shfl((int)base, 0);
+            const uint32_t slot = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            if (q && slot < kAnsvQCap) {
+                Q[slot] = (uint16_t)(li | (dir << 15));
+                X[li] = (uint16_t)(kQueued16 | slot);
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t nq = min(qn, kAnsvQCap);
+    for (uint32_t i = wave; i < nq; i += nw) {
+        const uint32_t item = Q[i], li = item & 0x7fffu, dir = item >> 15;
+        const uint32_t f = tree_find(t, dir == 0 ? b0 : b0 + kAnsvBlock - 1, V[li], (int)dir);
+        if (lane == 0) QR[i] = f;
+    }
+    __syncthreads();
+    // phase 4: every rank's links (in rank order; k_psa_links_text moves them to text order)
+    for (uint32_t sb = wave; sb < kAnsvSub; sb += nw) {
+        const uint32_t li = sb * 64 + lane, r = b0 + li;
+        const bool live = r < N;
+        const uint32_t v = V[li];
+        const uint32_t xp = PS[li], xn = NS[li];
+        uint32_t ps = xp == kNone16 ? kNoPos : (xp & kQueued16) == kQueued16 ? QR[xp & 0x3fffu] : b0 + xp;
+        uint32_t ns = xn == kNone16 ? kNoPos : (xn & kQueued16) == kQueued16 ? QR[xn & 0x3fffu] : b0 + xn;
+        if (ns != kNoPos && ns >= N) ns = kNoPos;
+        uint64_t need = __ballot(live && (xp == kNone16 || xn == kNone16));  // (queue overflow only)
+        while (need) {
+            const uint32_t l = (uint32_t)__ffsll((long long)need) - 1u;
+            need &= need - 1;
+            const uint32_t vi = (uint32_t)__shfl((int)v, (int)l);
+            const uint32_t pi = (uint32_t)__shfl((int)xp, (int)l);
+            const uint32_t ni = (uint32_t)__shfl((int)xn, (int)l);
+            const uint32_t fp = pi == kNone16 ? tree_find(t, b0, vi, 0) : 0u;
+            const uint32_t fn = ni == kNone16 ? tree_find(t, b0 + kAnsvBlock - 1, vi, 1) : 0u;
+            if (lane == l) {
+                if (pi == kNone16) ps = fp;
+                if (ni == kNone16) ns = fn;
+            }
+        }
+        if (!live) continue;
+        const PsaShard sh = shards[shard_of_rank(shards, nshards, r)];
+        const uint32_t lo = sh.base, hi = sh.base + sh.len;
+        const uint32_t pv = ps != kNoPos && ps >= lo ? (ps >= b0 ? V[ps - b0] : sa[ps]) : kNoPos;
+        const uint32_t nv = ns != kNoPos && ns < hi ? (ns < b0 + kAnsvBlock ? V[ns - b0] : sa[ns]) : kNoPos;
+        links[r] = make_uint2(pv, nv);
+    }
 }
 
 // the links in text order: one scattered 8-byte read per position instead of two
-// scattered 4-byte writes in k_psa_ansv (rank = the inverse suffix array)
+// scattered 4-byte writes in the ANSV kernel (rank = the inverse suffix array)
 __global__ void __launch_bounds__(256) k_psa_links_text(uint32_t N, const uint32_t *rank, const uint2 *links,
                                                         uint32_t *psvp, uint32_t *nsvp) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1689,7 +1772,7 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     auto *psvp = S.get<uint32_t>(n64 * 4), *nsvp = S.get<uint32_t>(n64 * 4);
     {
         auto *links = S.get<uint2>(n64 * 8);
-        k_psa_ansv<<<(uint32_t)((n64 + 255) / 256), 256, 0, s>>>(N, t, shards, nshards, links);
+        k_psa_ansv_blk<<<(uint32_t)((n64 + kAnsvBlock - 1) / kAnsvBlock), 512, 0, s>>>(N, t, shards, nshards, links);
         k_psa_links_text<<<blocks(N), tb, 0, s>>>(N, rank, links, psvp, nsvp);
         S.put(links);
     }
