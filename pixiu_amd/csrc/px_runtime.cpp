@@ -719,6 +719,21 @@ struct px_ctx {
         }
         return g;
     }
+    // take_gathers with the queries prepared by the resolving threads (pg: span == nullptr
+    // where the record has no table)
+    std::vector<GatherQuery> take_gathers_pre(DecodeQuery *qn, uint32_t lo, uint32_t hi, const GatherQuery *pg) {
+        std::vector<GatherQuery> g;
+        g.reserve(hi - lo);
+        for (uint32_t j = lo; j < hi; ++j) {
+            if (!pg[j].span || qn[j].chunk == kNone) continue;
+            g.push_back(pg[j]);
+            g.back().out_off = qn[j].out_off;
+            g.back().slot = j - lo;
+            qn[j].chunk = kNone;
+            qn[j].nrec = 0;
+        }
+        return g;
+    }
     // after the k_decode launch on the same stream (its skipped-query results are overwritten).
     // The launch's tiles (a tile = kGatherTile output bytes of one query; a query's tiles
     // are consecutive) go 64 to a wave, across queries when they are small; the queries go
@@ -1023,7 +1038,22 @@ struct px_ctx {
         using clk = std::chrono::steady_clock;
         std::vector<DecodeQuery> q(n);
         std::vector<uint32_t> pre(n, PX_OK);
-        auto resolve = [&](uint32_t lo, uint32_t hi) { resolve_range(lo, hi, keys, koff, mode, q.data(), pre.data()); };
+        // each key's gather query too (span table, compressed base), on the same host threads:
+        // its chunk metadata is in the resolving thread's cache, and the serial
+        // take_gathers_pre below then only reads this array
+        std::unique_ptr<GatherQuery[]> pg(new GatherQuery[n]);
+        const bool spans = spans_enabled();
+        auto resolve = [&](uint32_t lo, uint32_t hi) {
+            resolve_range(lo, hi, keys, koff, mode, q.data(), pre.data());
+            for (uint32_t j = lo; j < hi; ++j) {
+                pg[j].span = nullptr;
+                if (!spans || q[j].chunk == kNone) continue;
+                const SpanView sp = span_view(q[j]);
+                if (!sp.p) continue;
+                pg[j] = GatherQuery{sp.p, chunks[q[j].chunk].slots[q[j].idx].comp, 0, sp.n, sp.len, q[j].out_cap, 0,
+                                    sp.t, 0, 0};
+            }
+        };
         uint64_t total = 0;
         auto place = [&](uint32_t lo, uint32_t hi) {  // output offsets, in key order
             for (uint32_t i = lo; i < hi; ++i) {
@@ -1055,7 +1085,7 @@ struct px_ctx {
         auto *hr = (uint32_t *)hres_buf.get((uint64_t)n * 8);
         std::memcpy(qn, q.data(), (size_t)head * sizeof(DecodeQuery));
         phase.mark("head gathers + launch");
-        std::vector<GatherQuery> g1 = take_gathers(qn, 0, head, 0);
+        std::vector<GatherQuery> g1 = take_gathers_pre(qn, 0, head, pg.get());
         auto any_walk = [&](uint32_t lo, uint32_t hi) {
             for (uint32_t j = lo; j < hi; ++j)
                 if (qn[j].chunk != kNone) return true;
@@ -1084,7 +1114,7 @@ struct px_ctx {
         }
         phase.mark("tail gathers + launch");
         std::memcpy(qn + head, q.data() + head, (size_t)(n - head) * sizeof(DecodeQuery));
-        std::vector<GatherQuery> g2 = take_gathers(qn, head, n, 0);
+        std::vector<GatherQuery> g2 = take_gathers_pre(qn, head, n, pg.get());
         stats.last_gather_queries = (uint32_t)(g1.size() + g2.size());
         hcheck(hipStreamWaitEvent(stream2, ev0, 0));  // chunk table and head queries uploaded
         if (any_walk(head, n)) {
