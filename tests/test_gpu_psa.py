@@ -104,6 +104,25 @@ def test_psa_small_alphabets_match_oracle(store_factory, oracle):
         assert [comp[pos[i]] for i in rows] == want["comp"]
 
 
+def test_psa_long_runs_match_oracle(store_factory, oracle):
+    """Runs of one byte longer than an ANSV workgroup (4,096 ranks): a run's suffixes lie at
+    decreasing positions over consecutive ranks, so every rank of such a workgroup is one
+    of its prefix minima and its queue of global searches (512) overflows to the owning
+    waves (px_psa.hip k_psa_ansv_blk); bytes and placement equal the oracle's single
+    instance."""
+    keys = [b"run%d" % i for i in range(8)]
+    vals = [b"a" * 20000, b"xyz" + b"a" * 9000 + b"q", b"b" * 5000 + b"a" * 5000, bytes(range(1, 251)) * 20,
+            b"a" * 30000 + b"b", b"ab" * 6000, b"a" * 4097, b"\x00" * 12000]
+    st = store_factory(records_per_shard=0)
+    r = st.set_batch(keys, vals)
+    s = st.stats()
+    assert (s["last_psa_shards"], s["last_walk_shards"]) == (1, 0)
+    assert int(r["status"].max()) == 0
+    oc, ochunk, oidx = oracle.encode_docs([assemble(k, v) for k, v in zip(keys, vals)])
+    assert st.export(px.records_of(r)) == oc
+    assert r["chunk"].tolist() == ochunk and r["idx"].tolist() == oidx
+
+
 def test_psa_slot_full_chunk_then_next_batch(store_factory, oracle):
     """A PSA live chunk filled to 65,535 docs: the next batch rotates at its first doc and
     stays on PSA (new chunk), bytes and placement equal the oracle's single instance."""
