@@ -900,18 +900,6 @@ __global__ void __launch_bounds__(256) k_psa_links_text(uint32_t N, const uint32
     nsvp[p] = l.y;
 }
 
-// the first sort's radix digit width (experiments: PX_SORT_BITS 10 -- 11-bit digits overflow the histogram kernel's LDS; rocPRIM's tuned
-// onesweep otherwise)
-template <unsigned Bits>
-using FirstSortCfg = rocprim::radix_sort_config<
-    rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 12>, rocprim::kernel_config<512, 8>, Bits,
-                                        rocprim::block_radix_rank_algorithm::match>>;
-inline int first_sort_bits() {
-    const char *e = std::getenv("PX_SORT_BITS");
-    return e ? std::atoi(e) : 0;
-}
-
 // ---------------------------------------------------------------- lcp with those neighbours
 // text positions per thread (Kasai-style amortisation): 256, or fewer (a multiple of 8)
 // when that leaves fewer than 2^18 threads -- a one-chunk window of the single instance
@@ -1608,11 +1596,8 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     k_psa_key0<<<blocks(N), tb, 0, s>>>(N, G, pdoc, docs, dist, syms, keys, vals);
     {
         size_t t_sort = 0, t_scan = 0;
-        const int sort_bits = first_sort_bits();
         auto first_sort = [&](void *tmp, size_t &bytes) -> hipError_t {
-            const unsigned kb = 9 * syms + shard_bits;
-            if (sort_bits == 10) return rocprim::radix_sort_pairs<FirstSortCfg<10>>(tmp, bytes, keys, keys2, vals, sa, (size_t)N, 0, kb, s);
-            return rocprim::radix_sort_pairs(tmp, bytes, keys, keys2, vals, sa, (size_t)N, 0, kb, s);
+            return rocprim::radix_sort_pairs(tmp, bytes, keys, keys2, vals, sa, (size_t)N, 0, 9 * syms + shard_bits, s);
         };
         PSA_CHECK(first_sort(nullptr, t_sort));
         PSA_CHECK(rocprim::inclusive_scan(nullptr, t_scan, vals, vals, (size_t)N, Max(), s));
