@@ -128,27 +128,66 @@ def walk_cliff(local, corpus, records=8):
             "note": "one shard forced to the walk fallback (PX_DEBUG_PSA_FLAG_ROUND=1), host buffers, one call"}
 
 
-def small_batches(local, calls=300):
-    """Facade-shaped setitem: one record per call (PiXiuCtrl::setitem through px_set_batch,
-    n = 1) into one store at records_per_shard = 0, config-4 records (256 B).  Every call
-    re-encodes its shard's live chunk on the suffix-array path, so the time per call grows
-    with the chunk: reported for the first and the last 50 calls."""
+def small_batches(local, calls=50000, defer_mb=8):
+    """Facade-shaped setitem: one record per call (PiXiuCtrl::setitem, PiXiuCtrl.cpp:12-47,
+    through px_set_batch with n = 1) into one store at records_per_shard = 0: config 4's
+    first `calls` records (256 B; 50,000 cross a chunk rotation), through the write-behind
+    queue the facade uses (px_opts.defer_bytes = defer_mb MB, include/pixiu_amd.h px_flush).
+    Timed: every call plus the final flush.  Then (untimed) every record's compressed bytes,
+    slot and compat getitem against the reference's own digests for the same records
+    (tests/golden/refdig_c4_r0_n50000.npz)."""
     import pixiu_amd as px
     from pixiu_amd import synth
-    cp = synth.make(4, calls)
-    ts = []
-    with px.Store(records_per_shard=0, device=local) as st:
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _refdig
+    cp = synth.make(4)
+    keys = [cp.key(i) for i in range(calls)]
+    vals = [cp.val(i) for i in range(calls)]
+    raw = sum(len(k) + len(v) for k, v in zip(keys, vals))
+    ts = np.zeros(calls)
+    one = np.zeros(1, np.uint64)
+    with px.Store(records_per_shard=0, device=local, defer_bytes=defer_mb << 20) as st:
+        lib, h = st._lib, st._h
+        res = np.zeros(1, px.SET_RESULT_DTYPE)
+        rp = res.ctypes.data
+        ko = np.zeros(2, np.uint64)
+        vo = np.zeros(2, np.uint64)
+        kop, vop = ko.ctypes.data, vo.ctypes.data
+        replaced = 0
+        t_all = time.perf_counter()
         for i in range(calls):
-            k, v = cp.key(i), cp.val(i)
+            k, v = keys[i], vals[i]
+            ko[1], vo[1] = len(k), len(v)
             t0 = time.perf_counter()
-            st.set_batch([k], [v])
-            ts.append(time.perf_counter() - t0)
-        live = int(st.stats()["chunks"])
-    raw = int(cp.raw_bytes)
-    return {"calls": calls, "record_bytes": raw // calls, "chunks": live,
-            "ms_per_call_first50": round(float(np.mean(ts[:50])) * 1e3, 3),
-            "ms_per_call_last50": round(float(np.mean(ts[-50:])) * 1e3, 3),
-            "MBps": round(raw / sum(ts) / 1e6, 4)}
+            rc = lib.px_set_batch(h, 1, k, kop, v, vop, 0, rp)
+            ts[i] = time.perf_counter() - t0
+            if rc != px.PX_OK:
+                raise SystemExit(f"one_record_per_call: setitem {i} rc={rc}")
+            replaced += int(res["replaced"][0])
+        t0 = time.perf_counter()
+        st.flush()
+        t_flush = time.perf_counter() - t0
+        total = time.perf_counter() - t_all
+        s = st.stats()
+        out = {"calls": calls, "record_bytes": raw // calls, "chunks": int(s["chunks"]),
+               "defer_bytes": defer_mb << 20, "flushes": int(s["deferred_flushes"]),
+               "ms_per_call_first1000": round(float(ts[:1000].mean()) * 1e3, 4),
+               "ms_per_call_last1000": round(float(ts[-1000:].mean()) * 1e3, 4),
+               "ms_per_call_max": round(float(ts.max()) * 1e3, 3), "final_flush_ms": round(t_flush * 1e3, 3),
+               "MBps": round(raw / total / 1e6, 3), "replaced": replaced,
+               "deferred_mismatch": int(s["deferred_mismatch"])}
+        ref = _refdig.load(4, 0, calls)
+        if ref is not None:  # every record vs the reference fed the same records one call at a time
+            recs, sts = st.locate(keys)
+            r2 = np.zeros(calls, px.SET_RESULT_DTYPE)
+            r2["shard"], r2["chunk"], r2["idx"] = recs["shard"], recs["chunk"], recs["idx"]
+            import torch
+            cap = int(ref["get_len"].astype(np.int64).sum()) + 64 * calls + (1 << 20)
+            buf = torch.empty(cap, dtype=torch.uint8, device=torch.device("cuda", local))
+            rc, off, ln, gst, _ = st.get_batch_device(keys, buf.data_ptr(), cap, px.COMPAT)
+            chk = _refdig.check_store(ref, st, r2, buf, off, ln)
+            out["reference_check"] = dict(chk, fixture=os.path.relpath(_refdig.path(4, 0, calls), ROOT))
+    return out
 
 
 def cpu_calibration():
@@ -347,7 +386,7 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
         res = st.set_batch_device(n, kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), check=False)
         t_set = time.perf_counter() - t0
         sst = st.stats()
-        set_kms, walk_kms, emit_kms = sst["last_set_kernel_ms"], sst["last_walk_kernel_ms"], sst["last_emit_kernel_ms"]
+        set_kms, walk_kms, emit_kms = sst["last_set_stage_ms"], sst["last_encode_stage_ms"], sst["last_emit_kernel_ms"]
         psa = (sst["last_psa_ms"], int(sst["last_psa_shards"]), int(sst["last_walk_shards"]),
                sst["last_psa_sort_ms"], sst["last_psa_lcp_ms"], sst["last_psa_msg_ms"], int(sst["last_psa_iters"]),
                int(sst["last_psa_rounds"]), int(sst["last_psa_rotations"]), sst["last_psa_pool_ms"], int(sst["chunks"]))
@@ -393,8 +432,18 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
     T1 = time.perf_counter()
     r = {"corpus": corpus, "st": st, "runs": runs, "elapsed": T1 - T0, "n": n, "raw": raw_bytes,
          "out": out, "out_cap": out_cap, "keys_host": keys_host, "gathered": gathered[0]}
-    # exact-mode getitem (one timed call, outside the step loop) and parity counts
     last = runs[-1]
+    # every record against the reference's own output (per-record digests made from the
+    # compiled reference over the same corpus part and shards, tests/_refdig.py); only the
+    # canonical part 0 at full size has them
+    if rank == 0:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import _refdig
+        ref = _refdig.load(cfg, rps)
+        if ref is not None and int(ref["n"]) == n:
+            r["reference_check"] = dict(_refdig.check_store(ref, st, last["res"], out, last["off"], last["len"]),
+                                        fixture=os.path.relpath(_refdig.path(cfg, rps), ROOT))
+    # exact-mode getitem (one timed call, outside the step loop) and parity counts
     if a.no_exact:
         r["exact_s"], r["exact_dec_kms"], r["exact_exp"], r["exact_gather"] = 0.0, 0.0, 0, 0
         return r
@@ -414,6 +463,12 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
         ne_ce = _count_ne(out, last["off"], last["len"], out2, eoff, eln, dev)
         ne_eo = _count_ne(out2, eoff, eln, dbuf, doff[:-1], np.diff(doff), dev)
         r["parity_counts"] = {"records": n, "compat_ne_exact": ne_ce, "exact_ne_original": ne_eo}
+        if "reference_check" in r:
+            rc_ = r["reference_check"]
+            r["parity_counts"].update(compat_ne_reference=rc_["compat_ne_reference"],
+                                      comp_ne_reference=rc_["comp_ne_reference"],
+                                      placement_ne_reference=rc_["placement_ne_reference"],
+                                      reference_fixture=rc_["fixture"])
         del dbuf
     del out2
     return r
@@ -428,8 +483,13 @@ def check_gathered(cfg, r, rps, world, records, sample=300):
     import pixiu_amd as px
     from pixiu_amd import synth
     blobs = r["gathered"]
-    with px.Store(records_per_shard=rps) as st:
-        for b in blobs:
+    # every blob into one store; with records_per_shard = 0 (one shard: the reference's single
+    # instance) a store takes one blob only (px_load refuses a second into a non-empty single
+    # shard), so each rank's blob gets a store of its own
+    stores = [px.Store(records_per_shard=rps) for _ in (blobs if rps == 0 else [0])]
+    try:
+        for i, b in enumerate(blobs):
+            st = stores[i if rps == 0 else 0]
             if b.is_cuda:
                 st.load(b.data_ptr(), on_device=True, length=b.numel())
             else:
@@ -437,6 +497,7 @@ def check_gathered(cfg, r, rps, world, records, sample=300):
         checked = exact_eq = 0
         gathered_q = 0
         for rk in range(world):
+            st = stores[rk if rps == 0 else 0]
             cp = r["corpus"] if rk == 0 else synth.make(cfg, records, part=rk)
             rows = np.linspace(0, cp.n - 1, min(sample, cp.n)).astype(int).tolist()
             keys = [cp.key(i) for i in rows]
@@ -455,7 +516,11 @@ def check_gathered(cfg, r, rps, world, records, sample=300):
                 own_compat_eq = sum(x == y for x, y in zip(comp_loaded, comp_live))
         return {"ranks": world, "blob_bytes": [int(b.numel()) for b in blobs], "records_checked": checked,
                 "exact_equal": exact_eq, "rank0_compat_equal_live": own_compat_eq,
-                "rank0_gather_served": gathered_q, "records_per_rank_sampled": min(sample, r["n"])}
+                "rank0_gather_served": gathered_q, "records_per_rank_sampled": min(sample, r["n"]),
+                "stores": len(stores)}
+    finally:
+        for st in stores:
+            st.close()
 
 
 def check_single(r0):
@@ -717,6 +782,8 @@ def main():
             "psa_rounds": s0["encode_stage"].get("psa_rounds"),
             "encode_stage_ms": s0["kernel_ms"]["encode_stage"],
             "psa_split_ms": s0["encode_stage"].get("psa_split_ms"), "reference_check": check_single(r0)}
+        if "reference_check" in r0:  # every record's compat getitem / bytes / slot vs the reference's digests
+            line["single_instance"]["reference_digests"] = r0["reference_check"]
         if not a.no_cpu:
             c0 = cpu_single_instance(corpus, a.cpu_seconds)
             line["single_instance"]["cpu_baseline"] = {

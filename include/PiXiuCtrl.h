@@ -16,9 +16,19 @@
 // getitem and iter stream the compat expansion (PXSGen byte-for-byte).  Generators are
 // lazy: getitem only looks the record up and expands it (<= 64 KiB) at the first pull;
 // iter expands its records kIterWindow at a time as the caller advances, so host memory
-// stays bounded whatever the prefix matches.  reinsert(PiXiuChunk *&) compacts a closed
+// stays bounded whatever the prefix matches.  A generator pulled after free_prop() or
+// init_prop() yields nothing and reports PX_EINVAL in its `status` (an extension; the
+// reference's generators dangle there).  reinsert(PiXiuChunk *&) compacts a closed
 // slot-full chunk (PiXiuCtrl.cpp:88-114); chunk_at(seq) names one (an extension: the
 // reference reaches its chunks only through its internals).
+//
+// setitem is write-behind (px_opts.defer_bytes = kDeferBytes): a call queues its record
+// and returns the reference's value (0, or CBT_SET_REPLACE for a key already stored or
+// queued) at once; the queue is stored in one batch once kDeferBytes raw bytes are
+// pending, or before any read (getitem, contains, iter, delitem, the chunk view,
+// st.local_chunk.used_num).  So a stream of one-record calls costs one batch per
+// kDeferBytes instead of one suffix-array pass over the live chunk per call, with the
+// same stored bytes (include/pixiu_amd.h px_flush).
 #ifndef PIXIU_CTRL_FACADE_H
 #define PIXIU_CTRL_FACADE_H
 
@@ -43,12 +53,22 @@ struct PiXiuStr {  // compressed record as the reference lays it out (PiXiuStr.h
     uint8_t data[1];
 };
 
+// the context a PiXiuCtrl's generators expand through: free_prop / init_prop bump the
+// epoch (and free_prop clears ctx), so a generator outliving them yields nothing instead
+// of reading a freed context or a slot that now holds another record
+struct PxHandle {
+    px_ctx *ctx = nullptr;
+    uint64_t epoch = 0;
+};
+
 // PiXiuStr::parse(0, PXSG_MAX_TO)'s generator: the record is addressed at getitem time and
 // expanded on the GPU at the first pull (or handed over already expanded by CBTGen).
 struct PXSGen {
-    px_ctx *ctx = nullptr;
+    std::shared_ptr<PxHandle> h;
+    uint64_t epoch = 0;
     px_rec rec{};
     bool ready = false;
+    int status = PX_OK;  // extension: PX_OK, or why the expansion failed (then nothing is yielded)
     std::vector<uint8_t> buf;
     size_t cur = 0;
 
@@ -65,17 +85,24 @@ struct PXSGen {
   private:
     void expand() {
         ready = true;
+        if (!h || !h->ctx || h->epoch != epoch) {  // free_prop / init_prop since getitem
+            status = PX_EINVAL;
+            buf.clear();
+            return;
+        }
         // a compat expansion is at most PXSG_MAX_TO + 1 bytes (the over-yield of a range
         // ending inside a 251 pair); the call reports the exact need if it is short
         buf.resize(PXSG_MAX_TO + 1024);
         uint64_t off = 0, need = 0;
-        uint32_t len = 0, status = 0;
-        int rc = px_parse_batch(ctx, 1, &rec, PX_COMPAT, buf.data(), buf.size(), 0, &off, &len, &status, &need);
+        uint32_t len = 0, st = PX_EINVAL;
+        int rc = px_parse_batch(h->ctx, 1, &rec, PX_COMPAT, buf.data(), buf.size(), 0, &off, &len, &st, &need);
         if (rc == PX_ESPACE) {
             buf.resize(need);
-            rc = px_parse_batch(ctx, 1, &rec, PX_COMPAT, buf.data(), buf.size(), 0, &off, &len, &status, &need);
+            st = PX_EINVAL;
+            rc = px_parse_batch(h->ctx, 1, &rec, PX_COMPAT, buf.data(), buf.size(), 0, &off, &len, &st, &need);
         }
-        if (rc != PX_OK || status != PX_OK) {
+        if (rc != PX_OK || st != PX_OK) {
+            status = rc != PX_OK ? rc : (int)st;
             buf.clear();
             return;
         }
@@ -89,18 +116,22 @@ struct PXSGen {
 // expanded kIterWindow at a time, one batch per window, as the caller advances.
 struct CBTGen {
     static constexpr uint32_t kIterWindow = 64;
-    px_ctx *ctx = nullptr;
+    std::shared_ptr<PxHandle> h;
+    uint64_t epoch = 0;
     std::vector<px_rec> recs;
     std::vector<std::vector<uint8_t>> win;  // expansions of recs[base .. base + win.size())
+    std::vector<int> win_st;                // and their statuses
     size_t cur = 0, base = 0;
 
     bool operator()(PXSGen *&rv) {
         if (cur >= recs.size()) return false;
         if (cur >= base + win.size()) fill(cur);
         rv = new PXSGen();
-        rv->ctx = ctx;
+        rv->h = h;
+        rv->epoch = epoch;
         rv->rec = recs[cur];
         rv->ready = true;
+        rv->status = win_st[cur - base];
         rv->buf = std::move(win[cur - base]);
         ++cur;
         return true;
@@ -109,22 +140,27 @@ struct CBTGen {
   private:
     void fill(size_t at) {
         const uint32_t n = (uint32_t)std::min<size_t>(kIterWindow, recs.size() - at);
-        std::vector<uint8_t> out((size_t)n * (PXSG_MAX_TO + 1024));
-        std::vector<uint64_t> off(n);
-        std::vector<uint32_t> len(n), status(n);
-        uint64_t need = 0;
-        int rc = px_parse_batch(ctx, n, recs.data() + at, PX_COMPAT, out.data(), out.size(), 0, off.data(), len.data(),
-                                status.data(), &need);
-        if (rc == PX_ESPACE) {
-            out.resize(need);
-            rc = px_parse_batch(ctx, n, recs.data() + at, PX_COMPAT, out.data(), out.size(), 0, off.data(), len.data(),
-                                status.data(), &need);
-        }
         base = at;
         win.assign(n, std::vector<uint8_t>());
-        for (uint32_t i = 0; i < n; ++i)
-            if (status[i] == PX_OK)
-                win[i].assign(out.begin() + (long)off[i], out.begin() + (long)(off[i] + len[i]));
+        win_st.assign(n, PX_EINVAL);  // (a window that cannot be expanded yields failed generators)
+        if (!h || !h->ctx || h->epoch != epoch) return;
+        std::vector<uint8_t> out((size_t)n * (PXSG_MAX_TO + 1024));
+        std::vector<uint64_t> off(n);
+        std::vector<uint32_t> len(n), status(n, PX_EINVAL);
+        uint64_t need = 0;
+        int rc = px_parse_batch(h->ctx, n, recs.data() + at, PX_COMPAT, out.data(), out.size(), 0, off.data(),
+                                len.data(), status.data(), &need);
+        if (rc == PX_ESPACE) {
+            out.resize(need);
+            std::fill(status.begin(), status.end(), (uint32_t)PX_EINVAL);
+            rc = px_parse_batch(h->ctx, n, recs.data() + at, PX_COMPAT, out.data(), out.size(), 0, off.data(),
+                                len.data(), status.data(), &need);
+        }
+        for (uint32_t i = 0; i < n; ++i) {
+            // a failed call leaves its per-record statuses unwritten: every record fails with it
+            win_st[i] = rc != PX_OK && rc != (int)status[i] && status[i] == PX_OK ? rc : (int)status[i];
+            if (win_st[i] == PX_OK) win[i].assign(out.begin() + (long)off[i], out.begin() + (long)(off[i] + len[i]));
+        }
     }
 };
 
@@ -153,8 +189,16 @@ struct PiXiuChunk {
     PiXiuStr *getitem(int idx);
 };
 
+// PiXiuLocalChunk::used_num (the live chunk's record count, main.cpp:67): reading it
+// stores the write-behind queue first, so it counts every record set so far
+struct UsedNum {
+    PiXiuCtrl *owner = nullptr;
+    uint16_t n = 0;
+    operator uint16_t() const;
+};
+
 struct PiXiuLocalChunk {
-    uint16_t used_num = 0;
+    UsedNum used_num;
 };
 
 struct SuffixTree {
@@ -165,23 +209,39 @@ struct SuffixTree {
 struct CritBitTree {};
 
 struct PiXiuCtrl {
+    static constexpr uint32_t kDeferBytes = 8u << 20;  // write-behind queue of setitem (raw bytes)
     CritBitTree cbt;
     SuffixTree st;
     px_ctx *ctx = nullptr;
     PiXiuChunk chunk_view;
     int device = 0;
 
-    int setitem(uint8_t k[], int k_len, uint8_t v[], int v_len, bool = false) {
-        uint64_t koff[2] = {0, (uint64_t)k_len}, voff[2] = {0, (uint64_t)(v_len > 0 ? v_len : 0)};
-        uint8_t dummy = 0;
+    // PiXiuCtrl::setitem (PiXiuCtrl.cpp:12-47).  k_len == v_len == 0: k is a ready
+    // PiXiuStr doc (the reinsert path, PiXiuCtrl.cpp:39-40), stored as it is; `reinsert`
+    // skips the Glob_Reinsert_Chunk trigger (:26-29).  Returns 0, CBT_SET_REPLACE, or
+    // -px_status for an input the reference would assert on.
+    int setitem(uint8_t k[], int k_len, uint8_t v[], int v_len, bool reinsert = false) {
         px_set_result r;
-        int rc = px_set_batch(ctx, 1, k, koff, v ? v : &dummy, voff, 0, &r);
-        if (rc != PX_OK) return -rc;
-        if (r.chunk != chunk_view.chunk) {  // chunk rotation (PiXiuCtrl.cpp:13-25)
-            chunk_view.chunk = r.chunk;
-            chunk_view.cache.clear();
+        int rc;
+        if (!k_len && !v_len) {
+            if (!k) return -PX_EINVAL;
+            const PiXiuStr *doc = reinterpret_cast<const PiXiuStr *>(k);
+            uint64_t doff[2] = {0, doc->len};
+            rc = px_set_docs(ctx, 1, doc->data, doff, 0, reinsert ? 1 : 0, &r);
+        } else if (!k_len) {
+            return -PX_EINVAL;  // (the reference asserts k_len, PiXiuCtrl.cpp:42)
+        } else {
+            uint64_t koff[2] = {0, (uint64_t)k_len}, voff[2] = {0, (uint64_t)(v_len > 0 ? v_len : 0)};
+            uint8_t dummy = 0;
+            rc = px_set_batch(ctx, 1, k, koff, v ? v : &dummy, voff, 0, &r);
         }
-        st.local_chunk.used_num = (uint16_t)(r.idx + 1);
+        if (rc != PX_OK) return -rc;
+        if (r.chunk == PX_PENDING) {
+            pending = true;
+        } else {
+            pending = false;
+            apply(r);
+        }
         return (int)r.replaced;
     }
 
@@ -199,7 +259,8 @@ struct PiXiuCtrl {
         uint32_t status = 0;
         if (px_locate_batch(ctx, 1, k, koff, &r, &status) != PX_OK || status != PX_OK) return nullptr;
         PXSGen *g = new PXSGen();
-        g->ctx = ctx;
+        g->h = h;
+        g->epoch = h->epoch;
         g->rec = r;
         return g;
     }
@@ -215,7 +276,8 @@ struct PiXiuCtrl {
         }
         if (rc != PX_OK) return nullptr;
         CBTGen *g = new CBTGen();
-        g->ctx = ctx;
+        g->h = h;
+        g->epoch = h->epoch;
         recs.resize(n);
         g->recs = std::move(recs);
         return g;
@@ -234,20 +296,31 @@ struct PiXiuCtrl {
             memset(&o, 0, sizeof o);
             o.device = device;
             o.records_per_shard = 0;  // one shard: the reference's single instance
+            o.defer_bytes = kDeferBytes;
             ctx = px_open(&o);
         } else {
             px_reset(ctx);
         }
+        if (!h) h = std::make_shared<PxHandle>();
+        h->ctx = ctx;
+        h->epoch++;
+        pending = false;
         chunk_view = PiXiuChunk();
         chunk_view.owner = this;
         closed.clear();
         st.cbt_chunk = &chunk_view;
-        st.local_chunk.used_num = 0;
+        st.local_chunk.used_num.owner = this;
+        st.local_chunk.used_num.n = 0;
     }
 
     void free_prop(void) {
-        if (ctx) px_close(ctx);
+        if (ctx) px_close(ctx);  // (drops the write-behind queue, as the reference frees everything)
         ctx = nullptr;
+        if (h) {
+            h->ctx = nullptr;
+            h->epoch++;
+        }
+        pending = false;
         st.cbt_chunk = nullptr;
         closed.clear();
     }
@@ -257,6 +330,7 @@ struct PiXiuCtrl {
     // by the pool count, on which the reference dereferences NULL) are left as they are.
     void reinsert(PiXiuChunk *&chunk) {
         if (!chunk || !ctx) return;
+        sync_pending();
         if (px_reinsert(ctx, 0, chunk->chunk) == PX_OK) {
             closed.erase(chunk->chunk);
             chunk = nullptr;
@@ -265,6 +339,7 @@ struct PiXiuCtrl {
 
     // extension: the chunk with sequence number `seq` (0 = the first), for reinsert
     PiXiuChunk *chunk_at(uint32_t seq) {
+        sync_pending();
         if (seq == chunk_view.chunk) return &chunk_view;
         auto &p = closed[seq];
         if (!p) {
@@ -275,12 +350,38 @@ struct PiXiuCtrl {
         return p.get();
     }
 
+    // stores the write-behind queue and brings the live-chunk view up to date
+    void sync_pending() {
+        if (!pending || !ctx) return;
+        pending = false;
+        px_set_result last;
+        memset(&last, 0xff, sizeof last);  // (chunk 0xffffffff: nothing placed)
+        (void)px_flush(ctx, &last);
+        apply(last);
+    }
+
   private:
+    void apply(const px_set_result &r) {
+        if (r.chunk == 0xffffffffu) return;  // (not placed)
+        if (r.chunk != chunk_view.chunk) {   // chunk rotation (PiXiuCtrl.cpp:13-25)
+            chunk_view.chunk = r.chunk;
+            chunk_view.cache.clear();
+        }
+        st.local_chunk.used_num.n = (uint16_t)(r.idx + 1);
+    }
+    std::shared_ptr<PxHandle> h;
+    bool pending = false;
     std::map<uint32_t, std::unique_ptr<PiXiuChunk>> closed;
 };
 
+inline UsedNum::operator uint16_t() const {
+    if (owner) owner->sync_pending();
+    return n;
+}
+
 inline PiXiuStr *PiXiuChunk::getitem(int idx) {
     if (idx < 0) return nullptr;
+    if (owner) owner->sync_pending();
     if ((size_t)idx >= cache.size()) cache.resize((size_t)idx + 1);
     std::vector<uint8_t> &c = cache[(size_t)idx];
     if (c.empty()) {

@@ -15,6 +15,8 @@
  * Reference interfaces replaced (file:line in Thunderchen/PiXiu src/):
  *   px_open / px_close ........ PiXiuCtrl::init_prop / free_prop   (PiXiuCtrl.cpp:77-86)
  *   px_set_batch .............. PiXiuCtrl::setitem                  (PiXiuCtrl.cpp:12-47)
+ *   px_set_docs ............... PiXiuCtrl::setitem(k, 0, NULL, 0, reinsert)  (PiXiuCtrl.cpp:26-40, ready docs)
+ *   px_flush .................. (none: the write-behind queue of one-record setitem calls)
  *   px_get_batch .............. PiXiuCtrl::getitem + PXSGen drain   (PiXiuCtrl.cpp:59-61, PiXiuStr.h:129-198)
  *   px_contains_batch ......... PiXiuCtrl::contains                 (PiXiuCtrl.cpp:55-57)
  *   px_del_batch .............. PiXiuCtrl::delitem                  (PiXiuCtrl.cpp:63-69)
@@ -60,6 +62,13 @@ typedef struct px_opts {
     uint32_t decode_depth;      /* frames per decode stack; 0 = 4096 */
     uint32_t decode_waves;      /* concurrent decode wavefronts; 0 = one per query, up to 16,384 */
     uint32_t host_threads;      /* host threads for batch key lookups; 0 = min(16, cores) */
+    uint32_t defer_bytes;       /* write-behind of host px_set_batch calls (records_per_shard == 0
+                                   only): records are queued and stored together once this many
+                                   raw bytes are pending, or by px_flush / any other call on the
+                                   context; 0 = off (every call stores at once).  See px_flush. */
+    uint32_t retain_mb;         /* device memory the heap keeps cached in wholly free slabs after a
+                                   set batch (the rest goes back to the driver); 0 = 8,192 MiB,
+                                   0xffffffff = keep everything */
 } px_opts;
 
 typedef struct px_ctx px_ctx;
@@ -69,12 +78,15 @@ typedef struct px_set_result {
     uint32_t status;   /* px_status */
     uint32_t replaced; /* 1 = CBT_SET_REPLACE (duplicate key in the same shard) */
     uint32_t shard;
-    uint32_t chunk;    /* chunk sequence number inside the shard (rotation count) */
-    uint32_t idx;      /* chunk-local slot (the `idx` that references point at) */
-    uint32_t comp_len; /* compressed length */
+    uint32_t chunk;    /* chunk sequence number inside the shard (rotation count); PX_PENDING
+                          while a deferred record waits in the write-behind queue */
+    uint32_t idx;      /* chunk-local slot (the `idx` that references point at); PX_PENDING */
+    uint32_t comp_len; /* compressed length; PX_PENDING */
     uint32_t doc_len;  /* escaped doc length (esc(k)+[251,0]+esc(v)+[251,2]) */
     uint32_t pad;
 } px_set_result;
+
+#define PX_PENDING 0xffffffffu /* px_set_result field of a record still in the write-behind queue */
 
 /* a stored record, as addressed by px_parse_batch / px_export */
 typedef struct px_rec {
@@ -86,10 +98,16 @@ typedef struct px_stats {
     uint64_t records, shards, chunks;
     uint64_t raw_bytes, doc_bytes, comp_bytes;
     uint64_t ub_reads;        /* reads the reference makes out of bounds (UB there) */
-    uint64_t device_bytes;    /* device memory held */
-    double last_set_kernel_ms;    /* k_gst_encode + k_gst_emit time of the last px_set_batch */
-    double last_decode_kernel_ms; /* k_decode time of the last get/parse batch */
-    double last_walk_kernel_ms;   /* k_gst_encode (suffix-tree walk -> encoder messages) alone */
+    uint64_t device_bytes;    /* device memory held by the context's heap now (live + cached free) */
+    double last_set_stage_ms;     /* GPU events around the encode stage and k_gst_emit of the last
+                                     px_set_batch (= last_encode_stage_ms + last_emit_kernel_ms) */
+    double last_decode_kernel_ms; /* the getitem stage of the last get/parse batch: k_gather + k_decode
+                                     (GPU events around both launches) */
+    double last_encode_stage_ms;  /* the encode stage alone -- the text -> encoder-message pass: the
+                                     suffix-array pipeline (px_psa.hip, incl. its host-driven steps)
+                                     for suffix-array shards and k_gst_encode for walked ones, GPU
+                                     events from before the first to after the last of its kernels.
+                                     bench.py's roofline.achieved divides by this */
     double last_emit_kernel_ms;   /* k_gst_emit (stream encoder -> compressed bytes) alone */
     double last_get_lookup_ms;    /* host key -> record lookups of the last px_get_batch */
     double last_get_call_ms;      /* wall time inside the last px_get_batch call */
@@ -106,6 +124,13 @@ typedef struct px_stats {
     uint64_t last_psa_rounds;     /* suffix-array rounds of the last px_set_batch (one per chunk window) */
     uint64_t last_psa_rotations;  /* chunk rotations the suffix-array path found in it (MemPool emulation) */
     double last_psa_pool_ms;      /* MemPool emulation: leaves, split candidates, pool scan (GPU events) */
+    uint64_t device_live_bytes;   /* device memory in use by stored data (records, indexes, arenas) */
+    uint64_t device_peak_bytes;   /* the most the heap has held (set-batch scratch at its peak) */
+    uint64_t deferred_records;    /* records that went through the write-behind queue */
+    uint64_t deferred_flushes;    /* write-behind flushes (each one px_set_batch of the queue) */
+    uint64_t deferred_mismatch;   /* deferred records whose `replaced`, returned at call time, differed
+                                     from the stored result (only possible when a queued record's
+                                     compat-decoded key is not its key: reported, never hidden) */
 } px_stats;
 
 px_ctx *px_open(const px_opts *opts);
@@ -119,6 +144,24 @@ const char *px_strerror(int status);
  * record was stored, else the first failing status (others may have succeeded). */
 int px_set_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff,
                  const uint8_t *vals, const uint64_t *voff, int on_device, px_set_result *res);
+
+/* Ready docs (PiXiuCtrl::setitem(k, 0, NULL, 0, reinsert), PiXiuCtrl.cpp:26-40): record i
+ * is the escaped doc docs[doff[i] .. doff[i+1]) as PiXiuStr::data holds it, stored without
+ * escaping; its CritBit key is its prefix through the first 251,0.  reinsert != 0 skips
+ * the Glob_Reinsert_Chunk trigger (PiXiuCtrl.cpp:26-29), as the reference's flag does. */
+int px_set_docs(px_ctx *ctx, uint32_t n, const uint8_t *docs, const uint64_t *doff, int on_device, int reinsert,
+                px_set_result *res);
+
+/* Store every record of the write-behind queue (opts.defer_bytes).  A deferred px_set_batch
+ * returns at once: status PX_OK (or PX_EINVAL for an invalid record, which is not queued),
+ * `replaced` resolved at call time from the CritBit of the stored records and the queued
+ * keys (a key equal to a queued one flushes the queue first), doc_len, and PX_PENDING for
+ * chunk / idx / comp_len.  Every other call on the context flushes first, so reads always
+ * see every record set before them; px_reset / px_close drop the queue.  Chunk rotation
+ * depends only on the doc order, so the stored bytes equal those of one call per record.
+ * last (may be NULL): the result of the most recently stored record.  Returns PX_OK, or
+ * the first failing status among the records stored since the previous px_flush. */
+int px_flush(px_ctx *ctx, px_set_result *last);
 
 /* Batch getitem: keys are host CSR.  The expanded doc of key i lands in
  * out[out_off[i] .. out_off[i] + out_len[i]) (out is a device pointer when

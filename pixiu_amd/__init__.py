@@ -27,6 +27,7 @@ STATUS = {
     5: "PX_EHANG", 6: "PX_EDEPTH", 7: "PX_ESPACE", 8: "PX_ENOTFOUND", 9: "PX_EHIP", 10: "PX_ENOMEM",
 }
 PX_OK, PX_EINVAL, PX_ESPACE, PX_ENOTFOUND = 0, 1, 7, 8
+PX_PENDING = 0xFFFFFFFF  # px_set_result chunk / idx / comp_len of a record in the write-behind queue
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -44,7 +45,8 @@ class PxError(RuntimeError):
 
 class PxOpts(C.Structure):
     _fields_ = [("device", C.c_int), ("records_per_shard", C.c_uint32), ("decode_depth", C.c_uint32),
-                ("decode_waves", C.c_uint32), ("host_threads", C.c_uint32)]
+                ("decode_waves", C.c_uint32), ("host_threads", C.c_uint32), ("defer_bytes", C.c_uint32),
+                ("retain_mb", C.c_uint32)]
 
 
 class PxSetResult(C.Structure):
@@ -62,14 +64,17 @@ class PxStats(C.Structure):
     _fields_ = [("records", C.c_uint64), ("shards", C.c_uint64), ("chunks", C.c_uint64),
                 ("raw_bytes", C.c_uint64), ("doc_bytes", C.c_uint64), ("comp_bytes", C.c_uint64),
                 ("ub_reads", C.c_uint64), ("device_bytes", C.c_uint64),
-                ("last_set_kernel_ms", C.c_double), ("last_decode_kernel_ms", C.c_double),
-                ("last_walk_kernel_ms", C.c_double), ("last_emit_kernel_ms", C.c_double),
+                ("last_set_stage_ms", C.c_double), ("last_decode_kernel_ms", C.c_double),
+                ("last_encode_stage_ms", C.c_double), ("last_emit_kernel_ms", C.c_double),
                 ("last_get_lookup_ms", C.c_double), ("last_get_call_ms", C.c_double),
                 ("last_psa_ms", C.c_double), ("last_psa_shards", C.c_uint64), ("last_walk_shards", C.c_uint64),
                 ("last_psa_sort_ms", C.c_double), ("last_psa_lcp_ms", C.c_double), ("last_psa_msg_ms", C.c_double),
                 ("last_psa_iters", C.c_uint64), ("span_entries", C.c_uint64), ("last_gather_queries", C.c_uint64),
                 ("last_span_build_ms", C.c_double), ("last_psa_rounds", C.c_uint64),
-                ("last_psa_rotations", C.c_uint64), ("last_psa_pool_ms", C.c_double)]
+                ("last_psa_rotations", C.c_uint64), ("last_psa_pool_ms", C.c_double),
+                ("device_live_bytes", C.c_uint64), ("device_peak_bytes", C.c_uint64),
+                ("deferred_records", C.c_uint64), ("deferred_flushes", C.c_uint64),
+                ("deferred_mismatch", C.c_uint64)]
 
 
 SET_RESULT_DTYPE = np.dtype([("status", "<u4"), ("replaced", "<u4"), ("shard", "<u4"), ("chunk", "<u4"),
@@ -79,7 +84,8 @@ REC_DTYPE = np.dtype([("shard", "<u4"), ("chunk", "<u4"), ("idx", "<u4"), ("from
 # every symbol include/pixiu_amd.h declares
 EXPORTS = ["px_open", "px_close", "px_strerror", "px_set_batch", "px_get_batch", "px_parse_batch",
            "px_contains_batch", "px_del_batch", "px_export", "px_stats_get", "px_stream", "px_reset",
-           "px_last_store", "px_import_chunk", "px_iter", "px_save", "px_load", "px_locate_batch", "px_reinsert"]
+           "px_last_store", "px_import_chunk", "px_iter", "px_save", "px_load", "px_locate_batch", "px_reinsert",
+           "px_set_docs", "px_flush"]
 
 _LIB = None
 
@@ -116,6 +122,8 @@ def load_library() -> C.CDLL:
     lib.px_load.argtypes = [vp, vp, u64, i32, vp]
     lib.px_locate_batch.argtypes = [vp, u32, vp, vp, vp, vp]
     lib.px_reinsert.argtypes = [vp, u32, u32]
+    lib.px_set_docs.argtypes = [vp, u32, vp, vp, i32, i32, vp]
+    lib.px_flush.argtypes = [vp, vp]
     _LIB = lib
     return lib
 
@@ -140,9 +148,12 @@ class Store:
     i.e. exactly the reference's single PiXiuCtrl instance."""
 
     def __init__(self, records_per_shard: int = 0, device: int = 0, decode_depth: int = 0,
-                 decode_waves: int = 0, host_threads: int = 0):
+                 decode_waves: int = 0, host_threads: int = 0, defer_bytes: int = 0, retain_mb: int = 0):
+        """defer_bytes > 0 (records_per_shard == 0 only): host set_batch calls go through the
+        write-behind queue (px_flush); retain_mb: cached free device memory kept after a set
+        batch (0: 8 GiB, 0xFFFFFFFF: all)."""
         self._lib = load_library()
-        opts = PxOpts(device, records_per_shard, decode_depth, decode_waves, host_threads)
+        opts = PxOpts(device, records_per_shard, decode_depth, decode_waves, host_threads, defer_bytes, retain_mb)
         h = self._lib.px_open(C.byref(opts))
         if not h:
             raise PxError(9, "px_open (no usable HIP device?)")
@@ -183,6 +194,25 @@ class Store:
         rc = self._lib.px_set_batch(self._h, n, _ptr(kb), _ptr(ko), _ptr(vb), _ptr(vo), 0, _ptr(res))
         if check and rc != PX_OK:
             raise PxError(rc, "px_set_batch")
+        return res
+
+    def set_docs(self, docs, reinsert: bool = False, *, check: bool = True) -> np.ndarray:
+        """Ready escaped docs (PiXiuCtrl::setitem(k, 0, NULL, 0, reinsert)): list of bytes."""
+        db, do = docs if isinstance(docs, tuple) else csr(docs)
+        db, do = np.ascontiguousarray(db, np.uint8), np.ascontiguousarray(do, np.uint64)
+        n = len(do) - 1
+        res = np.zeros(n, SET_RESULT_DTYPE)
+        rc = self._lib.px_set_docs(self._h, n, _ptr(db), _ptr(do), 0, int(reinsert), _ptr(res))
+        if check and rc != PX_OK:
+            raise PxError(rc, "px_set_docs")
+        return res
+
+    def flush(self) -> np.ndarray:
+        """Store the write-behind queue; returns the last stored record's result (1 entry)."""
+        res = np.zeros(1, SET_RESULT_DTYPE)
+        rc = self._lib.px_flush(self._h, _ptr(res))
+        if rc != PX_OK:
+            raise PxError(rc, "px_flush")
         return res
 
     def set_batch_device(self, n: int, keys_ptr: int, koff_ptr: int, vals_ptr: int, voff_ptr: int,

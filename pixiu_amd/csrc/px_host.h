@@ -50,6 +50,7 @@ class BlockHeap {
             if (!s) return nullptr;
             slabs_.emplace(s, s + sz);
             held_ += sz;
+            peak_ = std::max(peak_, held_);
             add_free(s, sz);
             it = by_size_.lower_bound(n);
         }
@@ -92,6 +93,29 @@ class BlockHeap {
         add_free(p, sz);
     }
     uint64_t held() const { return held_; }
+    uint64_t peak() const { return peak_; }
+    // Give wholly free slabs back to Raw (largest first) until the free bytes cached in
+    // the slabs still held are <= keep; returns the bytes given back.
+    uint64_t trim(uint64_t keep) {
+        uint64_t free_b = cached_free(), back = 0;
+        if (free_b <= keep) return 0;
+        std::vector<std::pair<uint64_t, char *>> whole;  // (size, start) of wholly free slabs
+        for (const auto &s : slabs_) {
+            auto f = by_addr_.find(s.first);
+            if (f != by_addr_.end() && f->second == (uint64_t)(s.second - s.first)) whole.emplace_back(f->second, s.first);
+        }
+        std::sort(whole.begin(), whole.end(), [](const auto &a, const auto &b) { return a.first > b.first; });
+        for (const auto &w : whole) {
+            if (free_b <= keep) break;
+            erase_free(w.second, w.first);
+            slabs_.erase(w.second);
+            Raw::put(w.second);
+            held_ -= w.first;
+            free_b -= w.first;
+            back += w.first;
+        }
+        return back;
+    }
     uint64_t cached_free() const {  // bytes in free blocks of the slabs already held
         uint64_t f = 0;
         for (const auto &b : by_addr_) f += b.second;
@@ -121,7 +145,7 @@ class BlockHeap {
     std::map<char *, uint64_t> by_addr_;
     std::multimap<uint64_t, char *> by_size_;
     std::unordered_map<void *, uint64_t> live_;
-    uint64_t held_ = 0;
+    uint64_t held_ = 0, peak_ = 0;
 };
 
 // ---------------------------------------------------------------- key maps

@@ -290,6 +290,45 @@ struct px_ctx {
     px_stats stats{};
     int last_hip = 0;
 
+    // ------------------------------------------------------------ write-behind queue
+    // (opts.defer_bytes, records_per_shard == 0: the facade's one-record setitem calls).
+    // Queued records are stored together by flush_queue(), before any other call on the
+    // context and once defer_bytes raw bytes are pending.  The stored bytes equal those of
+    // one call per record: chunk rotation and the reinsert triggers depend only on the
+    // doc order, which the queue keeps, and set_ctrl evaluates the triggers between
+    // records exactly as it does for a one-record call.
+    std::vector<uint8_t> dq_k, dq_v;          // queued keys / values (host CSR)
+    std::vector<uint64_t> dq_ko{0}, dq_vo{0};
+    std::vector<uint32_t> dq_pred;            // `replaced` as returned at call time
+    std::unordered_set<std::string> dq_keys;  // their escaped keys
+    px_set_result last_res{};                 // the most recently stored record's result
+    bool have_last = false;
+    int dq_rc = PX_OK;                        // first failure among flushed records since px_flush
+    bool defer_on() const { return opts.defer_bytes != 0 && opts.records_per_shard == 0; }
+    int set_deferred(uint32_t n, const uint8_t *keys, const uint64_t *koff, const uint8_t *vals,
+                     const uint64_t *voff, px_set_result *res);
+    int flush_queue();
+    void drop_queue() {
+        dq_k.clear();
+        dq_v.clear();
+        dq_ko.assign(1, 0);
+        dq_vo.assign(1, 0);
+        dq_pred.clear();
+        dq_keys.clear();
+    }
+    void note_last(uint32_t n, const px_set_result *res) {
+        if (n && res) {
+            last_res = res[n - 1];
+            have_last = true;
+        }
+    }
+    // cached free device memory kept after a set batch (opts.retain_mb)
+    void trim_heap() {
+        const uint64_t keep = opts.retain_mb == 0xffffffffu ? ~0ull
+                              : (uint64_t)(opts.retain_mb ? opts.retain_mb : 8192u) << 20;
+        heap.trim(keep);
+    }
+
     // ------------------------------------------------------------ helpers
     // Host->device copies are staged in buffers owned until the next sync(), so the
     // caller's (pageable, possibly short-lived) source may go away immediately.
@@ -674,6 +713,9 @@ struct px_ctx {
         esc_key_into(q, k, n);
         return q;
     }
+    // the CritBit key of a set input: the escaped key, or a ready doc's prefix through its
+    // first 251,0 (raw_docs)
+    std::string crit_key(const uint8_t *k, uint64_t n) const;
 
     Shard *shard_for_key(const uint8_t *k, uint64_t n) const {
         if (opts.records_per_shard == 0) return shards.empty() ? nullptr : shards[0].get();
@@ -1324,6 +1366,11 @@ uint32_t key_end(const uint8_t *p, uint32_t n) {
 }
 }  // namespace
 
+std::string px_ctx::crit_key(const uint8_t *k, uint64_t n) const {
+    if (!raw_docs) return esc_key(k, n);
+    return std::string(reinterpret_cast<const char *>(k), key_end(k, (uint32_t)n));
+}
+
 int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, const uint8_t *vals,
                       const uint64_t *voff, int on_device, px_set_result *res) {
     if (n == 0) return PX_OK;
@@ -1349,8 +1396,8 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
                 while (b < n && (ko[b + 1] - ko[a]) + (vo[b + 1] - vo[a]) <= kMaxBatchRaw) ++b;
                 const int r2 = set_batch(b - a, keys, koff + a, vals, voff + a, on_device, res ? res + a : nullptr);
                 if (rc == PX_OK) rc = r2;
-                acc.last_set_kernel_ms += stats.last_set_kernel_ms;
-                acc.last_walk_kernel_ms += stats.last_walk_kernel_ms;
+                acc.last_set_stage_ms += stats.last_set_stage_ms;
+                acc.last_encode_stage_ms += stats.last_encode_stage_ms;
                 acc.last_emit_kernel_ms += stats.last_emit_kernel_ms;
                 acc.last_psa_ms += stats.last_psa_ms;
                 acc.last_psa_sort_ms += stats.last_psa_sort_ms;
@@ -1365,8 +1412,8 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
                 acc.last_psa_iters = std::max(acc.last_psa_iters, stats.last_psa_iters);
                 a = b;
             }
-            stats.last_set_kernel_ms = acc.last_set_kernel_ms;
-            stats.last_walk_kernel_ms = acc.last_walk_kernel_ms;
+            stats.last_set_stage_ms = acc.last_set_stage_ms;
+            stats.last_encode_stage_ms = acc.last_encode_stage_ms;
             stats.last_emit_kernel_ms = acc.last_emit_kernel_ms;
             stats.last_psa_ms = acc.last_psa_ms;
             stats.last_psa_sort_ms = acc.last_psa_sort_ms;
@@ -1841,9 +1888,9 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     {
         float ms = 0;
         hcheck(hipEventElapsedTime(&ms, ev0, ev1));
-        stats.last_set_kernel_ms = ms;
+        stats.last_set_stage_ms = ms;
         hcheck(hipEventElapsedTime(&ms, ev0, ev_mid));
-        stats.last_walk_kernel_ms = ms;
+        stats.last_encode_stage_ms = ms;
         hcheck(hipEventElapsedTime(&ms, ev_mid, ev1));
         stats.last_emit_kernel_ms = ms;
     }
@@ -2091,6 +2138,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     uint64_t ub = 0;
     for (auto &sp : shards) ub += sp->hs.ub_reads;
     stats.ub_reads = ub;
+    trim_heap();
     stats.device_bytes = heap.held();
     for (uint32_t r = 0; r < n; ++r) {
         px_status st = map_status(rstatus[r]);
@@ -2341,7 +2389,7 @@ int px_ctx::set_ctrl(uint32_t n, const uint8_t *keys, const uint64_t *koff, cons
                 std::unordered_map<uint32_t, uint32_t> dec;
                 std::unordered_set<std::string> seen;
                 for (uint32_t r = pos; r < end; ++r) {
-                    std::string q = esc_key(keys + ko[r], ko[r + 1] - ko[r]);
+                    std::string q = crit_key(keys + ko[r], ko[r + 1] - ko[r]);
                     Leaf l;
                     if (!seen.insert(q).second || !cbt_lookup(*s, q, &l)) continue;
                     const Chunk &ch = chunks[l.chunk];
@@ -2359,6 +2407,80 @@ int px_ctx::set_ctrl(uint32_t n, const uint8_t *keys, const uint64_t *koff, cons
         if (rc == PX_OK) rc = r2;
         pos = end;
     }
+    return rc;
+}
+
+// Write-behind setitem (px_opts.defer_bytes; include/pixiu_amd.h px_flush).  `replaced`
+// (CBT_SET_REPLACE, CritBitTree.cpp:32-43) is resolved at call time: the key is in the
+// CritBit of the stored records (the same lookup contains() makes) or equals a queued
+// key -- and a key equal to a queued one flushes the queue first, so the earlier record
+// is stored and the lookup exact.  The one case this cannot see is a queued record
+// whose compat-decoded key (what the reference's CritBit compares, CritBitTree.cpp:27-28)
+// is not its key, i.e. the reference decoder's bug inside a key; flush_queue counts any
+// such difference in stats.deferred_mismatch and says so on stderr.
+int px_ctx::set_deferred(uint32_t n, const uint8_t *keys, const uint64_t *koff, const uint8_t *vals,
+                         const uint64_t *voff, px_set_result *res) {
+    std::string q;
+    int rc = PX_OK;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t *k = keys + koff[i];
+        const uint64_t kn = koff[i + 1] - koff[i], vn = voff[i + 1] - voff[i];
+        const uint8_t *v = vn ? vals + voff[i] : nullptr;
+        uint64_t esc = 0;
+        for (uint64_t j = 0; j < kn; ++j) esc += k[j] == kEsc;
+        for (uint64_t j = 0; j < vn; ++j) esc += v[j] == kEsc;
+        const uint64_t dl = kn + 2 + (vn ? vn + 2 : 0) + esc;  // PiXiuCtrl.cpp:31-44
+        px_set_result r{PX_OK, 0, 0, PX_PENDING, PX_PENDING, PX_PENDING, (uint32_t)dl, 0};
+        if (kn == 0 || dl > (uint64_t)kMaxDoc) {  // as k_doc_len: never placed
+            r = px_set_result{PX_EINVAL, 0, 0, 0xffffffffu, 0xffffffffu, 0, 0, 0};
+            if (rc == PX_OK) rc = PX_EINVAL;
+            if (res) res[i] = r;
+            continue;
+        }
+        esc_key_into(q, k, kn);
+        if (dq_keys.count(q)) flush_queue();
+        Shard *s = shards.empty() ? nullptr : shards[0].get();
+        r.replaced = (dq_keys.count(q) || (s && cbt_contains(*s, q))) ? 1u : 0u;
+        dq_k.insert(dq_k.end(), k, k + kn);
+        if (vn) dq_v.insert(dq_v.end(), v, v + vn);
+        dq_ko.push_back(dq_k.size());
+        dq_vo.push_back(dq_v.size());
+        dq_pred.push_back(r.replaced);
+        dq_keys.insert(q);
+        stats.deferred_records++;
+        if (res) res[i] = r;
+        if (dq_k.size() + dq_v.size() >= opts.defer_bytes || dq_pred.size() >= (size_t)kChunkSlots) flush_queue();
+    }
+    return rc;
+}
+
+int px_ctx::flush_queue() {
+    const uint32_t n = (uint32_t)dq_pred.size();
+    if (!n) return PX_OK;
+    std::vector<px_set_result> r(n);
+    uint8_t dummy = 0;
+    // (moved out first: set_ctrl's reinsert triggers may re-enter nothing here, and a
+    // failure below must not leave the records queued twice)
+    std::vector<uint8_t> k, v;
+    std::vector<uint64_t> ko, vo;
+    std::vector<uint32_t> pred;
+    k.swap(dq_k);
+    v.swap(dq_v);
+    ko.swap(dq_ko);
+    vo.swap(dq_vo);
+    pred.swap(dq_pred);
+    drop_queue();
+    stats.deferred_flushes++;
+    const int rc = set_ctrl(n, k.data(), ko.data(), v.empty() ? &dummy : v.data(), vo.data(), 0, r.data());
+    uint64_t mism = 0;
+    for (uint32_t i = 0; i < n; ++i) mism += r[i].status == PX_OK && r[i].replaced != pred[i];
+    if (mism) {
+        stats.deferred_mismatch += mism;
+        fprintf(stderr, "pixiu_amd: %llu deferred setitem result(s) returned replaced != the stored result "
+                        "(a queued record's compat-decoded key differs from its key)\n", (unsigned long long)mism);
+    }
+    note_last(n, r.data());
+    if (rc != PX_OK && dq_rc == PX_OK) dq_rc = rc;
     return rc;
 }
 
@@ -2735,10 +2857,78 @@ const char *px_strerror(int s) {
         return PX_ENOMEM;                                \
     }
 
+// every call but px_set_batch / px_flush / px_reset / px_close stores the write-behind
+// queue first, so reads see every record set before them
+#define PX_FLUSHED(ctx) (void)(ctx)->flush_queue()
+
 int px_set_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff, const uint8_t *vals,
                  const uint64_t *voff, int on_device, px_set_result *res) {
     if (!ctx || (n && (!keys || !koff || !voff))) return PX_EINVAL;
-    PX_GUARD(return ctx->set_ctrl(n, keys, koff, vals, voff, on_device, res);)
+    PX_GUARD({
+        if (ctx->defer_on() && !on_device && n && n <= 64)
+            return ctx->set_deferred(n, keys, koff, vals, voff, res);
+        PX_FLUSHED(ctx);
+        const int rc = ctx->set_ctrl(n, keys, koff, vals, voff, on_device, res);
+        ctx->note_last(n, res);
+        return rc;
+    })
+}
+
+int px_set_docs(px_ctx *ctx, uint32_t n, const uint8_t *docs, const uint64_t *doff, int on_device, int reinsert,
+                px_set_result *res) {
+    if (!ctx || (n && (!docs || !doff))) return PX_EINVAL;
+    PX_GUARD({
+        PX_FLUSHED(ctx);
+        std::vector<uint64_t> zero(n + 1, 0);
+        uint8_t dummy = 0;
+        struct Raw {  // raw_docs for the duration of the call, restored on every exit
+            px_ctx *c;
+            bool saved;
+            ~Raw() { c->raw_docs = saved; }
+        } raw{ctx, ctx->raw_docs};
+        ctx->raw_docs = true;
+        int rc = PX_OK;
+        if (!reinsert || ctx->opts.records_per_shard != 0) {
+            // (the Glob_Reinsert_Chunk trigger only exists for the single instance)
+            rc = ctx->set_ctrl(n, docs, doff, &dummy, zero.data(), on_device, res);
+        } else {
+            // setitem(doc, reinsert = true): the rotation trigger only (PiXiuCtrl.cpp:13-29),
+            // evaluated before every record as reinsert_chunk does
+            std::vector<uint64_t> ho(n + 1);
+            if (on_device) {
+                ctx->d2h(ho.data(), doff, (size_t)(n + 1) * 8);
+                ctx->sync();
+            } else {
+                std::memcpy(ho.data(), doff, (size_t)(n + 1) * 8);
+            }
+            for (uint32_t pos = 0; pos < n;) {
+                Shard *s = ctx->shards.empty() ? nullptr : ctx->shards[0].get();
+                uint32_t end = n;
+                if (s) {
+                    ctx->reinsert_triggers(*s, px_ctx::kTrigReinsert);
+                    const uint32_t room = (uint32_t)kChunkSlots - std::min<uint32_t>(s->hs.n_docs, kChunkSlots);
+                    end = std::min(n, pos + std::max(room, 1u));
+                }
+                const int r2 = ctx->set_batch(end - pos, docs, ho.data() + pos, &dummy, zero.data(), on_device,
+                                              res ? res + pos : nullptr);
+                if (rc == PX_OK) rc = r2;
+                pos = end;
+            }
+        }
+        ctx->note_last(n, res);
+        return rc;
+    })
+}
+
+int px_flush(px_ctx *ctx, px_set_result *last) {
+    if (!ctx) return PX_EINVAL;
+    PX_GUARD({
+        ctx->flush_queue();
+        if (last && ctx->have_last) *last = ctx->last_res;
+        const int rc = ctx->dq_rc;
+        ctx->dq_rc = PX_OK;
+        return rc;
+    })
 }
 
 int px_get_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff, int mode, uint8_t *out,
@@ -2746,6 +2936,7 @@ int px_get_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *k
                  uint64_t *needed) {
     if (!ctx || (n && (!keys || !koff || !out_off || !out_len || !status))) return PX_EINVAL;
     PX_GUARD({
+        PX_FLUSHED(ctx);
         const auto t0 = std::chrono::steady_clock::now();
         int rc;
         double lookup_ms = 0;
@@ -2780,6 +2971,7 @@ int px_parse_batch(px_ctx *ctx, uint32_t n, const px_rec *recs, int mode, uint8_
                    int out_on_device, uint64_t *out_off, uint32_t *out_len, uint32_t *status, uint64_t *needed) {
     if (!ctx || (n && (!recs || !out_off || !out_len || !status))) return PX_EINVAL;
     PX_GUARD({
+        PX_FLUSHED(ctx);
         std::vector<DecodeQuery> q(n);
         std::vector<uint32_t> pre(n, PX_OK);
         for (uint32_t i = 0; i < n; ++i) {
@@ -2808,6 +3000,7 @@ int px_locate_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t
                     uint32_t *status) {
     if (!ctx || (n && (!keys || !koff || !recs || !status))) return PX_EINVAL;
     PX_GUARD({
+        PX_FLUSHED(ctx);
         std::string ek;
         for (uint32_t i = 0; i < n; ++i) {
             DecodeQuery q;
@@ -2829,6 +3022,7 @@ int px_locate_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t
 int px_reinsert(px_ctx *ctx, uint32_t shard, uint32_t chunk) {
     if (!ctx || shard >= ctx->shards.size()) return PX_EINVAL;
     PX_GUARD({
+        PX_FLUSHED(ctx);
         Shard &s = *ctx->shards[shard];
         if (chunk >= s.chunks.size()) return PX_EINVAL;
         const uint32_t c = s.chunks[chunk];
@@ -2846,6 +3040,7 @@ int px_reinsert(px_ctx *ctx, uint32_t shard, uint32_t chunk) {
 int px_contains_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff, uint32_t *result) {
     if (!ctx || (n && (!keys || !koff || !result))) return PX_EINVAL;
     PX_GUARD({
+        PX_FLUSHED(ctx);
         for (uint32_t i = 0; i < n; ++i) {
             Shard *s = ctx->shard_for_key(keys + koff[i], koff[i + 1] - koff[i]);
             result[i] = s && ctx->cbt_contains(*s, px_ctx::esc_key(keys + koff[i], koff[i + 1] - koff[i]));
@@ -2856,12 +3051,13 @@ int px_contains_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64
 
 int px_del_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff, uint32_t *result) {
     if (!ctx || (n && (!keys || !koff || !result))) return PX_EINVAL;
-    PX_GUARD(return ctx->del_ctrl(n, keys, koff, result);)
+    PX_GUARD(PX_FLUSHED(ctx); return ctx->del_ctrl(n, keys, koff, result);)
 }
 
 int px_iter(px_ctx *ctx, const uint8_t *prefix, uint64_t prefix_len, px_rec *recs, uint32_t cap, uint32_t *n_out) {
     if (!ctx || !n_out || (prefix_len && !prefix) || (cap && !recs)) return PX_EINVAL;
     PX_GUARD({
+        PX_FLUSHED(ctx);
         std::string p;  // PiXiuStr_init: 251 doubled, no terminator
         for (uint64_t i = 0; i < prefix_len; ++i) {
             p.push_back((char)prefix[i]);
@@ -2888,6 +3084,7 @@ int px_iter(px_ctx *ctx, const uint8_t *prefix, uint64_t prefix_len, px_rec *rec
 int px_export(px_ctx *ctx, uint32_t n, const px_rec *recs, uint8_t *out, uint64_t out_cap, uint64_t *out_off) {
     if (!ctx || (n && (!recs || !out_off))) return PX_EINVAL;
     PX_GUARD({
+        PX_FLUSHED(ctx);
         out_off[0] = 0;
         for (uint32_t i = 0; i < n; ++i) {
             const px_rec &r = recs[i];
@@ -2907,6 +3104,7 @@ int px_export(px_ctx *ctx, uint32_t n, const px_rec *recs, uint8_t *out, uint64_
 int px_last_store(px_ctx *ctx, uint8_t *dst, uint64_t cap, int dst_on_device, uint64_t *bytes) {
     if (!ctx) return PX_EINVAL;
     PX_GUARD({
+        PX_FLUSHED(ctx);
         if (bytes) *bytes = ctx->last_store_bytes;
         if (!dst) return PX_OK;
         if (cap < ctx->last_store_bytes) return PX_ESPACE;
@@ -2924,6 +3122,7 @@ int px_last_store(px_ctx *ctx, uint8_t *dst, uint64_t cap, int dst_on_device, ui
 int px_import_chunk(px_ctx *ctx, uint32_t n, const uint8_t *comp, const uint64_t *off, uint32_t *shard_out) {
     if (!ctx || !n || n > (uint32_t)kChunkSlots || !comp || !off) return PX_EINVAL;
     PX_GUARD({
+        PX_FLUSHED(ctx);
         // an imported record's source length is unknown up front: index the first
         // kMaxDoc source bytes (a lane asking past that goes to the serial path)
         const uint32_t pn = pidx_blocks(kMaxDoc);
@@ -2997,24 +3196,29 @@ int px_import_chunk(px_ctx *ctx, uint32_t n, const uint8_t *comp, const uint64_t
 
 int px_save(px_ctx *ctx, uint8_t *dst, uint64_t cap, int dst_on_device, uint64_t *bytes) {
     if (!ctx) return PX_EINVAL;
-    PX_GUARD(return ctx->save(dst, cap, dst_on_device, bytes);)
+    PX_GUARD(PX_FLUSHED(ctx); return ctx->save(dst, cap, dst_on_device, bytes);)
 }
 
 int px_load(px_ctx *ctx, const uint8_t *src, uint64_t len, int src_on_device, uint32_t *first_shard) {
     if (!ctx || (len && !src)) return PX_EINVAL;
-    PX_GUARD(return ctx->load(src, len, src_on_device, first_shard);)
+    PX_GUARD(PX_FLUSHED(ctx); return ctx->load(src, len, src_on_device, first_shard);)
 }
 
 int px_reset(px_ctx *ctx) {
     if (!ctx) return PX_EINVAL;
-    PX_GUARD(ctx->reset(); return PX_OK;)
+    PX_GUARD(ctx->drop_queue(); ctx->have_last = false; ctx->dq_rc = PX_OK; ctx->reset(); return PX_OK;)
 }
 
 int px_stats_get(px_ctx *ctx, px_stats *st) {
     if (!ctx || !st) return PX_EINVAL;
-    *st = ctx->stats;
-    st->device_bytes = ctx->heap.held();
-    return PX_OK;
+    PX_GUARD({
+        PX_FLUSHED(ctx);
+        *st = ctx->stats;
+        st->device_bytes = ctx->heap.held();
+        st->device_live_bytes = ctx->heap.live_bytes();
+        st->device_peak_bytes = ctx->heap.peak();
+        return PX_OK;
+    })
 }
 
 void *px_stream(px_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }

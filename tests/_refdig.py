@@ -1,0 +1,87 @@
+"""Per-record digests of the REFERENCE's output at the bench's full sizes — test
+infrastructure only (shared by tools/make_refdigests.py, the -m gpu tests and
+bench.py's parity counts).
+
+tests/golden/refdig_c{config}_r{rps}[_n{n}].npz holds, for every record of the canonical
+corpus part (synth.make(config); _n: its first n records only) stored in records_per_shard = rps shards (one
+reference PiXiuCtrl per shard, rps = 0: one over every record), in record order:
+
+  get_len, get_d32    length and digest32 of the reference's compat getitem drain
+                      (PiXiuCtrl::getitem + PXSGen, PiXiuCtrl.cpp:59-61, PiXiuStr.h:129-198)
+  comp_len, comp_d32  length and digest32 of the record's compressed bytes
+  chunk, idx          the chunk serial and chunk-local slot it landed in
+
+digest32(b) = the 4-byte BLAKE2b digest of b, little-endian.
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def digest32(b) -> int:
+    return int.from_bytes(hashlib.blake2b(b, digest_size=4).digest(), "little")
+
+
+def digests(buf: np.ndarray, off, ln) -> np.ndarray:
+    """digest32 of buf[off[i] : off[i] + ln[i]] for every i (host buffer)."""
+    mv = memoryview(np.ascontiguousarray(buf))
+    off = np.asarray(off, np.int64).tolist()
+    ln = np.asarray(ln, np.int64).tolist()
+    h = hashlib.blake2b
+    return np.fromiter((int.from_bytes(h(mv[o:o + n], digest_size=4).digest(), "little")
+                        for o, n in zip(off, ln)), np.uint32, count=len(off))
+
+
+def path(config: int, rps: int, n: int | None = None) -> str:
+    """n: a fixture over only the first n records of the full corpus"""
+    return os.path.join(GOLDEN, f"refdig_c{config}_r{rps}" + (f"_n{n}" if n else "") + ".npz")
+
+
+def load(config: int, rps: int, n: int | None = None):
+    """The reference's digests for (config, rps[, first n records]), or None without a fixture."""
+    p = path(config, rps, n)
+    if not os.path.exists(p):
+        return None
+    with np.load(p, allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def compare(ref, get_len, get_d32):
+    """Records whose compat getitem differs from the reference's (length or digest)."""
+    get_len = np.asarray(get_len, np.int64)
+    get_d32 = np.asarray(get_d32, np.uint32)
+    if len(get_len) != len(ref["get_len"]):
+        raise ValueError(f"{len(get_len)} records, the reference digests hold {len(ref['get_len'])}")
+    bad = (get_len != ref["get_len"].astype(np.int64)) | (get_d32 != ref["get_d32"])
+    return int(bad.sum()), np.nonzero(bad)[0]
+
+
+def check_store(ref, st, res, out, off, ln):
+    """A store's full-size result against the reference's digests (outside any timing).
+
+    st, res     the pixiu_amd.Store and its set_batch results for the corpus, in record order
+    out         the compat getitem output of every key in record order (a torch uint8 device
+                tensor or a host numpy buffer), record i at out[off[i] : off[i] + ln[i]]
+    Returns {records, compat_ne_reference, comp_ne_reference, placement_ne_reference,
+    first_bad}."""
+    import pixiu_amd as px
+    off = np.asarray(off, np.int64)
+    ln = np.asarray(ln, np.int64)
+    n = len(ln)
+    end = int((off + ln).max()) if n else 0
+    host = out[:end].cpu().numpy() if hasattr(out, "cpu") else np.asarray(out)[:end]
+    bad_get, idx = compare(ref, ln, digests(host, off, ln))
+    comp = st.export(px.records_of(res))
+    cl = np.fromiter((len(c) for c in comp), np.int64, count=n)
+    cd = np.fromiter((digest32(c) for c in comp), np.uint32, count=n)
+    bad_comp = int(((cl != ref["comp_len"].astype(np.int64)) | (cd != ref["comp_d32"])).sum())
+    bad_place = int(((np.asarray(res["chunk"], np.int64) != ref["chunk"].astype(np.int64))
+                     | (np.asarray(res["idx"], np.int64) != ref["idx"].astype(np.int64))).sum())
+    return {"records": n, "compat_ne_reference": bad_get, "comp_ne_reference": bad_comp,
+            "placement_ne_reference": bad_place, "first_bad": [int(i) for i in idx[:5]]}

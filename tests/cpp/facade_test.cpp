@@ -174,6 +174,83 @@ int main() {
         CBTGen_free(ig);
     }
     ctrl.free_prop();
+
+    // write-behind setitem: 3,000 one-record calls with repeated keys return what the
+    // reference returns at once, and store the same bytes in the same slots as a context
+    // without the queue fed the same calls
+    {
+        ctrl.init_prop();
+        px_opts o;
+        memset(&o, 0, sizeof o);
+        px_ctx *plain = px_open(&o);  // defer_bytes = 0
+        std::map<std::string, int> seen;
+        std::vector<std::string> ks;
+        unsigned t = 777;
+        auto rn = [&]() { return (t = t * 1103515245u + 12345u) >> 8; };
+        for (int i = 0; i < 3000; ++i) {
+            char b[32];
+            snprintf(b, sizeof b, "http://q/%05u", rn() % 2500);
+            std::string k = b, v = "::";
+            for (int j = 0, n = 20 + rn() % 200; j < n; ++j) v += "abcdefgh<>/="[rn() % 12];
+            const int r = ctrl.setitem((uint8_t *)k.c_str(), (int)k.size(), (uint8_t *)v.c_str(), (int)v.size());
+            CHECK(r == (seen.count(k) ? CBT_SET_REPLACE : 0));
+            uint64_t ko[2] = {0, k.size()}, vo[2] = {0, v.size()};
+            px_set_result pr;
+            CHECK(px_set_batch(plain, 1, (const uint8_t *)k.data(), ko, (const uint8_t *)v.data(), vo, 0, &pr) == PX_OK);
+            CHECK((int)pr.replaced == r && pr.chunk != PX_PENDING);
+            seen[k] = 1;
+            ks.push_back(k);
+        }
+        px_stats sd, sp;
+        CHECK(px_stats_get(ctrl.ctx, &sd) == PX_OK && px_stats_get(plain, &sp) == PX_OK);
+        CHECK(sd.deferred_records == 3000 && sd.deferred_flushes >= 1 && sd.deferred_mismatch == 0);
+        CHECK(sd.records == sp.records && sd.comp_bytes == sp.comp_bytes && sd.chunks == sp.chunks);
+        bool same = true;
+        for (size_t i = 0; i < ks.size(); i += 7) {
+            uint64_t ko[2] = {0, ks[i].size()};
+            px_rec ra, rb;
+            uint32_t sa = 0, sb = 0;
+            px_locate_batch(ctrl.ctx, 1, (const uint8_t *)ks[i].data(), ko, &ra, &sa);
+            px_locate_batch(plain, 1, (const uint8_t *)ks[i].data(), ko, &rb, &sb);
+            same = same && sa == PX_OK && sb == PX_OK && ra.chunk == rb.chunk && ra.idx == rb.idx;
+            std::vector<uint8_t> ba(70000), bb(70000);
+            uint64_t oa[2], ob[2];
+            px_export(ctrl.ctx, 1, &ra, ba.data(), ba.size(), oa);
+            px_export(plain, 1, &rb, bb.data(), bb.size(), ob);
+            same = same && oa[1] == ob[1] && memcmp(ba.data(), bb.data(), oa[1]) == 0;
+        }
+        CHECK(same);
+        // the CLI's chunk view after one more queued call (main.cpp:67)
+        std::string k = "BOBO1", v = "::https://www.zhihu.com/question/22454692";
+        ctrl.setitem((uint8_t *)k.c_str(), 5, (uint8_t *)v.c_str(), (int)v.size());
+        PiXiuStr *last = ctrl.st.cbt_chunk->getitem(ctrl.st.local_chunk.used_num - 1);
+        CHECK(last != NULL && last->len > 0);
+        px_close(plain);
+
+        // a ready doc (setitem(doc, 0, NULL, 0, reinsert), PiXiuCtrl.cpp:39-40): stored as it is
+        std::string doc = std::string("RAWKEY\xfb\x00", 8) + "raw value bytes" + std::string("\xfb\x02", 2);
+        std::vector<uint8_t> pxs(2 + doc.size());
+        const uint16_t dl = (uint16_t)doc.size();
+        memcpy(pxs.data(), &dl, 2);
+        memcpy(pxs.data() + 2, doc.data(), doc.size());
+        CHECK(ctrl.setitem(pxs.data(), 0, NULL, 0, true) == 0);
+        CHECK(ctrl.setitem(pxs.data(), 0, NULL, 0, false) == CBT_SET_REPLACE);
+        PXSGen *rg = ctrl.getitem((uint8_t *)"RAWKEY", 6);
+        CHECK(rg != NULL);
+        std::string rgot;
+        uint8_t c;
+        while (rg && (*rg)(c)) rgot.push_back((char)c);
+        PXSGen_free(rg);
+        CHECK(rgot == doc);
+        CHECK(ctrl.setitem(NULL, 0, (uint8_t *)"x", 1) < 0);  // (the reference asserts k_len)
+
+        // a generator that outlives free_prop yields nothing and says why
+        PXSGen *late = ctrl.getitem((uint8_t *)"RAWKEY", 6);
+        CHECK(late != NULL);
+        ctrl.free_prop();
+        CHECK(late && !(*late)(c) && late->status == PX_EINVAL);
+        PXSGen_free(late);
+    }
     printf("facade_test: %s (%zu live keys)\n", fails ? "FAILED" : "ok", ref.size());
     return fails ? 1 : 0;
 }

@@ -183,12 +183,31 @@ static void test_heap() {
                 live.pop_back();
             }
         }
-        for (auto &b : live) h.release(b.p);
+        // trim with live blocks: only wholly free slabs go back, the live ones stay intact
+        const size_t keep_live = std::min<size_t>(live.size(), 40);
+        for (size_t k = keep_live; k < live.size(); ++k) h.release(live[k].p);
+        live.resize(keep_live);
+        const uint64_t peak = h.peak(), before = h.held();
+        CHECK(peak >= before);
+        h.trim(0);
+        CHECK(h.held() <= before && h.held() >= h.live_bytes());
+        CHECK(h.peak() == peak);
+        for (auto &b : live) {
+            for (uint64_t j = 0; j < b.n; j += 97) CHECK(b.p[j] == b.tag);
+            h.release(b.p);
+        }
         CHECK(h.live_bytes() == 0);
         CHECK(h.cached_free() == h.held());
         held = h.held();
+        h.trim(1 << 20);  // keep at most one slab's worth of free bytes
+        CHECK(h.held() <= (1u << 20) || h.held() == 0 || h.cached_free() <= (1u << 20));
+        h.trim(0);
+        CHECK(h.held() == 0);
+        auto *p = (uint8_t *)h.alloc(5000);  // and the heap still works afterwards
+        CHECK(p != nullptr);
+        h.release(p);
     }
-    printf("heap: %llu bytes held at the end, all free\n", (unsigned long long)held);
+    printf("heap: %llu bytes held before trim, all free\n", (unsigned long long)held);
 }
 
 static void test_parallel_ranges() {

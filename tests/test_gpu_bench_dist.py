@@ -23,14 +23,19 @@ def _free_port():
     return p
 
 
-def test_bench_two_ranks_gloo():
+@pytest.mark.parametrize("rps", [None, 0], ids=["bench_rps", "rps0"])
+def test_bench_two_ranks_gloo(rps):
+    """rps 0: every rank is one single-instance shard; rank 0 loads each gathered blob into
+    a store of its own (a single shard takes one blob)"""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--backend", "gloo", "--records", "300", "--configs", "", "--steps", "1",
-           "--warmup", "0", "--no-cpu", "--no-single", "--no-pcie"]
+           "--warmup", "0", "--no-cpu", "--no-single", "--no-pcie", "--no-cliff"]
+    if rps is not None:
+        cmd += ["--rps", str(rps)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -45,3 +50,4 @@ def test_bench_two_ranks_gloo():
     assert g["rank0_compat_equal_live"] == g["records_per_rank_sampled"]
     assert g["rank0_gather_served"] > 0
     assert out["parity_counts"]["exact_ne_original"] == 0
+    assert g["stores"] == (2 if rps == 0 else 1)

@@ -16,7 +16,7 @@ buf = (C.c_ulonglong * 64)()
 lib.px_debug_prof_take(buf, 64)
 with px.Store(records_per_shard=rps) as st:
     st.set_batch((cp.keys, cp.koff.astype(np.uint64)), (cp.vals, cp.voff.astype(np.uint64)))
-    ms = st.stats()["last_set_kernel_ms"]
+    ms = st.stats()["last_set_stage_ms"]
 k = lib.px_debug_prof_take(buf, 64)
 v = dict(zip(NAMES, buf[:k]))
 b = max(v["bytes"], 1)

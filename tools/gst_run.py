@@ -10,5 +10,5 @@ cp = synth.make(cfg, n)
 with px.Store(records_per_shard=rps) as st:
     st.set_batch((cp.keys, cp.koff.astype(np.uint64)), (cp.vals, cp.voff.astype(np.uint64)))
     stt = st.stats()
-    print(f"config {cfg} n {n} rps {rps}: kernel {stt['last_set_kernel_ms']:.1f} ms raw {int(cp.koff[-1] + cp.voff[-1])} B "
+    print(f"config {cfg} n {n} rps {rps}: kernel {stt['last_set_stage_ms']:.1f} ms raw {int(cp.koff[-1] + cp.voff[-1])} B "
           f"ratio {stt['comp_bytes'] / max(stt['raw_bytes'], 1):.4f}")
