@@ -182,9 +182,7 @@ def small_batches(local, calls=50000, defer_mb=8):
             r2 = np.zeros(calls, px.SET_RESULT_DTYPE)
             r2["shard"], r2["chunk"], r2["idx"] = recs["shard"], recs["chunk"], recs["idx"]
             import torch
-            cap = int(ref["get_len"].astype(np.int64).sum()) + 64 * calls + (1 << 20)
-            buf = torch.empty(cap, dtype=torch.uint8, device=torch.device("cuda", local))
-            rc, off, ln, gst, _ = st.get_batch_device(keys, buf.data_ptr(), cap, px.COMPAT)
+            buf, off, ln = _refdig.compat_all(st, keys, torch.device("cuda", local))
             chk = _refdig.check_store(ref, st, r2, buf, off, ln)
             out["reference_check"] = dict(chk, fixture=os.path.relpath(_refdig.path(4, 0, calls), ROOT))
     return out

@@ -62,6 +62,26 @@ def compare(ref, get_len, get_d32):
     return int(bad.sum()), np.nonzero(bad)[0]
 
 
+def compat_all(st, keys, device):
+    """Every key's compat getitem into one device buffer (pixiu_amd.Store.get_batch_device,
+    grown once to the call's reported need): (buffer, offsets, lengths)."""
+    import torch
+    import pixiu_amd as px
+    kb, ko = keys if isinstance(keys, tuple) else px.csr(keys)
+    n = len(ko) - 1
+    cap = int(ko[-1]) * 2 + 400 * n + (1 << 20)
+    for _ in range(2):
+        out = torch.empty(cap, dtype=torch.uint8, device=device)
+        rc, off, ln, sts, need = st.get_batch_device((kb, ko), out.data_ptr(), cap, px.COMPAT)
+        if rc == px.PX_ESPACE and need > cap:
+            cap = int(need)
+            continue
+        if rc != px.PX_OK or (n and int(sts.max()) != 0):
+            raise RuntimeError(f"compat getitem rc={rc}")
+        return out, off, ln
+    raise RuntimeError("compat getitem: no room")
+
+
 def check_store(ref, st, res, out, off, ln):
     """A store's full-size result against the reference's digests (outside any timing).
 

@@ -35,11 +35,7 @@ def test_every_record_matches_reference_digests(cfg, rps):
     with px.Store(records_per_shard=rps) as st:
         res = st.set_batch((cp.keys, cp.koff.astype(np.uint64)), (cp.vals, cp.voff.astype(np.uint64)))
         assert int(res["status"].max()) == 0
-        cap = int(ref["get_len"].astype(np.int64).sum()) + 64 * cp.n + (1 << 20)
-        out = torch.empty(cap, dtype=torch.uint8, device=dev)
-        rc, off, ln, sts, need = st.get_batch_device((cp.keys, cp.koff.astype(np.uint64)), out.data_ptr(), cap,
-                                                     px.COMPAT)
-        assert rc == px.PX_OK and int(sts.max()) == 0
+        out, off, ln = _refdig.compat_all(st, (cp.keys, cp.koff.astype(np.uint64)), dev)
         r = _refdig.check_store(ref, st, res, out, off, ln)
     print(f"config {cfg} rps {rps}: {r}")
     assert r["placement_ne_reference"] == 0
