@@ -97,7 +97,8 @@ static_assert(sizeof(PsaShard) == 32, "PsaShard layout");
 struct PsaPoolOut {
     uint32_t rot_doc;
     int32_t pools, used;  // (after the docs that stay; the bound test leaves them 0 / 2,048)
-    uint32_t how;         // 0: the boundary chain ran, 1: the bound test (no rotation), 2: (rotation)
+    uint32_t how;         // 0: the boundary chain ran, 1: the bound test (no rotation), 2: (rotation),
+                          // 3: the chain stalled (no verdict: the shard goes to the walk)
 };
 // device scratch for px_psa.hip, borrowed from the runtime's heap
 struct PsaAlloc {

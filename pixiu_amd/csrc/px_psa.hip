@@ -23,9 +23,11 @@
 //
 // Pipeline over all PSA shards of a batch (one global position space, shard-major):
 //   k_psa_gather   docs -> global text G + doc id per position
-//   k_psa_key0     5-symbol keys (shard in the top bits) -> radix sort (rocPRIM)
-//   prefix doubling: keys (group, rank[p+h]) of unsorted suffixes only, stable radix
-//                  sort, group heads by max-scans, ranks and SA written back
+//   first sort     6 symbols of 9 bits per suffix, a segmented radix sort inside each
+//                  shard whose first pass reads the text (px_sort.hip, hand-written)
+//   prefix doubling: keys (group, rank[p+h]) of unsorted suffixes only, sorted inside their
+//                  groups (windows / registers / LDS; the largest by px_sort.hip's
+//                  segmented sort), group heads by max-scans, ranks and SA written back
 //   k_psa_minlvl / k_psa_ansv_blk   nearest smaller position left/right in SA order
 //                  (a 64-ary min tree; one wave per 64 ranks, ballot descents)
 //   k_psa_lce      lcp with those two neighbours, Kasai-style in text order
@@ -39,11 +41,9 @@
 #include <vector>
 
 #include <hip/hip_runtime.h>
-#include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_scan.hpp>
-#include <rocprim/iterator/reverse_iterator.hpp>
 
 #include "px_common.h"
+#include "px_sort.h"
 
 namespace px {
 
@@ -76,23 +76,6 @@ __global__ void __launch_bounds__(256) k_psa_gather(uint32_t ndocs, const PsaDoc
             dist[d.start + o] = (uint16_t)(d.len - o);  // 1..65,535
         }
     }
-}
-
-// initial keys: shard (top bits) | `syms` symbols of 9 bits (byte + 1; 0 past the doc end):
-// as many symbols as the shard count leaves room for (5 to 6)
-__global__ void __launch_bounds__(256) k_psa_key0(uint32_t N, const uint8_t *G, const uint32_t *pdoc,
-                                                  const PsaDoc *docs, const uint16_t *dist, uint32_t syms,
-                                                  uint64_t *keys, uint32_t *vals) {
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= N) return;
-    const uint32_t left = dist[p];
-    uint64_t k = (uint64_t)docs[pdoc[p]].shard << (9 * syms);
-    for (uint32_t s = 0; s < syms; ++s) {
-        const uint64_t sym = s < left ? (uint64_t)G[p + s] + 1 : 0;
-        k |= sym << (9 * (syms - 1 - s));
-    }
-    keys[p] = k;
-    vals[p] = p;
 }
 
 // group heads of the first sort: a new group at a key change, and every suffix shorter
@@ -680,10 +663,6 @@ __global__ void __launch_bounds__(256) k_big_next(uint32_t T, const uint32_t *hf
     if (k >= T) return;
     nf[k] = k + 1 == T ? T : (hf[k + 1] == k + 1 ? k + 1 : 0xffffffffu);
 }
-
-struct Min {
-    PSA_DEV uint32_t operator()(uint32_t a, uint32_t b) const { return a < b ? a : b; }
-};
 
 // ---------------------------------------------------------------- nearest smaller positions
 // 64-ary min tree over the suffix array's values (text positions)
@@ -1386,7 +1365,11 @@ __global__ void __launch_bounds__(kScanThreads) k_pool_scan(uint32_t nshards, co
     __syncthreads();
     if (sh_go) scan_stage(Pw[0], Cw[0], P, N, sh_wb, threadIdx.x, kScanThreads);
     __syncthreads();
-    uint32_t last_cur = kNone;  // (every window resolves >= 1 boundary or moves on; a stall ends the scan)
+    // every window resolves >= 1 boundary or moves on; a window that does neither would
+    // loop forever, so a stall ends the scan -- and is reported (how = 3: the host walks the
+    // shard instead of trusting a verdict the chain did not reach)
+    uint32_t last_cur = kNone;
+    bool stalled = false;
     while (sh_go) {
         wb = sh_wb;
         const uint32_t wend = wb + kScanWin;
@@ -1437,7 +1420,9 @@ __global__ void __launch_bounds__(kScanThreads) k_pool_scan(uint32_t nshards, co
         }
         __syncthreads();
         if (wave == 0) {
-            uint32_t go = more() && cur != last_cur ? 1u : 0u, nwb = wend, re = 0;
+            const bool m = more();
+            stalled = m && cur == last_cur;
+            uint32_t go = m && !stalled ? 1u : 0u, nwb = wend, re = 0;
             last_cur = cur;
             if (go) {
                 const uint32_t b = locate();
@@ -1475,13 +1460,10 @@ __global__ void __launch_bounds__(kScanThreads) k_pool_scan(uint32_t nshards, co
         }
         o.pools = pools;
         o.used = used;
+        if (stalled) o.how = 3;
         out[s] = o;
     }
 }
-
-struct Max {
-    PSA_DEV uint32_t operator()(uint32_t a, uint32_t b) const { return a > b ? a : b; }
-};
 
 }  // namespace
 
@@ -1547,7 +1529,8 @@ constexpr uint32_t kMaxSteps = 20;  // h doubles from >= 5 past 65,535 (the long
 // sizes only the device knows)
 constexpr uint32_t kGridWin = 16384, kGridReg = 2048, kGridBlk = 1024;
 // the cnt words of psa_run
-constexpr uint32_t kCntLong = 0, kCntSorted = 16, kCntActive = 48, kCntMax = 96, kCntCand = 200, kCntWords = 256;
+constexpr uint32_t kCntLong = 0, kCntSorted = 16, kCntActive = 48, kCntMax = 96, kCntCand = 200, kCntSortErr = 250,
+                   kCntWords = 256;
 static_assert(kCntSorted + kMaxSteps < kCntActive && kCntActive + kMaxSteps + 1 < kCntMax && kCntMax + kMaxSteps + 1 < kCntCand, "cnt layout");
 }  // namespace
 
@@ -1557,7 +1540,7 @@ static_assert(kCntSorted + kMaxSteps < kCntActive && kCntActive + kMaxSteps + 1 
 // With any_pools, the shards marked `pools` get the MemPool emulation: pool_out[k] (device)
 // says where shard k's live chunk rotates inside this window (see k_pool_scan).
 hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDoc *docs, uint32_t nshards,
-                   const PsaShard *shards, uint32_t N, uint32_t *rec_chunk, uint32_t *rec_idx, uint32_t *rec_status,
+                   const PsaShard *shards, const PsaShard *hshards, uint32_t N, uint32_t *rec_chunk, uint32_t *rec_idx, uint32_t *rec_status,
                    uint32_t *shard_flag, bool any_pools, PsaPoolOut *pool_out, PsaStats *st) {
     if (!N || !ndocs) return hipSuccess;
     if (nshards > kPsaMaxShards) return hipErrorInvalidValue;  // (the caller splits rounds below this)
@@ -1581,36 +1564,36 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     PSA_CHECK(hipMemsetAsync(G + N, 0, 64, s));  // (ld8 reads up to 15 bytes past the text)
     PSA_CHECK(hipMemsetAsync(cnt, 0, kCntWords * 4, s));
 
-    // ---- first sort: shard | `syms` symbols of 9 bits
-    int shard_bits = 1;
-    while ((1u << shard_bits) < nshards) ++shard_bits;
-    const uint32_t syms = std::min<uint32_t>(6, (64 - shard_bits) / 9);  // 5 or 6 symbols
+    // ---- first sort: 6 symbols of 9 bits per suffix, inside each shard (px_sort.hip: the
+    // shards are contiguous in position space and their suffix-array ranges are the same
+    // ranges, so each shard sorts on its own and no key carries the shard)
+    const uint32_t syms = 6;
     {
         const uint32_t slices = std::max<uint32_t>(1, std::min<uint32_t>(64, 16384 / ndocs));
         const uint64_t nw = (uint64_t)ndocs * slices;
         k_psa_gather<<<(uint32_t)std::min<uint64_t>((nw + 3) / 4, 65535u), 256, 0, s>>>(ndocs, docs, slices, G, pdoc, dist);
     }
+    const SortAlloc SA{A.alloc, A.release, A.self};
     auto *keys = S.get<uint64_t>(n64 * 8);
-    auto *keys2 = S.get<uint64_t>(n64 * 8);
-    auto *vals = S.get<uint32_t>(n64 * 4);
-    k_psa_key0<<<blocks(N), tb, 0, s>>>(N, G, pdoc, docs, dist, syms, keys, vals);
     {
-        size_t t_sort = 0, t_scan = 0;
-        auto first_sort = [&](void *tmp, size_t &bytes) -> hipError_t {
-            return rocprim::radix_sort_pairs(tmp, bytes, keys, keys2, vals, sa, (size_t)N, 0, 9 * syms + shard_bits, s);
-        };
-        PSA_CHECK(first_sort(nullptr, t_sort));
-        PSA_CHECK(rocprim::inclusive_scan(nullptr, t_scan, vals, vals, (size_t)N, Max(), s));
-        size_t t_bytes = std::max(t_sort, t_scan) + 256;
-        void *tmp = S.get<void>(t_bytes);
-        PSA_CHECK(first_sort(tmp, t_bytes));
-        uint32_t *hflag = (uint32_t *)keys, *head = (uint32_t *)keys + N;  // (the unsorted keys are spent)
+        std::vector<uint32_t> sst(nshards), slen(nshards);
+        for (uint32_t i = 0; i < nshards; ++i) {
+            sst[i] = hshards[i].base;
+            slen[i] = hshards[i].len;
+        }
+        std::vector<SegTile> tiles;
+        seg_tiles(sst.data(), slen.data(), nshards, tiles);
+        auto *keys2 = S.get<uint64_t>(n64 * 8);
+        auto *va = S.get<uint32_t>(n64 * 4), *vb = S.get<uint32_t>(n64 * 4);
+        // passes: text -> keys -> keys2 -> keys -> keys2 -> keys -> (keys2, sa)
+        PSA_CHECK(seg_sort_pairs(s, SA, tiles, sst, 9 * syms, 9, nullptr, nullptr, G, dist, syms, keys, va, keys2, vb,
+                                 keys2, sa, cnt + kCntSortErr));
+        S.put(va);
+        S.put(vb);
+        uint32_t *hflag = (uint32_t *)keys, *head = (uint32_t *)keys + N;  // (the pass buffers are spent)
         k_psa_head0<<<blocks(N), tb, 0, s>>>(N, keys2, hflag);
-        t_bytes = std::max(t_sort, t_scan) + 256;
-        PSA_CHECK(rocprim::inclusive_scan(tmp, t_bytes, hflag, head, (size_t)N, Max(), s));
-        S.put(tmp);
+        PSA_CHECK(scan_u32(s, SA, hflag, head, N, ScanOp::kMax, false));
         S.put(keys2);
-        S.put(vals);
     }
     // ---- the first groups, then prefix doubling over them
     auto *sd = S.get<uint16_t>(n64 * 2);
@@ -1678,39 +1661,34 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
                 auto *d_boff = S.get<uint32_t>((uint64_t)nbig * 4 + 64);
                 e = hipMemcpy(d_boff, boff.data(), (size_t)nbig * 4, hipMemcpyHostToDevice);
                 if (e != hipSuccess) return e;
-                auto *ck = S.get<uint64_t>(T * 8), *ck2 = S.get<uint64_t>(T * 8);
-                auto *cv = S.get<uint32_t>(T * 4), *cv2 = S.get<uint32_t>(T * 4);
+                auto *ck = S.get<uint64_t>(T * 8), *ck2 = S.get<uint64_t>(T * 8), *cka = S.get<uint64_t>(T * 8);
+                auto *cv = S.get<uint32_t>(T * 4), *cv2 = S.get<uint32_t>(T * 4), *cva = S.get<uint32_t>(T * 4);
                 auto *gp = S.get<uint32_t>(T * 4), *hf = S.get<uint32_t>(T * 4), *hk = S.get<uint32_t>(T * 4);
                 auto *nf = S.get<uint32_t>(T * 4), *nk = S.get<uint32_t>(T * 4);
                 auto *gd = S.get<uint16_t>(T * 2 + 64);
                 k_big_gather<<<blocks(T), tb, 0, s>>>((uint32_t)T, nbig, LL.lst[4], d_boff, sa, sd, key, ck, cv, gp, gd, ss);
-                int bbits = 1;
-                while ((1ull << bbits) < nbig) ++bbits;
-                size_t t1 = 0, t2 = 0, t3 = 0;
-                auto rev_in = rocprim::make_reverse_iterator(nf + T);
-                auto rev_out = rocprim::make_reverse_iterator(nk + T);
-                e = rocprim::radix_sort_pairs(nullptr, t1, ck, ck2, cv, cv2, (size_t)T, 0, 32 + bbits, s);
-                if (e == hipSuccess) e = rocprim::inclusive_scan(nullptr, t2, hf, hk, (size_t)T, Max(), s);
-                if (e == hipSuccess) e = rocprim::inclusive_scan(nullptr, t3, rev_in, rev_out, (size_t)T, Min(), s);
-                if (e != hipSuccess) return e;
-                const size_t tt0 = std::max({t1, t2, t3}) + 256;
-                void *tmp = S.get<void>(tt0);
-                size_t tt = tt0;
-                e = rocprim::radix_sort_pairs(tmp, tt, ck, ck2, cv, cv2, (size_t)T, 0, 32 + bbits, s);
+                // every group sorted by its 32-bit keys on its own (px_sort.hip): segments = groups
+                std::vector<uint32_t> gst(nbig), glen(nbig);
+                for (uint32_t b = 0; b < nbig; ++b) {
+                    gst[b] = boff[b];
+                    glen[b] = (uint32_t)(bl[b] >> 32);
+                }
+                std::vector<SegTile> gt;
+                seg_tiles(gst.data(), glen.data(), nbig, gt);
+                e = seg_sort_pairs(s, SA, gt, gst, 32, 8, ck, cv, nullptr, nullptr, 0, cka, cva, nullptr, nullptr, ck2, cv2,
+                                   cnt + kCntSortErr);
                 if (e != hipSuccess) return e;
                 k_big_head<<<blocks(T), tb, 0, s>>>((uint32_t)T, d_boff, ck2, hf);
                 k_big_next<<<blocks(T), tb, 0, s>>>((uint32_t)T, hf, nf);
-                tt = tt0;
-                e = rocprim::inclusive_scan(tmp, tt, hf, hk, (size_t)T, Max(), s);
-                if (e != hipSuccess) return e;
-                tt = tt0;
-                e = rocprim::inclusive_scan(tmp, tt, rev_in, rev_out, (size_t)T, Min(), s);
+                e = scan_u32(s, SA, hf, hk, T, ScanOp::kMax, false);
+                if (e == hipSuccess) e = scan_u32(s, SA, nf, nk, T, ScanOp::kMin, true);
                 if (e != hipSuccess) return e;
                 k_big_put<<<blocks(T), tb, 0, s>>>((uint32_t)T, LL.lst[4], d_boff, ck2, cv2, gp, gd, hf, hk, nk, tag, sa, sd,
                                                    act, gsz, rank, ss);
                 for (const void *q : {(const void *)d_boff, (const void *)ck, (const void *)ck2, (const void *)cv,
                                       (const void *)cv2, (const void *)gp, (const void *)hf, (const void *)hk,
-                                      (const void *)nf, (const void *)nk, (const void *)gd, (const void *)tmp})
+                                      (const void *)nf, (const void *)nk, (const void *)gd, (const void *)cka,
+                                      (const void *)cva})
                     S.put(q);
             }
         }
@@ -1750,7 +1728,7 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         }
     }
     PSA_CHECK(read_words(0, kCntWords));
-    if (pin[kCntActive + it] != 0 || pin[kCntLong + kLongClasses]) return hipErrorUnknown;
+    if (pin[kCntActive + it] != 0 || pin[kCntLong + kLongClasses] || pin[kCntSortErr]) return hipErrorUnknown;
     for (const void *q : {(const void *)sd, (const void *)act, (const void *)gsz, (const void *)key}) S.put(q);
     for (int c = 0; c < kLongClasses; ++c) S.put(LL.lst[c]);
     PSA_CHECK(hipEventRecord(e1, s));
@@ -1826,10 +1804,7 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         const uint32_t mask = (uint32_t)(cap - 1);
         k_pool_insert<<<blocks(N), tb, 0, s>>>(N, code, E, lcp_p, lcp_n, tab, mask);
         k_pool_blocks<<<blocks(N), tb, 0, s>>>(N, code, E, lcp_p, lcp_n, tab, mask, blk);
-        size_t tsz = 0;
-        PSA_CHECK(rocprim::inclusive_scan(nullptr, tsz, blk, P, (size_t)N, rocprim::plus<uint32_t>(), s));
-        void *tmp2 = S.get<void>(tsz + 256);
-        PSA_CHECK(rocprim::inclusive_scan(tmp2, tsz, blk, P, (size_t)N, rocprim::plus<uint32_t>(), s));
+        PSA_CHECK(scan_u32(s, SA, blk, P, N, ScanOp::kPlus, false));
         auto *C = S.get<uint32_t>(n64 / kPoolCoarse * 4 + 256);
         k_pool_coarse<<<blocks((N + kPoolCoarse - 1) / kPoolCoarse), tb, 0, s>>>(N, P, C);
         k_pool_scan<<<nshards, kScanThreads, 0, s>>>(nshards, shards, docs, P, C, N, pool_out,

@@ -37,7 +37,8 @@ hipError_t launch_scatter_slots(hipStream_t, uint32_t, const SlotPut *);
 hipError_t launch_gst_encode(hipStream_t, const GstShard *, uint32_t, const uint32_t *, uint8_t *const *,
                              const uint8_t *, uint32_t *, uint32_t *, uint32_t *, uint32_t *, ShardState *,
                              uint32_t *);
-hipError_t psa_run(hipStream_t, const PsaAlloc &, uint32_t, const PsaDoc *, uint32_t, const PsaShard *, uint32_t,
+hipError_t psa_run(hipStream_t, const PsaAlloc &, uint32_t, const PsaDoc *, uint32_t, const PsaShard *, const PsaShard *,
+                   uint32_t,
                    uint32_t *, uint32_t *, uint32_t *, uint32_t *, bool, PsaPoolOut *, PsaStats *);
 hipError_t launch_gst_emit(hipStream_t, uint32_t, const uint8_t *const *, const uint32_t *, uint8_t *const *,
                            const uint8_t *, const uint32_t *, uint32_t *, uint32_t *);
@@ -1715,7 +1716,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
                        [](void *self, void *p, uint64_t b) { static_cast<px_ctx *>(self)->heap.release(p, b); }, this,
                        static_cast<uint32_t *>(psa_pin.get(kPsaPinWords * 4))};
             PsaStats rst{};
-            hcheck(psa_run(stream, A, (uint32_t)pd.size(), d_pd, (uint32_t)ps.size(), d_ps, (uint32_t)gpos, d_chunk,
+            hcheck(psa_run(stream, A, (uint32_t)pd.size(), d_pd, (uint32_t)ps.size(), d_ps, ps.data(), (uint32_t)gpos, d_chunk,
                            d_idx, d_status, d_flag, any_pools, d_pool, &rst));
             std::vector<uint32_t> flag(ps.size());
             std::vector<PsaPoolOut> pout(ps.size());
@@ -1752,6 +1753,10 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             for (size_t i = 0; i < ps.size(); ++i) {
                 Run &u = runs[prun[i]];
                 Shard &sh = *work[u.k].s;
+                if (ps[i].pools && pout[i].how == 3) {  // (k_pool_scan reached no verdict: cannot happen)
+                    fprintf(stderr, "pixiu_amd: MemPool emulation stalled on shard %u; walking it\n", sh.id);
+                    flag[i] = 1;
+                }
                 if (flag[i]) {
                     // the stale-pair check fired: this shard's live chunk and its remaining docs
                     // go to the walk (the text copied includes them; their records keep reading

@@ -1,0 +1,47 @@
+// px_sort.h — hand-written segmented radix sort and u32 scans for the suffix-array pass
+// (px_psa.hip).  Host-side entry points; the kernels live in px_sort.hip.
+#pragma once
+#include <stdint.h>
+
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+namespace px {
+
+// A tile is kSortTile consecutive elements of ONE segment; a segment's tiles are
+// consecutive in the tile table and the first one carries first = 1.
+constexpr uint32_t kSortTile = 4096;
+struct SegTile {
+    uint32_t start, count, seg, first;
+};
+// device scratch borrowed from the caller (px_psa.hip's Scratch / the runtime heap)
+struct SortAlloc {
+    void *(*alloc)(void *self, uint64_t n);
+    void (*release)(void *self, void *p, uint64_t n);
+    void *self;
+};
+
+// tiles of the segments [start[i], start[i] + len[i]) (host)
+void seg_tiles(const uint32_t *start, const uint32_t *len, uint32_t nseg, std::vector<SegTile> &out);
+
+// Stable LSD radix sort of (key, value) pairs inside every segment by key bits [0, bits),
+// `rb`-bit digits (8 or 9).  Elements never leave their segment, so the scatter of every
+// pass stays inside one segment's range.  Pass 0 reads (k0, v0), or -- with G / dist
+// set -- computes each position's key from the text: `syms` 9-bit symbols (byte + 1, 0
+// past the doc end; value = the position).  The last pass writes (kout, vout).  Scratch
+// pairs: (ka, va) always; (kb, vb) when pass 0 reads the text and there are >= 3 passes
+// (otherwise k0 / v0 are reused).  kout may alias kb.  *err (device word, zeroed by the
+// caller) is set if a tile's look-back outlasted its bound (cannot happen; the sort is
+// then wrong and the caller must fail).
+hipError_t seg_sort_pairs(hipStream_t s, const SortAlloc &A, const std::vector<SegTile> &tiles,
+                          const std::vector<uint32_t> &seg_start, uint32_t bits, int rb, uint64_t *k0, uint32_t *v0,
+                          const uint8_t *G, const uint16_t *dist, uint32_t syms, uint64_t *ka, uint32_t *va,
+                          uint64_t *kb, uint32_t *vb, uint64_t *kout, uint32_t *vout, uint32_t *err);
+
+enum class ScanOp { kMax, kMin, kPlus };
+// inclusive scan of n u32 values (reverse: from the end), in-place allowed
+hipError_t scan_u32(hipStream_t s, const SortAlloc &A, const uint32_t *in, uint32_t *out, uint64_t n, ScanOp op,
+                    bool reverse);
+
+}  // namespace px

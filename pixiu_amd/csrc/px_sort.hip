@@ -1,0 +1,488 @@
+// px_sort.hip — the suffix-array pass's sorts and scans, hand-written for gfx950.
+//
+// seg_sort_pairs: stable LSD radix sort of (u64 key, u32 value) pairs inside segments
+// (the PSA shards of a round for the first suffix sort, the big groups of a doubling
+// step).  Every pass is one "onesweep" launch over tiles of 4,096 elements of ONE
+// segment: a tile ranks its elements per digit in LDS (wave ballots match equal digits;
+// each wave keeps its own running counts, so ranking needs no barrier), publishes its
+// per-digit counts, looks back over the earlier tiles of its segment for their running
+// totals (decoupled look-back: count and flag in one word, agent-scope atomic stores and
+// loads, so a flag is seen across XCDs), stages the tile in LDS in digit order and writes
+// it out in runs, so consecutive lanes store consecutive addresses of one digit's run.
+// The per-segment digit totals of every pass come from one histogram launch before the
+// first pass.  Keys never carry the segment id: a segment's elements stay inside its
+// range, which is what the rocPRIM sort over (shard | key) this replaces could not do.
+//
+// The first suffix sort's keys (6 symbols of 9 bits: byte + 1, 0 past the doc end;
+// px_psa.hip k_psa_key0's layout) are computed from the text by the histogram and the
+// first pass, so no key array is written before the sort.
+//
+// scan_u32: inclusive max / min / plus scans (forward or reverse) as reduce -> scan of
+// block partials -> apply.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "px_sort.h"
+
+namespace px {
+
+namespace {
+
+#define SD __device__ __forceinline__
+constexpr uint32_t kThreads = 256, kItems = 16, kWaves = kThreads / 64;
+static_assert(kThreads * kItems == kSortTile, "tile = threads x items");
+constexpr uint32_t kMaxPasses = 8;
+constexpr uint32_t kHistTiles = 16;       // tiles per histogram workgroup
+constexpr uint32_t kFlagAgg = 1u << 30, kFlagIncl = 2u << 30, kCountMask = (1u << 30) - 1u;
+constexpr uint32_t kSpinBound = 1u << 20;  // look-back polls before a tile gives up (cannot happen)
+
+SD uint32_t lane_id() { return threadIdx.x & 63u; }
+SD uint64_t lanes_below() { return (1ull << lane_id()) - 1ull; }
+
+// the first suffix sort's key of text position p (k_psa_key0's layout without the shard)
+SD uint64_t text_key(const uint8_t *G, const uint16_t *dist, uint32_t p, uint32_t syms) {
+    const uint32_t left = dist[p];
+    uint64_t k = 0;
+    for (uint32_t s = 0; s < syms; ++s) k = k << 9 | (s < left ? (uint64_t)G[p + s] + 1u : 0u);
+    return k;
+}
+
+// lanes (of `valid`) holding the same RB-bit digit as this lane
+template <int RB>
+SD uint64_t match_digit(uint32_t d, uint64_t valid) {
+    uint64_t m = valid;
+#pragma unroll
+    for (int b = 0; b < RB; ++b) {
+        const uint64_t x = __ballot((d >> b) & 1u);
+        m &= ((d >> b) & 1u) ? x : ~x;
+    }
+    return m;
+}
+
+// exclusive scan of one value per thread over the workgroup (256 threads); total -> *tot
+SD uint32_t block_excl_scan(uint32_t v, uint32_t *red, uint32_t *tot) {
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    uint32_t x = v;
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) red[w] = x;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+    for (uint32_t i = 0; i < kWaves; ++i) {
+        before += i < w ? red[i] : 0u;
+        all += red[i];
+    }
+    __syncthreads();  // (red is reused by the caller's next scan)
+    if (tot) *tot = all;
+    return before + x - v;
+}
+
+// ---------------------------------------------------------------- histogram
+// per segment and pass, the digit counts of its elements (one workgroup per kHistTiles
+// tiles; LDS counts flushed to the segment's global counts when the segment changes)
+template <int RB, bool TEXT>
+__global__ void __launch_bounds__(kThreads) k_seg_hist(const SegTile *tiles, uint32_t ntiles, const uint64_t *kin,
+                                                       const uint8_t *G, const uint16_t *dist, uint32_t syms,
+                                                       uint32_t passes, uint32_t *ghist) {
+    constexpr uint32_t BINS = 1u << RB;
+    __shared__ uint32_t h[kMaxPasses * BINS];
+    const uint32_t t0 = blockIdx.x * kHistTiles, t1 = min(ntiles, t0 + kHistTiles);
+    for (uint32_t i = threadIdx.x; i < passes * BINS; i += kThreads) h[i] = 0;
+    __syncthreads();
+    uint32_t seg = tiles[t0].seg;
+    auto flush = [&]() {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < passes * BINS; i += kThreads) {
+            if (h[i]) atomicAdd(ghist + (uint64_t)seg * passes * BINS + i, h[i]);
+            h[i] = 0;
+        }
+        __syncthreads();
+    };
+    for (uint32_t t = t0; t < t1; ++t) {
+        const SegTile T = tiles[t];
+        if (T.seg != seg) {  // (workgroup-uniform)
+            flush();
+            seg = T.seg;
+        }
+        for (uint32_t j0 = 0; j0 < T.count; j0 += kThreads) {
+            const uint32_t j = j0 + threadIdx.x;
+            const bool ok = j < T.count;
+            uint64_t k = 0;
+            if (ok) k = TEXT ? text_key(G, dist, T.start + j, syms) : kin[T.start + j];
+            const uint64_t valid = __ballot(ok);
+            for (uint32_t p = 0; p < passes; ++p) {
+                const uint32_t d = (uint32_t)(k >> (RB * p)) & (BINS - 1u);
+                const uint64_t m = match_digit<RB>(d, valid);
+                if (ok && (m & lanes_below()) == 0) atomicAdd(&h[p * BINS + d], (uint32_t)__popcll(m));
+            }
+        }
+    }
+    flush();
+}
+
+// where each digit's run of each segment starts: the segment's start + the exclusive
+// prefix of its digit counts (one workgroup per segment and pass)
+template <int RB>
+__global__ void __launch_bounds__(kThreads) k_seg_base(const uint32_t *ghist, const uint32_t *seg_start,
+                                                       uint32_t passes, uint32_t *base) {
+    constexpr uint32_t BINS = 1u << RB, BPT = BINS / kThreads;
+    __shared__ uint32_t red[kWaves];
+    const uint32_t sp = blockIdx.x, seg = sp / passes;
+    const uint32_t *hp = ghist + (uint64_t)sp * BINS;
+    uint32_t v[BPT], sum = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < BPT; ++i) {
+        v[i] = hp[threadIdx.x * BPT + i];
+        sum += v[i];
+    }
+    uint32_t run = seg_start[seg] + block_excl_scan(sum, red, nullptr);
+#pragma unroll
+    for (uint32_t i = 0; i < BPT; ++i) {
+        base[(uint64_t)sp * BINS + threadIdx.x * BPT + i] = run;
+        run += v[i];
+    }
+}
+
+// ---------------------------------------------------------------- one radix pass
+template <int RB, bool TEXT>
+__global__ void __launch_bounds__(kThreads) k_seg_pass(const SegTile *tiles, uint32_t *tile_ctr, const uint64_t *kin,
+                                                       const uint32_t *vin, uint64_t *kout, uint32_t *vout,
+                                                       uint32_t pass, uint32_t passes, const uint32_t *base,
+                                                       uint32_t *status, const uint8_t *G, const uint16_t *dist,
+                                                       uint32_t syms, uint32_t *err) {
+    constexpr uint32_t BINS = 1u << RB, BPT = BINS / kThreads;
+    __shared__ uint32_t s_tile;
+    __shared__ uint16_t wh[kWaves][BINS];  // per wave: running count, then the wave's offset in the tile
+    __shared__ uint32_t s_excl[BINS];      // tile-local start of each digit's run
+    __shared__ uint32_t s_dst[BINS];       // global position of that run's first element
+    __shared__ uint32_t red[kWaves];
+    __shared__ uint64_t lk[kSortTile];
+    __shared__ uint32_t lv[kSortTile];
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6, shift = RB * pass;
+    if (threadIdx.x == 0) s_tile = atomicAdd(tile_ctr, 1u);  // tiles start in order: look-back never waits on a later one
+    for (uint32_t i = threadIdx.x; i < kWaves * BINS; i += kThreads) (&wh[0][0])[i] = 0;
+    __syncthreads();
+    const uint32_t t = s_tile;
+    const SegTile T = tiles[t];
+    // ---- rank: wave w takes elements [w * 1024, (w + 1) * 1024) of the tile, 64 at a time
+    uint64_t k[kItems];
+    uint32_t v[kItems];
+    uint16_t r[kItems];
+#pragma unroll
+    for (uint32_t it = 0; it < kItems; ++it) {
+        const uint32_t j = w * (kItems * 64) + it * 64 + lane;
+        const bool ok = j < T.count;
+        k[it] = 0;
+        v[it] = 0;
+        if (ok) {
+            if (TEXT) {
+                k[it] = text_key(G, dist, T.start + j, syms);
+                v[it] = T.start + j;
+            } else {
+                k[it] = kin[T.start + j];
+                v[it] = vin[T.start + j];
+            }
+        }
+        const uint32_t d = (uint32_t)(k[it] >> shift) & (BINS - 1u);
+        const uint64_t m = match_digit<RB>(d, __ballot(ok));
+        uint32_t prev = 0;
+        if (ok) prev = wh[w][d];
+        const uint32_t below = (uint32_t)__popcll(m & lanes_below());
+        r[it] = (uint16_t)(prev + below);
+        if (ok && below == 0) wh[w][d] = (uint16_t)(prev + (uint32_t)__popcll(m));
+    }
+    __syncthreads();
+    // ---- per digit: the waves' offsets, the tile's count, its run start in the tile
+    uint32_t cnt[BPT], tsum = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < BPT; ++i) {
+        const uint32_t b = threadIdx.x * BPT + i;
+        uint32_t c = 0;
+        for (uint32_t x = 0; x < kWaves; ++x) {
+            const uint32_t y = wh[x][b];
+            wh[x][b] = (uint16_t)c;
+            c += y;
+        }
+        cnt[i] = c;
+        tsum += c;
+    }
+    uint32_t run = block_excl_scan(tsum, red, nullptr);
+#pragma unroll
+    for (uint32_t i = 0; i < BPT; ++i) {
+        s_excl[threadIdx.x * BPT + i] = run;
+        run += cnt[i];
+    }
+    // ---- look-back over the earlier tiles of this segment, per digit
+    const uint32_t *sb = base + ((uint64_t)T.seg * passes + pass) * BINS;
+    uint32_t fail = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < BPT; ++i) {
+        const uint32_t b = threadIdx.x * BPT + i;
+        uint32_t *mine = status + (uint64_t)t * BINS + b;
+        uint32_t excl = 0;
+        if (T.first) {
+            __hip_atomic_store(mine, kFlagIncl | cnt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(mine, kFlagAgg | cnt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint32_t j = t - 1, spins = 0;
+            while (true) {
+                const uint32_t x = __hip_atomic_load(status + (uint64_t)j * BINS + b, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                if ((x & ~kCountMask) == 0) {
+                    if (++spins > kSpinBound) {
+                        fail = 1;
+                        break;
+                    }
+                    continue;
+                }
+                excl += x & kCountMask;
+                if ((x & ~kCountMask) == kFlagIncl) break;
+                --j;
+            }
+            __hip_atomic_store(mine, kFlagIncl | (excl + cnt[i]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_dst[b] = sb[b] + excl;
+    }
+    if (fail) atomicOr(err, 1u);
+    __syncthreads();
+    // ---- stage the tile in digit order
+#pragma unroll
+    for (uint32_t it = 0; it < kItems; ++it) {
+        const uint32_t j = w * (kItems * 64) + it * 64 + lane;
+        if (j < T.count) {
+            const uint32_t d = (uint32_t)(k[it] >> shift) & (BINS - 1u);
+            const uint32_t at = s_excl[d] + wh[w][d] + r[it];
+            lk[at] = k[it];
+            lv[at] = v[it];
+        }
+    }
+    __syncthreads();
+    // ---- write each digit's run to its place (consecutive lanes, consecutive addresses)
+    for (uint32_t i = threadIdx.x; i < T.count; i += kThreads) {
+        const uint64_t kk = lk[i];
+        const uint32_t d = (uint32_t)(kk >> shift) & (BINS - 1u);
+        const uint32_t dst = s_dst[d] + (i - s_excl[d]);
+        kout[dst] = kk;
+        vout[dst] = lv[i];
+    }
+}
+
+// ---------------------------------------------------------------- scans
+template <ScanOp OP>
+SD uint32_t op_id() {
+    return OP == ScanOp::kMax ? 0u : OP == ScanOp::kMin ? 0xffffffffu : 0u;
+}
+template <ScanOp OP>
+SD uint32_t op_do(uint32_t a, uint32_t b) {
+    return OP == ScanOp::kMax ? max(a, b) : OP == ScanOp::kMin ? min(a, b) : a + b;
+}
+constexpr uint32_t kScanBlock = 4096;  // elements per workgroup (16 per thread)
+
+template <ScanOp OP, bool REV>
+SD uint64_t scan_at(uint64_t i, uint64_t n) { return REV ? n - 1 - i : i; }
+
+template <ScanOp OP>
+SD uint32_t block_incl_scan(uint32_t x, uint32_t *red, uint32_t *all) {
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+        if (lane >= o) x = op_do<OP>(x, y);
+    }
+    if (lane == 63) red[w] = x;
+    __syncthreads();
+    uint32_t before = op_id<OP>(), tot = op_id<OP>();
+    for (uint32_t i = 0; i < kWaves; ++i) {
+        if (i < w) before = op_do<OP>(before, red[i]);
+        tot = op_do<OP>(tot, red[i]);
+    }
+    __syncthreads();
+    if (all) *all = tot;
+    return op_do<OP>(before, x);
+}
+
+template <ScanOp OP, bool REV>
+__global__ void __launch_bounds__(kThreads) k_scan_reduce(const uint32_t *in, uint64_t n, uint32_t *part) {
+    __shared__ uint32_t red[kWaves];
+    const uint64_t b0 = (uint64_t)blockIdx.x * kScanBlock;
+    uint32_t acc = op_id<OP>();
+    for (uint32_t j = threadIdx.x; j < kScanBlock; j += kThreads) {
+        const uint64_t i = b0 + j;
+        if (i < n) acc = op_do<OP>(acc, in[scan_at<OP, REV>(i, n)]);
+    }
+    uint32_t all;
+    (void)block_incl_scan<OP>(acc, red, &all);
+    if (threadIdx.x == 0) part[blockIdx.x] = all;
+}
+// exclusive scan of the block partials, one workgroup
+template <ScanOp OP>
+__global__ void __launch_bounds__(1024) k_scan_parts(uint32_t *part, uint32_t nb) {
+    __shared__ uint32_t red[16];
+    const uint32_t per = (nb + 1023) / 1024, a = threadIdx.x * per, e = min(nb, a + per);
+    uint32_t acc = op_id<OP>();
+    for (uint32_t i = a; i < e; ++i) acc = op_do<OP>(acc, part[i]);
+    // exclusive scan of acc over the 1,024 threads (16 waves)
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    uint32_t x = acc;
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+        if (lane >= o) x = op_do<OP>(x, y);
+    }
+    if (lane == 63) red[w] = x;
+    __syncthreads();
+    uint32_t before = op_id<OP>();
+    for (uint32_t i = 0; i < w; ++i) before = op_do<OP>(before, red[i]);
+    uint32_t run = op_do<OP>(before, (uint32_t)__shfl_up((int)x, 1));
+    if (lane == 0) run = before;
+    for (uint32_t i = a; i < e; ++i) {
+        const uint32_t y = part[i];
+        part[i] = run;
+        run = op_do<OP>(run, y);
+    }
+}
+template <ScanOp OP, bool REV>
+__global__ void __launch_bounds__(kThreads) k_scan_apply(const uint32_t *in, uint32_t *out, uint64_t n,
+                                                         const uint32_t *part) {
+    __shared__ uint32_t red[kWaves];
+    const uint64_t b0 = (uint64_t)blockIdx.x * kScanBlock;
+    // each thread: 16 consecutive elements (in scan order)
+    const uint64_t i0 = b0 + (uint64_t)threadIdx.x * kItems;
+    uint32_t x[kItems], acc = op_id<OP>();
+#pragma unroll
+    for (uint32_t j = 0; j < kItems; ++j) {
+        const uint64_t i = i0 + j;
+        x[j] = i < n ? in[scan_at<OP, REV>(i, n)] : op_id<OP>();
+        acc = op_do<OP>(acc, x[j]);
+    }
+    const uint32_t incl = block_incl_scan<OP>(acc, red, nullptr);
+    // exclusive of this thread = the block carry + the threads before it
+    uint32_t run = (uint32_t)__shfl_up((int)incl, 1);
+    __shared__ uint32_t last[kWaves];
+    if (lane_id() == 63) last[threadIdx.x >> 6] = incl;
+    __syncthreads();
+    if (lane_id() == 0) run = threadIdx.x ? last[(threadIdx.x >> 6) - 1] : op_id<OP>();
+    run = op_do<OP>(part[blockIdx.x], run);
+#pragma unroll
+    for (uint32_t j = 0; j < kItems; ++j) {
+        const uint64_t i = i0 + j;
+        run = op_do<OP>(run, x[j]);
+        if (i < n) out[scan_at<OP, REV>(i, n)] = run;
+    }
+}
+
+template <ScanOp OP, bool REV>
+hipError_t scan_run(hipStream_t s, const SortAlloc &A, const uint32_t *in, uint32_t *out, uint64_t n) {
+    if (!n) return hipSuccess;
+    const uint64_t nb = (n + kScanBlock - 1) / kScanBlock;
+    if (nb > 0xffffffffull) return hipErrorInvalidValue;
+    auto *part = (uint32_t *)A.alloc(A.self, nb * 4 + 64);
+    if (!part) return hipErrorOutOfMemory;
+    k_scan_reduce<OP, REV><<<(uint32_t)nb, kThreads, 0, s>>>(in, n, part);
+    k_scan_parts<OP><<<1, 1024, 0, s>>>(part, (uint32_t)nb);
+    k_scan_apply<OP, REV><<<(uint32_t)nb, kThreads, 0, s>>>(in, out, n, part);
+    A.release(A.self, part, nb * 4 + 64);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+void seg_tiles(const uint32_t *start, const uint32_t *len, uint32_t nseg, std::vector<SegTile> &out) {
+    out.clear();
+    for (uint32_t g = 0; g < nseg; ++g)
+        for (uint32_t o = 0; o < len[g]; o += kSortTile)
+            out.push_back(SegTile{start[g] + o, std::min(kSortTile, len[g] - o), g, o == 0 ? 1u : 0u});
+}
+
+hipError_t seg_sort_pairs(hipStream_t s, const SortAlloc &A, const std::vector<SegTile> &tiles,
+                          const std::vector<uint32_t> &seg_start, uint32_t bits, int rb, uint64_t *k0, uint32_t *v0,
+                          const uint8_t *G, const uint16_t *dist, uint32_t syms, uint64_t *ka, uint32_t *va,
+                          uint64_t *kb, uint32_t *vb, uint64_t *kout, uint32_t *vout, uint32_t *err) {
+    if (tiles.empty()) return hipSuccess;
+    if (rb != 8 && rb != 9) return hipErrorInvalidValue;
+    const bool text = G != nullptr;
+    const uint32_t bins = 1u << rb, passes = (bits + rb - 1) / rb, nseg = (uint32_t)seg_start.size();
+    if (passes == 0 || passes > kMaxPasses) return hipErrorInvalidValue;
+    const uint32_t nt = (uint32_t)tiles.size();
+    // scratch: tiles, segment starts, digit counts and run starts, tile counters, look-back words
+    const uint64_t b_tiles = (uint64_t)nt * sizeof(SegTile), b_starts = (uint64_t)nseg * 4,
+                   b_hist = (uint64_t)nseg * passes * bins * 4, b_status = (uint64_t)nt * bins * 4;
+    const uint64_t o_starts = (b_tiles + 255) / 256 * 256, o_hist = o_starts + (b_starts + 255) / 256 * 256,
+                   o_base = o_hist + (b_hist + 255) / 256 * 256, o_ctr = o_base + (b_hist + 255) / 256 * 256,
+                   o_status = o_ctr + 256, total = o_status + b_status + 256;
+    auto *mem = (uint8_t *)A.alloc(A.self, total);
+    if (!mem) return hipErrorOutOfMemory;
+    auto *d_tiles = (SegTile *)mem;
+    auto *d_starts = (uint32_t *)(mem + o_starts);
+    auto *d_hist = (uint32_t *)(mem + o_hist);
+    auto *d_base = (uint32_t *)(mem + o_base);
+    auto *d_ctr = (uint32_t *)(mem + o_ctr);
+    auto *d_status = (uint32_t *)(mem + o_status);
+    hipError_t e = hipMemcpyAsync(d_tiles, tiles.data(), b_tiles, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_starts, seg_start.data(), b_starts, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemsetAsync(d_hist, 0, b_hist, s);
+    if (e == hipSuccess) e = hipMemsetAsync(d_ctr, 0, 256, s);
+    if (e != hipSuccess) {
+        A.release(A.self, mem, total);
+        return e;
+    }
+    // (the host-side tile table must outlive the copy: the caller keeps `tiles` until the
+    // stream passes this point -- it synchronises before releasing it)
+    const uint32_t hb = (nt + kHistTiles - 1) / kHistTiles;
+#define PX_SORT_RB(RB_)                                                                                            \
+    do {                                                                                                           \
+        if (text)                                                                                                  \
+            k_seg_hist<RB_, true><<<hb, kThreads, 0, s>>>(d_tiles, nt, nullptr, G, dist, syms, passes, d_hist);    \
+        else                                                                                                       \
+            k_seg_hist<RB_, false><<<hb, kThreads, 0, s>>>(d_tiles, nt, k0, nullptr, nullptr, 0, passes, d_hist);  \
+        k_seg_base<RB_><<<nseg * passes, kThreads, 0, s>>>(d_hist, d_starts, passes, d_base);                     \
+        const uint64_t *ki = k0;                                                                                   \
+        const uint32_t *vi = v0;                                                                                   \
+        for (uint32_t p = 0; p < passes && e == hipSuccess; ++p) {                                                 \
+            uint64_t *ko;                                                                                          \
+            uint32_t *vo;                                                                                          \
+            if (p + 1 == passes) {                                                                                 \
+                ko = kout;                                                                                         \
+                vo = vout;                                                                                         \
+            } else if (p % 2 == 0) {                                                                               \
+                ko = ka;                                                                                           \
+                vo = va;                                                                                           \
+            } else {                                                                                               \
+                ko = text ? kb : k0;                                                                               \
+                vo = text ? vb : v0;                                                                               \
+            }                                                                                                      \
+            e = hipMemsetAsync(d_status, 0, b_status, s);                                                          \
+            if (e != hipSuccess) break;                                                                            \
+            if (text && p == 0)                                                                                    \
+                k_seg_pass<RB_, true><<<nt, kThreads, 0, s>>>(d_tiles, d_ctr + p, nullptr, nullptr, ko, vo, p,     \
+                                                              passes, d_base, d_status, G, dist, syms, err);       \
+            else                                                                                                   \
+                k_seg_pass<RB_, false><<<nt, kThreads, 0, s>>>(d_tiles, d_ctr + p, ki, vi, ko, vo, p, passes,      \
+                                                               d_base, d_status, nullptr, nullptr, 0, err);        \
+            ki = ko;                                                                                               \
+            vi = vo;                                                                                               \
+            e = hipGetLastError();                                                                                 \
+        }                                                                                                          \
+    } while (0)
+    if (rb == 9)
+        PX_SORT_RB(9);
+    else
+        PX_SORT_RB(8);
+#undef PX_SORT_RB
+    if (e == hipSuccess) e = hipStreamSynchronize(s);  // (the tile table upload reads host memory)
+    A.release(A.self, mem, total);
+    return e;
+}
+
+hipError_t scan_u32(hipStream_t s, const SortAlloc &A, const uint32_t *in, uint32_t *out, uint64_t n, ScanOp op,
+                    bool reverse) {
+    switch (op) {
+    case ScanOp::kMax: return reverse ? scan_run<ScanOp::kMax, true>(s, A, in, out, n) : scan_run<ScanOp::kMax, false>(s, A, in, out, n);
+    case ScanOp::kMin: return reverse ? scan_run<ScanOp::kMin, true>(s, A, in, out, n) : scan_run<ScanOp::kMin, false>(s, A, in, out, n);
+    default: return reverse ? scan_run<ScanOp::kPlus, true>(s, A, in, out, n) : scan_run<ScanOp::kPlus, false>(s, A, in, out, n);
+    }
+}
+
+}  // namespace px
