@@ -131,6 +131,8 @@ typedef struct px_stats {
     uint64_t deferred_mismatch;   /* deferred records whose `replaced`, returned at call time, differed
                                      from the stored result (only possible when a queued record's
                                      compat-decoded key is not its key: reported, never hidden) */
+    uint64_t last_get_device_keys; /* keys of the last px_get_batch resolved by the device key index
+                                     (0: the batch resolved its keys on the host) */
 } px_stats;
 
 px_ctx *px_open(const px_opts *opts);

@@ -74,7 +74,7 @@ class PxStats(C.Structure):
                 ("last_psa_rotations", C.c_uint64), ("last_psa_pool_ms", C.c_double),
                 ("device_live_bytes", C.c_uint64), ("device_peak_bytes", C.c_uint64),
                 ("deferred_records", C.c_uint64), ("deferred_flushes", C.c_uint64),
-                ("deferred_mismatch", C.c_uint64)]
+                ("deferred_mismatch", C.c_uint64), ("last_get_device_keys", C.c_uint64)]
 
 
 SET_RESULT_DTYPE = np.dtype([("status", "<u4"), ("replaced", "<u4"), ("shard", "<u4"), ("chunk", "<u4"),

@@ -239,6 +239,26 @@ struct GatherQuery {
     uint32_t pad;
 };
 
+// ---- device key index (px_keyidx.hip): getitem's key -> record resolution on the GPU for
+// the keys the host's own fast path would answer (px_runtime.cpp resolve_key: the newest
+// record stored under the raw key, live, whose compat key prefix is the escaped key)
+struct DkRec {
+    const SpanEnt *sp;   // compat span table (null: none)
+    const uint32_t *t;
+    const SpanEnt *xsp;  // exact span table (null: none; == sp when the expansions agree)
+    const uint32_t *xt;
+    const uint8_t *comp;  // the record's compressed bytes
+    uint64_t key_off;     // its raw key in the index's key arena
+    uint32_t key_len, n, len, xn, xlen, doc_len, flags, pad;
+};
+static_assert(sizeof(DkRec) == 80, "DkRec layout");
+constexpr uint32_t kDkLive = 1, kDkClean = 2;
+struct DkSlot {
+    unsigned long long h;  // key hash | 1; 0: empty
+    uint32_t gid1;         // newest record id + 1 stored under the key
+    uint32_t pad;
+};
+
 // gather task (64 tiles): the first query, the span holding the task's first tile in its
 // table, and a bit per tile where a later query starts
 struct alignas(16) GatherTask {

@@ -311,10 +311,34 @@ __global__ void __launch_bounds__(256) k_dbl_win(uint32_t N, uint32_t tag, uint3
     uint32_t sorted = 0, active = 0, mx = 0;
     uint64_t pend = 0;  // pending long groups, lane i holds entry i
     uint32_t npend = 0;
-    for (uint32_t w = blockIdx.x * (blockDim.x >> 6) + wv; w < nwin; w += waves) {
+    // a wave takes 64 windows at a time and visits only those holding an unsorted slot
+    // (one 64-byte act load per lane finds them: late steps leave most windows empty, and
+    // testing them one by one was a dependent load per window)
+    // (lane l of chunk c tests window l * nch + c: a run of busy windows -- a template's
+    // copies -- is dealt over many waves instead of queueing on one)
+    const uint32_t nch = (nwin + 63) / 64;
+    for (uint32_t c = blockIdx.x * (blockDim.x >> 6) + wv; c < nch; c += waves) {
+      uint64_t todo;
+      {
+        const uint32_t wl = lane * nch + c, s0 = wl * 64;
+        bool any = false;
+        if (wl < nwin) {
+            if (s0 + 64 <= N) {
+                const uint4 *a4 = (const uint4 *)(act + s0);
+                const uint4 x = a4[0], y = a4[1], z = a4[2], u = a4[3];
+                any = ((x.x | x.y | x.z | x.w) | (y.x | y.y | y.z | y.w) | (z.x | z.y | z.z | z.w) |
+                       (u.x | u.y | u.z | u.w)) != 0;
+            } else {
+                for (uint32_t q = s0; q < N; ++q) any |= act[q] != 0;
+            }
+        }
+        todo = __ballot(any);
+      }
+      while (todo) {
+        const uint32_t w = lobit(todo) * nch + c;
+        todo &= todo - 1;
         const uint32_t b = w * 64, sA = b + lane, sB = b + 64 + lane;
         const bool inA = sA < N;
-        if (!__ballot(inA && act[sA])) continue;
         const uint32_t g = inA ? gsz[sA] : 0u;
         const bool start = (g & kTag) == tag && (g & kSizeMask) >= 2;
         const uint32_t gs = g & kSizeMask;
@@ -374,6 +398,7 @@ __global__ void __launch_bounds__(256) k_dbl_win(uint32_t N, uint32_t tag, uint3
         if (B.mem) win_put(B, b, lB, eB, tB, tag, sa, sd, act, gsz, rank, ac, mx);
         sorted += (uint32_t)__popcll(__ballot(A.mem)) + (uint32_t)__popcll(__ballot(B.mem));
         active += ac;
+      }
     }
     push_long(L, lane < npend, pend);
     active = wave_sum(active);
@@ -602,11 +627,16 @@ __global__ void __launch_bounds__(256) k_dbl_blk(const uint64_t *list, const uin
     block_stat(ss, tid == 0 ? sorted : 0u, active, mx);
 }
 
-// big groups (host-driven steps): gather every member with key (group << 32 | key), radix
-// sort (stable: ties keep suffix-array order), place back, heads by a max-scan, then ranks
-// and subgroups.  boff = exclusive prefix of the groups' sizes (host-computed).
+// big groups (host-driven steps): gather every member with key (group << 32 | key), sort
+// each group by its key (px_sort.hip: stable, ties keep suffix-array order), place back,
+// heads by a max-scan, then ranks and subgroups.  boff = exclusive prefix of the groups'
+// sizes (host-computed).  PACKED (fewer than 65,536 groups): the member's distance rides in
+// the key's top 16 bits and its position is the sorted value, so placing a member back
+// reads nothing scattered (otherwise the value is the gather index and the position and
+// distance come from gp / gd).
 // flat over the T gathered members: a block's 256 members span at most two groups (every
 // big group has > 4,096 members), found by one search of boff per block
+template <bool PACKED>
 __global__ void __launch_bounds__(256) k_big_gather(uint32_t T, uint32_t nb, const uint64_t *list, const uint32_t *boff,
                                                     const uint32_t *sa, const uint16_t *sd, const uint32_t *key,
                                                     uint64_t *ck, uint32_t *cv, uint32_t *gp, uint16_t *gd, StepStat ss) {
@@ -627,19 +657,38 @@ __global__ void __launch_bounds__(256) k_big_gather(uint32_t T, uint32_t nb, con
     if (b + 1 < nb && boff[b + 1] <= k) ++b;
     const uint64_t ent = list[b];
     const uint32_t start = (uint32_t)ent, o = boff[b], i = k - o;
-    ck[k] = (uint64_t)b << 32 | key[start + i];
-    cv[k] = k;
-    gp[k] = sa[start + i];
-    gd[k] = sd[start + i];
+    if (PACKED) {
+        ck[k] = (uint64_t)sd[start + i] << 48 | (uint64_t)b << 32 | key[start + i];
+        cv[k] = sa[start + i];
+    } else {
+        ck[k] = (uint64_t)b << 32 | key[start + i];
+        cv[k] = k;
+        gp[k] = sa[start + i];
+        gd[k] = sd[start + i];
+    }
     if (i == 0) stat_put(ss, b, (uint32_t)(ent >> 32), 0, 0);
 }
-__global__ void __launch_bounds__(256) k_big_head(uint32_t T, const uint32_t *boff, const uint64_t *ck2, uint32_t *hf) {
+// the segments of the sorts (px_sort.hip): the round's shards, the big groups
+__global__ void __launch_bounds__(256) k_psa_segs(uint32_t ns, const PsaShard *sh, uint32_t *start, uint32_t *len) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < ns) {
+        start[i] = sh[i].base;
+        len[i] = sh[i].len;
+    }
+}
+__global__ void __launch_bounds__(256) k_big_segs(uint32_t nb, const uint64_t *list, uint32_t *len) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nb) len[i] = (uint32_t)(list[i] >> 32);
+}
+__global__ void __launch_bounds__(256) k_big_head(uint32_t T, const uint32_t *boff, const uint64_t *ck2, uint32_t bmask,
+                                                  uint32_t *hf) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= T) return;
     const uint64_t c = ck2[k];
-    const uint32_t b = (uint32_t)(c >> 32), key = (uint32_t)c;
+    const uint32_t b = (uint32_t)(c >> 32) & bmask, key = (uint32_t)c;
     hf[k] = (k == boff[b] || key != (uint32_t)ck2[k - 1] || key == 0) ? k : 0u;
 }
+template <bool PACKED>
 __global__ void __launch_bounds__(256) k_big_put(uint32_t T, const uint64_t *list, const uint32_t *boff, const uint64_t *ck2,
                                                  const uint32_t *cv2, const uint32_t *gp, const uint16_t *gd,
                                                  const uint32_t *hf, const uint32_t *hk, const uint32_t *nk, uint32_t tag,
@@ -649,11 +698,11 @@ __global__ void __launch_bounds__(256) k_big_put(uint32_t T, const uint64_t *lis
     uint32_t ac = 0, mx = 0;
     if (k < T) {
         const uint64_t c = ck2[k];
-        const uint32_t b = (uint32_t)(c >> 32), key = (uint32_t)c, o = boff[b];
-        const uint32_t size = (uint32_t)(list[b] >> 32), q = k - o, src = cv2[k];
+        const uint32_t b = PACKED ? (uint32_t)(c >> 32) & 0xffffu : (uint32_t)(c >> 32), key = (uint32_t)c, o = boff[b];
+        const uint32_t size = (uint32_t)(list[b] >> 32), q = k - o, v = cv2[k];
         const uint32_t nxt = min(nk[k] - o, size);
-        put_sorted((uint32_t)list[b], q, gp[src], gd[src], key, hf[k] == k, hk[k] - o, nxt, tag, sa, sd, act, gsz, rank,
-                   ac, mx);
+        const uint32_t p = PACKED ? v : gp[v], d = PACKED ? (uint32_t)(c >> 48) : gd[v];
+        put_sorted((uint32_t)list[b], q, p, d, key, hf[k] == k, hk[k] - o, nxt, tag, sa, sd, act, gsz, rank, ac, mx);
     }
     block_stat(ss, 0, ac, mx);
 }
@@ -1576,18 +1625,16 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     const SortAlloc SA{A.alloc, A.release, A.self};
     auto *keys = S.get<uint64_t>(n64 * 8);
     {
-        std::vector<uint32_t> sst(nshards), slen(nshards);
-        for (uint32_t i = 0; i < nshards; ++i) {
-            sst[i] = hshards[i].base;
-            slen[i] = hshards[i].len;
-        }
-        std::vector<SegTile> tiles;
-        seg_tiles(sst.data(), slen.data(), nshards, tiles);
+        std::vector<uint32_t> slen(nshards);
+        for (uint32_t i = 0; i < nshards; ++i) slen[i] = hshards[i].len;
+        auto *segs = S.get<uint32_t>((uint64_t)nshards * 8 + 64);
+        k_psa_segs<<<(nshards + 255) / 256, 256, 0, s>>>(nshards, shards, segs, segs + nshards);
         auto *keys2 = S.get<uint64_t>(n64 * 8);
         auto *va = S.get<uint32_t>(n64 * 4), *vb = S.get<uint32_t>(n64 * 4);
         // passes: text -> keys -> keys2 -> keys -> keys2 -> keys -> (keys2, sa)
-        PSA_CHECK(seg_sort_pairs(s, SA, tiles, sst, 9 * syms, 9, nullptr, nullptr, G, dist, syms, keys, va, keys2, vb,
-                                 keys2, sa, cnt + kCntSortErr));
+        PSA_CHECK(seg_sort_pairs(s, SA, nshards, seg_tile_count(slen.data(), nshards), segs, segs + nshards, 9 * syms, 9,
+                                 nullptr, nullptr, G, dist, syms, keys, va, keys2, vb, keys2, sa, cnt + kCntSortErr));
+        S.put(segs);
         S.put(va);
         S.put(vb);
         uint32_t *hflag = (uint32_t *)keys, *head = (uint32_t *)keys + N;  // (the pass buffers are spent)
@@ -1666,25 +1713,33 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
                 auto *gp = S.get<uint32_t>(T * 4), *hf = S.get<uint32_t>(T * 4), *hk = S.get<uint32_t>(T * 4);
                 auto *nf = S.get<uint32_t>(T * 4), *nk = S.get<uint32_t>(T * 4);
                 auto *gd = S.get<uint16_t>(T * 2 + 64);
-                k_big_gather<<<blocks(T), tb, 0, s>>>((uint32_t)T, nbig, LL.lst[4], d_boff, sa, sd, key, ck, cv, gp, gd, ss);
+                const bool packed = nbig <= 0x10000u;
+                if (packed)
+                    k_big_gather<true><<<blocks(T), tb, 0, s>>>((uint32_t)T, nbig, LL.lst[4], d_boff, sa, sd, key, ck, cv,
+                                                                gp, gd, ss);
+                else
+                    k_big_gather<false><<<blocks(T), tb, 0, s>>>((uint32_t)T, nbig, LL.lst[4], d_boff, sa, sd, key, ck, cv,
+                                                                 gp, gd, ss);
                 // every group sorted by its 32-bit keys on its own (px_sort.hip): segments = groups
-                std::vector<uint32_t> gst(nbig), glen(nbig);
-                for (uint32_t b = 0; b < nbig; ++b) {
-                    gst[b] = boff[b];
-                    glen[b] = (uint32_t)(bl[b] >> 32);
-                }
-                std::vector<SegTile> gt;
-                seg_tiles(gst.data(), glen.data(), nbig, gt);
-                e = seg_sort_pairs(s, SA, gt, gst, 32, 8, ck, cv, nullptr, nullptr, 0, cka, cva, nullptr, nullptr, ck2, cv2,
-                                   cnt + kCntSortErr);
+                std::vector<uint32_t> glen(nbig);
+                for (uint32_t b = 0; b < nbig; ++b) glen[b] = (uint32_t)(bl[b] >> 32);
+                auto *d_glen = S.get<uint32_t>((uint64_t)nbig * 4 + 64);
+                k_big_segs<<<(nbig + 255) / 256, 256, 0, s>>>(nbig, LL.lst[4], d_glen);
+                e = seg_sort_pairs(s, SA, nbig, seg_tile_count(glen.data(), nbig), d_boff, d_glen, 32, 8, ck, cv, nullptr,
+                                   nullptr, 0, cka, cva, nullptr, nullptr, ck2, cv2, cnt + kCntSortErr);
+                S.put(d_glen);
                 if (e != hipSuccess) return e;
-                k_big_head<<<blocks(T), tb, 0, s>>>((uint32_t)T, d_boff, ck2, hf);
+                k_big_head<<<blocks(T), tb, 0, s>>>((uint32_t)T, d_boff, ck2, packed ? 0xffffu : 0xffffffffu, hf);
                 k_big_next<<<blocks(T), tb, 0, s>>>((uint32_t)T, hf, nf);
                 e = scan_u32(s, SA, hf, hk, T, ScanOp::kMax, false);
                 if (e == hipSuccess) e = scan_u32(s, SA, nf, nk, T, ScanOp::kMin, true);
                 if (e != hipSuccess) return e;
-                k_big_put<<<blocks(T), tb, 0, s>>>((uint32_t)T, LL.lst[4], d_boff, ck2, cv2, gp, gd, hf, hk, nk, tag, sa, sd,
-                                                   act, gsz, rank, ss);
+                if (packed)
+                    k_big_put<true><<<blocks(T), tb, 0, s>>>((uint32_t)T, LL.lst[4], d_boff, ck2, cv2, gp, gd, hf, hk, nk,
+                                                             tag, sa, sd, act, gsz, rank, ss);
+                else
+                    k_big_put<false><<<blocks(T), tb, 0, s>>>((uint32_t)T, LL.lst[4], d_boff, ck2, cv2, gp, gd, hf, hk, nk,
+                                                              tag, sa, sd, act, gsz, rank, ss);
                 for (const void *q : {(const void *)d_boff, (const void *)ck, (const void *)ck2, (const void *)cv,
                                       (const void *)cv2, (const void *)gp, (const void *)hf, (const void *)hk,
                                       (const void *)nf, (const void *)nk, (const void *)gd, (const void *)cka,

@@ -26,6 +26,7 @@
 #include "../../include/pixiu_amd.h"
 #include "px_common.h"
 #include "px_host.h"
+#include "px_sort.h"
 
 namespace px {
 hipError_t launch_doc_len(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, const uint8_t *,
@@ -54,6 +55,13 @@ hipError_t launch_decode_addr(hipStream_t, const DecodeQuery *, uint32_t, const 
 hipError_t launch_span_build(hipStream_t, uint32_t, const SpanJob *);
 hipError_t launch_gather(hipStream_t, uint32_t, void *, const GatherQuery *, uint32_t, uint8_t *, uint32_t *,
                          uint32_t *, bool);
+hipError_t launch_dk_insert(hipStream_t, uint32_t, uint32_t, const DkRec *, const uint8_t *, DkSlot *, uint32_t,
+                            uint32_t *);
+hipError_t launch_dk_kill(hipStream_t, uint32_t, const uint32_t *, DkRec *);
+hipError_t launch_dk_lookup(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, const DkSlot *, uint32_t,
+                            const DkRec *, const uint8_t *, uint32_t, GatherQuery *, uint32_t *, uint32_t *, uint32_t *);
+hipError_t launch_dk_fill(hipStream_t, uint32_t, const uint32_t *, const uint32_t *, const uint32_t *, const uint32_t *,
+                          GatherQuery *, uint64_t *);
 int debug_trace_take(int32_t *, uint32_t);
 int debug_prof_take(unsigned long long *, uint32_t);
 }  // namespace px
@@ -197,6 +205,7 @@ struct Chunk {
     std::string kp;  // concatenated compat key prefixes
     std::vector<uint64_t> kp_off;
     std::vector<uint32_t> kp_len;
+    std::vector<uint32_t> gid;  // device key index record id of each slot (kNone / past the end: none)
     // span tables (full-range getitem as a gather); sized lazily
     struct Span {
         const SpanEnt *p = nullptr;  // device; null: decode through the segment walk
@@ -323,6 +332,51 @@ struct px_ctx {
             have_last = true;
         }
     }
+    // ------------------------------------------------------------ device key index
+    // (px_keyidx.hip): raw key -> newest record stored under it, on the device, so a
+    // getitem batch whose every key the host's fast path would answer (resolve_key: that
+    // record live and its compat key prefix the escaped key) resolves without host
+    // lookups.  Any key it cannot answer sends the batch to the host path.
+    struct Dki {
+        bool valid = true;  // false after a mutation the index does not follow (px_load) until reset
+        uint32_t nrec = 0;  // record ids handed out
+        DkRec *rec = nullptr;
+        uint64_t rec_cap = 0;
+        uint8_t *keys = nullptr;
+        uint64_t keys_len = 0, keys_cap = 0;
+        DkSlot *tab = nullptr;
+        uint32_t tab_cap = 0;     // slots, a power of two >= 2 x records
+        uint32_t *err = nullptr;  // device word: an insert gave up (cannot happen)
+        std::vector<uint32_t> kills;  // ids killed (replace / delete) since the last commit
+        std::mutex mu;
+    } dki;
+    static bool dki_enabled() {  // PX_DKI=0: every getitem resolves its keys on the host
+        static const bool on = [] {
+            const char *e = std::getenv("PX_DKI");
+            return !(e && e[0] == '0');
+        }();
+        return on;
+    }
+    void dki_clear() {
+        if (dki.rec) heap.release(dki.rec, dki.rec_cap * sizeof(DkRec));
+        if (dki.keys) heap.release(dki.keys, dki.keys_cap);
+        if (dki.tab) heap.release(dki.tab, (uint64_t)dki.tab_cap * sizeof(DkSlot));
+        if (dki.err) heap.release(dki.err, 256);
+        dki.rec = nullptr;
+        dki.keys = nullptr;
+        dki.tab = nullptr;
+        dki.err = nullptr;
+        dki.rec_cap = dki.keys_cap = dki.keys_len = 0;
+        dki.tab_cap = dki.nrec = 0;
+        dki.kills.clear();
+        for (auto &c : chunks) c.gid.clear();
+    }
+    void dki_commit(uint32_t gid0, const std::vector<DkRec> &recs, const std::vector<uint8_t> &kb);
+    int dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int mode, uint8_t *out, uint64_t out_cap,
+                int out_on_device, uint64_t *out_off, uint32_t *out_len, uint32_t *status, uint64_t *needed);
+    DevBuf dk_qbuf, dk_obuf;
+    HostBuf dk_hbuf, dk_hres;
+
     // cached free device memory kept after a set batch (opts.retain_mb)
     void trim_heap() {
         const uint64_t keep = opts.retain_mb == 0xffffffffu ? ~0ull
@@ -648,6 +702,10 @@ struct px_ctx {
     // PiXiuChunk::delitem (PiXiuStr.cpp:178-187): dead mark, live count, Glob
     void chunk_delitem(Shard &s, const Leaf &l) {
         Chunk &ch = chunks[l.chunk];
+        if (l.idx < ch.gid.size() && ch.gid[l.idx] != kNone) {  // (shards insert on several host threads)
+            std::lock_guard<std::mutex> g(dki.mu);
+            dki.kills.push_back(ch.gid[l.idx]);
+        }
         if (!ch.dead[l.idx]) {
             ch.dead[l.idx] = 1;
             if (ch.used) ch.used--;
@@ -1207,6 +1265,8 @@ struct px_ctx {
     // drop every record, keep the device memory for reuse
     void reset() {
         sync();
+        dki_clear();
+        dki.valid = true;
         for (auto &sp : shards)
             if (sp->arena) heap.release(sp->arena, sp->arena_bytes);
         for (auto &c : chunks)
@@ -2072,6 +2132,56 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         stats.last_span_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts).count();
     }
 
+    // ---- device key index: ids for this batch's live records, in record order (before the
+    // CritBit inserts, whose replaces kill ids -- older ones and this batch's own)
+    const bool dk = dki_enabled() && dki.valid && !raw_docs;
+    const uint32_t dk_gid0 = dki.nrec;
+    std::vector<DkRec> dk_new;
+    std::vector<uint8_t> dk_kb;
+    if (dk) {
+        std::string q;
+        for (uint32_t r = 0; r < n; ++r) {
+            if (!live[r]) continue;
+            Chunk &ch = chunks[rgchunk[r]];
+            const uint32_t i = ridx[r];
+            if (ch.gid.size() <= i) ch.gid.resize(i + 1, kNone);
+            ch.gid[i] = dki.nrec++;
+            const uint8_t *k = hkeys.data() + hkoff[r];
+            const uint64_t kl = hkoff[r + 1] - hkoff[r];
+            DkRec d{};
+            d.key_off = dki.keys_len + dk_kb.size();
+            d.key_len = (uint32_t)kl;
+            dk_kb.insert(dk_kb.end(), k, k + kl);
+            if (i < ch.span.size() && ch.span[i].p) {
+                const Chunk::Span &sp = ch.span[i];
+                d.sp = sp.p;
+                d.t = sp.t;
+                d.n = sp.n;
+                d.len = sp.len;
+                if (sp.eq) {
+                    d.xsp = sp.p;
+                    d.xt = sp.t;
+                    d.xn = sp.n;
+                    d.xlen = sp.len;
+                } else {
+                    d.xsp = sp.xp;
+                    d.xt = sp.xt;
+                    d.xn = sp.xn;
+                    d.xlen = sp.xlen;
+                }
+            }
+            d.comp = ch.slots[i].comp;
+            d.doc_len = ch.doc_len[i];
+            esc_key_into(q, k, kl);
+            const bool clean = kp_matches(Leaf{rgchunk[r], i}, q);
+            d.flags = kDkLive | (clean ? kDkClean : 0u);
+            // (the single shard's CritBit walk is exact only over clean prefixes: one
+            // unclean record and that store resolves on the host from then on)
+            if (!clean && opts.records_per_shard == 0) dki.valid = false;
+            dk_new.push_back(d);
+        }
+    }
+
     phase.mark("CritBit inserts: every shard's own recor");
     // ---- CritBit inserts: every shard's own records in arrival order, shards on host
     // threads (their tries are independent); then a key that moved to a newer shard is
@@ -2130,6 +2240,20 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         const uint32_t r = mv.first;
         cbt_delete(*shards[mv.second], esc_key(hkeys.data() + hkoff[r], hkoff[r + 1] - hkoff[r]));
         replaced[r] = 1;
+    }
+
+    phase.mark("device key index");
+    if (dki.valid && dki_enabled()) {
+        if (dk) dki_commit(dk_gid0, dk_new, dk_kb);
+        std::vector<uint32_t> kills;
+        kills.swap(dki.kills);
+        if (!kills.empty() && dki.rec) {
+            auto *d = (uint32_t *)dk_qbuf.get(kills.size() * 4);
+            h2d(d, kills.data(), kills.size() * 4);
+            hcheck(launch_dk_kill(stream, (uint32_t)kills.size(), d, dki.rec));
+        }
+    } else if (dki.nrec) {
+        dki_clear();
     }
 
     for (auto &b : deferred_release) heap.release(b.first, b.second);
@@ -2486,6 +2610,135 @@ int px_ctx::flush_queue() {
     }
     note_last(n, r.data());
     if (rc != PX_OK && dq_rc == PX_OK) dq_rc = rc;
+    return rc;
+}
+
+// ====================================================================== device key index
+void px_ctx::dki_commit(uint32_t gid0, const std::vector<DkRec> &recs, const std::vector<uint8_t> &kb) {
+    const uint32_t nn = (uint32_t)recs.size();
+    if (!nn) return;
+    if (!dki.err) {
+        dki.err = (uint32_t *)heap.alloc(256);
+        hcheck(hipMemsetAsync(dki.err, 0, 256, stream));
+    }
+    const uint64_t need_rec = (uint64_t)gid0 + nn;
+    if (need_rec > dki.rec_cap) {  // (records only grow; ids are positions in this array)
+        const uint64_t cap = std::max<uint64_t>(need_rec, std::max<uint64_t>(4096, dki.rec_cap * 2));
+        auto *nr = (DkRec *)heap.alloc(cap * sizeof(DkRec));
+        if (dki.rec) {
+            hcheck(hipMemcpyAsync(nr, dki.rec, (size_t)gid0 * sizeof(DkRec), hipMemcpyDeviceToDevice, stream));
+            deferred_release.emplace_back(dki.rec, dki.rec_cap * sizeof(DkRec));
+        }
+        dki.rec = nr;
+        dki.rec_cap = cap;
+    }
+    if (dki.keys_len + kb.size() > dki.keys_cap) {
+        const uint64_t cap = std::max<uint64_t>(dki.keys_len + kb.size(), std::max<uint64_t>(1 << 16, dki.keys_cap * 2));
+        auto *nk = (uint8_t *)heap.alloc(cap);
+        if (dki.keys) {
+            hcheck(hipMemcpyAsync(nk, dki.keys, dki.keys_len, hipMemcpyDeviceToDevice, stream));
+            deferred_release.emplace_back(dki.keys, dki.keys_cap);
+        }
+        dki.keys = nk;
+        dki.keys_cap = cap;
+    }
+    h2d(dki.rec + gid0, recs.data(), (size_t)nn * sizeof(DkRec));
+    if (!kb.empty()) h2d(dki.keys + dki.keys_len, kb.data(), kb.size());
+    dki.keys_len += kb.size();
+    uint32_t first = gid0, count = nn;
+    if ((uint64_t)dki.nrec * 2 > dki.tab_cap) {  // a new table: every record again (newest id wins)
+        uint32_t cap = 1024;
+        while ((uint64_t)cap < (uint64_t)dki.nrec * 2) cap <<= 1;
+        if (dki.tab) deferred_release.emplace_back(dki.tab, (uint64_t)dki.tab_cap * sizeof(DkSlot));
+        dki.tab = (DkSlot *)heap.alloc((uint64_t)cap * sizeof(DkSlot));
+        dki.tab_cap = cap;
+        hcheck(hipMemsetAsync(dki.tab, 0, (size_t)cap * sizeof(DkSlot), stream));
+        first = 0;
+        count = dki.nrec;
+    }
+    hcheck(launch_dk_insert(stream, first, count, dki.rec, dki.keys, dki.tab, dki.tab_cap - 1, dki.err));
+}
+
+// getitem through the device key index into a device buffer.  Returns -1 (nothing
+// written, nothing reported) when any key is not one the index answers, or the output
+// does not fit: the caller then runs the host path, so results never depend on this.
+int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int mode, uint8_t *out, uint64_t out_cap,
+                    int out_on_device, uint64_t *out_off, uint32_t *out_len, uint32_t *status, uint64_t *needed) {
+    if (!dki_enabled() || !dki.valid || !dki.tab || !n || !spans_enabled()) return -1;
+    const uint64_t k0 = koff[0], kbytes = koff[n] - k0;
+    // device scratch: keys, offsets, gather queries, 4 u32 arrays, offsets out, lengths and
+    // statuses, tasks
+    const uint64_t o_off = round_up(kbytes + 8, 256), o_gq = o_off + round_up((uint64_t)(n + 1) * 8, 256),
+                   o_u32 = o_gq + round_up((uint64_t)n * sizeof(GatherQuery), 256),
+                   o_oo = o_u32 + round_up((uint64_t)n * 16, 256), o_dl = o_oo + round_up((uint64_t)n * 8, 256),
+                   o_end = o_dl + round_up((uint64_t)n * 8, 256) + 256;
+    auto *b = (uint8_t *)dk_qbuf.get(o_end);
+    auto *dkeys = b;
+    auto *doff = (uint64_t *)(b + o_off);
+    auto *gq = (GatherQuery *)(b + o_gq);
+    auto *cap16 = (uint32_t *)(b + o_u32), *tiles = cap16 + n, *icap = tiles + n, *itiles = icap + n;
+    auto *oo = (uint64_t *)(b + o_oo);
+    auto *dl = (uint32_t *)(b + o_dl), *ds = dl + n;
+    auto *miss = (uint32_t *)(b + o_end - 256);
+    // keys up through pinned memory (one copy of the bytes and the rebased offsets)
+    auto *hb = (uint8_t *)dk_hbuf.get(o_gq);
+    std::memcpy(hb, keys + k0, kbytes);
+    auto *ho = (uint64_t *)(hb + o_off);
+    for (uint32_t i = 0; i <= n; ++i) ho[i] = koff[i] - k0;
+    hcheck(hipMemcpyAsync(dkeys, hb, o_off + (uint64_t)(n + 1) * 8, hipMemcpyHostToDevice, stream));
+    hcheck(hipMemsetAsync(miss, 0, 8, stream));
+    flush_tab();
+    hcheck(hipEventRecord(ev0, stream));
+    hcheck(launch_dk_lookup(stream, n, dkeys, doff, dki.tab, dki.tab_cap - 1, dki.rec, dki.keys, (uint32_t)mode, gq,
+                            cap16, tiles, miss));
+    const SortAlloc SA{[](void *self, uint64_t bytes) -> void * { return static_cast<px_ctx *>(self)->heap.alloc(bytes); },
+                       [](void *self, void *p, uint64_t bytes) { static_cast<px_ctx *>(self)->heap.release(p, bytes); },
+                       this};
+    hcheck(scan_u32(stream, SA, cap16, icap, n, ScanOp::kPlus, false));
+    hcheck(scan_u32(stream, SA, tiles, itiles, n, ScanOp::kPlus, false));
+    hcheck(launch_dk_fill(stream, n, cap16, icap, tiles, itiles, gq, oo));
+    // what the host needs before launching: misses, total output, total tiles, insert errors
+    auto *hr = (uint32_t *)dk_hres.get(64);
+    hr[0] = hr[1] = hr[2] = hr[3] = 0xffffffffu;
+    hcheck(hipMemcpyAsync(hr, miss, 4, hipMemcpyDeviceToHost, stream));
+    hcheck(hipMemcpyAsync(hr + 1, icap + n - 1, 4, hipMemcpyDeviceToHost, stream));
+    hcheck(hipMemcpyAsync(hr + 2, itiles + n - 1, 4, hipMemcpyDeviceToHost, stream));
+    hcheck(hipMemcpyAsync(hr + 3, dki.err, 4, hipMemcpyDeviceToHost, stream));
+    hcheck(hipStreamSynchronize(stream));
+    if (hr[3]) {  // an insert gave up: the index is not trusted again until reset
+        fprintf(stderr, "pixiu_amd: device key index insert failed; getitem resolves on the host\n");
+        dki.valid = false;
+        return -1;
+    }
+    const uint64_t total = (uint64_t)hr[1] * 16;
+    if (hr[0] || total > out_cap) return -1;
+    const uint32_t ntask = (hr[2] + 63) / 64;
+    auto *task = heap.alloc((uint64_t)ntask * sizeof(GatherTask) + 64);
+    // (a host output buffer: gathered into device staging, then copied down once)
+    uint8_t *dout = out_on_device ? out : (uint8_t *)dk_obuf.get(total + 64);
+    hcheck(launch_gather(stream, ntask, task, gq, n, dout, dl, ds, true));
+    hcheck(hipEventRecord(ev1, stream));
+    auto *res = (uint8_t *)dk_hres.get((uint64_t)n * 16 + 64);
+    hcheck(hipMemcpyAsync(res, oo, (size_t)n * 8, hipMemcpyDeviceToHost, stream));
+    hcheck(hipMemcpyAsync(res + (uint64_t)n * 8, dl, (size_t)n * 8, hipMemcpyDeviceToHost, stream));
+    hcheck(hipStreamSynchronize(stream));
+    heap.release(task, (uint64_t)ntask * sizeof(GatherTask) + 64);
+    if (!out_on_device && total) d2h(out, dout, total);
+    sync();
+    float ms = 0;
+    hcheck(hipEventElapsedTime(&ms, ev0, ev1));
+    stats.last_decode_kernel_ms = ms;
+    stats.last_gather_queries = n;
+    stats.last_get_device_keys = n;
+    std::memcpy(out_off, res, (size_t)n * 8);
+    const uint32_t *rl = (const uint32_t *)(res + (uint64_t)n * 8), *rs = rl + n;
+    int rc = PX_OK;
+    for (uint32_t i = 0; i < n; ++i) {
+        out_len[i] = rl[i];
+        status[i] = map_status(rs[i]);
+        if (status[i] != PX_OK && rc == PX_OK) rc = (int)status[i];
+    }
+    if (needed) *needed = total;
     return rc;
 }
 
@@ -2945,7 +3198,13 @@ int px_get_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *k
         const auto t0 = std::chrono::steady_clock::now();
         int rc;
         double lookup_ms = 0;
-        if (out_on_device && n >= 4096 && ctx->opts.decode_waves == 0) {
+        ctx->stats.last_get_device_keys = 0;
+        rc = ctx->opts.decode_waves == 0
+                 ? ctx->dki_get(n, keys, koff, mode, out, out_cap, out_on_device, out_off, out_len, status, needed)
+                 : -1;
+        if (rc != -1) {
+            // (resolved on the device: no host lookups)
+        } else if (out_on_device && n >= 4096 && ctx->opts.decode_waves == 0) {
             rc = ctx->get_overlapped(n, keys, koff, mode, out, out_cap, out_off, out_len, status, needed, lookup_ms);
         } else {
             std::vector<DecodeQuery> q(n);
@@ -3206,7 +3465,9 @@ int px_save(px_ctx *ctx, uint8_t *dst, uint64_t cap, int dst_on_device, uint64_t
 
 int px_load(px_ctx *ctx, const uint8_t *src, uint64_t len, int src_on_device, uint32_t *first_shard) {
     if (!ctx || (len && !src)) return PX_EINVAL;
-    PX_GUARD(PX_FLUSHED(ctx); return ctx->load(src, len, src_on_device, first_shard);)
+    // (loaded records move the key map's hints; the device key index does not follow them)
+    PX_GUARD(PX_FLUSHED(ctx); ctx->dki.valid = false; ctx->dki_clear();
+             return ctx->load(src, len, src_on_device, first_shard);)
 }
 
 int px_reset(px_ctx *ctx) {

@@ -22,22 +22,24 @@ struct SortAlloc {
     void *self;
 };
 
-// tiles of the segments [start[i], start[i] + len[i]) (host)
-void seg_tiles(const uint32_t *start, const uint32_t *len, uint32_t nseg, std::vector<SegTile> &out);
+// tiles of segments of these lengths (host)
+uint32_t seg_tile_count(const uint32_t *len, uint32_t nseg);
 
 // Stable LSD radix sort of (key, value) pairs inside every segment by key bits [0, bits),
-// `rb`-bit digits (8 or 9).  Elements never leave their segment, so the scatter of every
-// pass stays inside one segment's range.  Pass 0 reads (k0, v0), or -- with G / dist
-// set -- computes each position's key from the text: `syms` 9-bit symbols (byte + 1, 0
-// past the doc end; value = the position).  The last pass writes (kout, vout).  Scratch
-// pairs: (ka, va) always; (kb, vb) when pass 0 reads the text and there are >= 3 passes
-// (otherwise k0 / v0 are reused).  kout may alias kb.  *err (device word, zeroed by the
-// caller) is set if a tile's look-back outlasted its bound (cannot happen; the sort is
-// then wrong and the caller must fail).
-hipError_t seg_sort_pairs(hipStream_t s, const SortAlloc &A, const std::vector<SegTile> &tiles,
-                          const std::vector<uint32_t> &seg_start, uint32_t bits, int rb, uint64_t *k0, uint32_t *v0,
-                          const uint8_t *G, const uint16_t *dist, uint32_t syms, uint64_t *ka, uint32_t *va,
-                          uint64_t *kb, uint32_t *vb, uint64_t *kout, uint32_t *vout, uint32_t *err);
+// `rb`-bit digits (8 or 9).  The segments [d_start[g], d_start[g] + d_len[g]) are given on
+// the device (ntiles = seg_tile_count of their lengths); the tile table is built there, so
+// the sort reads nothing from host memory and never synchronises the stream.  Elements
+// never leave their segment, so the scatter of every pass stays inside one segment's range.
+// Pass 0 reads (k0, v0), or -- with G / dist set -- computes each position's key from the
+// text: `syms` 9-bit symbols (byte + 1, 0 past the doc end; value = the position).  The
+// last pass writes (kout, vout).  Scratch pairs: (ka, va) always; (kb, vb) when pass 0 reads
+// the text and there are >= 3 passes (otherwise k0 / v0 are reused).  kout may alias kb.
+// *err (device word, zeroed by the caller) is set if a tile's look-back outlasted its bound
+// (cannot happen; the sort is then wrong and the caller must fail).
+hipError_t seg_sort_pairs(hipStream_t s, const SortAlloc &A, uint32_t nseg, uint32_t ntiles, const uint32_t *d_start,
+                          const uint32_t *d_len, uint32_t bits, int rb, uint64_t *k0, uint32_t *v0, const uint8_t *G,
+                          const uint16_t *dist, uint32_t syms, uint64_t *ka, uint32_t *va, uint64_t *kb, uint32_t *vb,
+                          uint64_t *kout, uint32_t *vout, uint32_t *err);
 
 enum class ScanOp { kMax, kMin, kPlus };
 // inclusive scan of n u32 values (reverse: from the end), in-place allowed

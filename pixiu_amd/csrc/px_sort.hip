@@ -41,11 +41,26 @@ constexpr uint32_t kSpinBound = 1u << 20;  // look-back polls before a tile give
 SD uint32_t lane_id() { return threadIdx.x & 63u; }
 SD uint64_t lanes_below() { return (1ull << lane_id()) - 1ull; }
 
-// the first suffix sort's key of text position p (k_psa_key0's layout without the shard)
+// global-address-space views: a flat access waits for every outstanding memory AND LDS
+// operation of the wave, which serialises the loads against the ranking's LDS traffic
+#define PX_GAS __attribute__((address_space(1)))
+typedef const PX_GAS uint64_t gcu64;
+typedef const PX_GAS uint32_t gcu32;
+typedef const PX_GAS uint16_t gcu16;
+typedef PX_GAS uint64_t gu64;
+typedef PX_GAS uint32_t gu32;
+
+// the first suffix sort's key of text position p (k_psa_key0's layout without the shard):
+// 8 text bytes by two aligned 8-byte loads and a funnel shift (G is 8-byte aligned and
+// padded), then `syms` symbols of 9 bits
 SD uint64_t text_key(const uint8_t *G, const uint16_t *dist, uint32_t p, uint32_t syms) {
-    const uint32_t left = dist[p];
+    gcu64 *G8 = (gcu64 *)G;
+    const uint32_t w = p >> 3, sh = (p & 7u) * 8u;
+    uint64_t x = G8[w];
+    if (sh) x = (x >> sh) | (G8[w + 1] << (64u - sh));
+    const uint32_t left = ((gcu16 *)dist)[p];
     uint64_t k = 0;
-    for (uint32_t s = 0; s < syms; ++s) k = k << 9 | (s < left ? (uint64_t)G[p + s] + 1u : 0u);
+    for (uint32_t s = 0; s < syms; ++s) k = k << 9 | (s < left ? ((x >> (8 * s)) & 0xffu) + 1u : 0u);
     return k;
 }
 
@@ -112,7 +127,7 @@ __global__ void __launch_bounds__(kThreads) k_seg_hist(const SegTile *tiles, uin
             const uint32_t j = j0 + threadIdx.x;
             const bool ok = j < T.count;
             uint64_t k = 0;
-            if (ok) k = TEXT ? text_key(G, dist, T.start + j, syms) : kin[T.start + j];
+            if (ok) k = TEXT ? text_key(G, dist, T.start + j, syms) : ((gcu64 *)kin)[T.start + j];
             const uint64_t valid = __ballot(ok);
             for (uint32_t p = 0; p < passes; ++p) {
                 const uint32_t d = (uint32_t)(k >> (RB * p)) & (BINS - 1u);
@@ -122,6 +137,44 @@ __global__ void __launch_bounds__(kThreads) k_seg_hist(const SegTile *tiles, uin
         }
     }
     flush();
+}
+
+// the tile table on the device: tiles before each segment (one workgroup), then one
+// thread per tile finds its segment by a binary search over that prefix
+__global__ void __launch_bounds__(1024) k_seg_tpre(uint32_t nseg, const uint32_t *len, uint32_t *pre) {
+    __shared__ uint32_t red[16];
+    const uint32_t per = (nseg + 1023) / 1024, a = threadIdx.x * per, e = min(nseg, a + per);
+    uint32_t acc = 0;
+    for (uint32_t g = a; g < e; ++g) acc += (len[g] + kSortTile - 1) / kSortTile;
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    uint32_t x = acc;
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) red[w] = x;
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t i = 0; i < w; ++i) before += red[i];
+    uint32_t run = before + x - acc;
+    for (uint32_t g = a; g < e; ++g) {
+        pre[g] = run;
+        run += (len[g] + kSortTile - 1) / kSortTile;
+    }
+    if (threadIdx.x == 1023) pre[nseg] = before + x;
+}
+__global__ void __launch_bounds__(256) k_seg_tfill(uint32_t nt, uint32_t nseg, const uint32_t *start, const uint32_t *len,
+                                                   const uint32_t *pre, SegTile *tiles) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nt) return;
+    uint32_t lo = 0, hi = nseg;  // the last segment g with pre[g] <= t
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pre[mid] <= t) lo = mid;
+        else hi = mid;
+    }
+    const uint32_t o = (t - pre[lo]) * kSortTile;
+    tiles[t] = SegTile{start[lo] + o, min(kSortTile, len[lo] - o), lo, o == 0 ? 1u : 0u};
 }
 
 // where each digit's run of each segment starts: the segment's start + the exclusive
@@ -149,8 +202,8 @@ __global__ void __launch_bounds__(kThreads) k_seg_base(const uint32_t *ghist, co
 
 // ---------------------------------------------------------------- one radix pass
 template <int RB, bool TEXT>
-__global__ void __launch_bounds__(kThreads) k_seg_pass(const SegTile *tiles, uint32_t *tile_ctr, const uint64_t *kin,
-                                                       const uint32_t *vin, uint64_t *kout, uint32_t *vout,
+__global__ void __launch_bounds__(kThreads) k_seg_pass(const SegTile *tiles, uint32_t *tile_ctr, const uint64_t *kin_,
+                                                       const uint32_t *vin_, uint64_t *kout_, uint32_t *vout_,
                                                        uint32_t pass, uint32_t passes, const uint32_t *base,
                                                        uint32_t *status, const uint8_t *G, const uint16_t *dist,
                                                        uint32_t syms, uint32_t *err) {
@@ -160,25 +213,29 @@ __global__ void __launch_bounds__(kThreads) k_seg_pass(const SegTile *tiles, uin
     __shared__ uint32_t s_excl[BINS];      // tile-local start of each digit's run
     __shared__ uint32_t s_dst[BINS];       // global position of that run's first element
     __shared__ uint32_t red[kWaves];
-    __shared__ uint64_t lk[kSortTile];
-    __shared__ uint32_t lv[kSortTile];
+    __shared__ uint64_t stage[kSortTile];  // the tile in digit order: keys, then values
+    __shared__ uint16_t sdig[kSortTile];   // and each staged element's digit
+    gcu64 *kin = (gcu64 *)kin_;
+    gcu32 *vin = (gcu32 *)vin_;
+    gu64 *kout = (gu64 *)kout_;
+    gu32 *vout = (gu32 *)vout_;
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6, shift = RB * pass;
     if (threadIdx.x == 0) s_tile = atomicAdd(tile_ctr, 1u);  // tiles start in order: look-back never waits on a later one
     for (uint32_t i = threadIdx.x; i < kWaves * BINS; i += kThreads) (&wh[0][0])[i] = 0;
     __syncthreads();
     const uint32_t t = s_tile;
     const SegTile T = tiles[t];
-    // ---- rank: wave w takes elements [w * 1024, (w + 1) * 1024) of the tile, 64 at a time
+    // ---- load: wave w takes elements [w * 1024, (w + 1) * 1024) of the tile, 64 at a time
     uint64_t k[kItems];
     uint32_t v[kItems];
     uint16_t r[kItems];
+    const uint32_t j0 = w * (kItems * 64) + lane;
 #pragma unroll
     for (uint32_t it = 0; it < kItems; ++it) {
-        const uint32_t j = w * (kItems * 64) + it * 64 + lane;
-        const bool ok = j < T.count;
+        const uint32_t j = j0 + it * 64;
         k[it] = 0;
         v[it] = 0;
-        if (ok) {
+        if (j < T.count) {
             if (TEXT) {
                 k[it] = text_key(G, dist, T.start + j, syms);
                 v[it] = T.start + j;
@@ -187,6 +244,11 @@ __global__ void __launch_bounds__(kThreads) k_seg_pass(const SegTile *tiles, uin
                 v[it] = vin[T.start + j];
             }
         }
+    }
+    // ---- rank: each wave counts its own digits (no barrier inside)
+#pragma unroll
+    for (uint32_t it = 0; it < kItems; ++it) {
+        const bool ok = j0 + it * 64 < T.count;
         const uint32_t d = (uint32_t)(k[it] >> shift) & (BINS - 1u);
         const uint64_t m = match_digit<RB>(d, __ballot(ok));
         uint32_t prev = 0;
@@ -216,58 +278,79 @@ __global__ void __launch_bounds__(kThreads) k_seg_pass(const SegTile *tiles, uin
         s_excl[threadIdx.x * BPT + i] = run;
         run += cnt[i];
     }
-    // ---- look-back over the earlier tiles of this segment, per digit
+    // ---- look-back over the earlier tiles of this segment, every digit of the thread at once
     const uint32_t *sb = base + ((uint64_t)T.seg * passes + pass) * BINS;
-    uint32_t fail = 0;
+    uint32_t excl[BPT], done = 0, fail = 0;
 #pragma unroll
     for (uint32_t i = 0; i < BPT; ++i) {
-        const uint32_t b = threadIdx.x * BPT + i;
-        uint32_t *mine = status + (uint64_t)t * BINS + b;
-        uint32_t excl = 0;
-        if (T.first) {
-            __hip_atomic_store(mine, kFlagIncl | cnt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(mine, kFlagAgg | cnt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            uint32_t j = t - 1, spins = 0;
-            while (true) {
-                const uint32_t x = __hip_atomic_load(status + (uint64_t)j * BINS + b, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-                if ((x & ~kCountMask) == 0) {
-                    if (++spins > kSpinBound) {
-                        fail = 1;
-                        break;
-                    }
+        excl[i] = 0;
+        uint32_t *mine = status + (uint64_t)t * BINS + threadIdx.x * BPT + i;
+        __hip_atomic_store(mine, (T.first ? kFlagIncl : kFlagAgg) | cnt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (T.first) done |= 1u << i;
+    }
+    if (done != (1u << BPT) - 1u) {
+        uint32_t j[BPT], spins = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < BPT; ++i) j[i] = t - 1;
+        while (done != (1u << BPT) - 1u) {
+            uint32_t x[BPT];
+#pragma unroll
+            for (uint32_t i = 0; i < BPT; ++i)
+                x[i] = (done >> i) & 1u ? 0u
+                                        : __hip_atomic_load(status + (uint64_t)j[i] * BINS + threadIdx.x * BPT + i,
+                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            bool waited = false;
+#pragma unroll
+            for (uint32_t i = 0; i < BPT; ++i) {
+                if ((done >> i) & 1u) continue;
+                if ((x[i] & ~kCountMask) == 0) {
+                    waited = true;
                     continue;
                 }
-                excl += x & kCountMask;
-                if ((x & ~kCountMask) == kFlagIncl) break;
-                --j;
+                excl[i] += x[i] & kCountMask;
+                if ((x[i] & ~kCountMask) == kFlagIncl) done |= 1u << i;
+                else --j[i];
             }
-            __hip_atomic_store(mine, kFlagIncl | (excl + cnt[i]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (waited && ++spins > kSpinBound) {
+                fail = 1;
+                break;
+            }
         }
-        s_dst[b] = sb[b] + excl;
+#pragma unroll
+        for (uint32_t i = 0; i < BPT; ++i)
+            __hip_atomic_store(status + (uint64_t)t * BINS + threadIdx.x * BPT + i, kFlagIncl | (excl[i] + cnt[i]),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+#pragma unroll
+    for (uint32_t i = 0; i < BPT; ++i) s_dst[threadIdx.x * BPT + i] = sb[threadIdx.x * BPT + i] + excl[i];
     if (fail) atomicOr(err, 1u);
     __syncthreads();
-    // ---- stage the tile in digit order
+    // ---- stage the keys in digit order, write each digit's run to its place
+    // (consecutive lanes, consecutive addresses); then the values the same way
+    uint16_t at[kItems];
 #pragma unroll
     for (uint32_t it = 0; it < kItems; ++it) {
-        const uint32_t j = w * (kItems * 64) + it * 64 + lane;
-        if (j < T.count) {
-            const uint32_t d = (uint32_t)(k[it] >> shift) & (BINS - 1u);
-            const uint32_t at = s_excl[d] + wh[w][d] + r[it];
-            lk[at] = k[it];
-            lv[at] = v[it];
+        const uint32_t d = (uint32_t)(k[it] >> shift) & (BINS - 1u);
+        at[it] = (uint16_t)(s_excl[d] + wh[w][d] + r[it]);
+        if (j0 + it * 64 < T.count) {
+            stage[at[it]] = k[it];
+            sdig[at[it]] = (uint16_t)d;
         }
     }
     __syncthreads();
-    // ---- write each digit's run to its place (consecutive lanes, consecutive addresses)
     for (uint32_t i = threadIdx.x; i < T.count; i += kThreads) {
-        const uint64_t kk = lk[i];
-        const uint32_t d = (uint32_t)(kk >> shift) & (BINS - 1u);
-        const uint32_t dst = s_dst[d] + (i - s_excl[d]);
-        kout[dst] = kk;
-        vout[dst] = lv[i];
+        const uint32_t d = sdig[i];
+        kout[s_dst[d] + (i - s_excl[d])] = stage[i];
+    }
+    __syncthreads();
+    uint32_t *sv = reinterpret_cast<uint32_t *>(&stage[0]);
+#pragma unroll
+    for (uint32_t it = 0; it < kItems; ++it)
+        if (j0 + it * 64 < T.count) sv[at[it]] = v[it];
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < T.count; i += kThreads) {
+        const uint32_t d = sdig[i];
+        vout[s_dst[d] + (i - s_excl[d])] = sv[i];
     }
 }
 
@@ -389,47 +472,44 @@ hipError_t scan_run(hipStream_t s, const SortAlloc &A, const uint32_t *in, uint3
 
 }  // namespace
 
-void seg_tiles(const uint32_t *start, const uint32_t *len, uint32_t nseg, std::vector<SegTile> &out) {
-    out.clear();
-    for (uint32_t g = 0; g < nseg; ++g)
-        for (uint32_t o = 0; o < len[g]; o += kSortTile)
-            out.push_back(SegTile{start[g] + o, std::min(kSortTile, len[g] - o), g, o == 0 ? 1u : 0u});
+uint32_t seg_tile_count(const uint32_t *len, uint32_t nseg) {
+    uint64_t t = 0;
+    for (uint32_t g = 0; g < nseg; ++g) t += (len[g] + kSortTile - 1) / kSortTile;
+    return (uint32_t)t;
 }
 
-hipError_t seg_sort_pairs(hipStream_t s, const SortAlloc &A, const std::vector<SegTile> &tiles,
-                          const std::vector<uint32_t> &seg_start, uint32_t bits, int rb, uint64_t *k0, uint32_t *v0,
-                          const uint8_t *G, const uint16_t *dist, uint32_t syms, uint64_t *ka, uint32_t *va,
-                          uint64_t *kb, uint32_t *vb, uint64_t *kout, uint32_t *vout, uint32_t *err) {
-    if (tiles.empty()) return hipSuccess;
+hipError_t seg_sort_pairs(hipStream_t s, const SortAlloc &A, uint32_t nseg, uint32_t nt, const uint32_t *d_start,
+                          const uint32_t *d_len, uint32_t bits, int rb, uint64_t *k0, uint32_t *v0, const uint8_t *G,
+                          const uint16_t *dist, uint32_t syms, uint64_t *ka, uint32_t *va, uint64_t *kb, uint32_t *vb,
+                          uint64_t *kout, uint32_t *vout, uint32_t *err) {
+    if (!nt) return hipSuccess;
     if (rb != 8 && rb != 9) return hipErrorInvalidValue;
     const bool text = G != nullptr;
-    const uint32_t bins = 1u << rb, passes = (bits + rb - 1) / rb, nseg = (uint32_t)seg_start.size();
+    const uint32_t bins = 1u << rb, passes = (bits + rb - 1) / rb;
     if (passes == 0 || passes > kMaxPasses) return hipErrorInvalidValue;
-    const uint32_t nt = (uint32_t)tiles.size();
-    // scratch: tiles, segment starts, digit counts and run starts, tile counters, look-back words
-    const uint64_t b_tiles = (uint64_t)nt * sizeof(SegTile), b_starts = (uint64_t)nseg * 4,
+    // scratch: tiles, tiles before each segment, digit counts and run starts, tile counters,
+    // look-back words
+    const uint64_t b_tiles = (uint64_t)nt * sizeof(SegTile), b_pre = ((uint64_t)nseg + 1) * 4,
                    b_hist = (uint64_t)nseg * passes * bins * 4, b_status = (uint64_t)nt * bins * 4;
-    const uint64_t o_starts = (b_tiles + 255) / 256 * 256, o_hist = o_starts + (b_starts + 255) / 256 * 256,
+    const uint64_t o_pre = (b_tiles + 255) / 256 * 256, o_hist = o_pre + (b_pre + 255) / 256 * 256,
                    o_base = o_hist + (b_hist + 255) / 256 * 256, o_ctr = o_base + (b_hist + 255) / 256 * 256,
                    o_status = o_ctr + 256, total = o_status + b_status + 256;
     auto *mem = (uint8_t *)A.alloc(A.self, total);
     if (!mem) return hipErrorOutOfMemory;
     auto *d_tiles = (SegTile *)mem;
-    auto *d_starts = (uint32_t *)(mem + o_starts);
+    auto *d_pre = (uint32_t *)(mem + o_pre);
     auto *d_hist = (uint32_t *)(mem + o_hist);
     auto *d_base = (uint32_t *)(mem + o_base);
     auto *d_ctr = (uint32_t *)(mem + o_ctr);
     auto *d_status = (uint32_t *)(mem + o_status);
-    hipError_t e = hipMemcpyAsync(d_tiles, tiles.data(), b_tiles, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_starts, seg_start.data(), b_starts, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemsetAsync(d_hist, 0, b_hist, s);
+    hipError_t e = hipMemsetAsync(d_hist, 0, b_hist, s);
     if (e == hipSuccess) e = hipMemsetAsync(d_ctr, 0, 256, s);
     if (e != hipSuccess) {
         A.release(A.self, mem, total);
         return e;
     }
-    // (the host-side tile table must outlive the copy: the caller keeps `tiles` until the
-    // stream passes this point -- it synchronises before releasing it)
+    k_seg_tpre<<<1, 1024, 0, s>>>(nseg, d_len, d_pre);
+    k_seg_tfill<<<(nt + 255) / 256, 256, 0, s>>>(nt, nseg, d_start, d_len, d_pre, d_tiles);
     const uint32_t hb = (nt + kHistTiles - 1) / kHistTiles;
 #define PX_SORT_RB(RB_)                                                                                            \
     do {                                                                                                           \
@@ -437,7 +517,7 @@ hipError_t seg_sort_pairs(hipStream_t s, const SortAlloc &A, const std::vector<S
             k_seg_hist<RB_, true><<<hb, kThreads, 0, s>>>(d_tiles, nt, nullptr, G, dist, syms, passes, d_hist);    \
         else                                                                                                       \
             k_seg_hist<RB_, false><<<hb, kThreads, 0, s>>>(d_tiles, nt, k0, nullptr, nullptr, 0, passes, d_hist);  \
-        k_seg_base<RB_><<<nseg * passes, kThreads, 0, s>>>(d_hist, d_starts, passes, d_base);                     \
+        k_seg_base<RB_><<<nseg * passes, kThreads, 0, s>>>(d_hist, d_start, passes, d_base);                      \
         const uint64_t *ki = k0;                                                                                   \
         const uint32_t *vi = v0;                                                                                   \
         for (uint32_t p = 0; p < passes && e == hipSuccess; ++p) {                                                 \
@@ -471,8 +551,7 @@ hipError_t seg_sort_pairs(hipStream_t s, const SortAlloc &A, const std::vector<S
     else
         PX_SORT_RB(8);
 #undef PX_SORT_RB
-    if (e == hipSuccess) e = hipStreamSynchronize(s);  // (the tile table upload reads host memory)
-    A.release(A.self, mem, total);
+    A.release(A.self, mem, total);  // (stream-ordered reuse: later work on this stream only)
     return e;
 }
 
