@@ -479,8 +479,10 @@ struct CritBit {
         return false;
     }
 
-    // CritBitTree::setitem; q = escaped key incl. 251,0.  Returns 1 on replace (the old
-    // leaf goes to del, the new one takes its place).
+    // CritBitTree::setitem; q = escaped key incl. 251,0.  Returns 0 when inserted, 1 on
+    // replace (the old leaf goes to del, the new one takes its place), 2 when the streams
+    // part right after a 251 and the reference skips the insert (`if (!spec_mode)
+    // insert()`, CritBitTree.cpp:96-100): the record is stored but no walk reaches it.
     template <class KP, class Del>
     int insert(const std::string &q, Leaf nl, KP kp, Del del) {
         CbtRef nref;
@@ -517,7 +519,7 @@ struct CritBit {
             }
             ++diff_at;
         }
-        if (spec) return 0;
+        if (spec) return 2;
         uint8_t mask = crit_rv ^ src_rv;
         mask |= mask >> 1;
         mask |= mask >> 2;

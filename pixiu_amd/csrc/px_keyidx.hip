@@ -20,7 +20,6 @@ namespace px {
 namespace {
 
 #define DK_DEV __device__ __forceinline__
-constexpr uint32_t kDkProbeBound = 1u << 20;  // probes before a lookup / insert gives up (cannot happen)
 
 DK_DEV unsigned long long dk_hash(const uint8_t *k, uint32_t n) {
     unsigned long long h = 0x9E3779B97F4A7C15ull ^ n;
@@ -50,21 +49,13 @@ __global__ void __launch_bounds__(256) k_dk_insert(uint32_t gid0, uint32_t n, co
     const unsigned long long h = dk_hash(k, r.key_len);
     uint32_t i = (uint32_t)h & mask;
     for (uint32_t probes = 0; probes <= mask; ++probes, i = (i + 1) & mask) {
+        // the slot of this hash: claimed by the first inserter, then every record with the
+        // hash takes it, the newest id winning.  (No waiting on another inserter's id: two
+        // lanes of one wave can carry the same key.  Two different keys that share all 64
+        // hash bits would share the slot; a lookup verifies the key bytes, so one of them
+        // then simply misses and its batch resolves on the host.)
         const unsigned long long prev = atomicCAS(&tab[i].h, 0ull, h);
         if (prev != 0ull && prev != h) continue;
-        if (prev == h) {  // the same hash: the same key only if its bytes agree
-            uint32_t g1 = 0;
-            for (uint32_t w = 0; w < kDkProbeBound && (g1 = __hip_atomic_load(&tab[i].gid1, __ATOMIC_RELAXED,
-                                                                               __HIP_MEMORY_SCOPE_AGENT)) == 0;
-                 ++w) {
-            }
-            if (!g1) {
-                atomicOr(err, 1u);
-                return;
-            }
-            const DkRec o = rec[g1 - 1];
-            if (o.key_len != r.key_len || !bytes_eq(keys + o.key_off, k, r.key_len)) continue;
-        }
         atomicMax(&tab[i].gid1, gid + 1);
         return;
     }

@@ -222,9 +222,9 @@ __global__ void __launch_bounds__(256) k_psa_groups0(uint32_t N, const uint32_t 
     if (r < N) {
         const uint32_t p = sa[r], hd = head[r];
         rank[p] = hd;
-        sd[r] = dist[p];
         const bool hn = r + 1 == N || head[r + 1] == r + 1;  // r + 1 starts the next group
         a = (hd != r || !hn) ? 1u : 0u;                       // in a group of >= 2
+        sd[r] = a ? dist[p] : 0u;  // (the doubling reads sd of grouped slots only: no scattered read for the rest)
         act[r] = (uint8_t)a;
         if (!(hd == r && !hn)) gsz[r] = 0;  // (not the start of a group of >= 2)
         if (hn && hd != r) {                // the last element of a group of >= 2

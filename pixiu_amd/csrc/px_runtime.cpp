@@ -206,6 +206,10 @@ struct Chunk {
     std::vector<uint64_t> kp_off;
     std::vector<uint32_t> kp_len;
     std::vector<uint32_t> gid;  // device key index record id of each slot (kNone / past the end: none)
+    // slots whose CritBit insert the reference skips (CritBitTree.cpp:96-100: the streams part
+    // right after a 251): stored and live, but no walk reaches them (past the end: 0)
+    std::vector<uint8_t> notree;
+    bool in_tree(uint32_t i) const { return i >= notree.size() || !notree[i]; }
     // span tables (full-range getitem as a gather); sized lazily
     struct Span {
         const SpanEnt *p = nullptr;  // device; null: decode through the segment walk
@@ -241,6 +245,9 @@ struct Shard : pxh::CritBit {
     // chunk a delete left under 80 % of 65,535 live records; -1 = NULL
     int64_t glob = -1;
     int64_t closed = -1;  // slot-full live chunk whose rotation trigger has run
+    // a leaf went into this shard's CritBit under a key its compat-decoded prefix does not
+    // equal: the trie is then only as consistent as the reference's, so every lookup walks it
+    bool unclean = false;
     uint32_t records = 0;
     std::vector<uint32_t> chunks;  // global chunk ids by chunk_seq
 };
@@ -372,6 +379,16 @@ struct px_ctx {
         for (auto &c : chunks) c.gid.clear();
     }
     void dki_commit(uint32_t gid0, const std::vector<DkRec> &recs, const std::vector<uint8_t> &kb);
+    // the live bit of every record killed since (replaces, deletes, reinsert), on the device
+    void dki_apply_kills() {
+        std::vector<uint32_t> kills;
+        kills.swap(dki.kills);
+        if (kills.empty() || !dki.rec) return;
+        auto *d = (uint32_t *)dk_kbuf.get(kills.size() * 4);
+        h2d(d, kills.data(), kills.size() * 4);
+        hcheck(launch_dk_kill(stream, (uint32_t)kills.size(), d, dki.rec));
+    }
+    DevBuf dk_kbuf;
     int dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int mode, uint8_t *out, uint64_t out_cap,
                 int out_on_device, uint64_t *out_off, uint32_t *out_len, uint32_t *status, uint64_t *needed);
     DevBuf dk_qbuf, dk_obuf;
@@ -696,7 +713,15 @@ struct px_ctx {
     }
     // CritBitTree::setitem; q = escaped key incl. 251,0.  Returns 1 on replace.
     int cbt_insert(Shard &s, const std::string &q, Leaf nl) {
-        return s.insert(q, nl, kp_fn(), [&](const Leaf &l) { chunk_delitem(s, l); });
+        const int rc = s.insert(q, nl, kp_fn(), [&](const Leaf &l) { chunk_delitem(s, l); });
+        if (rc == 2) {  // (the shard's own chunks only: shards insert on separate host threads)
+            Chunk &ch = chunks[nl.chunk];
+            if (ch.notree.size() <= nl.idx) ch.notree.resize(nl.idx + 1, 0);
+            ch.notree[nl.idx] = 1;
+        } else if (!kp_matches(nl, q)) {
+            s.unclean = true;
+        }
+        return rc;
     }
 
     // PiXiuChunk::delitem (PiXiuStr.cpp:178-187): dead mark, live count, Glob
@@ -1060,7 +1085,10 @@ struct px_ctx {
                 pre = PX_ENOTFOUND;
                 return;
             }
-            if (c < chunks.size() && i < chunks[c].n && !chunks[c].dead[i] && kp_matches(Leaf{c, i}, ek)) {
+            // (only while that record is in its shard's trie and the trie holds clean prefixes
+            // only: the reference skips some inserts, CritBitTree.cpp:96-100)
+            if (c < chunks.size() && i < chunks[c].n && !chunks[c].dead[i] && chunks[c].in_tree(i) &&
+                !shards[sh]->unclean && kp_matches(Leaf{c, i}, ek)) {
                 q.chunk = c;
                 q.idx = i;
                 q.out_cap = (uint32_t)round_up(chunks[c].doc_len[i] + 64, 16);
@@ -2137,6 +2165,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     const bool dk = dki_enabled() && dki.valid && !raw_docs;
     const uint32_t dk_gid0 = dki.nrec;
     std::vector<DkRec> dk_new;
+    std::vector<uint32_t> dk_r;  // the batch record of each entry
     std::vector<uint8_t> dk_kb;
     if (dk) {
         std::string q;
@@ -2174,11 +2203,9 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             d.doc_len = ch.doc_len[i];
             esc_key_into(q, k, kl);
             const bool clean = kp_matches(Leaf{rgchunk[r], i}, q);
-            d.flags = kDkLive | (clean ? kDkClean : 0u);
-            // (the single shard's CritBit walk is exact only over clean prefixes: one
-            // unclean record and that store resolves on the host from then on)
-            if (!clean && opts.records_per_shard == 0) dki.valid = false;
+            d.flags = kDkLive | (clean ? kDkClean : 0u);  // (and in its trie: settled after the inserts)
             dk_new.push_back(d);
+            dk_r.push_back(r);
         }
     }
 
@@ -2226,7 +2253,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             } else {
                 esc_key_into(q, hkeys.data() + hkoff[r], hkoff[r + 1] - hkoff[r]);
             }
-            replaced[r] |= (uint32_t)cbt_insert(s, q, Leaf{rgchunk[r], ridx[r]});
+            replaced[r] |= cbt_insert(s, q, Leaf{rgchunk[r], ridx[r]}) == 1 ? 1u : 0u;
         }
     };
     const uint32_t nthr = std::min<uint32_t>(host_threads(), (uint32_t)work.size());
@@ -2243,15 +2270,15 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     }
 
     phase.mark("device key index");
+    // a record the reference's CritBit skipped is answered by no walk: not by the index
+    // either; a shard whose trie took an unclean prefix walks every lookup from now on
+    for (size_t j = 0; j < dk_new.size(); ++j)
+        if (!chunks[rgchunk[dk_r[j]]].in_tree(ridx[dk_r[j]])) dk_new[j].flags &= ~kDkClean;
+    for (const Work &w : work)
+        if (w.s->unclean) dki.valid = false;
     if (dki.valid && dki_enabled()) {
         if (dk) dki_commit(dk_gid0, dk_new, dk_kb);
-        std::vector<uint32_t> kills;
-        kills.swap(dki.kills);
-        if (!kills.empty() && dki.rec) {
-            auto *d = (uint32_t *)dk_qbuf.get(kills.size() * 4);
-            h2d(d, kills.data(), kills.size() * 4);
-            hcheck(launch_dk_kill(stream, (uint32_t)kills.size(), d, dki.rec));
-        }
+        dki_apply_kills();
     } else if (dki.nrec) {
         dki_clear();
     }
@@ -2665,6 +2692,7 @@ void px_ctx::dki_commit(uint32_t gid0, const std::vector<DkRec> &recs, const std
 int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int mode, uint8_t *out, uint64_t out_cap,
                     int out_on_device, uint64_t *out_off, uint32_t *out_len, uint32_t *status, uint64_t *needed) {
     if (!dki_enabled() || !dki.valid || !dki.tab || !n || !spans_enabled()) return -1;
+    dki_apply_kills();  // (deletes since the last set batch)
     const uint64_t k0 = koff[0], kbytes = koff[n] - k0;
     // device scratch: keys, offsets, gather queries, 4 u32 arrays, offsets out, lengths and
     // statuses, tasks
@@ -3030,9 +3058,7 @@ int px_ctx::load(const uint8_t *src, uint64_t len, int src_on_device, uint32_t *
             if (prev >= 0 && (uint32_t)prev != s.id) cbt_delete(*shards[(size_t)prev], q);
             keymap.put(rk, raw.size(), s.id, jobs[j].chunk, k);
         }
-        if (cbt_insert(s, q, Leaf{jobs[j].chunk, k})) {
-            // a duplicate key inside the blob: the later record replaced the earlier
-        }
+        (void)cbt_insert(s, q, Leaf{jobs[j].chunk, k});  // (1: a duplicate key inside the blob replaced the earlier)
     }
     // span tables for the loaded records (compat only: without their docs compat == exact is
     // unknown, so exact getitems of loaded records keep the segment walk)

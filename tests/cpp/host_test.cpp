@@ -107,12 +107,57 @@ static void test_critbit() {
     pxh::CritBit u;
     kp.assign({esc_key("A"), esc_key("A\xfb"), esc_key("B")});
     CHECK(u.insert(kp[0], pxh::Leaf{0, 0}, kpf, [](const pxh::Leaf &) {}) == 0);
-    CHECK(u.insert(kp[1], pxh::Leaf{1, 0}, kpf, [](const pxh::Leaf &) {}) == 0);
+    CHECK(u.insert(kp[1], pxh::Leaf{1, 0}, kpf, [](const pxh::Leaf &) {}) == 2);
     CHECK(u.insert(kp[2], pxh::Leaf{2, 0}, kpf, [](const pxh::Leaf &) {}) == 0);
     pxh::Leaf l{~0u, 0};
     CHECK(u.lookup(kp[0], kpf, &l) && l.chunk == 0);
     CHECK(!u.lookup(kp[1], kpf, nullptr));
     CHECK(u.lookup(kp[2], kpf, &l) && l.chunk == 2);
+
+    // What the runtime's fast paths rely on (px_runtime.cpp resolve_key, the device key
+    // index): with clean prefixes (stored prefix = escaped key), every leaf an insert placed
+    // (0 or 1) and that no later replace or delete removed is reached by its key's walk --
+    // whatever was skipped (2), replaced or deleted since.  Random operations over an
+    // alphabet with 251 and 0 (prefix-related keys and skipped inserts everywhere).
+    const char alpha2[] = {'a', 'b', (char)251, (char)0};
+    for (int trial = 0; trial < 40; ++trial) {
+        pxh::CritBit w;
+        kp.clear();
+        std::map<std::string, uint32_t> placed;  // escaped key -> leaf a walk must reach
+        size_t skipped = 0;
+        for (int op = 0; op < 600; ++op) {
+            std::string raw;
+            for (int j = 0, n = 1 + (int)(rng() % 5); j < n; ++j) raw.push_back(alpha2[rng() % 4]);
+            const std::string q = esc_key(raw);
+            if (rng() % 5 < 4) {
+                const uint32_t id = (uint32_t)kp.size();
+                kp.push_back(q);
+                uint32_t gone = ~0u;
+                const int rc = w.insert(q, pxh::Leaf{id, 0}, kpf, [&](const pxh::Leaf &x) { gone = x.chunk; });
+                CHECK(rc >= 0 && rc <= 2);
+                if (rc == 1) {  // the replaced leaf held the same key
+                    CHECK(placed.count(q) && placed[q] == gone);
+                }
+                if (rc == 2) {
+                    ++skipped;
+                    CHECK(!w.lookup(q, kpf, nullptr) || placed.count(q));
+                } else {
+                    placed[q] = id;
+                }
+            } else {
+                uint32_t gone = ~0u;
+                if (w.remove(q, kpf, [&](const pxh::Leaf &x) { gone = x.chunk; }) == 0) {
+                    CHECK(placed.count(q) && placed[q] == gone);
+                    placed.erase(q);
+                }
+            }
+            for (auto &kv : placed) {
+                pxh::Leaf f{~0u, 0};
+                CHECK(w.lookup(kv.first, kpf, &f) && f.chunk == kv.second);
+            }
+        }
+        if (trial == 0) printf("critbit 251-alphabet: %zu placed keys, %zu skipped inserts\n", placed.size(), skipped);
+    }
 }
 
 static void test_keymaps() {

@@ -74,3 +74,35 @@ def test_sharded_device_buffer_and_replaces(store_factory, oracle):
         want[k] = sh.get(k)
     assert got == [want[k] for k in keys]
     assert st.get_batch(keys) == got
+
+
+@pytest.mark.parametrize("rps", [0, 16])
+def test_skipped_critbit_inserts(store_factory, oracle, rps):
+    """Keys that extend another key by a 251 (the reference's CritBit skips their insert,
+    CritBitTree.cpp:96-100: stored, but no walk reaches them): getitem / contains answer
+    NULL / 0 for them like the reference, on the device path and the host path alike
+    (the key map's hint must not shortcut the walk for them)."""
+    import random
+    rng = random.Random(251)
+    keys, seen = [], set()
+    while len(keys) < 160:
+        k = bytes(rng.choice(b"ab\xfb") for _ in range(rng.randint(1, 5)))
+        if k not in seen:
+            seen.add(k)
+            keys.append(k)
+    vals = [bytes(rng.choice(b"xyz\xfb") for _ in range(rng.randint(0, 40))) for _ in keys]
+    st = store_factory(records_per_shard=rps)
+    st.set_batch(keys, vals)
+    want = []
+    step = rps or len(keys)
+    for s0 in range(0, len(keys), step):
+        sh = oracle.new()
+        for k, v in zip(keys[s0:s0 + step], vals[s0:s0 + step]):
+            sh.set(k, v)
+        want += [sh.get(k) for k in keys[s0:s0 + step]]
+    assert any(w is None for w in want)  # (the quirk is exercised)
+    got = st.get_batch(keys)
+    assert got == want
+    assert st.contains(keys).tolist() == [w is not None for w in want]
+    found = [k for k, w in zip(keys, want) if w is not None]
+    assert st.get_batch(found) == [w for w in want if w is not None]
