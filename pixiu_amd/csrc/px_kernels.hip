@@ -2266,20 +2266,42 @@ PX_DEV u32x4 mask_piece(u32x4 v, int lo, int hi) {
 }
 
 // the task table: per 64-tile task, its first query, the span holding the task's first tile
-// in that query's table, and the tiles (bits) where later queries start.  The caller zeroes it.
-__global__ void __launch_bounds__(256) k_gather_tasks(uint32_t nq, const GatherQuery *qs, GatherTask *task) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nq) return;
-    const GatherQuery q = qs[i];
-    const uint32_t nt = max(1u, (min(q.len, q.cap) + kGatherTile - 1) / kGatherTile);
-    const uint32_t ntix = (q.len + kGatherTile - 1) / kGatherTile;  // (the tile index's length)
-    for (uint32_t t = (q.tile0 + 63) & ~63u; t < q.tile0 + nt; t += 64) {
-        GatherTask &d = task[t >> 6];
-        d.q0 = i;
-        d.k0 = t - q.tile0 < ntix ? q.tix[t - q.tile0] : 0u;
+// in that query's table, and the tiles (bits) where later queries start.  One wave per query:
+// a query owns the tasks whose first tile is one of its tiles (every task has exactly one
+// owner, so nothing is zeroed and nothing is atomic); only its last owned task can hold the
+// starts of later queries (tile0 rises strictly), found by one load per lane.  `ctl`
+// (device-driven launches, px_keyidx.hip): skip everything unless no key missed and the
+// output fits -- the task table is sized for that bound.
+__global__ void __launch_bounds__(256) k_gather_tasks(uint32_t nq, const GatherQuery *qs, GatherTask *task,
+                                                      const uint32_t *ctl, uint64_t out_cap) {
+    const uint32_t q = uni(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)), lane = lane_id();
+    if (q >= nq) return;
+    if (ctl && (uni(ctl[0]) != 0u || (uint64_t)uni(ctl[1]) * 16u > out_cap)) return;
+    const GatherQuery &Q = qs[q];
+    const uint32_t len = uni(Q.len), tile0 = uni(Q.tile0);
+    const uint32_t nt = max(1u, (min(len, uni(Q.cap)) + kGatherTile - 1) / kGatherTile);
+    const uint32_t ntix = (len + kGatherTile - 1) / kGatherTile;  // (the tile index's length)
+    const uint32_t T0 = (tile0 + 63u) >> 6, T1 = (tile0 + nt - 1u) >> 6;
+    if (T0 > T1) return;  // (the query lies inside a task owned by an earlier one)
+    unsigned long long M = 0;
+    {
+        const uint32_t j = q + 1u + lane;
+        if (j < nq) {
+            const uint32_t t0 = qs[j].tile0;
+            if (t0 < 64u * (T1 + 1u)) M = 1ull << (t0 - 64u * T1);
+        }
+#pragma unroll
+        for (int o = 32; o; o >>= 1) M |= __shfl_xor(M, o);
     }
-    const uint32_t b = q.tile0 & 63u;
-    if (b) atomicOr(&task[q.tile0 >> 6].M, 1ull << b);
+    const uint32_t *tix = Q.tix;
+    for (uint32_t T = T0 + lane; T <= T1; T += 64) {
+        const uint32_t g = 64u * T - tile0;
+        GatherTask d;
+        d.q0 = q;
+        d.k0 = g < ntix ? tix[g] : 0u;
+        d.M = T == T1 ? M : 0ull;
+        task[T] = d;
+    }
 }
 
 // Gather (see the comment above shl_bytes): one wave per task of 64 tiles.  The TA (the
@@ -2290,19 +2312,9 @@ __global__ void __launch_bounds__(256) k_gather_tasks(uint32_t nq, const GatherQ
 // task's first tile on are staged in LDS by two coalesced loads per lane and each lane finds
 // its own span there, and a source load is issued only by the lanes whose span has a piece.
 constexpr uint32_t kGatherStage = 256;
-__global__ void __launch_bounds__(256) k_gather(uint32_t ntask, const GatherTask *task, const GatherQuery *qs, uint32_t nq,
-                                                uint8_t *out_, uint32_t *out_len, uint32_t *status, uint32_t remap) {
-    __shared__ uint2 stage_all[4][kGatherStage];
-    __shared__ u32x4 tile_all[4][64 * 3];  // per lane: its 32-byte tile and a 16-byte pad
+PX_DEV void gather_task(uint32_t ti, const GatherTask *task, const GatherQuery *qs, uint32_t nq, uint8_t *out_,
+                        uint32_t *out_len, uint32_t *status, uint2 *stage, uint8_t *tl) {
     const uint32_t lane = lane_id();
-    uint32_t lb = blockIdx.x;
-    if (remap) {  // XCD-aware order, as k_decode
-        const uint32_t nb = gridDim.x, x = blockIdx.x & 7u, per = nb >> 3, rem = nb & 7u;
-        lb = x * per + min(x, rem) + (blockIdx.x >> 3);
-    }
-    const uint32_t ti = uni(lb * (blockDim.x >> 6) + (threadIdx.x >> 6));
-    if (ti >= ntask) return;
-    uint2 *stage = stage_all[threadIdx.x >> 6];
     const uint32_t g0 = ti * 64, q0 = uni(task[ti].q0), k0 = uni(task[ti].k0);
     const uint64_t M = ((uint64_t)uni((uint32_t)(task[ti].M >> 32)) << 32) | uni((uint32_t)task[ti].M);
     const uint32_t qi = q0 + (uint32_t)__popcll(M & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull)));
@@ -2368,7 +2380,6 @@ __global__ void __launch_bounds__(256) k_gather(uint32_t ntask, const GatherTask
     // the tile is assembled in LDS: each span piece is written whole (16 unaligned bytes from
     // its first source byte, at its output offset), in output order, so the bytes a write puts
     // past its piece are overwritten by the pieces after it (the last one's land in the pad)
-    uint8_t *tl = (uint8_t *)&tile_all[threadIdx.x >> 6][lane * 3];
     for (;;) {
         uint32_t en[16];
         if (fast && k - k0 + 8 <= nst) {  // (staged)
@@ -2429,6 +2440,29 @@ __global__ void __launch_bounds__(256) k_gather(uint32_t ntask, const GatherTask
     PX_GAS uint8_t *o = (PX_GAS uint8_t *)out_ + q.out_off + a;
     *(PX_GAS u32x4 *)o = r0;
     if (B < e) *(PX_GAS u32x4 *)(o + 16) = r1;
+}
+
+// One wave per task.  The tasks are cut into eight contiguous ranges, one per XCD
+// (blockIdx.x & 7: neighbouring tasks read neighbouring span tables and chunks through the
+// same L2); the waves of an XCD's range go out in task order.  `ctl` (device-driven
+// launches): the grid is sized for an upper bound on the tasks, the real count comes from
+// the device (waves past it exit at once), with the same skip as k_gather_tasks.
+__global__ void __launch_bounds__(256) k_gather(uint32_t ntask_h, const uint32_t *ctl, uint64_t out_cap,
+                                                const GatherTask *task, const GatherQuery *qs, uint32_t nq,
+                                                uint8_t *out_, uint32_t *out_len, uint32_t *status) {
+    __shared__ uint2 stage_all[4][kGatherStage];
+    __shared__ u32x4 tile_all[4][64 * 3];  // per lane: its 32-byte tile and a 16-byte pad
+    uint32_t ntask = ntask_h;
+    if (ctl) {
+        if (uni(ctl[0]) != 0u || (uint64_t)uni(ctl[1]) * 16u > out_cap) return;
+        ntask = (uni(ctl[2]) + 63u) / 64u;
+    }
+    const uint32_t w = threadIdx.x >> 6, per = (ntask + 7u) / 8u;
+    const uint32_t j = (blockIdx.x >> 3) * (blockDim.x >> 6) + w;  // (the wave's place in its XCD's range)
+    if (j >= per) return;
+    const uint32_t ti = uni((blockIdx.x & 7u) * per + j);
+    if (ti >= ntask) return;
+    gather_task(ti, task, qs, nq, out_, out_len, status, stage_all[w], (uint8_t *)&tile_all[w][lane_id() * 3]);
 }
 
 // ====================================================================== migrate
@@ -2569,14 +2603,17 @@ hipError_t launch_span_build(hipStream_t s, uint32_t n, const SpanJob *jobs) {
     return hipGetLastError();
 }
 
-hipError_t launch_gather(hipStream_t s, uint32_t ntask, void *task_buf, const GatherQuery *qs, uint32_t nq,
-                         uint8_t *out, uint32_t *out_len, uint32_t *status, bool remap) {
-    if (!ntask) return hipSuccess;
+// ntask: the tasks (ctl null), or (ctl: device-driven) an upper bound on them; task_buf holds
+// gather_task_bytes(ntask)
+uint64_t gather_task_bytes(uint32_t ntask) { return (uint64_t)ntask * sizeof(GatherTask) + 64; }
+hipError_t launch_gather(hipStream_t s, uint32_t ntask, const uint32_t *ctl, uint64_t out_cap, void *task_buf,
+                         const GatherQuery *qs, uint32_t nq, uint8_t *out, uint32_t *out_len, uint32_t *status) {
+    if (!ntask || !nq) return hipSuccess;
     GatherTask *task = (GatherTask *)task_buf;
-    hipError_t e = hipMemsetAsync(task, 0, (size_t)ntask * sizeof(GatherTask), s);
-    if (e != hipSuccess) return e;
-    k_gather_tasks<<<(nq + 255) / 256, 256, 0, s>>>(nq, qs, task);
-    k_gather<<<(ntask + 3) / 4, 256, 0, s>>>(ntask, task, qs, nq, out, out_len, status, remap ? 1u : 0u);
+    k_gather_tasks<<<(nq + 3) / 4, 256, 0, s>>>(nq, qs, task, ctl, out_cap);
+    // eight XCD ranges of ceil(ntask / 8) waves, 4 waves a workgroup
+    const uint32_t grid = 8u * (((ntask + 7u) / 8u + 3u) / 4u);
+    k_gather<<<grid, 256, 0, s>>>(ntask, ctl, out_cap, task, qs, nq, out, out_len, status);
     return hipGetLastError();
 }
 

@@ -10,8 +10,13 @@
 //
 //   k_dk_insert   a set batch's new records (newest record id wins on a repeated key)
 //   k_dk_kill     records the batch killed (replaces, deletes): live bit cleared
-//   k_dk_lookup   one thread per query key: probe, verify, pick the span table, out_cap
-//   k_dk_fill     output offsets and tile numbers from the two scans, the host's arrays
+//   k_dk_lookup   one thread per query key: probe, verify, pick the span table; the batch's
+//                 output offsets and first tiles in the same pass (a chained scan over the
+//                 workgroups, decoupled look-back)
+// The batch then goes straight to the gather (k_gather_tasks, k_gather) with no host round
+// trip: ctl[0] = keys missed, ctl[1] = output bytes / 16, ctl[2] = tiles, ctl[3] = the
+// index's insert-error word, ctl[4] = workgroup ticket; both gather kernels skip the batch
+// unless nothing missed and the output fits.
 #include <hip/hip_runtime.h>
 
 #include "px_common.h"
@@ -21,11 +26,26 @@ namespace {
 
 #define DK_DEV __device__ __forceinline__
 
-DK_DEV unsigned long long dk_hash(const uint8_t *k, uint32_t n) {
+// keys are read 16 bytes at a time (unaligned loads; both key buffers keep >= 16 bytes of
+// slack past their last key), the bytes past a key's end masked off
+#define DK_GAS __attribute__((address_space(1)))
+typedef uint32_t dk_u4 __attribute__((ext_vector_type(4), aligned(1)));
+DK_DEV uint32_t dk_word(const dk_u4 &v, int j, uint32_t left) {  // word j of v, bytes past `left` zeroed
+    const uint32_t x = j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
+    const uint32_t lo = 4u * (uint32_t)j;
+    return left >= lo + 4u ? x : left <= lo ? 0u : x & ((1u << (8u * (left - lo))) - 1u);
+}
+
+DK_DEV unsigned long long dk_hash(const uint8_t *k_, uint32_t n) {
+    const DK_GAS uint8_t *k = (const DK_GAS uint8_t *)k_;
     unsigned long long h = 0x9E3779B97F4A7C15ull ^ n;
-    for (uint32_t i = 0; i < n; ++i) {
-        h ^= k[i];
-        h *= 0x100000001B3ull;
+    for (uint32_t i = 0; i < n; i += 16) {
+        const dk_u4 v = *(const DK_GAS dk_u4 *)(k + i);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            h ^= dk_word(v, j, n - i);
+            h *= 0x100000001B3ull;
+        }
     }
     h ^= h >> 29;
     h *= 0xBF58476D1CE4E5B9ull;
@@ -33,9 +53,15 @@ DK_DEV unsigned long long dk_hash(const uint8_t *k, uint32_t n) {
     return h | 1ull;
 }
 
-DK_DEV bool bytes_eq(const uint8_t *a, const uint8_t *b, uint32_t n) {
-    for (uint32_t i = 0; i < n; ++i)
-        if (a[i] != b[i]) return false;
+DK_DEV bool bytes_eq(const uint8_t *a_, const uint8_t *b_, uint32_t n) {
+    const DK_GAS uint8_t *a = (const DK_GAS uint8_t *)a_, *b = (const DK_GAS uint8_t *)b_;
+    for (uint32_t i = 0; i < n; i += 16) {
+        const dk_u4 x = *(const DK_GAS dk_u4 *)(a + i), y = *(const DK_GAS dk_u4 *)(b + i);
+        uint32_t d = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d |= dk_word(x, j, n - i) ^ dk_word(y, j, n - i);
+        if (d) return false;
+    }
     return true;
 }
 
@@ -67,15 +93,28 @@ __global__ void __launch_bounds__(256) k_dk_kill(uint32_t n, const uint32_t *gid
     if (j < n) rec[gids[j]].flags &= ~kDkLive;
 }
 
-// per query key: its record's gather query (out_off / tile0 filled by k_dk_fill), its output
-// room in 16-byte units and its tiles; a key the index cannot answer counts in *miss
+// per query key (q = ticket * 256 + thread: workgroups are numbered in the order they start,
+// so every predecessor a look-back waits on is running or done): its record's gather query,
+// its output room in 16-byte units and its tiles; their exclusive prefix over the batch gives
+// the query's output offset and first tile.  chain: two 64-bit words per workgroup (room,
+// tiles), flag in the top two bits (1: this workgroup's own sum, 2: inclusive prefix), zeroed
+// by the caller with ctl.
+constexpr unsigned long long kChAgg = 1ull << 62, kChIncl = 2ull << 62, kChVal = (1ull << 62) - 1;
+constexpr uint32_t kChSpin = 1u << 24;
 __global__ void __launch_bounds__(256) k_dk_lookup(uint32_t nq, const uint8_t *qkeys, const uint64_t *qoff,
                                                    const DkSlot *tab, uint32_t mask, const DkRec *rec,
-                                                   const uint8_t *keys, uint32_t mode, GatherQuery *gq, uint32_t *cap16,
-                                                   uint32_t *tiles, uint32_t *miss) {
-    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+                                                   const uint8_t *keys, uint32_t mode, GatherQuery *gq,
+                                                   uint64_t *out_off, uint32_t *ctl, unsigned long long *chain,
+                                                   const uint32_t *ins_err) {
+    __shared__ uint32_t s_bid, s_wa[4], s_wt[4];
+    __shared__ unsigned long long s_pa, s_pt;
+    if (threadIdx.x == 0) s_bid = atomicAdd(&ctl[4], 1u);
+    __syncthreads();
+    const uint32_t bid = s_bid, q = bid * 256u + threadIdx.x, lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     bool ok = false;
-    if (q < nq) {
+    uint32_t c16 = 0, nt = 0;
+    GatherQuery G{};
+    if (q < nq && !*ins_err) {  // (an insert that gave up: every key goes to the host)
         const uint8_t *k = qkeys + qoff[q];
         const uint32_t n = (uint32_t)(qoff[q + 1] - qoff[q]);
         const unsigned long long h = dk_hash(k, n);
@@ -92,7 +131,6 @@ __global__ void __launch_bounds__(256) k_dk_lookup(uint32_t nq, const uint8_t *q
                 break;
             }
         }
-        uint32_t c16 = 0, nt = 0;
         if (g != kNone) {
             const DkRec r = rec[g];
             const SpanEnt *sp = mode == 0 ? r.sp : r.xsp;
@@ -102,27 +140,92 @@ __global__ void __launch_bounds__(256) k_dk_lookup(uint32_t nq, const uint8_t *q
                 const uint32_t cap = (r.doc_len + 64u + 15u) & ~15u;  // the host's out_cap
                 c16 = cap / 16;
                 nt = max(1u, (min(len, cap) + kGatherTile - 1) / kGatherTile);
-                gq[q] = GatherQuery{sp, r.comp, 0, ns, len, cap, q, t, 0, 0};
+                G = GatherQuery{sp, r.comp, 0, ns, len, cap, q, t, 0, 0};
                 ok = true;
             }
         }
-        cap16[q] = c16;
-        tiles[q] = nt;
     }
     const unsigned long long m = __ballot(q < nq && !ok);
-    if (m && (threadIdx.x & 63u) == 0) atomicAdd(miss, (uint32_t)__popcll(m));
-}
-
-// inclusive scans of cap16 / tiles -> every query's output offset and first tile
-__global__ void __launch_bounds__(256) k_dk_fill(uint32_t nq, const uint32_t *cap16, const uint32_t *incl_cap16,
-                                                 const uint32_t *tiles, const uint32_t *incl_tiles, GatherQuery *gq,
-                                                 uint64_t *out_off) {
-    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= nq) return;
-    const uint64_t off = (uint64_t)(incl_cap16[q] - cap16[q]) * 16u;
-    gq[q].out_off = off;
-    gq[q].tile0 = incl_tiles[q] - tiles[q];
-    out_off[q] = off;
+    if (m && lane == 0) atomicAdd(&ctl[0], (uint32_t)__popcll(m));
+    if (bid == 0 && threadIdx.x == 0) ctl[3] = *ins_err;
+    // the workgroup's inclusive scan of (room, tiles)
+    uint32_t ia = c16, it = nt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t xa = __shfl_up(ia, o), xt = __shfl_up(it, o);
+        if (lane >= (uint32_t)o) {
+            ia += xa;
+            it += xt;
+        }
+    }
+    if (lane == 63) {
+        s_wa[w] = ia;
+        s_wt[w] = it;
+    }
+    __syncthreads();
+    uint32_t pa = 0, pt = 0;
+    for (uint32_t v = 0; v < w; ++v) {
+        pa += s_wa[v];
+        pt += s_wt[v];
+    }
+    if (threadIdx.x == 0) {  // ---- look-back over the earlier workgroups
+        const unsigned long long ta = s_wa[0] + s_wa[1] + s_wa[2] + s_wa[3], tt = s_wt[0] + s_wt[1] + s_wt[2] + s_wt[3];
+        unsigned long long ea = 0, et = 0;
+        if (bid == 0) {
+            __hip_atomic_store(chain, kChIncl | ta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(chain + 1, kChIncl | tt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(chain + 2ull * bid, kChAgg | ta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(chain + 2ull * bid + 1, kChAgg | tt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            bool da = false, dt = false;
+            uint32_t ja = bid - 1, jt = bid - 1, spins = 0;
+            while (!(da && dt)) {
+                const unsigned long long xa =
+                    da ? 0ull : __hip_atomic_load(chain + 2ull * ja, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long xt =
+                    dt ? 0ull : __hip_atomic_load(chain + 2ull * jt + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                bool waited = false;
+                if (!da) {
+                    if (!(xa >> 62)) {
+                        waited = true;
+                    } else {
+                        ea += xa & kChVal;
+                        if ((xa >> 62) == 2) da = true;
+                        else --ja;
+                    }
+                }
+                if (!dt) {
+                    if (!(xt >> 62)) {
+                        waited = true;
+                    } else {
+                        et += xt & kChVal;
+                        if ((xt >> 62) == 2) dt = true;
+                        else --jt;
+                    }
+                }
+                if (waited && ++spins > kChSpin) {  // (cannot happen; the batch then goes to the host)
+                    atomicAdd(&ctl[0], 1u << 30);
+                    break;
+                }
+            }
+            __hip_atomic_store(chain + 2ull * bid, kChIncl | (ea + ta), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(chain + 2ull * bid + 1, kChIncl | (et + tt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_pa = ea;
+        s_pt = et;
+        if (bid == gridDim.x - 1) {
+            ctl[1] = (uint32_t)(ea + ta);
+            ctl[2] = (uint32_t)(et + tt);
+        }
+    }
+    __syncthreads();
+    if (ok) {
+        const uint64_t off = (s_pa + pa + ia - c16) * 16ull;
+        G.out_off = off;
+        G.tile0 = (uint32_t)(s_pt + pt + it - nt);
+        gq[q] = G;
+        out_off[q] = off;
+    }
 }
 
 }  // namespace
@@ -138,17 +241,13 @@ hipError_t launch_dk_kill(hipStream_t s, uint32_t n, const uint32_t *gids, DkRec
     k_dk_kill<<<(n + 255) / 256, 256, 0, s>>>(n, gids, rec);
     return hipGetLastError();
 }
+// ctl: 32 bytes, chain: 16 bytes per 256 keys, both zeroed by the caller
 hipError_t launch_dk_lookup(hipStream_t s, uint32_t nq, const uint8_t *qkeys, const uint64_t *qoff, const DkSlot *tab,
                             uint32_t mask, const DkRec *rec, const uint8_t *keys, uint32_t mode, GatherQuery *gq,
-                            uint32_t *cap16, uint32_t *tiles, uint32_t *miss) {
+                            uint64_t *out_off, uint32_t *ctl, unsigned long long *chain, const uint32_t *ins_err) {
     if (!nq) return hipSuccess;
-    k_dk_lookup<<<(nq + 255) / 256, 256, 0, s>>>(nq, qkeys, qoff, tab, mask, rec, keys, mode, gq, cap16, tiles, miss);
-    return hipGetLastError();
-}
-hipError_t launch_dk_fill(hipStream_t s, uint32_t nq, const uint32_t *cap16, const uint32_t *incl_cap16,
-                          const uint32_t *tiles, const uint32_t *incl_tiles, GatherQuery *gq, uint64_t *out_off) {
-    if (!nq) return hipSuccess;
-    k_dk_fill<<<(nq + 255) / 256, 256, 0, s>>>(nq, cap16, incl_cap16, tiles, incl_tiles, gq, out_off);
+    k_dk_lookup<<<(nq + 255) / 256, 256, 0, s>>>(nq, qkeys, qoff, tab, mask, rec, keys, mode, gq, out_off, ctl, chain,
+                                                 ins_err);
     return hipGetLastError();
 }
 

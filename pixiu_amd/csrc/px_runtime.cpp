@@ -53,15 +53,15 @@ hipError_t launch_rehash(hipStream_t, const uint4 *, uint32_t, uint32_t, uint4 *
 hipError_t launch_decode_addr(hipStream_t, const DecodeQuery *, uint32_t, const RecSlot *const *, int32_t *,
                               uint32_t *, uint32_t *, Frame *, uint32_t, uint32_t);
 hipError_t launch_span_build(hipStream_t, uint32_t, const SpanJob *);
-hipError_t launch_gather(hipStream_t, uint32_t, void *, const GatherQuery *, uint32_t, uint8_t *, uint32_t *,
-                         uint32_t *, bool);
+uint64_t gather_task_bytes(uint32_t);
+hipError_t launch_gather(hipStream_t, uint32_t, const uint32_t *, uint64_t, void *, const GatherQuery *, uint32_t,
+                         uint8_t *, uint32_t *, uint32_t *);
 hipError_t launch_dk_insert(hipStream_t, uint32_t, uint32_t, const DkRec *, const uint8_t *, DkSlot *, uint32_t,
                             uint32_t *);
 hipError_t launch_dk_kill(hipStream_t, uint32_t, const uint32_t *, DkRec *);
 hipError_t launch_dk_lookup(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, const DkSlot *, uint32_t,
-                            const DkRec *, const uint8_t *, uint32_t, GatherQuery *, uint32_t *, uint32_t *, uint32_t *);
-hipError_t launch_dk_fill(hipStream_t, uint32_t, const uint32_t *, const uint32_t *, const uint32_t *, const uint32_t *,
-                          GatherQuery *, uint64_t *);
+                            const DkRec *, const uint8_t *, uint32_t, GatherQuery *, uint64_t *, uint32_t *,
+                            unsigned long long *, const uint32_t *);
 int debug_trace_take(int32_t *, uint32_t);
 int debug_prof_take(unsigned long long *, uint32_t);
 }  // namespace px
@@ -877,11 +877,11 @@ struct px_ctx {
         const uint64_t qb = round_up(g.size() * sizeof(GatherQuery), 64);
         auto *hg = (GatherQuery *)hg_buf[which].get(g.size() * sizeof(GatherQuery));
         std::memcpy(hg, g.data(), g.size() * sizeof(GatherQuery));
-        dbuf = (GatherQuery *)heap.alloc(qb + (uint64_t)ntask * sizeof(GatherTask));
+        dbuf = (GatherQuery *)heap.alloc(qb + gather_task_bytes(ntask));
         void *task = (uint8_t *)dbuf + qb;  // per task: GatherTask
         hcheck(hipMemcpyAsync(dbuf, hg, g.size() * sizeof(GatherQuery), hipMemcpyHostToDevice, st));
-        hcheck(launch_gather(st, ntask, task, dbuf, (uint32_t)g.size(), out, dl, ds, true));
-        gather_bytes[dbuf] = qb + (uint64_t)ntask * sizeof(GatherTask);
+        hcheck(launch_gather(st, ntask, nullptr, 0, task, dbuf, (uint32_t)g.size(), out, dl, ds));
+        gather_bytes[dbuf] = qb + gather_task_bytes(ntask);
     }
     std::map<void *, uint64_t> gather_bytes;  // launch_gathers' device buffers -> their sizes
     void release_gathers(GatherQuery *d) {
@@ -2659,8 +2659,9 @@ void px_ctx::dki_commit(uint32_t gid0, const std::vector<DkRec> &recs, const std
         dki.rec = nr;
         dki.rec_cap = cap;
     }
-    if (dki.keys_len + kb.size() > dki.keys_cap) {
-        const uint64_t cap = std::max<uint64_t>(dki.keys_len + kb.size(), std::max<uint64_t>(1 << 16, dki.keys_cap * 2));
+    if (dki.keys_len + kb.size() + 16 > dki.keys_cap) {  // (16 bytes of slack: the index reads 16 at a time)
+        const uint64_t cap =
+            std::max<uint64_t>(dki.keys_len + kb.size() + 16, std::max<uint64_t>(1 << 16, dki.keys_cap * 2));
         auto *nk = (uint8_t *)heap.alloc(cap);
         if (dki.keys) {
             hcheck(hipMemcpyAsync(nk, dki.keys, dki.keys_len, hipMemcpyDeviceToDevice, stream));
@@ -2694,65 +2695,59 @@ int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int m
     if (!dki_enabled() || !dki.valid || !dki.tab || !n || !spans_enabled()) return -1;
     dki_apply_kills();  // (deletes since the last set batch)
     const uint64_t k0 = koff[0], kbytes = koff[n] - k0;
-    // device scratch: keys, offsets, gather queries, 4 u32 arrays, offsets out, lengths and
-    // statuses, tasks
-    const uint64_t o_off = round_up(kbytes + 8, 256), o_gq = o_off + round_up((uint64_t)(n + 1) * 8, 256),
-                   o_u32 = o_gq + round_up((uint64_t)n * sizeof(GatherQuery), 256),
-                   o_oo = o_u32 + round_up((uint64_t)n * 16, 256), o_dl = o_oo + round_up((uint64_t)n * 8, 256),
-                   o_end = o_dl + round_up((uint64_t)n * 8, 256) + 256;
-    auto *b = (uint8_t *)dk_qbuf.get(o_end);
+    // device scratch: keys, offsets, gather queries, the look-back chain, then what comes back
+    // in one copy (ctl: misses, output / 16, tiles, insert error, ticket; offsets out; lengths;
+    // statuses), then the gather's task table
+    const uint64_t nb = (n + 255) / 256;
+    const uint64_t o_off = round_up(kbytes + 16, 256), o_gq = o_off + round_up((uint64_t)(n + 1) * 8, 256),
+                   o_chain = o_gq + round_up((uint64_t)n * sizeof(GatherQuery), 256), o_ctl = o_chain + nb * 16,
+                   o_oo = o_ctl + 32, o_dl = o_oo + (uint64_t)n * 8, o_end = o_dl + (uint64_t)n * 8,
+                   o_task = round_up(o_end, 256);
+    // the tasks: at most one per 64 tiles, a tile per 16 bytes of the output that fits
+    // (every query's tiles <= its cap / 16), so the launch can go before the totals are known
+    // (a host buffer: device staging up to 4 GiB; a batch past it goes the host path)
+    const uint64_t cap_fit = out_on_device ? out_cap : std::min<uint64_t>(out_cap, 4ull << 30);
+    const uint64_t ntask_max = std::min<uint64_t>(cap_fit / 1024 + 2, 0xffffffffull);
+    auto *b = (uint8_t *)dk_qbuf.get(o_task + gather_task_bytes((uint32_t)ntask_max));
     auto *dkeys = b;
     auto *doff = (uint64_t *)(b + o_off);
     auto *gq = (GatherQuery *)(b + o_gq);
-    auto *cap16 = (uint32_t *)(b + o_u32), *tiles = cap16 + n, *icap = tiles + n, *itiles = icap + n;
+    auto *chain = (unsigned long long *)(b + o_chain);
+    auto *ctl = (uint32_t *)(b + o_ctl);
     auto *oo = (uint64_t *)(b + o_oo);
     auto *dl = (uint32_t *)(b + o_dl), *ds = dl + n;
-    auto *miss = (uint32_t *)(b + o_end - 256);
+    void *task = b + o_task;
     // keys up through pinned memory (one copy of the bytes and the rebased offsets)
     auto *hb = (uint8_t *)dk_hbuf.get(o_gq);
     std::memcpy(hb, keys + k0, kbytes);
     auto *ho = (uint64_t *)(hb + o_off);
     for (uint32_t i = 0; i <= n; ++i) ho[i] = koff[i] - k0;
     hcheck(hipMemcpyAsync(dkeys, hb, o_off + (uint64_t)(n + 1) * 8, hipMemcpyHostToDevice, stream));
-    hcheck(hipMemsetAsync(miss, 0, 8, stream));
+    hcheck(hipMemsetAsync(chain, 0, nb * 16 + 32, stream));
     flush_tab();
     hcheck(hipEventRecord(ev0, stream));
     hcheck(launch_dk_lookup(stream, n, dkeys, doff, dki.tab, dki.tab_cap - 1, dki.rec, dki.keys, (uint32_t)mode, gq,
-                            cap16, tiles, miss));
-    const SortAlloc SA{[](void *self, uint64_t bytes) -> void * { return static_cast<px_ctx *>(self)->heap.alloc(bytes); },
-                       [](void *self, void *p, uint64_t bytes) { static_cast<px_ctx *>(self)->heap.release(p, bytes); },
-                       this};
-    hcheck(scan_u32(stream, SA, cap16, icap, n, ScanOp::kPlus, false));
-    hcheck(scan_u32(stream, SA, tiles, itiles, n, ScanOp::kPlus, false));
-    hcheck(launch_dk_fill(stream, n, cap16, icap, tiles, itiles, gq, oo));
-    // what the host needs before launching: misses, total output, total tiles, insert errors
-    auto *hr = (uint32_t *)dk_hres.get(64);
-    hr[0] = hr[1] = hr[2] = hr[3] = 0xffffffffu;
-    hcheck(hipMemcpyAsync(hr, miss, 4, hipMemcpyDeviceToHost, stream));
-    hcheck(hipMemcpyAsync(hr + 1, icap + n - 1, 4, hipMemcpyDeviceToHost, stream));
-    hcheck(hipMemcpyAsync(hr + 2, itiles + n - 1, 4, hipMemcpyDeviceToHost, stream));
-    hcheck(hipMemcpyAsync(hr + 3, dki.err, 4, hipMemcpyDeviceToHost, stream));
+                            oo, ctl, chain, dki.err));
+    // (a host output buffer: gathered into device staging of cap_fit bytes, then copied down)
+    uint8_t *dout = out_on_device ? out : (uint8_t *)dk_obuf.get(cap_fit + 64);
+    hcheck(launch_gather(stream, (uint32_t)ntask_max, ctl, cap_fit, task, gq, n, dout, dl, ds));
+    hcheck(hipEventRecord(ev1, stream));
+    // one copy, one round trip: ctl, offsets, lengths and statuses
+    auto *hr = (uint32_t *)dk_hres.get(o_end - o_ctl);
+    hcheck(hipMemcpyAsync(hr, ctl, o_end - o_ctl, hipMemcpyDeviceToHost, stream));
     hcheck(hipStreamSynchronize(stream));
+    const uint8_t *res = (const uint8_t *)hr + 32;
     if (hr[3]) {  // an insert gave up: the index is not trusted again until reset
         fprintf(stderr, "pixiu_amd: device key index insert failed; getitem resolves on the host\n");
         dki.valid = false;
         return -1;
     }
     const uint64_t total = (uint64_t)hr[1] * 16;
-    if (hr[0] || total > out_cap) return -1;
-    const uint32_t ntask = (hr[2] + 63) / 64;
-    auto *task = heap.alloc((uint64_t)ntask * sizeof(GatherTask) + 64);
-    // (a host output buffer: gathered into device staging, then copied down once)
-    uint8_t *dout = out_on_device ? out : (uint8_t *)dk_obuf.get(total + 64);
-    hcheck(launch_gather(stream, ntask, task, gq, n, dout, dl, ds, true));
-    hcheck(hipEventRecord(ev1, stream));
-    auto *res = (uint8_t *)dk_hres.get((uint64_t)n * 16 + 64);
-    hcheck(hipMemcpyAsync(res, oo, (size_t)n * 8, hipMemcpyDeviceToHost, stream));
-    hcheck(hipMemcpyAsync(res + (uint64_t)n * 8, dl, (size_t)n * 8, hipMemcpyDeviceToHost, stream));
-    hcheck(hipStreamSynchronize(stream));
-    heap.release(task, (uint64_t)ntask * sizeof(GatherTask) + 64);
-    if (!out_on_device && total) d2h(out, dout, total);
-    sync();
+    if (hr[0] || total > cap_fit) return -1;  // (nothing was gathered: the host path answers)
+    if (!out_on_device && total) {
+        d2h(out, dout, total);
+        sync();  // (d2h may finish through pinned staging at the sync)
+    }
     float ms = 0;
     hcheck(hipEventElapsedTime(&ms, ev0, ev1));
     stats.last_decode_kernel_ms = ms;
