@@ -222,6 +222,11 @@ struct SpanJob {
     uint32_t *count;      // count pass: spans | kSpanBad, eq flag in bit 30
     uint32_t *tix;        // write pass: tile index (kGatherTile bytes per tile), or null
 };
+// span build source of one record: its escaped doc on the device (compat == exact test) or null
+struct SpanSrc {
+    const uint8_t *doc;
+    uint32_t doc_len, pad;
+};
 // the gather's tile: one lane assembles kGatherTile output bytes; tix[t] = the span
 // holding output byte t * kGatherTile
 constexpr uint32_t kGatherTile = 32;

@@ -2179,50 +2179,97 @@ __global__ void __launch_bounds__(64 * kDecWaves) k_decode_addr(const DecodeQuer
 // address is not the previous one + 1.  Count pass: spans (| kSpanBad for a source out
 // of the relative range, | kSpanEq when the expansion equals the doc, i.e. compat ==
 // exact).  Write pass: {rel, start} entries plus the {0, len} sentinel.
-__global__ void __launch_bounds__(256) k_span_build(uint32_t n, const SpanJob *jobs) {
+PX_DEV void span_job(const SpanJob &jb) {
+    const uint32_t lane = lane_id();
+    const PX_GAS int32_t *a = (const PX_GAS int32_t *)jb.addr;
+    const PX_GAS uint8_t *base = (const PX_GAS uint8_t *)jb.base;
+    const PX_GAS uint8_t *doc = (const PX_GAS uint8_t *)jb.doc;
+    PX_GAS SpanEnt *out = (PX_GAS SpanEnt *)jb.out;
+    const uint32_t len = uni(jb.len);
+    uint32_t cnt = 0;
+    bool bad = false, eq = doc && len == uni(jb.doc_len);
+    int32_t prev_last = kAddrNone;  // address of byte k0 - 1 (lane 63 of the last step)
+    for (uint32_t k0 = 0; k0 < len; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        const bool in = k < len;
+        const int32_t v = in ? a[k] : 0;
+        int32_t pv = __shfl_up(v, 1);
+        if (lane == 0) pv = prev_last;
+        const bool start = in && (k == 0 || pv == kAddrNone || v != pv + 1);
+        bad = bad || (bool)ballot(in && v == kAddrNone);
+        if (eq) eq = !ballot(in && (v == kAddrNone || base[v] != doc[k]));
+        const uint64_t m = ballot(start);
+        if (out && !bad) {
+            const uint32_t rank =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+            if (start) {
+                PX_GAS uint32_t *e = (PX_GAS uint32_t *)(out + cnt + rank);
+                e[0] = (uint32_t)v;
+                e[1] = k;
+            }
+            // tile index: the span holding byte k, at every tile start
+            if (jb.tix && in && (k % kGatherTile) == 0)
+                ((PX_GAS uint32_t *)jb.tix)[k / kGatherTile] = cnt + rank + (start ? 1u : 0u) - 1u;
+        }
+        cnt += (uint32_t)__popcll(m);
+        prev_last = __shfl(v, 63);
+    }
+    if (out && !bad && lane == 0) {
+        PX_GAS uint32_t *e = (PX_GAS uint32_t *)(out + cnt);
+        e[0] = 0;
+        e[1] = len;
+    }
+    if (!out && lane == 0) jb.count[0] = cnt | (bad ? kSpanBad : 0u) | (eq ? kSpanEq : 0u);
+}
+
+// The span build's jobs straight from the address decode's own queries and results (no job
+// table from the host): job j is query j (chunk-ordered), its addresses at out_off, its
+// compressed bytes from the chunk's slot table, its doc from src[j].  Count pass (tab null):
+// cnt[j] = spans | kSpanBad | kSpanEq (kSpanBad also for a failed decode), ents[j] = its
+// entries with the sentinel, tiles[j] = its tile-index words (both 0 without a table).
+// Write pass: the table and tile index at the inclusive scans' offsets.
+__global__ void __launch_bounds__(256) k_span_jobs(uint32_t n, const DecodeQuery *dq, const uint32_t *dl,
+                                                   const uint32_t *ds, const SpanSrc *src,
+                                                   const RecSlot *const *chunk_slots, const int32_t *addr,
+                                                   uint32_t *cnt, uint32_t *ents, uint32_t *tiles,
+                                                   const uint32_t *eoff_incl, const uint32_t *toff_incl, SpanEnt *tab,
+                                                   uint32_t *tixb) {
     const uint32_t lane = lane_id();
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);
     for (uint32_t j = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); j < n; j += waves) {
-        const SpanJob jb = jobs[j];
-        const PX_GAS int32_t *a = (const PX_GAS int32_t *)jb.addr;
-        const PX_GAS uint8_t *base = (const PX_GAS uint8_t *)jb.base;
-        const PX_GAS uint8_t *doc = (const PX_GAS uint8_t *)jb.doc;
-        PX_GAS SpanEnt *out = (PX_GAS SpanEnt *)jb.out;
-        const uint32_t len = uni(jb.len);
-        uint32_t cnt = 0;
-        bool bad = false, eq = doc && len == uni(jb.doc_len);
-        int32_t prev_last = kAddrNone;  // address of byte k0 - 1 (lane 63 of the last step)
-        for (uint32_t k0 = 0; k0 < len; k0 += 64) {
-            const uint32_t k = k0 + lane;
-            const bool in = k < len;
-            const int32_t v = in ? a[k] : 0;
-            int32_t pv = __shfl_up(v, 1);
-            if (lane == 0) pv = prev_last;
-            const bool start = in && (k == 0 || pv == kAddrNone || v != pv + 1);
-            bad = bad || (bool)ballot(in && v == kAddrNone);
-            if (eq) eq = !ballot(in && (v == kAddrNone || base[v] != doc[k]));
-            const uint64_t m = ballot(start);
-            if (out && !bad) {
-                const uint32_t rank =
-                    __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-                if (start) {
-                    PX_GAS uint32_t *e = (PX_GAS uint32_t *)(out + cnt + rank);
-                    e[0] = (uint32_t)v;
-                    e[1] = k;
+        const DecodeQuery &q = dq[j];
+        const uint32_t st = uni(ds[j]), len = uni(dl[j]);
+        SpanJob jb;
+        jb.addr = addr + q.out_off;
+        jb.base = chunk_slots[uni(q.chunk)][uni(q.idx)].comp;
+        jb.doc = src[j].doc;
+        jb.len = len;
+        jb.doc_len = uni(src[j].doc_len);
+        jb.count = cnt + j;
+        jb.out = nullptr;
+        jb.tix = nullptr;
+        if (!tab) {
+            if (st != kOk) {
+                if (lane == 0) {
+                    cnt[j] = kSpanBad;
+                    ents[j] = 0;
+                    tiles[j] = 0;
                 }
-                // tile index: the span holding byte k, at every tile start
-                if (jb.tix && in && (k % kGatherTile) == 0)
-                    ((PX_GAS uint32_t *)jb.tix)[k / kGatherTile] = cnt + rank + (start ? 1u : 0u) - 1u;
+                continue;
             }
-            cnt += (uint32_t)__popcll(m);
-            prev_last = __shfl(v, 63);
+            span_job(jb);
+            if (lane == 0) {
+                const uint32_t c = cnt[j];
+                const bool ok = !(c & kSpanBad);
+                ents[j] = ok ? (c & ~(kSpanBad | kSpanEq)) + 1u : 0u;
+                tiles[j] = ok ? (len + kGatherTile - 1) / kGatherTile : 0u;
+            }
+        } else {
+            if (uni(cnt[j]) & kSpanBad) continue;
+            jb.out = tab + (eoff_incl[j] - ents[j]);
+            jb.tix = tixb + (toff_incl[j] - tiles[j]);
+            span_job(jb);
         }
-        if (out && !bad && lane == 0) {
-            PX_GAS uint32_t *e = (PX_GAS uint32_t *)(out + cnt);
-            e[0] = 0;
-            e[1] = len;
-        }
-        if (!out && lane == 0) jb.count[0] = cnt | (bad ? kSpanBad : 0u) | (eq ? kSpanEq : 0u);
     }
 }
 
@@ -2597,9 +2644,13 @@ hipError_t launch_decode_addr(hipStream_t s, const DecodeQuery *qs, uint32_t nq,
     return hipGetLastError();
 }
 
-hipError_t launch_span_build(hipStream_t s, uint32_t n, const SpanJob *jobs) {
+hipError_t launch_span_jobs(hipStream_t s, uint32_t n, const DecodeQuery *dq, const uint32_t *dl, const uint32_t *ds,
+                            const SpanSrc *src, const RecSlot *const *chunk_slots, const int32_t *addr, uint32_t *cnt,
+                            uint32_t *ents, uint32_t *tiles, const uint32_t *eoff_incl, const uint32_t *toff_incl,
+                            SpanEnt *tab, uint32_t *tixb) {
     if (!n) return hipSuccess;
-    k_span_build<<<std::min<uint32_t>((n + 3) / 4, 16384), 256, 0, s>>>(n, jobs);
+    k_span_jobs<<<std::min<uint32_t>((n + 3) / 4, 16384), 256, 0, s>>>(n, dq, dl, ds, src, chunk_slots, addr, cnt, ents,
+                                                                       tiles, eoff_incl, toff_incl, tab, tixb);
     return hipGetLastError();
 }
 

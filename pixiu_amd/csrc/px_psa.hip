@@ -1012,60 +1012,69 @@ __global__ void __launch_bounds__(256) k_psa_lce(uint32_t N, const uint64_t *G8,
     uint32_t kp = 0, kn = 0, qprev = kNoPos - 1, sprev = kNoPos - 1;
     for (uint32_t b = p0; b < p1; b += 8) {
         const uint32_t nb = min(8u, p1 - b);
-        uint16_t dv[8], op[8], on[8];
-        uint32_t qv[8], sv[8];
+        // (register arrays: every index below is a compile-time constant)
+        uint32_t dv[8], qv[8], sv[8], op[4] = {0, 0, 0, 0}, on[4] = {0, 0, 0, 0};
         if (nb == 8) {  // b is a multiple of 8: aligned vector loads
-            *(uint4 *)dv = *(const uint4 *)(dist + b);
-            *(uint4 *)qv = *(const uint4 *)(psvp + b);
-            *(uint4 *)(qv + 4) = *(const uint4 *)(psvp + b + 4);
-            *(uint4 *)sv = *(const uint4 *)(nsvp + b);
-            *(uint4 *)(sv + 4) = *(const uint4 *)(nsvp + b + 4);
+            const uint4 d4 = *(const uint4 *)(dist + b);
+            const uint4 qa = *(const uint4 *)(psvp + b), qb = *(const uint4 *)(psvp + b + 4);
+            const uint4 sa = *(const uint4 *)(nsvp + b), sb = *(const uint4 *)(nsvp + b + 4);
+            const uint32_t dw[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+            for (uint32_t i = 0; i < 8; ++i) dv[i] = (dw[i >> 1] >> (16u * (i & 1u))) & 0xffffu;
+            qv[0] = qa.x, qv[1] = qa.y, qv[2] = qa.z, qv[3] = qa.w, qv[4] = qb.x, qv[5] = qb.y, qv[6] = qb.z, qv[7] = qb.w;
+            sv[0] = sa.x, sv[1] = sa.y, sv[2] = sa.z, sv[3] = sa.w, sv[4] = sb.x, sv[5] = sb.y, sv[6] = sb.z, sv[7] = sb.w;
         } else {
-            for (uint32_t i = 0; i < nb; ++i) {
-                dv[i] = dist[b + i];
-                qv[i] = psvp[b + i];
-                sv[i] = nsvp[b + i];
+#pragma unroll
+            for (uint32_t i = 0; i < 8; ++i) {
+                const bool in = i < nb;
+                dv[i] = in ? dist[b + i] : 0u;
+                qv[i] = in ? psvp[b + i] : kNoPos;
+                sv[i] = in ? nsvp[b + i] : kNoPos;
             }
         }
 #pragma unroll
         for (uint32_t i = 0; i < 8; ++i) {
-            if (i >= nb) break;
-            const uint32_t p = b + i, dp = dv[i], q = qv[i], sn = sv[i];
-            // the shifted pair: lcp(p-1, q') = L >= 2 gives lcp(p, q'+1) = L - 1 exactly
-            // (same mismatch, or the same doc end, one byte on; both stay in their docs),
-            // so a neighbour that continues the previous one needs no text at all
-            const bool shp = q != kNoPos && q == qprev + 1 && kp >= 2;
-            const bool shn = sn != kNoPos && sn == sprev + 1 && kn >= 2;
-            kp = kp ? kp - 1 : 0;
-            kn = kn ? kn - 1 : 0;
-            if (p == p0) {  // (k_psa_lce_seed)
-                kp = seed_p;
-                kn = seed_n;
-            } else if (q == kNoPos) {
-                kp = 0;
-            } else if (!shp) {
-                const uint32_t lim = min(dp, (uint32_t)dist[q]);
-                kp = lce(G8, p, q, min(kp, lim), lim);
+            if (i < nb) {
+                const uint32_t p = b + i, dp = dv[i], q = qv[i], sn = sv[i];
+                // the shifted pair: lcp(p-1, q') = L >= 2 gives lcp(p, q'+1) = L - 1 exactly
+                // (same mismatch, or the same doc end, one byte on; both stay in their docs),
+                // so a neighbour that continues the previous one needs no text at all
+                const bool shp = q != kNoPos && q == qprev + 1 && kp >= 2;
+                const bool shn = sn != kNoPos && sn == sprev + 1 && kn >= 2;
+                kp = kp ? kp - 1 : 0;
+                kn = kn ? kn - 1 : 0;
+                if (p == p0) {  // (k_psa_lce_seed)
+                    kp = seed_p;
+                    kn = seed_n;
+                } else if (q == kNoPos) {
+                    kp = 0;
+                } else if (!shp) {
+                    const uint32_t lim = min(dp, (uint32_t)dist[q]);
+                    kp = lce(G8, p, q, min(kp, lim), lim);
+                }
+                if (p == p0) {
+                } else if (sn == kNoPos) {
+                    kn = 0;
+                } else if (!shn) {
+                    const uint32_t lim = min(dp, (uint32_t)dist[sn]);
+                    kn = lce(G8, p, sn, min(kn, lim), lim);
+                }
+                qprev = q;
+                sprev = sn;
+                op[i >> 1] |= (kp & 0xffffu) << (16u * (i & 1u));
+                on[i >> 1] |= (kn & 0xffffu) << (16u * (i & 1u));
             }
-            if (p == p0) {
-            } else if (sn == kNoPos) {
-                kn = 0;
-            } else if (!shn) {
-                const uint32_t lim = min(dp, (uint32_t)dist[sn]);
-                kn = lce(G8, p, sn, min(kn, lim), lim);
-            }
-            qprev = q;
-            sprev = sn;
-            op[i] = (uint16_t)kp;
-            on[i] = (uint16_t)kn;
         }
         if (nb == 8) {
-            *(uint4 *)(lcp_p + b) = *(const uint4 *)op;
-            *(uint4 *)(lcp_n + b) = *(const uint4 *)on;
+            *(uint4 *)(lcp_p + b) = make_uint4(op[0], op[1], op[2], op[3]);
+            *(uint4 *)(lcp_n + b) = make_uint4(on[0], on[1], on[2], on[3]);
         } else {
-            for (uint32_t i = 0; i < nb; ++i) {
-                lcp_p[b + i] = op[i];
-                lcp_n[b + i] = on[i];
+#pragma unroll
+            for (uint32_t i = 0; i < 8; ++i) {
+                if (i < nb) {
+                    lcp_p[b + i] = (uint16_t)(op[i >> 1] >> (16u * (i & 1u)));
+                    lcp_n[b + i] = (uint16_t)(on[i >> 1] >> (16u * (i & 1u)));
+                }
             }
         }
     }

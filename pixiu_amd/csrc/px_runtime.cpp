@@ -52,7 +52,9 @@ hipError_t launch_decode(hipStream_t, const DecodeQuery *, uint32_t, const RecSl
 hipError_t launch_rehash(hipStream_t, const uint4 *, uint32_t, uint32_t, uint4 *, uint32_t);
 hipError_t launch_decode_addr(hipStream_t, const DecodeQuery *, uint32_t, const RecSlot *const *, int32_t *,
                               uint32_t *, uint32_t *, Frame *, uint32_t, uint32_t);
-hipError_t launch_span_build(hipStream_t, uint32_t, const SpanJob *);
+hipError_t launch_span_jobs(hipStream_t, uint32_t, const DecodeQuery *, const uint32_t *, const uint32_t *,
+                            const SpanSrc *, const RecSlot *const *, const int32_t *, uint32_t *, uint32_t *,
+                            uint32_t *, const uint32_t *, const uint32_t *, SpanEnt *, uint32_t *);
 uint64_t gather_task_bytes(uint32_t);
 hipError_t launch_gather(hipStream_t, uint32_t, const uint32_t *, uint64_t, void *, const GatherQuery *, uint32_t,
                          uint8_t *, uint32_t *, uint32_t *);
@@ -970,96 +972,116 @@ struct px_ctx {
         }
     }
 
-    // Span tables for new records (k_decode_addr -> k_span_build count -> allocate ->
-    // k_span_build write).  docs: each record's escaped doc on the device (for the
-    // compat == exact flag), or null.  A record whose compat expansion overran its
-    // doc + 64 bytes, or reaches a source beyond +-2 GiB, keeps using the walk.
+    // Span tables for new records: k_decode_addr -> k_span_jobs count -> two scans -> (one
+    // round trip: counts and lengths down, the table allocated) -> k_span_jobs write.  The
+    // jobs are built on the device from the decode's own queries, in chunk order.  docs: each
+    // record's escaped doc on the device (for the compat == exact flag), or null.  A record
+    // whose compat expansion overran its doc + 64 bytes, or reaches a source beyond +-2 GiB,
+    // keeps using the walk.
     struct SpanReq {
         uint32_t chunk, idx;
         const uint8_t *doc;
     };
-    void build_spans(const std::vector<SpanReq> &reqs, uint32_t mode = 0, bool exact_too = true) {
-        if (reqs.empty() || !spans_enabled()) return;
-        std::vector<DecodeQuery> q;
-        q.reserve(reqs.size());
+    void build_spans(const std::vector<SpanReq> &reqs_in, uint32_t mode = 0, bool exact_too = true) {
+        if (reqs_in.empty() || !spans_enabled()) return;
+        std::vector<SpanReq> sorted_reqs;
+        const std::vector<SpanReq> *rp = &reqs_in;
+        for (size_t k = 1; k < reqs_in.size(); ++k)
+            if (reqs_in[k].chunk < reqs_in[k - 1].chunk) {  // (k_decode's XCD grouping wants chunk order)
+                sorted_reqs = reqs_in;
+                std::stable_sort(sorted_reqs.begin(), sorted_reqs.end(),
+                                 [](const SpanReq &x, const SpanReq &y) { return x.chunk < y.chunk; });
+                rp = &sorted_reqs;
+                break;
+            }
+        const std::vector<SpanReq> &reqs = *rp;
+        const uint32_t n = (uint32_t)reqs.size();
+        // queries (pinned) and sources
+        auto *qn = (DecodeQuery *)hq_buf.get((uint64_t)n * sizeof(DecodeQuery));
+        std::vector<SpanSrc> src(n);
         uint64_t tot = 0;
-        for (const SpanReq &r : reqs) {
-            const uint32_t cap = (uint32_t)round_up(chunks[r.chunk].doc_len[r.idx] + 64, 16);
-            q.push_back(DecodeQuery{r.chunk, r.idx, 0, kMaxDoc, tot, cap, mode});
+        for (uint32_t k = 0; k < n; ++k) {
+            const SpanReq &r = reqs[k];
+            const Chunk &ch = chunks[r.chunk];
+            const uint32_t cap = (uint32_t)round_up(ch.doc_len[r.idx] + 64, 16);
+            qn[k] = DecodeQuery{r.chunk, r.idx, 0, kMaxDoc, tot, cap, mode, ch.n, 0};
+            src[k] = SpanSrc{r.doc, ch.doc_len[r.idx], 0};
             tot += cap;
         }
         auto *addr = (int32_t *)heap.alloc(tot * 4 + 64);
-        std::vector<uint32_t> len, st;
-        run_decode(q, nullptr, len, st, false, addr);
-        std::vector<SpanJob> jobs;
-        std::vector<uint32_t> ji;
-        for (size_t k = 0; k < reqs.size(); ++k) {
-            if (st[k] != kOk) continue;
-            const Chunk &ch = chunks[reqs[k].chunk];
-            jobs.push_back(SpanJob{addr + q[k].out_off, ch.slots[reqs[k].idx].comp, reqs[k].doc, nullptr, len[k],
-                                   ch.doc_len[reqs[k].idx], nullptr, nullptr});
-            ji.push_back((uint32_t)k);
-        }
-        if (!jobs.empty()) {
-            const size_t nj = jobs.size();
-            auto *dcnt = (uint32_t *)heap.alloc(nj * 4 + 64);
-            for (size_t j = 0; j < nj; ++j) jobs[j].count = dcnt + j;
-            auto *djobs = (SpanJob *)heap.alloc(nj * sizeof(SpanJob));
-            h2d(djobs, jobs.data(), nj * sizeof(SpanJob));
-            hcheck(launch_span_build(stream, (uint32_t)nj, djobs));
-            std::vector<uint32_t> cnt(nj);
-            d2h(cnt.data(), dcnt, nj * 4);
-            sync();
-            uint64_t ents = 0, tiles = 0;
-            for (size_t j = 0; j < nj; ++j)
-                if (!(cnt[j] & kSpanBad)) {
-                    ents += (cnt[j] & ~(kSpanBad | kSpanEq)) + 1;
-                    tiles += (len[ji[j]] + kGatherTile - 1) / kGatherTile;
-                }
-            if (ents) {
-                // entries, then every record's tile index (4 B per kGatherTile output bytes)
-                const uint64_t tab_bytes = round_up(ents * sizeof(SpanEnt), 64) + tiles * 4 + 64;
-                auto *tab = (SpanEnt *)heap.alloc(tab_bytes);
-                store_blocks.emplace_back(tab, tab_bytes);
-                auto *tixb = (uint32_t *)((uint8_t *)tab + round_up(ents * sizeof(SpanEnt), 64));
-                uint64_t o = 0, to = 0;
-                for (size_t j = 0; j < nj; ++j) {
-                    const uint32_t k = ji[j];
-                    Chunk &ch = chunks[reqs[k].chunk];
-                    if (ch.span.size() < ch.n) ch.span.resize(ch.n);
-                    if (cnt[j] & kSpanBad) {
-                        jobs[j].out = nullptr;
-                        jobs[j].tix = nullptr;
-                        jobs[j].len = 0;
-                        continue;
-                    }
-                    const uint32_t ns = cnt[j] & ~(kSpanBad | kSpanEq);
-                    jobs[j].out = tab + o;
-                    jobs[j].tix = tixb + to;
-                    Chunk::Span &sp = ch.span[reqs[k].idx];
-                    if (mode == 0) {
-                        sp.p = tab + o;
-                        sp.t = tixb + to;
-                        sp.n = ns;
-                        sp.len = len[k];
-                        sp.eq = (cnt[j] & kSpanEq) != 0;
-                    } else {
-                        sp.xp = tab + o;
-                        sp.xt = tixb + to;
-                        sp.xn = ns;
-                        sp.xlen = len[k];
-                    }
-                    o += ns + 1;
-                    to += (len[k] + kGatherTile - 1) / kGatherTile;
-                    stats.span_entries += ns + 1;
-                }
-                h2d(djobs, jobs.data(), nj * sizeof(SpanJob));
-                hcheck(launch_span_build(stream, (uint32_t)nj, djobs));
+        // device: queries, lengths + statuses, sources, counts / entries / tiles and their scans
+        const uint64_t o_dl = round_up((uint64_t)n * sizeof(DecodeQuery), 256), o_src = o_dl + round_up((uint64_t)n * 8, 256),
+                       o_u32 = o_src + round_up((uint64_t)n * sizeof(SpanSrc), 256), o_end = o_u32 + (uint64_t)n * 20 + 256;
+        auto *wb = (uint8_t *)heap.alloc(o_end);
+        auto *dq = (DecodeQuery *)wb;
+        auto *dl = (uint32_t *)(wb + o_dl), *ds = dl + n;
+        auto *dsrc = (SpanSrc *)(wb + o_src);
+        auto *cnt = (uint32_t *)(wb + o_u32), *ents = cnt + n, *tiles = ents + n, *eoff = tiles + n, *toff = eoff + n;
+        hcheck(hipMemcpyAsync(dq, qn, (size_t)n * sizeof(DecodeQuery), hipMemcpyHostToDevice, stream));
+        h2d(dsrc, src.data(), (size_t)n * sizeof(SpanSrc));
+        flush_tab();
+        const uint32_t depth = opts.decode_depth ? opts.decode_depth : 4096;
+        const uint32_t waves = std::min<uint32_t>(opts.decode_waves ? opts.decode_waves : 16384, n);
+        auto *frames = (Frame *)scratch_frames.get((uint64_t)waves * depth * sizeof(Frame));
+        static const bool xcd = [] {
+            const char *e = std::getenv("PX_DEC_XCD");
+            return !(e && e[0] == '0');
+        }();
+        const auto *ctab = (const RecSlot *const *)chunk_tab;
+        hcheck(launch_decode_addr(stream, dq, n, ctab, addr, dl, ds, frames, depth, waves | (xcd ? 0x80000000u : 0u)));
+        hcheck(launch_span_jobs(stream, n, dq, dl, ds, dsrc, ctab, addr, cnt, ents, tiles, nullptr, nullptr, nullptr,
+                                nullptr));
+        const SortAlloc SA{[](void *self, uint64_t bytes) -> void * { return static_cast<px_ctx *>(self)->heap.alloc(bytes); },
+                           [](void *self, void *p, uint64_t bytes) { static_cast<px_ctx *>(self)->heap.release(p, bytes); },
+                           this};
+        hcheck(scan_u32(stream, SA, ents, eoff, n, ScanOp::kPlus, false));
+        hcheck(scan_u32(stream, SA, tiles, toff, n, ScanOp::kPlus, false));
+        // counts and lengths down (one round trip)
+        auto *hr = (uint32_t *)hres_buf.get((uint64_t)n * 8 + 16);
+        hcheck(hipMemcpyAsync(hr, cnt, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
+        hcheck(hipMemcpyAsync(hr + n, dl, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
+        hcheck(hipStreamSynchronize(stream));
+        const uint32_t *hc = hr, *hl = hr + n;
+        uint64_t nents = 0, ntiles = 0;
+        for (uint32_t j = 0; j < n; ++j)
+            if (!(hc[j] & kSpanBad)) {
+                nents += (hc[j] & ~(kSpanBad | kSpanEq)) + 1;
+                ntiles += (hl[j] + kGatherTile - 1) / kGatherTile;
             }
-            sync();
-            heap.release(djobs, nj * sizeof(SpanJob));
-            heap.release(dcnt, nj * 4 + 64);
+        if (nents) {
+            // entries, then every record's tile index (4 B per kGatherTile output bytes); the
+            // host's running offsets are the device scans' (same counts, same order)
+            const uint64_t tab_bytes = round_up(nents * sizeof(SpanEnt), 64) + ntiles * 4 + 64;
+            auto *tab = (SpanEnt *)heap.alloc(tab_bytes);
+            store_blocks.emplace_back(tab, tab_bytes);
+            auto *tixb = (uint32_t *)((uint8_t *)tab + round_up(nents * sizeof(SpanEnt), 64));
+            hcheck(launch_span_jobs(stream, n, dq, dl, ds, dsrc, ctab, addr, cnt, ents, tiles, eoff, toff, tab, tixb));
+            uint64_t o = 0, to = 0;
+            for (uint32_t j = 0; j < n; ++j) {
+                if (hc[j] & kSpanBad) continue;
+                Chunk &ch = chunks[reqs[j].chunk];
+                if (ch.span.size() < ch.n) ch.span.resize(ch.n);
+                const uint32_t ns = hc[j] & ~(kSpanBad | kSpanEq);
+                Chunk::Span &sp = ch.span[reqs[j].idx];
+                if (mode == 0) {
+                    sp.p = tab + o;
+                    sp.t = tixb + to;
+                    sp.n = ns;
+                    sp.len = hl[j];
+                    sp.eq = (hc[j] & kSpanEq) != 0;
+                } else {
+                    sp.xp = tab + o;
+                    sp.xt = tixb + to;
+                    sp.xn = ns;
+                    sp.xlen = hl[j];
+                }
+                o += ns + 1;
+                to += (hl[j] + kGatherTile - 1) / kGatherTile;
+                stats.span_entries += ns + 1;
+            }
         }
+        sync();
+        heap.release(wb, o_end);
         heap.release(addr, tot * 4 + 64);
         if (mode == 0 && exact_too) {  // exact tables for the records whose compat expansion is not the doc
             std::vector<SpanReq> x;

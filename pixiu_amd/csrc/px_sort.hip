@@ -139,6 +139,66 @@ __global__ void __launch_bounds__(kThreads) k_seg_hist(const SegTile *tiles, uin
     flush();
 }
 
+// The first suffix sort's histograms from one symbol histogram: pass p's digit of suffix j
+// is its symbol s = syms-1-p, i.e. the first symbol of suffix j+s while j+s stays in j's
+// doc, else 0 (past the doc end).  So pass p's counts = the first-symbol counts (pass
+// syms-1's own), less the symbols at offsets < s of every doc, plus one 0 per suffix within
+// s of its doc's end.  One match per element instead of `syms`; a doc's first thread (the
+// segment's first position, or one after a doc's last, dist == 1) takes its first offsets'
+// corrections from the 8 text bytes it loaded, every suffix near its doc's end its zeros.
+// (Counts wrap: the corrections are subtracted in u32 and the sums are exact.)
+__global__ void __launch_bounds__(kThreads) k_seg_hist_text(const SegTile *tiles, uint32_t ntiles, const uint8_t *G,
+                                                            const uint16_t *dist, uint32_t syms, uint32_t *ghist) {
+    constexpr uint32_t BINS = 512;
+    __shared__ uint32_t h[kMaxPasses * BINS];  // pass syms-1: the first-symbol counts; others: corrections
+    const uint32_t t0 = blockIdx.x * kHistTiles, t1 = min(ntiles, t0 + kHistTiles), top = syms - 1;
+    for (uint32_t i = threadIdx.x; i < syms * BINS; i += kThreads) h[i] = 0;
+    __syncthreads();
+    uint32_t seg = tiles[t0].seg;
+    auto flush = [&]() {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < syms * BINS; i += kThreads) {
+            const uint32_t p = i / BINS, v = i % BINS;
+            const uint32_t c = p == top ? h[i] : h[i] + h[top * BINS + v];
+            if (c) atomicAdd(ghist + (uint64_t)seg * syms * BINS + i, c);
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < syms * BINS; i += kThreads) h[i] = 0;
+        __syncthreads();
+    };
+    gcu64 *G8 = (gcu64 *)G;
+    for (uint32_t t = t0; t < t1; ++t) {
+        const SegTile T = tiles[t];
+        if (T.seg != seg) {  // (workgroup-uniform)
+            flush();
+            seg = T.seg;
+        }
+        for (uint32_t j0 = 0; j0 < T.count; j0 += kThreads) {
+            const uint32_t j = j0 + threadIdx.x;
+            const bool ok = j < T.count;
+            uint32_t d = 0;
+            if (ok) {
+                const uint32_t pos = T.start + j, w = pos >> 3, sh = (pos & 7u) * 8u;
+                uint64_t x = G8[w];
+                if (sh) x = (x >> sh) | (G8[w + 1] << (64u - sh));
+                const uint32_t left = ((gcu16 *)dist)[pos];  // (>= 1)
+                d = (uint32_t)(x & 0xffu) + 1u;
+                for (uint32_t s = left; s <= top; ++s) atomicAdd(&h[(top - s) * BINS], 1u);  // past the doc end
+                const bool doc0 = (T.first && j == 0) || ((gcu16 *)dist)[pos - 1] == 1;
+                if (doc0) {
+                    for (uint32_t o = 0; o + 1 <= top && o < left; ++o) {
+                        const uint32_t v = (uint32_t)((x >> (8 * o)) & 0xffu) + 1u;
+                        for (uint32_t s = o + 1; s <= top; ++s) atomicSub(&h[(top - s) * BINS + v], 1u);
+                    }
+                }
+            }
+            const uint64_t m = match_digit<9>(d, __ballot(ok));
+            if (ok && (m & lanes_below()) == 0) atomicAdd(&h[top * BINS + d], (uint32_t)__popcll(m));
+        }
+    }
+    flush();
+}
+
 // the tile table on the device: tiles before each segment (one workgroup), then one
 // thread per tile finds its segment by a binary search over that prefix
 __global__ void __launch_bounds__(1024) k_seg_tpre(uint32_t nseg, const uint32_t *len, uint32_t *pre) {
@@ -513,7 +573,9 @@ hipError_t seg_sort_pairs(hipStream_t s, const SortAlloc &A, uint32_t nseg, uint
     const uint32_t hb = (nt + kHistTiles - 1) / kHistTiles;
 #define PX_SORT_RB(RB_)                                                                                            \
     do {                                                                                                           \
-        if (text)                                                                                                  \
+        if (text && RB_ == 9 && passes == syms)                                                                    \
+            k_seg_hist_text<<<hb, kThreads, 0, s>>>(d_tiles, nt, G, dist, syms, d_hist);                           \
+        else if (text)                                                                                             \
             k_seg_hist<RB_, true><<<hb, kThreads, 0, s>>>(d_tiles, nt, nullptr, G, dist, syms, passes, d_hist);    \
         else                                                                                                       \
             k_seg_hist<RB_, false><<<hb, kThreads, 0, s>>>(d_tiles, nt, k0, nullptr, nullptr, 0, passes, d_hist);  \
