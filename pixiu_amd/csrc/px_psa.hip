@@ -929,9 +929,13 @@ __global__ void __launch_bounds__(256) k_psa_links_text(uint32_t N, const uint32
 }
 
 // ---------------------------------------------------------------- lcp with those neighbours
-// text positions per thread (Kasai-style amortisation): 256, or fewer (a multiple of 8)
-// when that leaves fewer than 2^18 threads -- a one-chunk window of the single instance
-constexpr uint32_t kLceSpan = 256;
+// text positions per thread (Kasai-style amortisation): 16 (a multiple of 8; the span starts
+// are seeded cooperatively by k_psa_lce_seed).  Longer spans re-fetch their lines: a thread's
+// 16-byte step through five per-position arrays leaves each line before it is used up, and
+// the lines of all threads in flight do not stay cached (config 3, r04: links + lcp 48.6 /
+// 48.4 / 46.8 / 44.4 / 42.7 ms at 256 / 128 / 64 / 32 / 16 positions per thread; PMC at
+// 256: 86 GB fetched by k_psa_lce per batch)
+constexpr uint32_t kLceSpan = 16;
 inline uint32_t lce_span(uint64_t n) {
     if (const char *e = std::getenv("PX_LCE_SPAN")) return (uint32_t)std::max(8, std::atoi(e) / 8 * 8);  // (experiments)
     uint64_t sp = kLceSpan;
