@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group for N > 1 (nccl = RCCL over xGMI; gloo: CPU transport, for tests)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r03aq.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r04.json"),
                     help="per-kernel PMC summary (tools/pmc_summary.py); used only if its workload matches")
     return ap.parse_args()
 
@@ -433,8 +433,8 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
     last = runs[-1]
     # every record against the reference's own output (per-record digests made from the
     # compiled reference over the same corpus part and shards, tests/_refdig.py); only the
-    # canonical part 0 at full size has them
-    if rank == 0:
+    # canonical part 0 at full size has them (not in --no-checks runs: the profiling legs)
+    if rank == 0 and checks:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import _refdig
         ref = _refdig.load(cfg, rps)
@@ -592,7 +592,7 @@ def summarize(cfg, r, rps, world, a, pmc_path):
             if w.get("config") == cfg and w.get("rps") == rps and w.get("records") == r["n"]:
                 if dominant == dec_name:  # the stage's launches (one compat batch in the profile run)
                     tot_b = sum(v["hbm_bytes_per_launch"] * v["dispatches"] for k, v in pmc.items()
-                                if isinstance(v, dict) and k in ("k_decode", "k_gather"))
+                                if isinstance(v, dict) and k in ("k_decode", "k_gather", "k_gather_tasks", "k_dk_lookup"))
                     traffic = tot_b or None
                 else:  # every kernel of the encode stage, summed over its launches
                     tot_b = 0.0

@@ -157,6 +157,108 @@ struct DevBuf {
     }
 };
 
+// Record stores in one reserved virtual range, mapped on demand and allocated by a bump
+// pointer (they are only ever freed together, at reset).  Span tables address a record's
+// source bytes relative to the record itself with 32-bit offsets (SpanEnt::rel), so every
+// record of a chunk has to lie within +-2 GiB of the others; separate heap allocations gave
+// no such bound (a single instance's batch stored in two 512 MB pieces put one chunk's
+// records in blocks further apart than that once the heap had been reused, and those
+// records lost their span tables).  Appended in order, a chunk's records are as far apart
+// as the bytes stored while the chunk was live.  Without virtual memory management the
+// caller falls back to the heap.
+struct StoreArena {
+    char *base = nullptr;
+    uint64_t reserved = 0, mapped = 0, top = 0, gran = 0;
+    bool off = false;
+    int device = 0;
+    hipMemAllocationProp prop{};
+    std::vector<std::pair<hipMemGenericAllocationHandle_t, uint64_t>> maps;  // in address order
+    static constexpr uint64_t kReserve = 1ull << 40;                      // 1 TiB of addresses
+    bool owns(const void *p) const { return base && (const char *)p >= base && (const char *)p < base + reserved; }
+    void *alloc(uint64_t bytes) {
+        if (off || std::getenv("PX_NO_STORE_ARENA")) return nullptr;
+        if (!base) {
+            int vmm = 0;
+            if (hipGetDevice(&device) != hipSuccess ||
+                hipDeviceGetAttribute(&vmm, hipDeviceAttributeVirtualMemoryManagementSupported, device) != hipSuccess || !vmm) {
+                off = true;
+                return nullptr;
+            }
+            prop.type = hipMemAllocationTypePinned;
+            prop.location.type = hipMemLocationTypeDevice;
+            prop.location.id = device;
+            size_t g = 0;
+            if (hipMemGetAllocationGranularity(&g, &prop, hipMemAllocationGranularityRecommended) != hipSuccess || !g ||
+                hipMemAddressReserve((void **)&base, kReserve, 0, nullptr, 0) != hipSuccess || !base) {
+                base = nullptr;
+                off = true;
+                return nullptr;
+            }
+            gran = round_up(std::max<uint64_t>(g, 64ull << 20), g);  // (every mapping 64 MiB-aligned: the
+                                                                    // minimum granularity let a second
+                                                                    // mapping's access grant fail)
+            reserved = kReserve;
+        }
+        static const bool verbose = std::getenv("PX_ARENA_VERBOSE") != nullptr;
+        const uint64_t at = round_up(top, 256), end = at + bytes;
+        if (verbose) fprintf(stderr, "arena: alloc %lu at %lu (mapped %lu)\n", (unsigned long)bytes, (unsigned long)at, (unsigned long)mapped);
+        if (end > reserved) return nullptr;
+        if (end > mapped) {  // map more: what is needed, at least 64 MiB and a quarter of what is mapped
+            uint64_t want = std::max<uint64_t>(end - mapped, std::max<uint64_t>(64ull << 20, mapped / 4));
+            want = round_up(want, gran);
+            if (mapped + want > reserved) want = reserved - mapped;
+            hipMemGenericAllocationHandle_t h{};
+            hipError_t e = hipMemCreate(&h, want, &prop, 0);
+            if (verbose) fprintf(stderr, "arena: create %lu -> %d\n", (unsigned long)want, (int)e);
+            if (e != hipSuccess) {
+                (void)hipGetLastError();  // (not sticky for the caller's next launch check)
+                return nullptr;
+            }
+            e = hipMemMap(base + mapped, want, 0, h, 0);
+            if (verbose) fprintf(stderr, "arena: map at %lu -> %d\n", (unsigned long)mapped, (int)e);
+            if (e != hipSuccess) {
+                (void)hipMemRelease(h);
+                (void)hipGetLastError();
+                return nullptr;
+            }
+            hipMemAccessDesc d{};
+            d.location = prop.location;
+            d.flags = hipMemAccessFlagsProtReadWrite;
+            e = hipMemSetAccess(base + mapped, want, &d, 1);
+            if (e != hipSuccess) {  // (ROCm grants access to a later mapping with the whole range)
+                (void)hipGetLastError();
+                e = hipMemSetAccess(base, mapped + want, &d, 1);
+            }
+            if (verbose) fprintf(stderr, "arena: access -> %d\n", (int)e);
+            if (e != hipSuccess) {
+                (void)hipMemUnmap(base + mapped, want);
+                (void)hipMemRelease(h);
+                (void)hipGetLastError();
+                return nullptr;
+            }
+            maps.emplace_back(h, want);
+            mapped += want;
+        }
+        top = end;
+        return base + at;
+    }
+    // every block at once; the mapped memory stays for reuse (remapping an address range the
+    // device has used was measured to leave copies and kernels reading the old pages: a store
+    // reset and reloaded read back corrupt records)
+    void reset() { top = 0; }
+    ~StoreArena() {
+        if (!base) return;
+        (void)hipDeviceSynchronize();
+        uint64_t o = 0;
+        for (auto &m : maps) {
+            (void)hipMemUnmap(base + o, m.second);
+            (void)hipMemRelease(m.first);
+            o += m.second;
+        }
+        (void)hipMemAddressFree(base, reserved);
+    }
+};
+
 // pinned host staging buffer (grown on demand): small per-batch transfers without the
 // runtime's pageable-copy path
 struct HostBuf {
@@ -277,6 +379,11 @@ struct px_ctx {
     std::vector<std::pair<ShardState *, ShardState>> pending_state;  // states set after the zeroing (loaded shards)
     PartKeyMap keymap;  // raw key -> shard (multi-shard only)
     std::vector<std::pair<void *, uint64_t>> store_blocks;  // packed record stores + segment indexes
+    StoreArena arena;                                        // (record stores: StoreArena above)
+    void *store_alloc(uint64_t bytes) {
+        if (void *p = arena.alloc(bytes)) return p;
+        return heap.alloc(bytes);
+    }
     uint8_t *last_store = nullptr;  // packed compressed bytes of the last set batch
     uint64_t last_store_bytes = 0;
     DevBuf scratch_frames, dq_buf, dstat_buf, dlen_buf, in_buf, tmp_buf, link_buf, iter_buf, init_buf, stout_buf,
@@ -1042,6 +1149,23 @@ struct px_ctx {
         hcheck(hipMemcpyAsync(hr + n, dl, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
         hcheck(hipStreamSynchronize(stream));
         const uint32_t *hc = hr, *hl = hr + n;
+        if (std::getenv("PX_SPAN_VERBOSE")) {  // (diagnostics: why records get no table)
+            std::vector<uint32_t> hs(n);
+            hcheck(hipMemcpy(hs.data(), ds, (size_t)n * 4, hipMemcpyDeviceToHost));
+            std::map<uint32_t, uint32_t> why;
+            uint32_t bad = 0;
+            for (uint32_t j = 0; j < n; ++j)
+                if (hc[j] & kSpanBad) {
+                    ++bad;
+                    ++why[hs[j]];
+                    if (bad <= 5)
+                        fprintf(stderr, "span: no table for chunk %u idx %u: decode status %u len %u doc_len %u\n",
+                                reqs[j].chunk, reqs[j].idx, hs[j], hl[j], chunks[reqs[j].chunk].doc_len[reqs[j].idx]);
+                }
+            fprintf(stderr, "span: mode %u, %u records, %u without a table:", mode, n, bad);
+            for (auto &w : why) fprintf(stderr, " status %u x%u", w.first, w.second);
+            fprintf(stderr, "\n");
+        }
         uint64_t nents = 0, ntiles = 0;
         for (uint32_t j = 0; j < n; ++j)
             if (!(hc[j] & kSpanBad)) {
@@ -1321,8 +1445,10 @@ struct px_ctx {
             if (sp->arena) heap.release(sp->arena, sp->arena_bytes);
         for (auto &c : chunks)
             if (c.dev) heap.release(c.dev, (uint64_t)c.dev_cap * sizeof(RecSlot));
-        for (auto &b : store_blocks) heap.release(b.first, b.second);
+        for (auto &b : store_blocks)
+            if (!arena.owns(b.first)) heap.release(b.first, b.second);
         store_blocks.clear();
+        arena.reset();
         last_store = nullptr;
         last_store_bytes = 0;
         shards.clear();
@@ -2032,7 +2158,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     // reaches its record's bytes by a 32-bit relative offset (LaneEnt::rel)
     const uint64_t lane_at = round_up(coff[n] + 64, 16);
     const uint64_t store_bytes = lane_at + soff[n] / 2 + 64;  // LaneEnt is half a SegEnt
-    auto *store = (uint8_t *)heap.alloc(store_bytes);
+    auto *store = (uint8_t *)store_alloc(store_bytes);
     auto *segs = (uint8_t *)heap.alloc(soff[n] + poff[n] + 64);
     store_blocks.emplace_back(store, store_bytes);
     last_store = store;
@@ -2317,7 +2443,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     for (auto &sp : shards) ub += sp->hs.ub_reads;
     stats.ub_reads = ub;
     trim_heap();
-    stats.device_bytes = heap.held();
+    stats.device_bytes = heap.held() + arena.mapped;
     for (uint32_t r = 0; r < n; ++r) {
         px_status st = map_status(rstatus[r]);
         if (st != PX_OK && rc == PX_OK) rc = st;
@@ -2965,7 +3091,7 @@ int px_ctx::load(const uint8_t *src, uint64_t len, int src_on_device, uint32_t *
     }
     // the store keeps data and lane entries in one allocation (LaneEnt::rel is relative)
     const uint64_t lane_at = data_cap, store_bytes = lane_at + soff[n] / 2 + 64;
-    auto *store = (uint8_t *)heap.alloc(store_bytes);
+    auto *store = (uint8_t *)store_alloc(store_bytes);
     hcheck(hipMemcpyAsync(store, data, h.data_bytes, hipMemcpyDeviceToDevice, stream));
     auto *segs = (uint8_t *)heap.alloc(soff[n] + poff[n] + 64);
     store_blocks.emplace_back(store, store_bytes);
@@ -3446,7 +3572,7 @@ int px_import_chunk(px_ctx *ctx, uint32_t n, const uint8_t *comp, const uint64_t
         std::vector<uint64_t> loff(n + 1, 0);
         for (uint32_t r = 0; r < n; ++r) loff[r + 1] = loff[r] + nents[r] * sizeof(LaneEnt);
         const uint64_t lane_at = round_up(coff[n] + 64, 16), store_bytes = lane_at + loff[n] + 64;
-        auto *store = (uint8_t *)ctx->heap.alloc(store_bytes);
+        auto *store = (uint8_t *)ctx->store_alloc(store_bytes);
         auto *segs = (uint8_t *)ctx->heap.alloc(soff[n] + 64);
         ctx->store_blocks.emplace_back(store, store_bytes);
         ctx->store_blocks.emplace_back(segs, soff[n] + 64);
@@ -3523,8 +3649,8 @@ int px_stats_get(px_ctx *ctx, px_stats *st) {
     PX_GUARD({
         PX_FLUSHED(ctx);
         *st = ctx->stats;
-        st->device_bytes = ctx->heap.held();
-        st->device_live_bytes = ctx->heap.live_bytes();
+        st->device_bytes = ctx->heap.held() + ctx->arena.mapped;
+        st->device_live_bytes = ctx->heap.live_bytes() + ctx->arena.top;
         st->device_peak_bytes = ctx->heap.peak();
         return PX_OK;
     })

@@ -34,7 +34,8 @@ namespace {
 constexpr uint32_t kThreads = 256, kItems = 16, kWaves = kThreads / 64;
 static_assert(kThreads * kItems == kSortTile, "tile = threads x items");
 constexpr uint32_t kMaxPasses = 8;
-constexpr uint32_t kHistTiles = 16;       // tiles per histogram workgroup
+constexpr uint32_t kHistTiles = 16;       // tiles per histogram workgroup, at most (fewer for small sorts)
+constexpr uint32_t kHistGroups = 1024;    // histogram workgroups a sort aims for
 constexpr uint32_t kFlagAgg = 1u << 30, kFlagIncl = 2u << 30, kCountMask = (1u << 30) - 1u;
 constexpr uint32_t kSpinBound = 1u << 20;  // look-back polls before a tile gives up (cannot happen)
 
@@ -97,15 +98,15 @@ SD uint32_t block_excl_scan(uint32_t v, uint32_t *red, uint32_t *tot) {
 }
 
 // ---------------------------------------------------------------- histogram
-// per segment and pass, the digit counts of its elements (one workgroup per kHistTiles
+// per segment and pass, the digit counts of its elements (one workgroup per `tpw` <= kHistTiles
 // tiles; LDS counts flushed to the segment's global counts when the segment changes)
 template <int RB, bool TEXT>
-__global__ void __launch_bounds__(kThreads) k_seg_hist(const SegTile *tiles, uint32_t ntiles, const uint64_t *kin,
+__global__ void __launch_bounds__(kThreads) k_seg_hist(const SegTile *tiles, uint32_t ntiles, uint32_t tpw, const uint64_t *kin,
                                                        const uint8_t *G, const uint16_t *dist, uint32_t syms,
                                                        uint32_t passes, uint32_t *ghist) {
     constexpr uint32_t BINS = 1u << RB;
     __shared__ uint32_t h[kMaxPasses * BINS];
-    const uint32_t t0 = blockIdx.x * kHistTiles, t1 = min(ntiles, t0 + kHistTiles);
+    const uint32_t t0 = blockIdx.x * tpw, t1 = min(ntiles, t0 + tpw);
     for (uint32_t i = threadIdx.x; i < passes * BINS; i += kThreads) h[i] = 0;
     __syncthreads();
     uint32_t seg = tiles[t0].seg;
@@ -147,11 +148,11 @@ __global__ void __launch_bounds__(kThreads) k_seg_hist(const SegTile *tiles, uin
 // segment's first position, or one after a doc's last, dist == 1) takes its first offsets'
 // corrections from the 8 text bytes it loaded, every suffix near its doc's end its zeros.
 // (Counts wrap: the corrections are subtracted in u32 and the sums are exact.)
-__global__ void __launch_bounds__(kThreads) k_seg_hist_text(const SegTile *tiles, uint32_t ntiles, const uint8_t *G,
+__global__ void __launch_bounds__(kThreads) k_seg_hist_text(const SegTile *tiles, uint32_t ntiles, uint32_t tpw, const uint8_t *G,
                                                             const uint16_t *dist, uint32_t syms, uint32_t *ghist) {
     constexpr uint32_t BINS = 512;
     __shared__ uint32_t h[kMaxPasses * BINS];  // pass syms-1: the first-symbol counts; others: corrections
-    const uint32_t t0 = blockIdx.x * kHistTiles, t1 = min(ntiles, t0 + kHistTiles), top = syms - 1;
+    const uint32_t t0 = blockIdx.x * tpw, t1 = min(ntiles, t0 + tpw), top = syms - 1;
     for (uint32_t i = threadIdx.x; i < syms * BINS; i += kThreads) h[i] = 0;
     __syncthreads();
     uint32_t seg = tiles[t0].seg;
@@ -570,15 +571,18 @@ hipError_t seg_sort_pairs(hipStream_t s, const SortAlloc &A, uint32_t nseg, uint
     }
     k_seg_tpre<<<1, 1024, 0, s>>>(nseg, d_len, d_pre);
     k_seg_tfill<<<(nt + 255) / 256, 256, 0, s>>>(nt, nseg, d_start, d_len, d_pre, d_tiles);
-    const uint32_t hb = (nt + kHistTiles - 1) / kHistTiles;
+    // (a small sort -- the big groups of a single-instance round -- spreads its tiles thin:
+    // 16 tiles per workgroup left ~30 workgroups, each walking 64 K elements alone)
+    const uint32_t tpw = std::max<uint32_t>(1, std::min<uint32_t>(kHistTiles, (nt + kHistGroups - 1) / kHistGroups));
+    const uint32_t hb = (nt + tpw - 1) / tpw;
 #define PX_SORT_RB(RB_)                                                                                            \
     do {                                                                                                           \
         if (text && RB_ == 9 && passes == syms)                                                                    \
-            k_seg_hist_text<<<hb, kThreads, 0, s>>>(d_tiles, nt, G, dist, syms, d_hist);                           \
+            k_seg_hist_text<<<hb, kThreads, 0, s>>>(d_tiles, nt, tpw, G, dist, syms, d_hist);                           \
         else if (text)                                                                                             \
-            k_seg_hist<RB_, true><<<hb, kThreads, 0, s>>>(d_tiles, nt, nullptr, G, dist, syms, passes, d_hist);    \
+            k_seg_hist<RB_, true><<<hb, kThreads, 0, s>>>(d_tiles, nt, tpw, nullptr, G, dist, syms, passes, d_hist);    \
         else                                                                                                       \
-            k_seg_hist<RB_, false><<<hb, kThreads, 0, s>>>(d_tiles, nt, k0, nullptr, nullptr, 0, passes, d_hist);  \
+            k_seg_hist<RB_, false><<<hb, kThreads, 0, s>>>(d_tiles, nt, tpw, k0, nullptr, nullptr, 0, passes, d_hist);  \
         k_seg_base<RB_><<<nseg * passes, kThreads, 0, s>>>(d_hist, d_start, passes, d_base);                      \
         const uint64_t *ki = k0;                                                                                   \
         const uint32_t *vi = v0;                                                                                   \

@@ -106,3 +106,35 @@ def test_skipped_critbit_inserts(store_factory, oracle, rps):
     assert st.contains(keys).tolist() == [w is not None for w in want]
     found = [k for k, w in zip(keys, want) if w is not None]
     assert st.get_batch(found) == [w for w in want if w is not None]
+
+
+def test_pieces_keep_span_tables(store_factory):
+    """A batch over 512 MB raw into one shard is stored in pieces; every record keeps its
+    span table (its chunk's records stay within the span entries' 2 GiB reach: the record
+    stores share one reserved address range) and every key resolves on the device, also
+    after resets that reuse the memory."""
+    import numpy as np
+    import torch
+    from pixiu_amd import synth
+    cp = synth.make(3)
+    dev = torch.device("cuda", 0)
+    kb = torch.from_numpy(cp.keys).to(dev)
+    ko = torch.from_numpy(cp.koff.astype(np.int64)).to(dev)
+    vb = torch.from_numpy(cp.vals).to(dev)
+    vo = torch.from_numpy(cp.voff.astype(np.int64)).to(dev)
+    keys = (np.ascontiguousarray(cp.keys), cp.koff.astype(np.uint64))
+    cap = int(2 * cp.raw_bytes + 256 * cp.n + (1 << 20))
+    out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    st = store_factory(records_per_shard=0)
+    first = None
+    for _ in range(3):
+        st.reset()
+        st.set_batch_device(cp.n, kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), check=True)
+        rc, off, ln, sts, _ = st.get_batch_device(keys, out.data_ptr(), cap, px.COMPAT)
+        assert rc == px.PX_OK
+        s = st.stats()
+        assert s["last_get_device_keys"] == cp.n and s["last_gather_queries"] == cp.n
+        got = out[: int(off[-1]) + int(ln[-1])].cpu().numpy()
+        h = hash(got.tobytes())
+        first = h if first is None else first
+        assert h == first
