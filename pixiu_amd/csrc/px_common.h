@@ -180,6 +180,12 @@ struct SlotPut {
     RecSlot *dst;
     RecSlot val;
 };
+// a set batch's record r: where its slot goes in its chunk's device table (null: not
+// placed), its slot number and the chunk's record count (k_slot_place)
+struct SlotDst {
+    RecSlot *dst;
+    uint32_t idx, nrec;
+};
 
 // k_link work item: one record whose record tokens get their target entries
 struct LinkJob {

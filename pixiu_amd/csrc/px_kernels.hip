@@ -1132,6 +1132,29 @@ __global__ void __launch_bounds__(256) k_scatter_slots(uint32_t n, const SlotPut
     dst[2] = src[2];
 }
 
+// The batch's slots into their chunks' device tables, with the segment counts k_tokenize
+// found (px_runtime.cpp set_nseg's rule), and each record's link job (a no-op job for a
+// record that was not placed).  Replaces a host-built table of (destination, slot) pairs.
+__global__ void __launch_bounds__(256) k_slot_place(uint32_t n, const RecSlot *src, const uint32_t *tok,
+                                                    const SlotDst *d, LinkJob *jobs) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const SlotDst sd = d[r];
+    if (!sd.dst) {
+        jobs[r] = LinkJob{nullptr, nullptr, nullptr, 0u, 0u};
+        return;
+    }
+    RecSlot s = src[r];
+    const uint32_t t = tok[r];
+    s.nseg = t & ~(1u << 31);  // (bit 31: k_tokenize's kNoPidx, no position index)
+    if (t >> 31) {
+        s.pidx_n = 0;
+        s.lane = nullptr;
+    }
+    *sd.dst = s;
+    jobs[r] = LinkJob{const_cast<SegEnt *>(s.seg), const_cast<LaneEnt *>(s.lane), sd.dst - sd.idx, s.nseg, sd.nrec};
+}
+
 // ====================================================================== store
 // Copy each record's compressed bytes from scratch into the packed store.
 __global__ void __launch_bounds__(256) k_compact(uint32_t n, uint8_t *const *src, const uint32_t *len,
@@ -2644,6 +2667,12 @@ hipError_t launch_decode_addr(hipStream_t s, const DecodeQuery *qs, uint32_t nq,
     return hipGetLastError();
 }
 
+hipError_t launch_slot_place(hipStream_t s, uint32_t n, const RecSlot *src, const uint32_t *tok, const SlotDst *d,
+                             LinkJob *jobs) {
+    if (!n) return hipSuccess;
+    k_slot_place<<<(n + 255) / 256, 256, 0, s>>>(n, src, tok, d, jobs);
+    return hipGetLastError();
+}
 hipError_t launch_span_jobs(hipStream_t s, uint32_t n, const DecodeQuery *dq, const uint32_t *dl, const uint32_t *ds,
                             const SpanSrc *src, const RecSlot *const *chunk_slots, const int32_t *addr, uint32_t *cnt,
                             uint32_t *ents, uint32_t *tiles, const uint32_t *eoff_incl, const uint32_t *toff_incl,

@@ -52,6 +52,7 @@ hipError_t launch_decode(hipStream_t, const DecodeQuery *, uint32_t, const RecSl
 hipError_t launch_rehash(hipStream_t, const uint4 *, uint32_t, uint32_t, uint4 *, uint32_t);
 hipError_t launch_decode_addr(hipStream_t, const DecodeQuery *, uint32_t, const RecSlot *const *, int32_t *,
                               uint32_t *, uint32_t *, Frame *, uint32_t, uint32_t);
+hipError_t launch_slot_place(hipStream_t, uint32_t, const RecSlot *, const uint32_t *, const SlotDst *, LinkJob *);
 hipError_t launch_span_jobs(hipStream_t, uint32_t, const DecodeQuery *, const uint32_t *, const uint32_t *,
                             const SpanSrc *, const RecSlot *const *, const int32_t *, uint32_t *, uint32_t *,
                             uint32_t *, const uint32_t *, const uint32_t *, SpanEnt *, uint32_t *);
@@ -1103,6 +1104,8 @@ struct px_ctx {
             }
         const std::vector<SpanReq> &reqs = *rp;
         const uint32_t n = (uint32_t)reqs.size();
+        PhaseClock phase(mode ? "build_spans (exact)" : "build_spans", "PX_SET_VERBOSE");
+        phase.mark("queries and sources");
         // queries (pinned) and sources
         auto *qn = (DecodeQuery *)hq_buf.get((uint64_t)n * sizeof(DecodeQuery));
         std::vector<SpanSrc> src(n);
@@ -1124,6 +1127,7 @@ struct px_ctx {
         auto *dl = (uint32_t *)(wb + o_dl), *ds = dl + n;
         auto *dsrc = (SpanSrc *)(wb + o_src);
         auto *cnt = (uint32_t *)(wb + o_u32), *ents = cnt + n, *tiles = ents + n, *eoff = tiles + n, *toff = eoff + n;
+        phase.mark("uploads, decode, count, scans");
         hcheck(hipMemcpyAsync(dq, qn, (size_t)n * sizeof(DecodeQuery), hipMemcpyHostToDevice, stream));
         h2d(dsrc, src.data(), (size_t)n * sizeof(SpanSrc));
         flush_tab();
@@ -1147,7 +1151,9 @@ struct px_ctx {
         auto *hr = (uint32_t *)hres_buf.get((uint64_t)n * 8 + 16);
         hcheck(hipMemcpyAsync(hr, cnt, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
         hcheck(hipMemcpyAsync(hr + n, dl, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
+        phase.mark("wait (decode + count)");
         hcheck(hipStreamSynchronize(stream));
+        phase.mark("table sizes, write pass, views");
         const uint32_t *hc = hr, *hl = hr + n;
         if (std::getenv("PX_SPAN_VERBOSE")) {  // (diagnostics: why records get no table)
             std::vector<uint32_t> hs(n);
@@ -1204,9 +1210,11 @@ struct px_ctx {
                 stats.span_entries += ns + 1;
             }
         }
+        phase.mark("wait (write pass)");
         sync();
         heap.release(wb, o_end);
         heap.release(addr, tot * 4 + 64);
+        phase.mark("exact tables");
         if (mode == 0 && exact_too) {  // exact tables for the records whose compat expansion is not the doc
             std::vector<SpanReq> x;
             for (const SpanReq &r : reqs) {
@@ -1473,9 +1481,13 @@ struct px_ctx {
     // kp table; a prefix that overran `cap` is decoded again with the whole doc's room.
     // st[i] = kOk or the decode's failure status.
     void decode_key_prefixes(const std::vector<KpJob> &jobs, std::vector<uint32_t> &st) {
+        PhaseClock phase("decode_key_prefixes", "PX_SET_VERBOSE");
+        phase.mark("queries");
         st.assign(jobs.size(), kOk);
         std::vector<DecodeQuery> q;
         std::vector<uint32_t> qj;
+        q.reserve(jobs.size());
+        qj.reserve(jobs.size());
         uint64_t qo = 0;
         for (size_t i = 0; i < jobs.size(); ++i) {
             q.push_back(DecodeQuery{jobs[i].chunk, jobs[i].idx, 0, kMaxDoc, qo, jobs[i].cap, 0});
@@ -1483,15 +1495,18 @@ struct px_ctx {
             qo += round_up(jobs[i].cap, 16);
         }
         for (int pass = 0; pass < 2 && !q.empty(); ++pass) {
+            phase.mark(pass ? "decode (again)" : "decode");
             auto *kbuf = (uint8_t *)heap.alloc(qo + 64);
             std::vector<uint32_t> ql, qs;
             run_decode(q, kbuf, ql, qs, false);
+            phase.mark("copy down");
             // (uninitialised: 1 M key prefixes are ~80 MB, which a zero fill would write twice)
             std::unique_ptr<uint8_t[]> hk_store(new uint8_t[qo + 1]);
             uint8_t *hk = hk_store.get();
             d2h(hk, kbuf, qo);
             sync();
             heap.release(kbuf, qo + 64);
+            phase.mark("append to the chunks' prefix stores");
             std::vector<DecodeQuery> again;
             std::vector<uint32_t> again_j;
             uint64_t ao = 0;
@@ -2192,7 +2207,6 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     heap.release(d_dst, (uint64_t)n * 8);
     heap.release(d_cdst, (uint64_t)n * 8);
     heap.release(d_coff, (uint64_t)n * 8);
-    heap.release(d_slots, (uint64_t)n * sizeof(RecSlot));
 
     phase.mark("register records in their chunks");
     // ---- register records in their chunks
@@ -2233,44 +2247,38 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         stats.doc_bytes += doc_len[r];
         stats.comp_bytes += comp_len[r];
     }
-    // push new slot entries to the device tables (one copy per touched chunk range)
+    phase.mark("register: slot tables and link jobs");
+    // push new slot entries to the device tables and resolve the new records' tokens to
+    // their target entries: per record its destination (the slots themselves are on the
+    // device since k_tokenize), one kernel for both (k_slot_place), then k_link
     {
-        // chunk -> [lo, hi) of its new slots (a flat table over chunk ids: a batch of 1 M
-        // records paid a std::map lookup per record here)
-        std::vector<std::pair<uint32_t, uint32_t>> span_of(chunks.size(), {kNone, 0});
         std::vector<uint32_t> touched;
+        {
+            std::vector<uint8_t> seen(chunks.size(), 0);
+            for (uint32_t r = 0; r < n; ++r)
+                if (rgchunk[r] != kNone && !seen[rgchunk[r]]) {
+                    seen[rgchunk[r]] = 1;
+                    touched.push_back(rgchunk[r]);
+                }
+        }
+        for (uint32_t c : touched) chunk_reserve(c, chunks[c].n);
+        std::vector<SlotDst> sd(n);
         for (uint32_t r = 0; r < n; ++r) {
-            if (rgchunk[r] == kNone) continue;
-            auto &t = span_of[rgchunk[r]];
-            if (t.first == kNone) {
-                t = {ridx[r], ridx[r] + 1};
-                touched.push_back(rgchunk[r]);
-            } else {
-                t.second = ridx[r] + 1;
+            if (rgchunk[r] == kNone) {
+                sd[r] = SlotDst{nullptr, 0, 0};
+                continue;
             }
-        }
-        std::sort(touched.begin(), touched.end());
-        std::vector<SlotPut> puts;
-        puts.reserve(n);
-        for (uint32_t c : touched) {
-            chunk_reserve(c, chunks[c].n);
-            Chunk &ch = chunks[c];
-            for (uint32_t i = span_of[c].first; i < span_of[c].second; ++i) puts.push_back(SlotPut{ch.dev + i, ch.slots[i]});
-        }
-        if (!puts.empty()) {
-            auto *d = (SlotPut *)slotput_buf.get(puts.size() * sizeof(SlotPut));
-            h2d(d, puts.data(), puts.size() * sizeof(SlotPut));
-            hcheck(launch_scatter_slots(stream, (uint32_t)puts.size(), d));
-        }
-        // resolve the new records' tokens to their target entries
-        std::vector<LinkJob> jobs;
-        for (uint32_t r = 0; r < n; ++r) {
-            if (rgchunk[r] == kNone) continue;
             const Chunk &ch = chunks[rgchunk[r]];
-            jobs.push_back(LinkJob{const_cast<SegEnt *>(slots[r].seg), const_cast<LaneEnt *>(slots[r].lane), ch.dev,
-                                   slots[r].nseg, ch.n});
+            sd[r] = SlotDst{ch.dev + ridx[r], ridx[r], ch.n};
         }
-        link(jobs);
+        auto *d = (uint8_t *)slotput_buf.get(round_up((uint64_t)n * sizeof(SlotDst), 256) + (uint64_t)n * sizeof(LinkJob));
+        auto *dsd = (SlotDst *)d;
+        auto *dj = (LinkJob *)(d + round_up((uint64_t)n * sizeof(SlotDst), 256));
+        h2d(dsd, sd.data(), (size_t)n * sizeof(SlotDst));
+        hcheck(launch_slot_place(stream, n, d_slots, d_nseg, dsd, dj));
+        hcheck(launch_link(stream, n, dj));
+        sync();  // (d_slots and the job table are released / reused next)
+        heap.release(d_slots, (uint64_t)n * sizeof(RecSlot));
     }
 
     phase.mark("compat key prefixes (GPU decode of each ");
@@ -2278,11 +2286,16 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     {
         std::vector<KpJob> jobs;
         std::vector<uint32_t> jrec;
+        jobs.reserve(n);
+        jrec.reserve(n);
         for (uint32_t r = 0; r < n; ++r) {
             if (!live[r]) continue;
             uint64_t klen = hkoff[r + 1] - hkoff[r];
+            // first decode's room: the key, its 251,0 and a few escapes (a prefix that does
+            // not fit is decoded again with the whole doc's room; 1 M keys copied 2 klen + 66
+            // bytes each down for ~klen + 2 used)
             jobs.push_back(KpJob{rgchunk[r], ridx[r], doc_len[r],
-                                 (uint32_t)std::min<uint64_t>(doc_len[r] + 64, 2 * klen + 2 + 64)});
+                                 (uint32_t)std::min<uint64_t>(doc_len[r] + 64, klen + 2 + 30)});
             jrec.push_back(r);
         }
         std::vector<uint32_t> kst;
@@ -2301,6 +2314,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     // ---- span tables of the new records (full-range getitem as a gather)
     {
         std::vector<SpanReq> reqs;
+        reqs.reserve(n);
         for (uint32_t r = 0; r < n; ++r)
             if (live[r]) reqs.push_back(SpanReq{rgchunk[r], ridx[r], dst[r]});
         const auto ts = std::chrono::steady_clock::now();
@@ -2316,19 +2330,35 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     std::vector<uint32_t> dk_r;  // the batch record of each entry
     std::vector<uint8_t> dk_kb;
     if (dk) {
+        // live records in order: their ids and key-arena places by prefix sums, then the
+        // entries on host threads (a batch of 1 M records spent ~45 ms here on one)
+        for (uint32_t r = 0; r < n; ++r)
+            if (live[r]) dk_r.push_back(r);
+        const uint32_t m = (uint32_t)dk_r.size();
+        std::vector<uint64_t> kbo(m + 1, 0);
+        for (uint32_t j = 0; j < m; ++j) {
+            const uint32_t r = dk_r[j];
+            kbo[j + 1] = kbo[j] + (hkoff[r + 1] - hkoff[r]);
+            Chunk &ch = chunks[rgchunk[r]];
+            if (ch.gid.size() <= ridx[r]) ch.gid.resize(ridx[r] + 1, kNone);  // (sized before the threads)
+        }
+        dk_new.resize(m);
+        dk_kb.resize(kbo[m]);
+        const uint32_t gid0 = dki.nrec;
+        dki.nrec += m;
+        parallel_ranges(m, m >= 4096 ? host_threads() : 1, [&](uint32_t lo, uint32_t hi) {
         std::string q;
-        for (uint32_t r = 0; r < n; ++r) {
-            if (!live[r]) continue;
+        for (uint32_t j = lo; j < hi; ++j) {
+            const uint32_t r = dk_r[j];
             Chunk &ch = chunks[rgchunk[r]];
             const uint32_t i = ridx[r];
-            if (ch.gid.size() <= i) ch.gid.resize(i + 1, kNone);
-            ch.gid[i] = dki.nrec++;
+            ch.gid[i] = gid0 + j;
             const uint8_t *k = hkeys.data() + hkoff[r];
             const uint64_t kl = hkoff[r + 1] - hkoff[r];
             DkRec d{};
-            d.key_off = dki.keys_len + dk_kb.size();
+            d.key_off = dki.keys_len + kbo[j];
             d.key_len = (uint32_t)kl;
-            dk_kb.insert(dk_kb.end(), k, k + kl);
+            if (kl) std::memcpy(dk_kb.data() + kbo[j], k, kl);
             if (i < ch.span.size() && ch.span[i].p) {
                 const Chunk::Span &sp = ch.span[i];
                 d.sp = sp.p;
@@ -2352,9 +2382,9 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             esc_key_into(q, k, kl);
             const bool clean = kp_matches(Leaf{rgchunk[r], i}, q);
             d.flags = kDkLive | (clean ? kDkClean : 0u);  // (and in its trie: settled after the inserts)
-            dk_new.push_back(d);
-            dk_r.push_back(r);
+            dk_new[j] = d;
         }
+        });
     }
 
     phase.mark("CritBit inserts: every shard's own recor");
@@ -2841,6 +2871,8 @@ void px_ctx::dki_commit(uint32_t gid0, const std::vector<DkRec> &recs, const std
 int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int mode, uint8_t *out, uint64_t out_cap,
                     int out_on_device, uint64_t *out_off, uint32_t *out_len, uint32_t *status, uint64_t *needed) {
     if (!dki_enabled() || !dki.valid || !dki.tab || !n || !spans_enabled()) return -1;
+    PhaseClock phase("dki_get", "PX_GET_VERBOSE");
+    phase.mark("kills, scratch, keys to pinned");
     dki_apply_kills();  // (deletes since the last set batch)
     const uint64_t k0 = koff[0], kbytes = koff[n] - k0;
     // device scratch: keys, offsets, gather queries, the look-back chain, then what comes back
@@ -2870,6 +2902,7 @@ int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int m
     std::memcpy(hb, keys + k0, kbytes);
     auto *ho = (uint64_t *)(hb + o_off);
     for (uint32_t i = 0; i <= n; ++i) ho[i] = koff[i] - k0;
+    phase.mark("uploads and launches");
     hcheck(hipMemcpyAsync(dkeys, hb, o_off + (uint64_t)(n + 1) * 8, hipMemcpyHostToDevice, stream));
     hcheck(hipMemsetAsync(chain, 0, nb * 16 + 32, stream));
     flush_tab();
@@ -2883,7 +2916,9 @@ int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int m
     // one copy, one round trip: ctl, offsets, lengths and statuses
     auto *hr = (uint32_t *)dk_hres.get(o_end - o_ctl);
     hcheck(hipMemcpyAsync(hr, ctl, o_end - o_ctl, hipMemcpyDeviceToHost, stream));
+    phase.mark("wait for the device");
     hcheck(hipStreamSynchronize(stream));
+    phase.mark("results");
     const uint8_t *res = (const uint8_t *)hr + 32;
     if (hr[3]) {  // an insert gave up: the index is not trusted again until reset
         fprintf(stderr, "pixiu_amd: device key index insert failed; getitem resolves on the host\n");
