@@ -31,6 +31,7 @@ if [ "${SKIP_KS:-0}" != 1 ]; then
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/${TAG}_ks -o ks --output-format csv \
   -- python3 $PROF > $O/${TAG}_ks.log 2>&1 || { echo "KTRACE FAILED"; tail -20 $O/${TAG}_ks.log; exit 1; }
 fi
+if [ "${SKIP_PMC:-0}" = 1 ]; then find $O/${TAG}_ks -name '*kernel_trace.csv' -delete 2>/dev/null; echo DONE; exit 0; fi
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $O/${TAG}_pmc_f -o f --output-format csv \
   -- python3 $PROF > $O/${TAG}_pmc_f.log 2>&1 || { echo "PMC FETCH FAILED"; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $O/${TAG}_pmc_w -o w --output-format csv \
