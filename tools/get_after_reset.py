@@ -1,9 +1,9 @@
 import os, sys, time
 import numpy as np, torch
-sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import pixiu_amd as px
 from pixiu_amd import synth
-cp = synth.make(3)
+cp = synth.make(int(sys.argv[2]) if len(sys.argv) > 2 else 3)
 dev = torch.device("cuda", 0)
 kb = torch.from_numpy(cp.keys).to(dev); ko = torch.from_numpy(cp.koff.astype(np.int64)).to(dev)
 vb = torch.from_numpy(cp.vals).to(dev); vo = torch.from_numpy(cp.voff.astype(np.int64)).to(dev)
