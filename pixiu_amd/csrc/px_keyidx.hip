@@ -15,7 +15,7 @@
 //                 workgroups, decoupled look-back)
 // The batch then goes straight to the gather (k_gather_tasks, k_gather) with no host round
 // trip: ctl[0] = keys missed, ctl[1] = output bytes / 16, ctl[2] = tiles, ctl[3] = the
-// index's insert-error word, ctl[4] = workgroup ticket; both gather kernels skip the batch
+// index's insert-error word, ctl[4] = workgroup ticket, ctl[5] = queries past their room; both gather kernels skip the batch
 // unless nothing missed and the output fits.
 #include <hip/hip_runtime.h>
 
@@ -104,7 +104,7 @@ constexpr uint32_t kChSpin = 1u << 24;
 __global__ void __launch_bounds__(256) k_dk_lookup(uint32_t nq, const uint8_t *qkeys, const uint64_t *qoff,
                                                    const DkSlot *tab, uint32_t mask, const DkRec *rec,
                                                    const uint8_t *keys, uint32_t mode, GatherQuery *gq,
-                                                   uint64_t *out_off, uint32_t *ctl, unsigned long long *chain,
+                                                   uint32_t *out_off16, uint32_t *ctl, unsigned long long *chain,
                                                    const uint32_t *ins_err) {
     __shared__ uint32_t s_bid, s_wa[4], s_wt[4];
     __shared__ unsigned long long s_pa, s_pt;
@@ -142,6 +142,7 @@ __global__ void __launch_bounds__(256) k_dk_lookup(uint32_t nq, const uint8_t *q
                 nt = max(1u, (min(len, cap) + kGatherTile - 1) / kGatherTile);
                 G = GatherQuery{sp, r.comp, 0, ns, len, cap, q, t, 0, 0};
                 ok = true;
+                if (len > cap) atomicAdd(&ctl[5], 1u);  // (the gather's PX_ESPACE statuses)
             }
         }
     }
@@ -224,7 +225,7 @@ __global__ void __launch_bounds__(256) k_dk_lookup(uint32_t nq, const uint8_t *q
         G.out_off = off;
         G.tile0 = (uint32_t)(s_pt + pt + it - nt);
         gq[q] = G;
-        out_off[q] = off;
+        out_off16[q] = (uint32_t)(off >> 4);  // (16-byte units: half the bytes copied down)
     }
 }
 
@@ -244,9 +245,9 @@ hipError_t launch_dk_kill(hipStream_t s, uint32_t n, const uint32_t *gids, DkRec
 // ctl: 32 bytes, chain: 16 bytes per 256 keys, both zeroed by the caller
 hipError_t launch_dk_lookup(hipStream_t s, uint32_t nq, const uint8_t *qkeys, const uint64_t *qoff, const DkSlot *tab,
                             uint32_t mask, const DkRec *rec, const uint8_t *keys, uint32_t mode, GatherQuery *gq,
-                            uint64_t *out_off, uint32_t *ctl, unsigned long long *chain, const uint32_t *ins_err) {
+                            uint32_t *out_off16, uint32_t *ctl, unsigned long long *chain, const uint32_t *ins_err) {
     if (!nq) return hipSuccess;
-    k_dk_lookup<<<(nq + 255) / 256, 256, 0, s>>>(nq, qkeys, qoff, tab, mask, rec, keys, mode, gq, out_off, ctl, chain,
+    k_dk_lookup<<<(nq + 255) / 256, 256, 0, s>>>(nq, qkeys, qoff, tab, mask, rec, keys, mode, gq, out_off16, ctl, chain,
                                                  ins_err);
     return hipGetLastError();
 }

@@ -63,7 +63,7 @@ hipError_t launch_dk_insert(hipStream_t, uint32_t, uint32_t, const DkRec *, cons
                             uint32_t *);
 hipError_t launch_dk_kill(hipStream_t, uint32_t, const uint32_t *, DkRec *);
 hipError_t launch_dk_lookup(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, const DkSlot *, uint32_t,
-                            const DkRec *, const uint8_t *, uint32_t, GatherQuery *, uint64_t *, uint32_t *,
+                            const DkRec *, const uint8_t *, uint32_t, GatherQuery *, uint32_t *, uint32_t *,
                             unsigned long long *, const uint32_t *);
 int debug_trace_take(int32_t *, uint32_t);
 int debug_prof_take(unsigned long long *, uint32_t);
@@ -2881,8 +2881,8 @@ int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int m
     const uint64_t nb = (n + 255) / 256;
     const uint64_t o_off = round_up(kbytes + 16, 256), o_gq = o_off + round_up((uint64_t)(n + 1) * 8, 256),
                    o_chain = o_gq + round_up((uint64_t)n * sizeof(GatherQuery), 256), o_ctl = o_chain + nb * 16,
-                   o_oo = o_ctl + 32, o_dl = o_oo + (uint64_t)n * 8, o_end = o_dl + (uint64_t)n * 8,
-                   o_task = round_up(o_end, 256);
+                   o_oo = o_ctl + 32, o_dl = o_oo + (uint64_t)n * 4, o_ds = o_dl + (uint64_t)n * 4,
+                   o_end = o_ds + (uint64_t)n * 4, o_task = round_up(o_end, 256);
     // the tasks: at most one per 64 tiles, a tile per 16 bytes of the output that fits
     // (every query's tiles <= its cap / 16), so the launch can go before the totals are known
     // (a host buffer: device staging up to 4 GiB; a batch past it goes the host path)
@@ -2894,8 +2894,8 @@ int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int m
     auto *gq = (GatherQuery *)(b + o_gq);
     auto *chain = (unsigned long long *)(b + o_chain);
     auto *ctl = (uint32_t *)(b + o_ctl);
-    auto *oo = (uint64_t *)(b + o_oo);
-    auto *dl = (uint32_t *)(b + o_dl), *ds = dl + n;
+    auto *oo = (uint32_t *)(b + o_oo);  // output offsets in 16-byte units
+    auto *dl = (uint32_t *)(b + o_dl), *ds = (uint32_t *)(b + o_ds);
     void *task = b + o_task;
     // keys up through pinned memory (one copy of the bytes and the rebased offsets)
     auto *hb = (uint8_t *)dk_hbuf.get(o_gq);
@@ -2913,9 +2913,10 @@ int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int m
     uint8_t *dout = out_on_device ? out : (uint8_t *)dk_obuf.get(cap_fit + 64);
     hcheck(launch_gather(stream, (uint32_t)ntask_max, ctl, cap_fit, task, gq, n, dout, dl, ds));
     hcheck(hipEventRecord(ev1, stream));
-    // one copy, one round trip: ctl, offsets, lengths and statuses
+    // one copy, one round trip: ctl, offsets and lengths (the statuses only when some query
+    // ran past its room, ctl[5])
     auto *hr = (uint32_t *)dk_hres.get(o_end - o_ctl);
-    hcheck(hipMemcpyAsync(hr, ctl, o_end - o_ctl, hipMemcpyDeviceToHost, stream));
+    hcheck(hipMemcpyAsync(hr, ctl, o_ds - o_ctl, hipMemcpyDeviceToHost, stream));
     phase.mark("wait for the device");
     hcheck(hipStreamSynchronize(stream));
     phase.mark("results");
@@ -2936,13 +2937,19 @@ int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int m
     stats.last_decode_kernel_ms = ms;
     stats.last_gather_queries = n;
     stats.last_get_device_keys = n;
-    std::memcpy(out_off, res, (size_t)n * 8);
-    const uint32_t *rl = (const uint32_t *)(res + (uint64_t)n * 8), *rs = rl + n;
+    const uint32_t *ro = (const uint32_t *)res, *rl = ro + n;
+    for (uint32_t i = 0; i < n; ++i) out_off[i] = (uint64_t)ro[i] * 16;
+    std::memcpy(out_len, rl, (size_t)n * 4);
     int rc = PX_OK;
-    for (uint32_t i = 0; i < n; ++i) {
-        out_len[i] = rl[i];
-        status[i] = map_status(rs[i]);
-        if (status[i] != PX_OK && rc == PX_OK) rc = (int)status[i];
+    if (hr[5]) {
+        uint32_t *rs = (uint32_t *)dk_hres.get(o_end - o_ctl) + (o_ds - o_ctl) / 4;
+        hcheck(hipMemcpy(rs, ds, (size_t)n * 4, hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < n; ++i) {
+            status[i] = map_status(rs[i]);
+            if (status[i] != PX_OK && rc == PX_OK) rc = (int)status[i];
+        }
+    } else {
+        std::fill(status, status + n, (uint32_t)PX_OK);
     }
     if (needed) *needed = total;
     return rc;
