@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--no-cliff", action="store_true", help="skip the walk-fallback leg (one forced-flag shard)")
     ap.add_argument("--no-exact", action="store_true",
                     help="skip the exact-mode getitem (profiling runs: one compat batch per step only)")
+    ap.add_argument("--retain-mb", type=int, default=0,
+                    help="px_opts.retain_mb of the benchmarked stores (0: the batch's own peak stays cached)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group for N > 1 (nccl = RCCL over xGMI; gloo: CPU transport, for tests)")
@@ -376,9 +378,10 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
     out = torch.empty(out_cap, dtype=torch.uint8, device=dev)
     gather_buf = [None]
     gathered = [None]
-    st = px.Store(records_per_shard=rps, device=local)
+    st = px.Store(records_per_shard=rps, device=local, retain_mb=a.retain_mb)
 
     def step():
+        tr = time.perf_counter()
         st.reset()
         t0 = time.perf_counter()
         res = st.set_batch_device(n, kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), check=False)
@@ -394,7 +397,7 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
         gst = st.stats()
         dec_kms, look_ms, call_ms = gst["last_decode_kernel_ms"], gst["last_get_lookup_ms"], gst["last_get_call_ms"]
         spans = (int(gst["last_gather_queries"]), int(sst["span_entries"]), sst["last_span_build_ms"],
-                 int(sst["device_bytes"]))
+                 int(sst["device_bytes"]), int(sst["last_set_peak_bytes"]), int(sst["device_live_bytes"]))
         g_ms = 0.0
         if world > 1:  # every rank's chunk blob (pixiu_amd/blob.py) to rank 0, RCCL over xGMI
             tg = time.perf_counter()
@@ -412,7 +415,7 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
             bad = int((res["status"] != 0).sum())
             raise SystemExit(f"rank {rank} config {cfg}: setitem failures={bad} getitem rc={rc}")
         # setitem's one exchange (the compressed-blob gather to rank 0) counts as setitem time
-        return {"set_s": t_set + g_ms * 1e-3, "get_s": t2 - t1, "set_kms": set_kms, "walk_kms": walk_kms,
+        return {"set_s": t_set + g_ms * 1e-3, "get_s": t2 - t1, "reset_s": t0 - tr, "set_kms": set_kms, "walk_kms": walk_kms,
                 "emit_kms": emit_kms, "dec_kms": dec_kms, "gather_ms": g_ms, "look_ms": look_ms,
                 "call_ms": call_ms, "comp": int(res["comp_len"].sum()), "exp": int(ln.sum()), "res": res,
                 "off": off, "len": ln, "psa": psa, "spans": spans}
@@ -547,6 +550,13 @@ def check_single(r0):
             "comp_bytes_equal": sum(map(len, comp)) == g["comp_bytes"]}
 
 
+def _mmm(v, nd=3):
+    """[min, median, max] of a list (rounded to nd places; nd = 0: ints)."""
+    v = sorted(v)
+    q = [v[0], v[len(v) // 2] if len(v) % 2 else (v[len(v) // 2 - 1] + v[len(v) // 2]) / 2, v[-1]]
+    return [int(x) for x in q] if nd == 0 else [round(float(x), nd) for x in q]
+
+
 def summarize(cfg, r, rps, world, a, pmc_path):
     """Aggregate one config's runs (whole-job volumes over ranks) into its report."""
     import torch
@@ -571,7 +581,8 @@ def summarize(cfg, r, rps, world, a, pmc_path):
     dec_kms = float(np.mean([x["dec_kms"] for x in runs]))
     # roofline: algorithmic bytes per launch / avg launch time, HIP events
     # on the context's stream (px_stats).  The setitem encode stage is the suffix-array
-    # pipeline (px_psa.hip: rocPRIM sorts + k_psa_*) for PSA shards and k_gst_encode for
+    # pipeline (px_psa.hip + px_sort.hip: hand-written segmented radix sorts and k_psa_* / k_dbl_* /
+    # k_pool_*) for PSA shards and k_gst_encode for
     # walked ones; its span is timed as one stage.
     psa_shards = int(np.mean([x["psa"][1] for x in runs]))
     walk_shards = int(np.mean([x["psa"][2] for x in runs]))
@@ -645,7 +656,16 @@ def summarize(cfg, r, rps, world, a, pmc_path):
         "roofline_kernels_GBps": {"encode_stage": round(set_gbps, 3), "k_gst_emit": round(emit_gbps, 3),
                                   "getitem_stage": round(dec_gbps, 3)},
         "gather_ms": round(float(np.mean([x["gather_ms"] for x in runs])), 3),
+        # every timed step on this rank (min / median / max): set and get are the two timed
+        # calls, reset the untimed px_reset before each set; device bytes after the set batch
+        # (heap held + store arena), at its peak, and live
+        "per_step": {k: _mmm([x[f] * 1e3 for x in runs]) for k, f in
+                     (("set_ms", "set_s"), ("get_ms", "get_s"), ("reset_ms", "reset_s"))},
     }
+    out["per_step"]["set_max_over_min"] = round(out["per_step"]["set_ms"][2] / max(out["per_step"]["set_ms"][0], 1e-9), 3)
+    out["per_step"]["device_bytes_after_set"] = _mmm([x["spans"][3] for x in runs], 0)
+    out["per_step"]["device_peak_bytes_in_set"] = _mmm([x["spans"][4] for x in runs], 0)
+    out["per_step"]["device_live_bytes"] = runs[-1]["spans"][5]
     if "parity_counts" in r:
         out["parity_counts"] = r["parity_counts"]
     return out
@@ -715,7 +735,8 @@ def main():
                    "parallelism": f"dp{world} (record-range shards, no cross-GPU refs)"},
     }
     for k in ("setitem_MBps", "getitem_MBps", "getitem_exact_MBps", "compression_ratio", "kernel_ms",
-              "encode_stage", "getitem_path", "roofline", "roofline_kernels_GBps", "gather_ms", "parity_counts"):
+              "encode_stage", "getitem_path", "roofline", "roofline_kernels_GBps", "gather_ms", "per_step",
+              "parity_counts"):
         if k in main_sum:
             line[k] = main_sum[k]
     line["getitem_split_ms"] = {k: round(v, 3) for k, v in get_split.items()}
@@ -794,6 +815,11 @@ def main():
                 line["single_instance"]["cpu_baseline"]["reference_equivalent_value"] = round(
                     c0["set_MBps"] * cal["ref_over_port_set"] + c0["get_MBps"] * cal["ref_over_port_get"], 4)
         r0["st"].close()
+    # the headline's parts again at the end of the line (a reader of the line's tail sees them)
+    line["headline_parts"] = {
+        "setitem_MBps": line.get("setitem_MBps"), "getitem_MBps": line.get("getitem_MBps"),
+        "setitem_MBps_pcie_inclusive": line.get("pcie_inclusive", {}).get("set_MBps"),
+        "ms_per_step": line["ms_per_step"], "per_step": line.get("per_step")}
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -235,6 +235,10 @@ struct PiXiuCtrl {
             uint8_t dummy = 0;
             rc = px_set_batch(ctx, 1, k, koff, v ? v : &dummy, voff, 0, &r);
         }
+        if (rc == PX_OK && flush_rc != PX_OK) {  // an earlier queued record failed to store
+            rc = flush_rc;
+            flush_rc = PX_OK;
+        }
         if (rc != PX_OK) return -rc;
         if (r.chunk == PX_PENDING) {
             pending = true;
@@ -305,6 +309,7 @@ struct PiXiuCtrl {
         h->ctx = ctx;
         h->epoch++;
         pending = false;
+        flush_rc = PX_OK;
         chunk_view = PiXiuChunk();
         chunk_view.owner = this;
         closed.clear();
@@ -350,14 +355,30 @@ struct PiXiuCtrl {
         return p.get();
     }
 
-    // stores the write-behind queue and brings the live-chunk view up to date
+    // stores the write-behind queue and brings the live-chunk view up to date.  A failure
+    // (a queued record could not be stored) is kept and returned, as -status, by the next
+    // setitem -- the call whose record would otherwise be missing silently -- or by flush()
     void sync_pending() {
         if (!pending || !ctx) return;
         pending = false;
         px_set_result last;
         memset(&last, 0xff, sizeof last);  // (chunk 0xffffffff: nothing placed)
-        (void)px_flush(ctx, &last);
+        const int rc = px_flush(ctx, &last);
+        if (rc != PX_OK && flush_rc == PX_OK) flush_rc = rc;
         apply(last);
+    }
+
+    // extension: store the write-behind queue now; PX_OK or the first failure since the last
+    // report (a record queued by an earlier setitem that could not be stored)
+    int flush() {
+        sync_pending();
+        if (ctx) {
+            const int rc = px_flush(ctx, nullptr);
+            if (rc != PX_OK && flush_rc == PX_OK) flush_rc = rc;
+        }
+        const int rc = flush_rc;
+        flush_rc = PX_OK;
+        return rc;
     }
 
   private:
@@ -371,6 +392,7 @@ struct PiXiuCtrl {
     }
     std::shared_ptr<PxHandle> h;
     bool pending = false;
+    int flush_rc = PX_OK;  // a write-behind failure not yet returned to the caller
     std::map<uint32_t, std::unique_ptr<PiXiuChunk>> closed;
 };
 

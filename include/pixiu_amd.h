@@ -67,8 +67,10 @@ typedef struct px_opts {
                                    raw bytes are pending, or by px_flush / any other call on the
                                    context; 0 = off (every call stores at once).  See px_flush. */
     uint32_t retain_mb;         /* device memory the heap keeps cached in wholly free slabs after a
-                                   set batch (the rest goes back to the driver); 0 = 8,192 MiB,
-                                   0xffffffff = keep everything */
+                                   set batch (the rest goes back to the driver); 0 = what that
+                                   batch needed at its peak beyond what stays live (similar
+                                   batches then never re-allocate), 0xffffffff = keep everything.
+                                   px_trim returns cached memory on request. */
 } px_opts;
 
 typedef struct px_ctx px_ctx;
@@ -98,7 +100,8 @@ typedef struct px_stats {
     uint64_t records, shards, chunks;
     uint64_t raw_bytes, doc_bytes, comp_bytes;
     uint64_t ub_reads;        /* reads the reference makes out of bounds (UB there) */
-    uint64_t device_bytes;    /* device memory held by the context's heap now (live + cached free) */
+    uint64_t device_bytes;    /* device memory held now: the heap (live + cached free) plus the
+                                 mapped record-store arena */
     double last_set_stage_ms;     /* GPU events around the encode stage and k_gst_emit of the last
                                      px_set_batch (= last_encode_stage_ms + last_emit_kernel_ms) */
     double last_decode_kernel_ms; /* the getitem stage of the last get/parse batch: k_gather + k_decode
@@ -133,6 +136,8 @@ typedef struct px_stats {
                                      compat-decoded key is not its key: reported, never hidden) */
     uint64_t last_get_device_keys; /* keys of the last px_get_batch resolved by the device key index
                                      (0: the batch resolved its keys on the host) */
+    uint64_t last_set_peak_bytes;  /* device memory in use at the peak of the last px_set_batch
+                                     (heap live bytes incl. scratch, plus the mapped store arena) */
 } px_stats;
 
 px_ctx *px_open(const px_opts *opts);
@@ -249,6 +254,10 @@ int px_load(px_ctx *ctx, const uint8_t *src, uint64_t len, int src_on_device, ui
 /* Drop every stored record (PiXiuCtrl::free_prop + init_prop, PiXiuCtrl.cpp:77-86) while
  * keeping the context's device memory for reuse. */
 int px_reset(px_ctx *ctx);
+
+/* Give cached free device memory back to the driver until at most keep_bytes stay cached
+ * (wholly free 1 GiB heap slabs; live data is never moved). */
+int px_trim(px_ctx *ctx, uint64_t keep_bytes);
 
 /* HIP stream the context runs on (a hipStream_t), for callers that order their
  * own work against it. */

@@ -26,7 +26,7 @@ STATUS = {
     0: "PX_OK", 1: "PX_EINVAL", 2: "PX_ECAPACITY", 3: "PX_EREFCRASH", 4: "PX_ECORRUPT",
     5: "PX_EHANG", 6: "PX_EDEPTH", 7: "PX_ESPACE", 8: "PX_ENOTFOUND", 9: "PX_EHIP", 10: "PX_ENOMEM",
 }
-PX_OK, PX_EINVAL, PX_ESPACE, PX_ENOTFOUND = 0, 1, 7, 8
+PX_OK, PX_EINVAL, PX_ESPACE, PX_ENOTFOUND, PX_EHIP, PX_ENOMEM = 0, 1, 7, 8, 9, 10
 PX_PENDING = 0xFFFFFFFF  # px_set_result chunk / idx / comp_len of a record in the write-behind queue
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -74,7 +74,8 @@ class PxStats(C.Structure):
                 ("last_psa_rotations", C.c_uint64), ("last_psa_pool_ms", C.c_double),
                 ("device_live_bytes", C.c_uint64), ("device_peak_bytes", C.c_uint64),
                 ("deferred_records", C.c_uint64), ("deferred_flushes", C.c_uint64),
-                ("deferred_mismatch", C.c_uint64), ("last_get_device_keys", C.c_uint64)]
+                ("deferred_mismatch", C.c_uint64), ("last_get_device_keys", C.c_uint64),
+                ("last_set_peak_bytes", C.c_uint64)]
 
 
 SET_RESULT_DTYPE = np.dtype([("status", "<u4"), ("replaced", "<u4"), ("shard", "<u4"), ("chunk", "<u4"),
@@ -85,7 +86,7 @@ REC_DTYPE = np.dtype([("shard", "<u4"), ("chunk", "<u4"), ("idx", "<u4"), ("from
 EXPORTS = ["px_open", "px_close", "px_strerror", "px_set_batch", "px_get_batch", "px_parse_batch",
            "px_contains_batch", "px_del_batch", "px_export", "px_stats_get", "px_stream", "px_reset",
            "px_last_store", "px_import_chunk", "px_iter", "px_save", "px_load", "px_locate_batch", "px_reinsert",
-           "px_set_docs", "px_flush"]
+           "px_set_docs", "px_flush", "px_trim"]
 
 _LIB = None
 
@@ -124,6 +125,7 @@ def load_library() -> C.CDLL:
     lib.px_reinsert.argtypes = [vp, u32, u32]
     lib.px_set_docs.argtypes = [vp, u32, vp, vp, i32, i32, vp]
     lib.px_flush.argtypes = [vp, vp]
+    lib.px_trim.argtypes = [vp, u64]
     _LIB = lib
     return lib
 
@@ -151,7 +153,7 @@ class Store:
                  decode_waves: int = 0, host_threads: int = 0, defer_bytes: int = 0, retain_mb: int = 0):
         """defer_bytes > 0 (records_per_shard == 0 only): host set_batch calls go through the
         write-behind queue (px_flush); retain_mb: cached free device memory kept after a set
-        batch (0: 8 GiB, 0xFFFFFFFF: all)."""
+        batch (0: what the batch needed at its peak, 0xFFFFFFFF: all; see trim())."""
         self._lib = load_library()
         opts = PxOpts(device, records_per_shard, decode_depth, decode_waves, host_threads, defer_bytes, retain_mb)
         h = self._lib.px_open(C.byref(opts))
@@ -175,6 +177,12 @@ class Store:
 
     def __exit__(self, *a):
         self.close()
+
+    def trim(self, keep_bytes: int = 0) -> None:
+        """Give cached free device memory back to the driver (px_trim)."""
+        rc = self._lib.px_trim(self._h, int(keep_bytes))
+        if rc != PX_OK:
+            raise PxError(rc, "px_trim")
 
     @property
     def stream(self) -> int:

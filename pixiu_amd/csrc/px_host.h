@@ -63,6 +63,8 @@ class BlockHeap {
             sz = n;
         }
         live_[p] = sz;
+        live_total_ += sz;
+        live_peak_ = std::max(live_peak_, live_total_);
         return p;
     }
     void release(void *v) {
@@ -72,6 +74,7 @@ class BlockHeap {
         if (lv == live_.end()) return;
         uint64_t sz = lv->second;
         live_.erase(lv);
+        live_total_ -= sz;
         auto slab = std::prev(slabs_.upper_bound(p));  // the slab holding p
         // merge with the free block right after and right before, inside the slab
         auto nx = by_addr_.find(p + sz);
@@ -121,11 +124,10 @@ class BlockHeap {
         for (const auto &b : by_addr_) f += b.second;
         return f;
     }
-    uint64_t live_bytes() const {
-        uint64_t f = 0;
-        for (const auto &b : live_) f += b.second;
-        return f;
-    }
+    uint64_t live_bytes() const { return live_total_; }
+    // the most bytes live at once since the last mark_peak() (a set batch's scratch peak)
+    uint64_t live_peak() const { return live_peak_; }
+    void mark_peak() { live_peak_ = live_total_; }
 
   private:
     void add_free(char *p, uint64_t sz) {
@@ -146,6 +148,7 @@ class BlockHeap {
     std::multimap<uint64_t, char *> by_size_;
     std::unordered_map<void *, uint64_t> live_;
     uint64_t held_ = 0, peak_ = 0;
+    uint64_t live_total_ = 0, live_peak_ = 0;
 };
 
 // ---------------------------------------------------------------- key maps

@@ -465,6 +465,7 @@ struct px_ctx {
         uint32_t tab_cap = 0;     // slots, a power of two >= 2 x records
         uint32_t *err = nullptr;  // device word: an insert gave up (cannot happen)
         std::vector<uint32_t> kills;  // ids killed (replace / delete) since the last commit
+        uint32_t miss_streak = 0, skipped = 0;  // getitem batches in a row the index could not answer
         std::mutex mu;
     } dki;
     static bool dki_enabled() {  // PX_DKI=0: every getitem resolves its keys on the host
@@ -485,6 +486,7 @@ struct px_ctx {
         dki.err = nullptr;
         dki.rec_cap = dki.keys_cap = dki.keys_len = 0;
         dki.tab_cap = dki.nrec = 0;
+        dki.miss_streak = 0;
         dki.kills.clear();
         for (auto &c : chunks) c.gid.clear();
     }
@@ -504,10 +506,17 @@ struct px_ctx {
     DevBuf dk_qbuf, dk_obuf;
     HostBuf dk_hbuf, dk_hres;
 
-    // cached free device memory kept after a set batch (opts.retain_mb)
+    // cached free device memory kept after a set batch (opts.retain_mb).  0 (the default):
+    // what the batch itself needed at its peak beyond what stays live, so a workload of
+    // similar batches never hands memory back to the driver and maps it again (round 4
+    // freed ~25 GB after every config-3 batch and re-allocated it inside the next one);
+    // memory beyond that (a batch larger than the ones after it) goes back.  px_trim()
+    // returns cached memory on request.
     void trim_heap() {
-        const uint64_t keep = opts.retain_mb == 0xffffffffu ? ~0ull
-                              : (uint64_t)(opts.retain_mb ? opts.retain_mb : 8192u) << 20;
+        if (opts.retain_mb == 0xffffffffu) return;
+        const uint64_t live = heap.live_bytes();
+        const uint64_t keep = opts.retain_mb ? (uint64_t)opts.retain_mb << 20
+                                             : heap.live_peak() - std::min(heap.live_peak(), live);
         heap.trim(keep);
     }
 
@@ -1662,6 +1671,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
                 acc.last_psa_shards = std::max(acc.last_psa_shards, stats.last_psa_shards);
                 acc.last_walk_shards = std::max(acc.last_walk_shards, stats.last_walk_shards);
                 acc.last_psa_iters = std::max(acc.last_psa_iters, stats.last_psa_iters);
+                acc.last_set_peak_bytes = std::max(acc.last_set_peak_bytes, stats.last_set_peak_bytes);
                 a = b;
             }
             stats.last_set_stage_ms = acc.last_set_stage_ms;
@@ -1678,10 +1688,13 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             stats.last_psa_shards = acc.last_psa_shards;
             stats.last_walk_shards = acc.last_walk_shards;
             stats.last_psa_iters = acc.last_psa_iters;
+            stats.last_set_peak_bytes = acc.last_set_peak_bytes;
             return rc;
         }
     }
     PhaseClock phase("set_batch", "PX_SET_VERBOSE");
+    if (std::getenv("PX_DEBUG_SET_THROW")) throw std::bad_alloc();  // (test hook: a failing batch)
+    heap.mark_peak();  // (this batch's scratch peak: trim_heap keeps that much cached)
     phase.mark("inputs on device; raw keys also on host ");
     // ---- inputs on device; raw keys also on host (the CritBit needs them)
     std::vector<uint64_t> hkoff(n + 1), hvoff(n + 1);
@@ -2325,6 +2338,15 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     // ---- device key index: ids for this batch's live records, in record order (before the
     // CritBit inserts, whose replaces kill ids -- older ones and this batch's own)
     const bool dk = dki_enabled() && dki.valid && !raw_docs;
+    // ids are handed out here and written by dki_commit below: a batch that throws in
+    // between leaves ids with no entry, so the index is then off until the next reset
+    struct DkiTxn {
+        px_ctx *c;
+        bool done;
+        ~DkiTxn() {
+            if (!done) c->dki.valid = false;
+        }
+    } dk_txn{this, !dk};
     const uint32_t dk_gid0 = dki.nrec;
     std::vector<DkRec> dk_new;
     std::vector<uint32_t> dk_r;  // the batch record of each entry
@@ -2395,18 +2417,45 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     std::vector<uint32_t> replaced(n, 0);
     std::vector<std::pair<uint32_t, uint32_t>> moved;  // (record, older shard)
     if (opts.records_per_shard != 0) {
-        // key -> shard upserts, one key-map partition per task (keys in record order)
+        // key -> shard upserts, one key-map partition per task (keys in record order); the
+        // map holds raw keys: a ready doc's is its key prefix unescaped
+        std::vector<std::string> rawk;
+        if (raw_docs) {
+            rawk.resize(n);
+            for (uint32_t r = 0; r < n; ++r) {
+                if (!live[r]) continue;
+                const uint8_t *d = hkeys.data() + hkoff[r];
+                const uint32_t e = key_end(d, (uint32_t)(hkoff[r + 1] - hkoff[r]));
+                std::string &k = rawk[r];
+                for (uint32_t i = 0; i + 2 < e; ++i) {  // (e - 2: the 251,0 terminator)
+                    k.push_back((char)d[i]);
+                    if (d[i] == kEsc) ++i;  // 251,251 -> 251
+                }
+            }
+        }
+        auto raw_key = [&](uint32_t r, uint64_t *len) -> const uint8_t * {
+            if (raw_docs) {
+                *len = rawk[r].size();
+                return reinterpret_cast<const uint8_t *>(rawk[r].data());
+            }
+            *len = hkoff[r + 1] - hkoff[r];
+            return hkeys.data() + hkoff[r];
+        };
         std::vector<uint8_t> part(n);
         for (uint32_t r = 0; r < n; ++r)
-            if (live[r]) part[r] = (uint8_t)PartKeyMap::part_of(hkeys.data() + hkoff[r], hkoff[r + 1] - hkoff[r]);
+            if (live[r]) {
+                uint64_t kl;
+                const uint8_t *kp = raw_key(r, &kl);
+                part[r] = (uint8_t)PartKeyMap::part_of(kp, kl);
+            }
         std::vector<std::vector<std::pair<uint32_t, uint32_t>>> mv(PartKeyMap::kParts);
         const std::function<void(uint32_t)> job = [&](uint32_t pi) {
             KeyMap &m = keymap.part(pi);
             m.reserve(n / PartKeyMap::kParts + 64);
             for (uint32_t r = 0; r < n; ++r) {
                 if (!live[r] || part[r] != pi) continue;
-                const uint8_t *kp = hkeys.data() + hkoff[r];
-                const uint64_t klen = hkoff[r + 1] - hkoff[r];
+                uint64_t klen;
+                const uint8_t *kp = raw_key(r, &klen);
                 const int64_t prev = m.upsert(kp, klen, rec_shard[r], rgchunk[r], ridx[r]);
                 if (prev >= 0 && (uint32_t)prev != rec_shard[r]) mv[pi].emplace_back(r, (uint32_t)prev);
             }
@@ -2443,7 +2492,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     }
     for (const auto &mv : moved) {  // cross-shard replace
         const uint32_t r = mv.first;
-        cbt_delete(*shards[mv.second], esc_key(hkeys.data() + hkoff[r], hkoff[r + 1] - hkoff[r]));
+        cbt_delete(*shards[mv.second], crit_key(hkeys.data() + hkoff[r], hkoff[r + 1] - hkoff[r]));
         replaced[r] = 1;
     }
 
@@ -2460,6 +2509,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     } else if (dki.nrec) {
         dki_clear();
     }
+    dk_txn.done = true;
 
     for (auto &b : deferred_release) heap.release(b.first, b.second);
     deferred_release.clear();
@@ -2472,6 +2522,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     uint64_t ub = 0;
     for (auto &sp : shards) ub += sp->hs.ub_reads;
     stats.ub_reads = ub;
+    stats.last_set_peak_bytes = heap.live_peak() + arena.mapped;
     trim_heap();
     stats.device_bytes = heap.held() + arena.mapped;
     for (uint32_t r = 0; r < n; ++r) {
@@ -2667,8 +2718,11 @@ void px_ctx::reinsert_chunk(Shard &s, uint32_t c, bool via_glob) {
         pos = end;
     }
     raw_docs = saved;
-    // PiXiuChunk_free: the chunk's records are gone
+    // PiXiuChunk_free: the chunk's records are gone (and out of the device key index: a record
+    // whose re-set CritBit insert was skipped would otherwise still be answered from here)
     Chunk &ch = chunks[c];
+    for (uint32_t i = 0; i < ch.n && i < ch.gid.size(); ++i)
+        if (!ch.dead[i] && ch.gid[i] != kNone) dki.kills.push_back(ch.gid[i]);
     std::fill(ch.dead.begin(), ch.dead.end(), (uint8_t)1);
     ch.used = 0;
     s.glob = via_glob ? -1 : curr;
@@ -2805,7 +2859,24 @@ int px_ctx::flush_queue() {
     pred.swap(dq_pred);
     drop_queue();
     stats.deferred_flushes++;
-    const int rc = set_ctrl(n, k.data(), ko.data(), v.empty() ? &dummy : v.data(), vo.data(), 0, r.data());
+    int rc;
+    try {
+        rc = set_ctrl(n, k.data(), ko.data(), v.empty() ? &dummy : v.data(), vo.data(), 0, r.data());
+    } catch (...) {
+        // the queued records are gone with the failed batch: the caller that triggered the
+        // flush gets the error from PX_GUARD, and px_flush reports it afterwards too
+        int code = PX_EHIP;
+        try {
+            throw;
+        } catch (const PxFail &f) {
+            code = f.code;
+        } catch (const std::bad_alloc &) {
+            code = PX_ENOMEM;
+        } catch (...) {
+        }
+        if (dq_rc == PX_OK) dq_rc = code;
+        throw;
+    }
     uint64_t mism = 0;
     for (uint32_t i = 0; i < n; ++i) mism += r[i].status == PX_OK && r[i].replaced != pred[i];
     if (mism) {
@@ -2822,6 +2893,7 @@ int px_ctx::flush_queue() {
 void px_ctx::dki_commit(uint32_t gid0, const std::vector<DkRec> &recs, const std::vector<uint8_t> &kb) {
     const uint32_t nn = (uint32_t)recs.size();
     if (!nn) return;
+    dki.miss_streak = 0;
     if (!dki.err) {
         dki.err = (uint32_t *)heap.alloc(256);
         hcheck(hipMemsetAsync(dki.err, 0, 256, stream));
@@ -2871,6 +2943,9 @@ void px_ctx::dki_commit(uint32_t gid0, const std::vector<DkRec> &recs, const std
 int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int mode, uint8_t *out, uint64_t out_cap,
                     int out_on_device, uint64_t *out_off, uint32_t *out_len, uint32_t *status, uint64_t *needed) {
     if (!dki_enabled() || !dki.valid || !dki.tab || !n || !spans_enabled()) return -1;
+    // a store whose batches keep missing (8 in a row: records the index does not hold, e.g. reinserted or
+    // set as ready docs) tries it only every 16th batch until a set batch adds records
+    if (dki.miss_streak >= 8 && (++dki.skipped & 15)) return -1;
     PhaseClock phase("dki_get", "PX_GET_VERBOSE");
     phase.mark("kills, scratch, keys to pinned");
     dki_apply_kills();  // (deletes since the last set batch)
@@ -2886,7 +2961,8 @@ int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int m
     // the tasks: at most one per 64 tiles, a tile per 16 bytes of the output that fits
     // (every query's tiles <= its cap / 16), so the launch can go before the totals are known
     // (a host buffer: device staging up to 4 GiB; a batch past it goes the host path)
-    const uint64_t cap_fit = out_on_device ? out_cap : std::min<uint64_t>(out_cap, 4ull << 30);
+    // (output offsets travel as u32 counts of 16 bytes: below 64 GiB on the device too)
+    const uint64_t cap_fit = std::min<uint64_t>(out_cap, out_on_device ? (1ull << 36) - 16 : 4ull << 30);
     const uint64_t ntask_max = std::min<uint64_t>(cap_fit / 1024 + 2, 0xffffffffull);
     auto *b = (uint8_t *)dk_qbuf.get(o_task + gather_task_bytes((uint32_t)ntask_max));
     auto *dkeys = b;
@@ -2927,7 +3003,11 @@ int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int m
         return -1;
     }
     const uint64_t total = (uint64_t)hr[1] * 16;
-    if (hr[0] || total > cap_fit) return -1;  // (nothing was gathered: the host path answers)
+    if (hr[0] || total > cap_fit) {  // (nothing was gathered: the host path answers)
+        dki.miss_streak += hr[0] ? 1 : 0;
+        return -1;
+    }
+    dki.miss_streak = 0;
     if (!out_on_device && total) {
         d2h(out, dout, total);
         sync();  // (d2h may finish through pinned staging at the sync)
@@ -3694,6 +3774,16 @@ int px_stats_get(px_ctx *ctx, px_stats *st) {
         st->device_bytes = ctx->heap.held() + ctx->arena.mapped;
         st->device_live_bytes = ctx->heap.live_bytes() + ctx->arena.top;
         st->device_peak_bytes = ctx->heap.peak();
+        return PX_OK;
+    })
+}
+
+int px_trim(px_ctx *ctx, uint64_t keep_bytes) {
+    if (!ctx) return PX_EINVAL;
+    PX_GUARD({
+        ctx->sync();
+        ctx->heap.trim(keep_bytes);
+        ctx->stats.device_bytes = ctx->heap.held() + ctx->arena.mapped;
         return PX_OK;
     })
 }

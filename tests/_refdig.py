@@ -6,12 +6,14 @@ tests/golden/refdig_c{config}_r{rps}[_n{n}].npz holds, for every record of the c
 corpus part (synth.make(config); _n: its first n records only) stored in records_per_shard = rps shards (one
 reference PiXiuCtrl per shard, rps = 0: one over every record), in record order:
 
-  get_len, get_d32    length and digest32 of the reference's compat getitem drain
+  get_len, get_d64    length and digest64 of the reference's compat getitem drain
                       (PiXiuCtrl::getitem + PXSGen, PiXiuCtrl.cpp:59-61, PiXiuStr.h:129-198)
-  comp_len, comp_d32  length and digest32 of the record's compressed bytes
+  comp_len, comp_d64  length and digest64 of the record's compressed bytes
   chunk, idx          the chunk serial and chunk-local slot it landed in
 
-digest32(b) = the 4-byte BLAKE2b digest of b, little-endian.
+digest64(b) = the 8-byte BLAKE2b digest of b, little-endian (round 5; the round-4 fixtures held
+4-byte digests, get_d32 / comp_d32, which compare() still reads: a 2^-32 chance per record that
+a wrong record matches, ~2.6e-4 over the 1.13 M records, against 2^-64 now).
 """
 from __future__ import annotations
 
@@ -24,18 +26,36 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
+def digest(b, size: int = 8) -> int:
+    return int.from_bytes(hashlib.blake2b(b, digest_size=size).digest(), "little")
+
+
 def digest32(b) -> int:
-    return int.from_bytes(hashlib.blake2b(b, digest_size=4).digest(), "little")
+    return digest(b, 4)
 
 
-def digests(buf: np.ndarray, off, ln) -> np.ndarray:
-    """digest32 of buf[off[i] : off[i] + ln[i]] for every i (host buffer)."""
+def digest64(b) -> int:
+    return digest(b, 8)
+
+
+def width(ref) -> int:
+    """digest bytes a fixture holds: 8 (get_d64 / comp_d64) or 4 (round 4's get_d32 / comp_d32)"""
+    return 8 if "get_d64" in ref else 4
+
+
+def _dig(ref, kind):
+    return ref[f"{kind}_d64"] if "get_d64" in ref else ref[f"{kind}_d32"]
+
+
+def digests(buf: np.ndarray, off, ln, size: int = 8) -> np.ndarray:
+    """digest of buf[off[i] : off[i] + ln[i]] for every i (host buffer), `size` bytes."""
     mv = memoryview(np.ascontiguousarray(buf))
     off = np.asarray(off, np.int64).tolist()
     ln = np.asarray(ln, np.int64).tolist()
     h = hashlib.blake2b
-    return np.fromiter((int.from_bytes(h(mv[o:o + n], digest_size=4).digest(), "little")
-                        for o, n in zip(off, ln)), np.uint32, count=len(off))
+    dt = np.uint64 if size == 8 else np.uint32
+    return np.fromiter((int.from_bytes(h(mv[o:o + n], digest_size=size).digest(), "little")
+                        for o, n in zip(off, ln)), dt, count=len(off))
 
 
 def path(config: int, rps: int, n: int | None = None) -> str:
@@ -52,13 +72,15 @@ def load(config: int, rps: int, n: int | None = None):
         return {k: z[k] for k in z.files}
 
 
-def compare(ref, get_len, get_d32):
-    """Records whose compat getitem differs from the reference's (length or digest)."""
+def compare(ref, get_len, get_dig):
+    """Records whose compat getitem differs from the reference's (length or digest; get_dig
+    made with the fixture's width())."""
     get_len = np.asarray(get_len, np.int64)
-    get_d32 = np.asarray(get_d32, np.uint32)
+    want = _dig(ref, "get")
+    get_dig = np.asarray(get_dig, want.dtype)
     if len(get_len) != len(ref["get_len"]):
         raise ValueError(f"{len(get_len)} records, the reference digests hold {len(ref['get_len'])}")
-    bad = (get_len != ref["get_len"].astype(np.int64)) | (get_d32 != ref["get_d32"])
+    bad = (get_len != ref["get_len"].astype(np.int64)) | (get_dig != want)
     return int(bad.sum()), np.nonzero(bad)[0]
 
 
@@ -96,12 +118,13 @@ def check_store(ref, st, res, out, off, ln):
     n = len(ln)
     end = int((off + ln).max()) if n else 0
     host = out[:end].cpu().numpy() if hasattr(out, "cpu") else np.asarray(out)[:end]
-    bad_get, idx = compare(ref, ln, digests(host, off, ln))
+    w = width(ref)
+    bad_get, idx = compare(ref, ln, digests(host, off, ln, w))
     comp = st.export(px.records_of(res))
     cl = np.fromiter((len(c) for c in comp), np.int64, count=n)
-    cd = np.fromiter((digest32(c) for c in comp), np.uint32, count=n)
-    bad_comp = int(((cl != ref["comp_len"].astype(np.int64)) | (cd != ref["comp_d32"])).sum())
+    cd = np.fromiter((digest(c, w) for c in comp), np.uint64 if w == 8 else np.uint32, count=n)
+    bad_comp = int(((cl != ref["comp_len"].astype(np.int64)) | (cd != _dig(ref, "comp"))).sum())
     bad_place = int(((np.asarray(res["chunk"], np.int64) != ref["chunk"].astype(np.int64))
                      | (np.asarray(res["idx"], np.int64) != ref["idx"].astype(np.int64))).sum())
     return {"records": n, "compat_ne_reference": bad_get, "comp_ne_reference": bad_comp,
-            "placement_ne_reference": bad_place, "first_bad": [int(i) for i in idx[:5]]}
+            "placement_ne_reference": bad_place, "first_bad": [int(i) for i in idx[:5]], "digest_bits": 8 * w}

@@ -1,6 +1,7 @@
 // Client code written against the reference's PiXiuCtrl API (README.md:121-150,
 // main.cpp:40-75), compiled unchanged against include/PiXiuCtrl.h.
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -243,6 +244,17 @@ int main() {
         PXSGen_free(rg);
         CHECK(rgot == doc);
         CHECK(ctrl.setitem(NULL, 0, (uint8_t *)"x", 1) < 0);  // (the reference asserts k_len)
+
+        // a queued record whose store fails is reported, not lost silently (PX_DEBUG_SET_THROW:
+        // the batch throws bad_alloc inside the flush a read triggers)
+        CHECK(ctrl.setitem((uint8_t *)"FAILKEY", 7, (uint8_t *)"v", 1) == 0);
+        setenv("PX_DEBUG_SET_THROW", "1", 1);
+        CHECK(!ctrl.contains((uint8_t *)"FAILKEY", 7));
+        unsetenv("PX_DEBUG_SET_THROW");
+        CHECK(ctrl.flush() == PX_ENOMEM);
+        CHECK(ctrl.flush() == PX_OK);
+        CHECK(ctrl.setitem((uint8_t *)"FAILKEY", 7, (uint8_t *)"v", 1) == 0);
+        CHECK(ctrl.flush() == PX_OK && ctrl.contains((uint8_t *)"FAILKEY", 7));
 
         // a generator that outlives free_prop yields nothing and says why
         PXSGen *late = ctrl.getitem((uint8_t *)"RAWKEY", 6);

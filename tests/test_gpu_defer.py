@@ -81,3 +81,26 @@ def test_defer_slot_rotation_matches_oracle(store_factory, oracle):
     assert (st == 0).all()
     assert recs["chunk"].tolist() == ref["chunk"] and recs["idx"].tolist() == ref["idx"]
     assert a.export(recs[::97]) == ref["comp"][::97]
+
+
+def test_failed_flush_is_reported(store_factory, monkeypatch):
+    """A queued record whose flush fails (here: PX_DEBUG_SET_THROW makes the batch throw
+    bad_alloc) is not silently lost: the read that triggered the flush fails, and a later
+    px_flush still reports the failure once (flush_queue emptied the queue
+    before the store and dropped the error)."""
+    st = store_factory(records_per_shard=0, defer_bytes=1 << 20)
+    r = st.set_batch([b"k/1"], [b"v" * 100])
+    assert int(r["status"][0]) == 0 and int(r["chunk"][0]) == px.PX_PENDING
+    monkeypatch.setenv("PX_DEBUG_SET_THROW", "1")
+    with pytest.raises(px.PxError) as e:  # a read flushes first: the batch fails
+        st.contains([b"k/1"])
+    assert e.value.code == px.PX_ENOMEM
+    monkeypatch.delenv("PX_DEBUG_SET_THROW")
+    with pytest.raises(px.PxError) as e:  # ... and px_flush reports it afterwards
+        st.flush()
+    assert e.value.code == px.PX_ENOMEM
+    st.flush()  # reported once
+    assert not st.contains([b"k/1"])[0]
+    # the store keeps working
+    st.set_batch([b"k/2"], [b"w" * 50])
+    assert st.get_batch([b"k/2"])[0] is not None

@@ -138,3 +138,33 @@ def test_pieces_keep_span_tables(store_factory):
         h = hash(got.tobytes())
         first = h if first is None else first
         assert h == first
+
+
+@pytest.mark.parametrize("rps", [0, 64])
+def test_after_set_docs(store_factory, oracle, rps):
+    """Records stored as ready docs (px_set_docs) have no device-index entry; they replace
+    indexed records, so batches holding their keys go to the host path, batches of other keys
+    stay on the device, and every answer equals the oracle fed the same records as setitem
+    (a ready doc equal to assemble(k, v) stores what setitem(k, v) stores)."""
+    import _oracle
+    ks, vs = _ops(seed=11, n=600, keyspace=400)
+    st = store_factory(records_per_shard=rps)
+    st.set_batch(ks[:500], vs[:500])
+    st.set_docs([_oracle.assemble(k, v) for k, v in zip(ks[500:], vs[500:])])
+    # shards of rps records, each its own oracle instance; a key answers from the shard of
+    # its newest copy (later shards win)
+    step = rps or 600
+    shards = []
+    for s0 in range(0, 600, step):
+        sh = oracle.new()
+        for k, v in zip(ks[s0:s0 + step], vs[s0:s0 + step]):
+            sh.set(k, v)
+        shards.append(sh)
+    newest = {k: i for i, k in enumerate(ks)}
+    live = sorted(newest)
+    want = {k: shards[newest[k] // step].get(k) for k in live}
+    assert st.get_batch(live) == [want[k] for k in live]
+    assert st.stats()["last_get_device_keys"] == 0  # (ready-doc keys: the host path)
+    only_old = [k for k in live if k not in set(ks[500:])]
+    assert st.get_batch(only_old) == [want[k] for k in only_old]
+    assert st.stats()["last_get_device_keys"] == len(only_old)

@@ -21,11 +21,13 @@ def test_oracle_reproduces_reference_digest_prefix(cfg, rps, oracle):
     k = LEAD[cfg]
     cp = synth.make(cfg)  # (the full corpus: a generator's draws depend on its record count)
     r = oracle.run([cp.key(i) for i in range(k)], [cp.val(i) for i in range(k)])
-    d = _refdig.digest32
+    w = _refdig.width(ref)
+    d = lambda b: _refdig.digest(b, w)  # noqa: E731
+    dk = "d64" if w == 8 else "d32"
     assert [len(g) for g in r["get"]] == ref["get_len"][:k].tolist()
-    assert [d(g) for g in r["get"]] == ref["get_d32"][:k].tolist()
+    assert [d(g) for g in r["get"]] == ref[f"get_{dk}"][:k].tolist()
     assert [len(c) for c in r["comp"]] == ref["comp_len"][:k].tolist()
-    assert [d(c) for c in r["comp"]] == ref["comp_d32"][:k].tolist()
+    assert [d(c) for c in r["comp"]] == ref[f"comp_{dk}"][:k].tolist()
     assert r["chunk"] == ref["chunk"][:k].tolist() and r["idx"] == ref["idx"][:k].tolist()
 
 
@@ -35,7 +37,8 @@ def test_fixture_shapes():
         if ref is None:
             continue
         n = int(ref["n"])
-        for f in ("get_len", "get_d32", "comp_len", "comp_d32", "chunk", "idx"):
+        dk = "d64" if _refdig.width(ref) == 8 else "d32"
+        for f in ("get_len", f"get_{dk}", "comp_len", f"comp_{dk}", "chunk", "idx"):
             assert ref[f].shape == (n,), (cfg, rps, f)
-        assert ref["get_d32"].dtype == np.uint32
+        assert ref[f"get_{dk}"].dtype == (np.uint64 if dk == "d64" else np.uint32)
         assert b"Reference" in ref["generator"].tobytes()

@@ -50,9 +50,9 @@ def _shard(job):
     vals = [cp.val(i) for i in range(a, a + cnt)]
     t = time.time()
     r = _REF.run(keys, vals, do_get=True)
-    d = _refdig.digest32
-    return (cfg, rps, a, np.array([len(g) for g in r["get"]], np.uint32), np.array([d(g) for g in r["get"]], np.uint32),
-            np.array([len(c) for c in r["comp"]], np.uint32), np.array([d(c) for c in r["comp"]], np.uint32),
+    d = _refdig.digest64
+    return (cfg, rps, a, np.array([len(g) for g in r["get"]], np.uint32), np.array([d(g) for g in r["get"]], np.uint64),
+            np.array([len(c) for c in r["comp"]], np.uint32), np.array([d(c) for c in r["comp"]], np.uint64),
             np.array(r["chunk"], np.uint32), np.array(r["idx"], np.uint32), time.time() - t)
 
 
@@ -92,8 +92,8 @@ def main():
                 cp = _CORPUS[cfg]
                 h = hashlib.sha256(cp.keys.tobytes() + cp.vals.tobytes()).hexdigest()  # (the full corpus)
                 np.savez_compressed(_refdig.path(cfg, rps, lim), config=np.int64(cfg), rps=np.int64(rps),
-                                    n=np.int64(n), get_len=cols[0], get_d32=cols[1], comp_len=cols[2],
-                                    comp_d32=cols[3], chunk=cols[4], idx=cols[5],
+                                    n=np.int64(n), get_len=cols[0], get_d64=cols[1], comp_len=cols[2],
+                                    comp_d64=cols[3], chunk=cols[4], idx=cols[5],
                                     input_sha256=np.frombuffer(h.encode(), np.uint8),
                                     generator=np.frombuffer(b"Reference (oracle/_ref/libpxref.so)", np.uint8),
                                     reference_seconds=np.float64(secs[(cfg, rps)]))
