@@ -233,10 +233,16 @@ class Store:
         return res
 
     # ------------------------------------------------------------ getitem
-    def _expand(self, fn, n, args, out_dev_ptr, out_cap):
-        off = np.zeros(max(n, 1), np.uint64)
-        ln = np.zeros(max(n, 1), np.uint32)
-        st = np.zeros(max(n, 1), np.uint32)
+    def _expand(self, fn, n, args, out_dev_ptr, out_cap, into=None):
+        if into is not None:  # caller-owned (offsets u64, lengths u32, statuses u32) of >= n entries
+            off, ln, st = into
+            if len(off) < n or len(ln) < n or len(st) < n or off.dtype != np.uint64 or ln.dtype != np.uint32 \
+                    or st.dtype != np.uint32 or not all(a.flags.c_contiguous for a in (off, ln, st)):
+                raise ValueError("into: C-contiguous uint64 / uint32 / uint32 arrays of >= n entries")
+        else:
+            off = np.zeros(max(n, 1), np.uint64)
+            ln = np.zeros(max(n, 1), np.uint32)
+            st = np.zeros(max(n, 1), np.uint32)
         need = np.zeros(1, np.uint64)
         if out_dev_ptr is not None:
             rc = fn(self._h, n, *args, out_dev_ptr, out_cap, 1, _ptr(off), _ptr(ln), _ptr(st), _ptr(need))
@@ -265,12 +271,14 @@ class Store:
                 res.append(out[int(off[i]):int(off[i]) + int(ln[i])].tobytes())
         return res
 
-    def get_batch_device(self, keys, out_ptr: int, out_cap: int, mode: int = COMPAT):
-        """Expand into a device buffer; returns (rc, offsets, lengths, statuses, needed)."""
+    def get_batch_device(self, keys, out_ptr: int, out_cap: int, mode: int = COMPAT, into=None):
+        """Expand into a device buffer; returns (rc, offsets, lengths, statuses, needed).
+        into: optional (offsets, lengths, statuses) host arrays to fill (reused by a caller that
+        repeats batches: fresh result arrays cost a page fault per 4 KB on first write)."""
         kb, ko = keys if isinstance(keys, tuple) else csr(keys)
         n = len(ko) - 1
         rc, _, off, ln, st, need = self._expand(self._lib.px_get_batch, n, (_ptr(kb), _ptr(ko), mode),
-                                                out_ptr, out_cap)
+                                                out_ptr, out_cap, into)
         return rc, off, ln, st, need
 
     def get_batch_host(self, keys, out: np.ndarray, mode: int = COMPAT):

@@ -1244,11 +1244,13 @@ __global__ void __launch_bounds__(256) k_tokenize(uint32_t n, const RecSlot *slo
             pend_w = w;
             have = true;
         };
-        // two aligned 64-byte windows, [wb, wb + 64) in b and the next one in bn: a token
-        // starting in the first is wholly inside the pair, and the next window's load is
-        // issued a whole window ahead (its wait does not drain this window's stores)
+        // aligned 64-byte windows, [wb, wb + 64) in b and the next ones in bn, b2, b3: a token
+        // starting in the first is wholly inside the first two, and each window's load is
+        // issued three windows ahead (a window is consumed faster than one load's latency)
         uint32_t b = lane < len ? comp[lane] : 0;
         uint32_t bn = 64 + lane < len ? comp[64 + lane] : 0;
+        uint32_t b2 = 128 + lane < len ? comp[128 + lane] : 0;
+        uint32_t b3 = 192 + lane < len ? comp[192 + lane] : 0;
         auto byte_at = [&](uint32_t q) -> uint32_t {  // q < wb + 128
             const uint32_t d = q - wb;
             const uint32_t r0 = readlane(b, d & 63u), r1 = readlane(bn, d & 63u);
@@ -1258,7 +1260,9 @@ __global__ void __launch_bounds__(256) k_tokenize(uint32_t n, const RecSlot *slo
             while (p >= wb + 64) {
                 wb += 64;
                 b = bn;
-                bn = wb + 64 + lane < len ? comp[wb + 64 + lane] : 0;
+                bn = b2;
+                b2 = b3;
+                b3 = wb + 192 + lane < len ? comp[wb + 192 + lane] : 0;
             }
             if (!plain_open) {
                 plain_open = true;
@@ -2673,6 +2677,28 @@ hipError_t launch_slot_place(hipStream_t s, uint32_t n, const RecSlot *src, cons
     k_slot_place<<<(n + 255) / 256, 256, 0, s>>>(n, src, tok, d, jobs);
     return hipGetLastError();
 }
+// A record decoded in pieces (the exact span build: exact parses of consecutive ranges are
+// the consecutive slices of the doc): its length = the pieces' sum, its status = the first
+// failing piece's.  first[k] .. first[k + 1] are record k's pieces.
+__global__ void __launch_bounds__(256) k_span_agg(uint32_t n, const uint32_t *first, const uint32_t *pl,
+                                                  const uint32_t *ps, uint32_t *dl, uint32_t *ds) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    uint32_t len = 0, st = kOk;
+    for (uint32_t j = first[k]; j < first[k + 1]; ++j) {
+        len += pl[j];
+        if (st == kOk) st = ps[j];
+    }
+    dl[k] = len;
+    ds[k] = st;
+}
+hipError_t launch_span_agg(hipStream_t s, uint32_t n, const uint32_t *first, const uint32_t *pl, const uint32_t *ps,
+                           uint32_t *dl, uint32_t *ds) {
+    if (!n) return hipSuccess;
+    k_span_agg<<<(n + 255) / 256, 256, 0, s>>>(n, first, pl, ps, dl, ds);
+    return hipGetLastError();
+}
+
 hipError_t launch_span_jobs(hipStream_t s, uint32_t n, const DecodeQuery *dq, const uint32_t *dl, const uint32_t *ds,
                             const SpanSrc *src, const RecSlot *const *chunk_slots, const int32_t *addr, uint32_t *cnt,
                             uint32_t *ents, uint32_t *tiles, const uint32_t *eoff_incl, const uint32_t *toff_incl,

@@ -84,9 +84,9 @@ __global__ void __launch_bounds__(256) k_psa_gather(uint32_t ndocs, const PsaDoc
 __global__ void __launch_bounds__(256) k_psa_head0(uint32_t N, const uint64_t *keys, uint32_t *hflag) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= N) return;
-    const uint64_t k = keys[r];
+    const uint64_t k = keys[r] & kKeyMask;
     const bool complete = (k & 511u) == 0;
-    hflag[r] = (r == 0 || k != keys[r - 1] || complete) ? r : 0u;
+    hflag[r] = (r == 0 || k != (keys[r - 1] & kKeyMask) || complete) ? r : 0u;
 }
 
 // ---------------------------------------------------------------- unsorted groups
@@ -114,6 +114,164 @@ struct LongLists {
 PSA_DEV uint32_t long_class(uint32_t size) {
     return size <= 128 ? 0u : size <= 256 ? 1u : size <= kRegMax ? 2u : size <= kMedMax ? 3u : 4u;
 }
+
+// ---------------------------------------------------------------- retired groups
+// A group G (slots [g, g + size)) whose members all keep one key K at a step with offset h
+// -- every suffix h further on lies in the group G' that starts at slot t = K - 1 -- and
+// whose G' has exactly |G| members is a shifted copy of G': the map p -> p + h is a
+// bijection G -> G', the members share their first h symbols and none ends inside them, so
+// G's final order is G''s, shifted by h (equal suffixes stay in position order too).  Such a
+// group leaves the doubling at once instead of being re-keyed at every later step until its
+// copies diverge (the templates every page of a shard repeats: ~80 M suffixes for 8 steps on
+// config 3).  Its members' ranks name its entry (id | kRetired).  An entry links G to the
+// slot range [T, T + size) that holds its members shifted by D (at first T = t, D = h); a
+// rank read that hits a member q is answered through the link: g + (rank(q + D) - T) -- G
+// mirrors the current partition of the range, so these ranks refine the current level and
+// order the suffixes as the true ranks do, which is all a doubling key needs -- and so on
+// through any retired group there.  When one retired group covers a link's range exactly
+// (the same-step chains of a template's offsets), the link can take that group's own link
+// instead (path compression while reading; pointer jumping over all entries at the end).
+// After the doubling every retired member's rank read through its links is its final slot.
+// (tools/proto/retire_proto.py is the CPU prototype, checked against a naive suffix sort.)
+constexpr uint32_t kRetired = 1u << 31;  // (ranks are slot indices < 2^31)
+constexpr uint32_t kMaxHops = 1u << 20;  // link hops of one rank read (cannot be reached: positions rise every hop)
+// Entries are handed out from kRetShards counters, each on a line of its own and owning
+// `per` consecutive ids (one counter for the whole launch serialised every retiring wave on
+// one address: k_dbl_win went from 3 to 29 ms a step)
+constexpr uint32_t kRetShards = 64, kRetStride = 32;
+struct RetList {
+    uint4 *ent;               // g, size, q0 (a member's position), first shift
+    unsigned long long *lnk;  // T | D << 32 (64-bit atomic: read and shortened concurrently)
+    uint32_t *cnt;            // [1] a link led out of range (cannot happen), [2] links changed
+    uint32_t *sc;             // entries handed out per shard (stride kRetStride)
+    uint32_t per, cap, n;     // ids per shard, kRetShards * per, text positions (every link target is checked against n)
+};
+// `k` consecutive ids from shard `shard` (wave-wide: lane `leader` asks); ids past the
+// shard's end are >= the returned limit and must not be used
+PSA_DEV uint32_t ret_alloc(const RetList &R, uint32_t shard, uint32_t k, uint32_t leader, uint32_t *lim) {
+    shard &= kRetShards - 1u;
+    uint32_t base = 0;
+    if (lane_id() == leader) base = atomicAdd(R.sc + shard * kRetStride, k);
+    base = (uint32_t)__shfl((int)base, (int)leader);
+    *lim = shard * R.per + R.per;
+    return shard * R.per + min(base, R.per);
+}
+// is id a handed-out entry?
+PSA_DEV bool ret_used(const RetList &R, uint32_t id) {
+    const uint32_t sh = id / R.per;
+    return id - sh * R.per < min(__hip_atomic_load(R.sc + sh * kRetStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), R.per);
+}
+PSA_DEV uint64_t lnk_load(const unsigned long long *l, uint32_t id) {
+    return __hip_atomic_load(l + id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+PSA_DEV void lnk_store(unsigned long long *l, uint32_t id, uint32_t T, uint32_t D) {
+    __hip_atomic_store(l + id, (unsigned long long)D << 32 | T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the rank of suffix q whose stored rank r names a retired group (see above); links followed
+// through exactly covering groups are stored back shortened
+PSA_DEV uint32_t live_rank(const RetList &R, const uint32_t *rank, uint32_t q, uint32_t r) {
+    uint32_t acc = 0, hops = 0;
+    while (r & kRetired) {
+        const uint32_t id = r & ~kRetired;
+        const uint4 e = R.ent[id];
+        const uint64_t l = lnk_load(R.lnk, id);
+        uint32_t T = (uint32_t)l, D = (uint32_t)(l >> 32);
+        if (q + D >= R.n) {
+            atomicOr(R.cnt + 1, 1u);
+            return 0;
+        }
+        uint32_t x = rank[q + D];
+        bool shorter = false;
+        while (x & kRetired) {  // the range is one retired group: its own link
+            const uint32_t id2 = x & ~kRetired;
+            const uint4 e2 = R.ent[id2];
+            if (e2.x != T || e2.y != e.y) break;
+            const uint64_t l2 = lnk_load(R.lnk, id2);
+            if (q + D + (uint32_t)(l2 >> 32) >= R.n) break;
+            T = (uint32_t)l2;
+            D += (uint32_t)(l2 >> 32);
+            x = rank[q + D];
+            shorter = true;
+            if (++hops > kMaxHops) break;
+        }
+        if (shorter) lnk_store(R.lnk, id, T, D);
+        acc += e.x - T;
+        q += D;
+        r = x;
+        if (++hops > kMaxHops) {
+            atomicOr(R.cnt + 1, 1u);
+            return 0;
+        }
+    }
+    return acc + r;
+}
+// may group [g, g + size) with the one key K (>= 1) retire this step (the tag's step)?  Reads
+// the target's size word while other waves may rewrite it: only an unrewritten word (the
+// step's own tag) is taken; a target that retires or splits meanwhile is still a valid link
+PSA_DEV bool retire_ok(const RetList &R, uint32_t g, uint32_t size, uint32_t K, uint32_t tag, const uint32_t *gsz) {
+    if (!R.ent || K == 0 || K - 1 == g) return false;
+    const uint32_t x = __hip_atomic_load(gsz + (K - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (x & kTag) == tag && (x & kSizeMask) == size;
+}
+PSA_DEV void retire_put(const RetList &R, uint32_t id, uint32_t g, uint32_t size, uint32_t q0, uint32_t K, uint32_t h) {
+    R.ent[id] = make_uint4(g, size, q0, h);
+    lnk_store(R.lnk, id, K - 1, h);
+}
+// pointer jumping over every entry's link (after the doubling): a link whose range one
+// retired group covers exactly takes that group's link (read from src, written to dst);
+// cnt[2] counts the links that changed
+__global__ void __launch_bounds__(256) k_ret_jump(RetList R, const unsigned long long *src, unsigned long long *dst,
+                                                  const uint32_t *rank) {
+    uint32_t changed = 0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < R.cap; i += gridDim.x * blockDim.x) {
+        if (!ret_used(R, i)) continue;
+        const uint4 e = R.ent[i];
+        const uint64_t l = src[i];
+        uint32_t T = (uint32_t)l, D = (uint32_t)(l >> 32);
+        const uint32_t x = e.z + D < R.n ? rank[e.z + D] : 0u;
+        if (x & kRetired) {
+            const uint4 e2 = R.ent[x & ~kRetired];
+            if (e2.x == T && e2.y == e.y) {
+                const uint64_t l2 = src[x & ~kRetired];
+                T = (uint32_t)l2;
+                D += (uint32_t)(l2 >> 32);
+                ++changed;
+            }
+        }
+        dst[i] = (unsigned long long)D << 32 | T;
+    }
+    if (__syncthreads_or(changed != 0) && threadIdx.x == 0) atomicAdd(R.cnt + 2, 1u);
+}
+// resolution (every live suffix's rank is its final slot): one wave per entry.  A: each
+// member's final slot through its links into fin[slot] (members read from sa, nothing
+// written that a rank read follows).  B: rank[q] = final slot, inv[final slot] = q.  C: the
+// group's sa from inv.  (A final slot lies in the member's own group's range.)
+template <int PH>
+__global__ void __launch_bounds__(256) k_ret_resolve(RetList R, uint32_t *sa, uint32_t *rank, uint32_t *fin, uint32_t *inv) {
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t i = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < R.cap; i += waves) {
+        if (!ret_used(R, i)) continue;
+        const uint4 e = R.ent[i];
+        for (uint32_t j = lane_id(); j < e.y; j += 64) {
+            const uint32_t s = e.x + j;
+            if (PH == 0) {
+                const uint32_t q = sa[s];
+                fin[s] = live_rank(R, rank, q, rank[q]);
+            } else if (PH == 1) {
+                const uint32_t q = sa[s], f = fin[s];
+                if (f - e.x >= e.y) {  // (outside the group: cannot happen; the batch fails)
+                    atomicOr(R.cnt + 1, 1u);
+                    continue;
+                }
+                rank[q] = f;
+                inv[f] = q;
+            } else {
+                sa[s] = inv[s];
+            }
+        }
+    }
+}
+
 // per-step counters: suffixes sorted, slots still in groups after the step, largest group
 // left.  Kept in kStatShards shards on lines of their own (one line per shard and counter
 // set: a single address taking one atomic per wave serialises the whole launch), summed by
@@ -211,11 +369,12 @@ PSA_DEV void push_long(const LongLists &L, bool valid, uint64_t ent) {
     }
 }
 
-// rank = group head index, sd = doc distance in suffix-array order, act / gsz of the first
-// groups (tag 0: step 0 sorts them).  A group's size is written at its start by its last
-// element; every other slot writes its own gsz (0)
+// rank = group head index, sd = the doubling reach in suffix-array order (the sorted keys'
+// kDlShift bits: steps whose key is a rank), act / gsz of the first groups (tag 0: step 0
+// sorts them).  A group's size is written at its start by its last element; every other
+// slot writes its own gsz (0)
 __global__ void __launch_bounds__(256) k_psa_groups0(uint32_t N, const uint32_t *sa, const uint32_t *head,
-                                                     const uint16_t *dist, uint32_t *rank, uint16_t *sd, uint8_t *act,
+                                                     const uint64_t *skeys, uint32_t *rank, uint16_t *sd, uint8_t *act,
                                                      uint32_t *gsz, StepStat ss) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t a = 0, mx = 0;
@@ -224,7 +383,7 @@ __global__ void __launch_bounds__(256) k_psa_groups0(uint32_t N, const uint32_t 
         rank[p] = hd;
         const bool hn = r + 1 == N || head[r + 1] == r + 1;  // r + 1 starts the next group
         a = (hd != r || !hn) ? 1u : 0u;                       // in a group of >= 2
-        sd[r] = a ? dist[p] : 0u;  // (the doubling reads sd of grouped slots only: no scattered read for the rest)
+        sd[r] = a ? (uint16_t)((skeys[r] >> kDlShift) & 15u) : (uint16_t)0;
         act[r] = (uint8_t)a;
         if (!(hd == r && !hn)) gsz[r] = 0;  // (not the start of a group of >= 2)
         if (hn && hd != r) {                // the last element of a group of >= 2
@@ -235,11 +394,13 @@ __global__ void __launch_bounds__(256) k_psa_groups0(uint32_t N, const uint32_t 
     block_stat(ss, 0, a, mx);
 }
 
-// this step's keys: rank of the suffix h further on (+1), 0 past the doc end.  Flat over the
-// suffix array, 16 slots per thread: every scattered rank read of the step in flight at once
-__global__ void __launch_bounds__(256) k_dbl_key(uint32_t N, uint32_t h, const uint8_t *act, const uint32_t *sa,
+// this step's keys: rank of the suffix h further on (+1), 0 past the doc end (step `it` of
+// the doubling, h = syms << it: the suffix reaches h further inside its doc iff it < sd).
+// Flat over the suffix array, 16 slots per thread: every scattered rank read of the step in
+// flight at once
+__global__ void __launch_bounds__(256) k_dbl_key(uint32_t N, uint32_t h, uint32_t it, const uint8_t *act, const uint32_t *sa,
                                                  const uint16_t *sd, const uint32_t *rank, uint32_t *key,
-                                                 uint32_t *long_cnt) {
+                                                 uint32_t *long_cnt, RetList R) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t < 8) long_cnt[t] = 0;  // (the step's long-group lists start empty: k_dbl_win fills them)
     const uint32_t s0 = t * 16;
@@ -252,13 +413,29 @@ __global__ void __launch_bounds__(256) k_dbl_key(uint32_t N, uint32_t h, const u
         for (int q = 0; q < 4; ++q) *(uint4 *)(p + 4 * q) = *(const uint4 *)(sa + s0 + 4 * q);
         for (int q = 0; q < 2; ++q) *(uint4 *)(d + 8 * q) = *(const uint4 *)(sd + s0 + 8 * q);
         const uint32_t aw[4] = {av.x, av.y, av.z, av.w};
+        bool any_ret = false;
 #pragma unroll
-        for (int i = 0; i < 16; ++i)  // (slots outside groups get a key nobody reads)
-            k[i] = ((aw[i >> 2] >> (8 * (i & 3))) & 0xffu) && h < d[i] ? rank[p[i] + h] + 1u : 0u;
+        for (int i = 0; i < 16; ++i) {  // (slots outside groups get a key nobody reads)
+            k[i] = ((aw[i >> 2] >> (8 * (i & 3))) & 0xffu) && it < d[i] ? rank[p[i] + h] + 1u : 0u;
+            any_ret = any_ret || (k[i] != 0 && ((k[i] - 1u) & kRetired) != 0);
+        }
+        if (any_ret) {  // (ranks of retired groups: through their links)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                if (k[i] != 0 && ((k[i] - 1u) & kRetired)) k[i] = live_rank(R, rank, p[i] + h, k[i] - 1u) + 1u;
+        }
         for (int q = 0; q < 4; ++q) *(uint4 *)(key + s0 + 4 * q) = *(const uint4 *)(k + 4 * q);
     } else {
         for (uint32_t s = s0; s < N; ++s)
-            if (act[s]) key[s] = h < sd[s] ? rank[sa[s] + h] + 1u : 0u;
+            if (act[s]) {
+                uint32_t r = 0;
+                if (it < sd[s]) {
+                    r = rank[sa[s] + h];
+                    if (r & kRetired) r = live_rank(R, rank, sa[s] + h, r);
+                    ++r;
+                }
+                key[s] = r;
+            }
     }
 }
 
@@ -300,9 +477,9 @@ PSA_DEV void win_put(const WinElem &e, uint32_t b, uint32_t lt, uint32_t eqb, ui
     ac += grp;
     if (head && grp) mx = max(mx, size);
 }
-__global__ void __launch_bounds__(256) k_dbl_win(uint32_t N, uint32_t tag, uint32_t *sa, uint16_t *sd, uint8_t *act,
+__global__ void __launch_bounds__(256) k_dbl_win(uint32_t N, uint32_t tag, uint32_t h, uint32_t *sa, uint16_t *sd, uint8_t *act,
                                                  uint32_t *gsz, const uint32_t *key, uint32_t *rank, LongLists L,
-                                                 StepStat ss) {
+                                                 StepStat ss, RetList R) {
     __shared__ uint32_t lks[4][128];
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
     uint32_t *lk = lks[wv];
@@ -369,13 +546,40 @@ __global__ void __launch_bounds__(256) k_dbl_win(uint32_t N, uint32_t tag, uint3
             const uint64_t split = __ballot(A.mem && (A.key != k0A || A.key == 0)) |
                                    __ballot(B.mem && (B.key != k0B || B.key == 0));
             if (!split) {
+                // groups that are shifted copies of another leave the doubling (see RetList)
+                uint64_t Rm = __ballot(((S >> lane) & 1ull) && retire_ok(R, b + lane, gs, A.key, tag, gsz));
+                uint32_t id = 0;
+                if (Rm) {
+                    uint32_t lim;
+                    const uint32_t base = ret_alloc(R, w, (uint32_t)__popcll(Rm), 0, &lim);
+                    id = base + (uint32_t)__popcll(Rm & ((1ull << lane) - 1ull));
+                    Rm &= __ballot(id < lim);  // (past the shard's end: those groups stay; every id below it is written)
+                }
+                const bool rA = A.mem && ((Rm >> A.c) & 1ull), rB = B.mem && ((Rm >> B.c) & 1ull);
+                const uint32_t idA = (uint32_t)__shfl((int)id, (int)A.c), idB = (uint32_t)__shfl((int)id, (int)B.c);
+                uint32_t pA = 0;
+                if (rA) {
+                    act[sA] = 0;
+                    pA = sa[sA];
+                    rank[pA] = idA | kRetired;
+                }
+                if (rB) {
+                    act[sB] = 0;
+                    rank[sa[sB]] = idB | kRetired;
+                }
                 if ((S >> lane) & 1ull) {
-                    gsz[sA] = gs | (tag ^ kTag);
-                    mx = max(mx, gs);
+                    if ((Rm >> lane) & 1ull) {
+                        gsz[sA] = 0;
+                        retire_put(R, id, b + lane, gs, pA, A.key, h);
+                    } else {
+                        gsz[sA] = gs | (tag ^ kTag);
+                        mx = max(mx, gs);
+                    }
                 }
                 const uint32_t m = (uint32_t)__popcll(__ballot(A.mem)) + (uint32_t)__popcll(__ballot(B.mem));
+                const uint32_t mr = (uint32_t)__popcll(__ballot(rA)) + (uint32_t)__popcll(__ballot(rB));
                 sorted += m;
-                active += lane == 0 ? m : 0u;
+                active += lane == 0 ? m - mr : 0u;
                 continue;
             }
         }
@@ -429,9 +633,9 @@ PSA_DEV void put_sorted(uint32_t start, uint32_t q, uint32_t p, uint32_t d, uint
 // One wave per group of 65..64*E suffixes: E elements per lane (lane l holds positions
 // l*E .. l*E+E-1), bitonic sort in registers; payloads through LDS.
 template <uint32_t E>
-__global__ void __launch_bounds__(256) k_dbl_reg(const uint64_t *list, const uint32_t *cnt_p, uint32_t tag, uint32_t *sa,
-                                                 uint16_t *sd, uint8_t *act, uint32_t *gsz, const uint32_t *key,
-                                                 uint32_t *rank, StepStat ss) {
+__global__ void __launch_bounds__(256) k_dbl_reg(const uint64_t *list, const uint32_t *cnt_p, uint32_t tag, uint32_t h,
+                                                 uint32_t *sa, uint16_t *sd, uint8_t *act, uint32_t *gsz, const uint32_t *key,
+                                                 uint32_t *rank, StepStat ss, RetList R) {
     __shared__ uint32_t lp[4][64 * E];
     __shared__ uint16_t ld[4][64 * E];
     const uint32_t cnt = __hip_atomic_load(cnt_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -451,10 +655,34 @@ __global__ void __launch_bounds__(256) k_dbl_reg(const uint64_t *list, const uin
             x[r] = i < size ? (uint64_t)k << 11 | i : ~0ull;
             split = split || k != key0 || k == 0;
         }
-        if (!__ballot(split)) {  // one key: the group stays as it is (see k_dbl_win)
+        if (!__ballot(split)) {  // one key: the group stays as it is (see k_dbl_win) or retires
+            uint32_t id = kNoPos;
+            if (retire_ok(R, start, size, key0, tag, gsz)) {
+                uint32_t lim;
+                id = ret_alloc(R, gi, 1, 0, &lim);
+                if (id >= lim) id = kNoPos;
+            }
+            sorted += size;
+            if (id != kNoPos) {
+                uint32_t p0 = 0;
+#pragma unroll
+                for (uint32_t r = 0; r < E; ++r) {
+                    const uint32_t i = lane * E + r;
+                    if (i < size) {
+                        act[start + i] = 0;
+                        const uint32_t p = sa[start + i];
+                        rank[p] = id | kRetired;
+                        if (i == 0) p0 = p;
+                    }
+                }
+                if (lane == 0) {
+                    gsz[start] = 0;
+                    retire_put(R, id, start, size, p0, key0, h);
+                }
+                continue;
+            }
             if (lane == 0) gsz[start] = size | (tag ^ kTag);
             mx = max(mx, size);
-            sorted += size;
             active += size;
             continue;
         }
@@ -537,9 +765,9 @@ __global__ void __launch_bounds__(256) k_dbl_reg(const uint64_t *list, const uin
 // each thread takes C = P / 256 consecutive positions: their heads as a mask, their payloads
 // gathered before any slot of the group is rewritten, and the subgroup bounds across threads
 // from two block scans
-__global__ void __launch_bounds__(256) k_dbl_blk(const uint64_t *list, const uint32_t *cnt_p, uint32_t tag, uint32_t *sa,
-                                                 uint16_t *sd, uint8_t *act, uint32_t *gsz, const uint32_t *key,
-                                                 uint32_t *rank, StepStat ss) {
+__global__ void __launch_bounds__(256) k_dbl_blk(const uint64_t *list, const uint32_t *cnt_p, uint32_t tag, uint32_t h,
+                                                 uint32_t *sa, uint16_t *sd, uint8_t *act, uint32_t *gsz, const uint32_t *key,
+                                                 uint32_t *rank, StepStat ss, RetList R) {
     __shared__ uint64_t sk[kMedMax];
     __shared__ uint32_t sl[256], sf[256];
     constexpr uint32_t kC = kMedMax / 256;
@@ -558,13 +786,40 @@ __global__ void __launch_bounds__(256) k_dbl_blk(const uint64_t *list, const uin
             split = split || k != key0 || k == 0;
             sk[i] = i < size ? (uint64_t)k << 12 | i : ~0ull;
         }
-        if (!__syncthreads_or(split)) {  // one key: the group stays as it is (see k_dbl_win)
+        if (!__syncthreads_or(split)) {  // one key: the group stays as it is (see k_dbl_win) or retires
+            __shared__ uint32_t s_id;
             if (tid == 0) {
-                gsz[start] = size | (tag ^ kTag);
-                active += size;
+                uint32_t id = kNoPos;
+                if (retire_ok(R, start, size, key0, tag, gsz)) {
+                    const uint32_t sh = gi & (kRetShards - 1u);
+                    id = atomicAdd(R.sc + sh * kRetStride, 1u);
+                    id = id < R.per ? sh * R.per + id : kNoPos;
+                }
+                s_id = id;
             }
-            mx = max(mx, size);
+            __syncthreads();
+            const uint32_t id = s_id;
             sorted += size;
+            if (id != kNoPos) {
+                uint32_t p0 = 0;
+                for (uint32_t i = tid; i < size; i += 256) {
+                    act[start + i] = 0;
+                    const uint32_t p = sa[start + i];
+                    rank[p] = id | kRetired;
+                    if (i == 0) p0 = p;
+                }
+                if (tid == 0) {
+                    gsz[start] = 0;
+                    retire_put(R, id, start, size, p0, key0, h);
+                }
+            } else {
+                if (tid == 0) {
+                    gsz[start] = size | (tag ^ kTag);
+                    active += size;
+                }
+                mx = max(mx, size);
+            }
+            __syncthreads();  // (s_id is rewritten by the next group)
             continue;  // (the barrier above: nobody reads sk any more)
         }
         for (uint32_t kk = 2; kk <= P; kk <<= 1)
@@ -1592,7 +1847,7 @@ constexpr uint32_t kMaxSteps = 20;  // h doubles from >= 5 past 65,535 (the long
 constexpr uint32_t kGridWin = 16384, kGridReg = 2048, kGridBlk = 1024;
 // the cnt words of psa_run
 constexpr uint32_t kCntLong = 0, kCntSorted = 16, kCntActive = 48, kCntMax = 96, kCntCand = 200, kCntSortErr = 250,
-                   kCntWords = 256;
+                   kCntRet = 252, kCntWords = 256;
 static_assert(kCntSorted + kMaxSteps < kCntActive && kCntActive + kMaxSteps + 1 < kCntMax && kCntMax + kMaxSteps + 1 < kCntCand, "cnt layout");
 }  // namespace
 
@@ -1637,12 +1892,12 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     }
     const SortAlloc SA{A.alloc, A.release, A.self};
     auto *keys = S.get<uint64_t>(n64 * 8);
+    auto *keys2 = S.get<uint64_t>(n64 * 8);  // (the sorted keys: the first grouping reads their reach)
     {
         std::vector<uint32_t> slen(nshards);
         for (uint32_t i = 0; i < nshards; ++i) slen[i] = hshards[i].len;
         auto *segs = S.get<uint32_t>((uint64_t)nshards * 8 + 64);
         k_psa_segs<<<(nshards + 255) / 256, 256, 0, s>>>(nshards, shards, segs, segs + nshards);
-        auto *keys2 = S.get<uint64_t>(n64 * 8);
         auto *va = S.get<uint32_t>(n64 * 4), *vb = S.get<uint32_t>(n64 * 4);
         // passes: text -> keys -> keys2 -> keys -> keys2 -> keys -> (keys2, sa)
         PSA_CHECK(seg_sort_pairs(s, SA, nshards, seg_tile_count(slen.data(), nshards), segs, segs + nshards, 9 * syms, 9,
@@ -1653,7 +1908,6 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         uint32_t *hflag = (uint32_t *)keys, *head = (uint32_t *)keys + N;  // (the pass buffers are spent)
         k_psa_head0<<<blocks(N), tb, 0, s>>>(N, keys2, hflag);
         PSA_CHECK(scan_u32(s, SA, hflag, head, N, ScanOp::kMax, false));
-        S.put(keys2);
     }
     // ---- the first groups, then prefix doubling over them
     auto *sd = S.get<uint16_t>(n64 * 2);
@@ -1666,9 +1920,10 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     PSA_CHECK(hipMemsetAsync(stat_sh, 0, (size_t)(kMaxSteps + 1) * kStatShards * kStatStride * 4, s));
     auto region = [&](uint32_t k) { return StepStat{stat_sh + (uint64_t)k * kStatShards * kStatStride}; };
     auto stats_of = [&](uint32_t k) { return region(k + 1); };
-    k_psa_groups0<<<blocks(N), tb, 0, s>>>(N, sa, (const uint32_t *)keys + N, dist, rank, sd, act, gsz, region(0));
+    k_psa_groups0<<<blocks(N), tb, 0, s>>>(N, sa, (const uint32_t *)keys + N, keys2, rank, sd, act, gsz, region(0));
     k_stat_sum<<<1, 64, 0, s>>>(region(0).sh, cnt + kCntSorted + kMaxSteps, cnt + kCntActive, cnt + kCntMax);
     S.put(keys);
+    S.put(keys2);
     auto *key = S.get<uint32_t>(n64 * 4 + 64);
     LongLists LL;
     {
@@ -1679,6 +1934,21 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         }
         LL.cnt = cnt + kCntLong;
     }
+    // retired groups (see RetList; off unless PX_PSA_RETIRE=1: measured on config 3 they take
+    // 6 ms off the window sorter but add 4 ms of link walks to the key gathers and 11 ms of
+    // resolution): list capped at N / 32 (groups past it stay in the doubling)
+    RetList R{};
+    if (env_on("PX_PSA_RETIRE")) {
+        R.per = (uint32_t)std::min<uint64_t>((n64 / 32 + 4096) / kRetShards + 1, 0x7fffffffull / kRetShards);
+        R.cap = R.per * kRetShards;
+        R.ent = S.get<uint4>((uint64_t)R.cap * 16);
+        R.lnk = S.get<unsigned long long>((uint64_t)R.cap * 8);
+        R.sc = S.get<uint32_t>(kRetShards * kRetStride * 4);
+        PSA_CHECK(hipMemsetAsync(R.sc, 0, kRetShards * kRetStride * 4, s));
+        R.cnt = cnt + kCntRet;
+        R.n = N;
+    }
+    const uint32_t gret = std::min<uint32_t>((R.cap + 255) / 256, 2048);
     uint32_t *pin = A.pin;  // pinned host words: counts come back through them
     auto read_words = [&](uint32_t at, uint32_t n) -> hipError_t {  // -> pin[at .. at + n)
         hipError_t e = hipMemcpyAsync(pin + at, cnt + at, n * 4, hipMemcpyDeviceToHost, s);
@@ -1694,12 +1964,12 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         const uint32_t tag = (it & 1u) ? kTag : 0u;
         const StepStat ss = stats_of(it);
         hipError_t e = hipSuccess;
-        k_dbl_key<<<blocks((n64 + 15) / 16), tb, 0, s>>>(N, h, act, sa, sd, rank, key, cnt + kCntLong);
-        k_dbl_win<<<gwin, 256, 0, s>>>(N, tag, sa, sd, act, gsz, key, rank, LL, ss);
-        k_dbl_reg<2><<<kGridReg, 256, 0, s>>>(LL.lst[0], LL.cnt + 0, tag, sa, sd, act, gsz, key, rank, ss);
-        k_dbl_reg<4><<<kGridReg, 256, 0, s>>>(LL.lst[1], LL.cnt + 1, tag, sa, sd, act, gsz, key, rank, ss);
-        k_dbl_reg<8><<<kGridReg, 256, 0, s>>>(LL.lst[2], LL.cnt + 2, tag, sa, sd, act, gsz, key, rank, ss);
-        k_dbl_blk<<<kGridBlk, 256, 0, s>>>(LL.lst[3], LL.cnt + 3, tag, sa, sd, act, gsz, key, rank, ss);
+        k_dbl_key<<<blocks((n64 + 15) / 16), tb, 0, s>>>(N, h, it, act, sa, sd, rank, key, cnt + kCntLong, R);
+        k_dbl_win<<<gwin, 256, 0, s>>>(N, tag, h, sa, sd, act, gsz, key, rank, LL, ss, R);
+        k_dbl_reg<2><<<kGridReg, 256, 0, s>>>(LL.lst[0], LL.cnt + 0, tag, h, sa, sd, act, gsz, key, rank, ss, R);
+        k_dbl_reg<4><<<kGridReg, 256, 0, s>>>(LL.lst[1], LL.cnt + 1, tag, h, sa, sd, act, gsz, key, rank, ss, R);
+        k_dbl_reg<8><<<kGridReg, 256, 0, s>>>(LL.lst[2], LL.cnt + 2, tag, h, sa, sd, act, gsz, key, rank, ss, R);
+        k_dbl_blk<<<kGridBlk, 256, 0, s>>>(LL.lst[3], LL.cnt + 3, tag, h, sa, sd, act, gsz, key, rank, ss, R);
         auto sum = [&]() {
             k_stat_sum<<<1, 64, 0, s>>>(ss.sh, cnt + kCntSorted + it, cnt + kCntActive + 1 + it, cnt + kCntMax + 1 + it);
         };
@@ -1795,8 +2065,34 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
             }
         }
     }
+    if (R.ent) {  // the retired groups' final order (every live suffix's rank is final now)
+        // pointer jumping until no link changes (a template's same-step chain: log2 of its length)
+        auto *lnk2 = S.get<unsigned long long>((uint64_t)R.cap * 8);
+        unsigned long long *a = R.lnk, *b = lnk2;
+        for (uint32_t round = 0; round < 32; ++round) {
+            PSA_CHECK(hipMemsetAsync(cnt + kCntRet + 2, 0, 4, s));
+            k_ret_jump<<<gret, 256, 0, s>>>(R, a, b, rank);
+            std::swap(a, b);
+            PSA_CHECK(read_words(kCntRet, 4));
+            if (pin[kCntRet + 2] == 0) break;
+        }
+        RetList Rf = R;
+        Rf.lnk = a;
+        const uint32_t gw = std::min<uint32_t>((R.cap + 3) / 4, 8192);
+        k_ret_resolve<0><<<gw, 256, 0, s>>>(Rf, sa, rank, key, gsz);
+        k_ret_resolve<1><<<gw, 256, 0, s>>>(Rf, sa, rank, key, gsz);
+        k_ret_resolve<2><<<gw, 256, 0, s>>>(Rf, sa, rank, key, gsz);
+    }
     PSA_CHECK(read_words(0, kCntWords));
-    if (pin[kCntActive + it] != 0 || pin[kCntLong + kLongClasses] || pin[kCntSortErr]) return hipErrorUnknown;
+    if (pin[kCntActive + it] != 0 || pin[kCntLong + kLongClasses] || pin[kCntSortErr] || pin[kCntRet + 1])
+        return hipErrorUnknown;
+    if (verbose && R.ent) {
+        std::vector<uint32_t> sc(kRetShards * kRetStride);
+        PSA_CHECK(hipMemcpy(sc.data(), R.sc, sc.size() * 4, hipMemcpyDeviceToHost));
+        uint64_t nr = 0;
+        for (uint32_t k = 0; k < kRetShards; ++k) nr += std::min(sc[k * kRetStride], R.per);
+        fprintf(stderr, "psa: %llu groups retired (list %u)\n", (unsigned long long)nr, R.cap);
+    }
     for (const void *q : {(const void *)sd, (const void *)act, (const void *)gsz, (const void *)key}) S.put(q);
     for (int c = 0; c < kLongClasses; ++c) S.put(LL.lst[c]);
     PSA_CHECK(hipEventRecord(e1, s));

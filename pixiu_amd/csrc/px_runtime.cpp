@@ -53,6 +53,8 @@ hipError_t launch_rehash(hipStream_t, const uint4 *, uint32_t, uint32_t, uint4 *
 hipError_t launch_decode_addr(hipStream_t, const DecodeQuery *, uint32_t, const RecSlot *const *, int32_t *,
                               uint32_t *, uint32_t *, Frame *, uint32_t, uint32_t);
 hipError_t launch_slot_place(hipStream_t, uint32_t, const RecSlot *, const uint32_t *, const SlotDst *, LinkJob *);
+hipError_t launch_span_agg(hipStream_t, uint32_t, const uint32_t *, const uint32_t *, const uint32_t *, uint32_t *,
+                           uint32_t *);
 hipError_t launch_span_jobs(hipStream_t, uint32_t, const DecodeQuery *, const uint32_t *, const uint32_t *,
                             const SpanSrc *, const RecSlot *const *, const int32_t *, uint32_t *, uint32_t *,
                             uint32_t *, const uint32_t *, const uint32_t *, SpanEnt *, uint32_t *);
@@ -1148,7 +1150,47 @@ struct px_ctx {
             return !(e && e[0] == '0');
         }();
         const auto *ctab = (const RecSlot *const *)chunk_tab;
-        hcheck(launch_decode_addr(stream, dq, n, ctab, addr, dl, ds, frames, depth, waves | (xcd ? 0x80000000u : 0u)));
+        // exact tables: every record decoded in pieces of kExactPiece bytes, one wave each (an exact
+        // parse of [a, b) is the doc's slice, so the pieces' addresses land side by side; the
+        // ~1,000 records of a config-3 batch with compat != exact kept 1,000 waves busy for 6.8 ms)
+        constexpr uint32_t kExactPiece = 4096;
+        uint64_t sub_bytes = 0;
+        uint8_t *sub_buf = nullptr;
+        if (mode == 1) {
+            std::vector<DecodeQuery> sq;
+            std::vector<uint32_t> first(n + 1, 0);
+            for (uint32_t k = 0; k < n; ++k) {
+                first[k] = (uint32_t)sq.size();
+                const uint32_t L = src[k].doc_len;
+                for (uint32_t a = 0; a < L || (a == 0 && L == 0); a += kExactPiece) {
+                    const uint32_t b = std::min(L, a + kExactPiece);
+                    DecodeQuery d = qn[k];
+                    d.from = (int32_t)a;
+                    d.to = (int32_t)b;
+                    d.out_off = qn[k].out_off + a;
+                    d.out_cap = b - a + 16;  // (exactly b - a bytes come; room past them keeps the cap from firing)
+                    sq.push_back(d);
+                    if (L == 0) break;
+                }
+            }
+            first[n] = (uint32_t)sq.size();
+            const uint32_t ns = (uint32_t)sq.size();
+            const uint64_t o_first = round_up((uint64_t)ns * sizeof(DecodeQuery), 256);
+            const uint64_t o_pl = o_first + round_up((uint64_t)(n + 1) * 4, 256);
+            sub_bytes = o_pl + (uint64_t)ns * 8 + 256;
+            sub_buf = (uint8_t *)heap.alloc(sub_bytes);
+            auto *sdq = (DecodeQuery *)sub_buf;
+            auto *dfirst = (uint32_t *)(sub_buf + o_first);
+            auto *pl = (uint32_t *)(sub_buf + o_pl), *ps = pl + ns;
+            h2d(sdq, sq.data(), (size_t)ns * sizeof(DecodeQuery));
+            h2d(dfirst, first.data(), (size_t)(n + 1) * 4);
+            const uint32_t sw = std::min<uint32_t>(opts.decode_waves ? opts.decode_waves : 16384, ns);
+            auto *sframes = (Frame *)scratch_frames.get((uint64_t)sw * depth * sizeof(Frame));
+            hcheck(launch_decode_addr(stream, sdq, ns, ctab, addr, pl, ps, sframes, depth, sw | (xcd ? 0x80000000u : 0u)));
+            hcheck(launch_span_agg(stream, n, dfirst, pl, ps, dl, ds));
+        } else {
+            hcheck(launch_decode_addr(stream, dq, n, ctab, addr, dl, ds, frames, depth, waves | (xcd ? 0x80000000u : 0u)));
+        }
         hcheck(launch_span_jobs(stream, n, dq, dl, ds, dsrc, ctab, addr, cnt, ents, tiles, nullptr, nullptr, nullptr,
                                 nullptr));
         const SortAlloc SA{[](void *self, uint64_t bytes) -> void * { return static_cast<px_ctx *>(self)->heap.alloc(bytes); },
@@ -1221,6 +1263,7 @@ struct px_ctx {
         }
         phase.mark("wait (write pass)");
         sync();
+        if (sub_buf) heap.release(sub_buf, sub_bytes);
         heap.release(wb, o_end);
         heap.release(addr, tot * 4 + 64);
         phase.mark("exact tables");
@@ -2975,9 +3018,13 @@ int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int m
     void *task = b + o_task;
     // keys up through pinned memory (one copy of the bytes and the rebased offsets)
     auto *hb = (uint8_t *)dk_hbuf.get(o_gq);
-    std::memcpy(hb, keys + k0, kbytes);
     auto *ho = (uint64_t *)(hb + o_off);
-    for (uint32_t i = 0; i <= n; ++i) ho[i] = koff[i] - k0;
+    // (a million-key batch: 16 MB staged, on the host threads)
+    parallel_ranges(n + 1, n >= 65536 ? host_threads() : 1, [&](uint32_t lo, uint32_t hi) {
+        const uint64_t a = koff[lo] - k0, b = (hi > n ? koff[n] : koff[hi]) - k0;
+        std::memcpy(hb + a, keys + k0 + a, b - a);
+        for (uint32_t i = lo; i < hi; ++i) ho[i] = koff[i] - k0;
+    });
     phase.mark("uploads and launches");
     hcheck(hipMemcpyAsync(dkeys, hb, o_off + (uint64_t)(n + 1) * 8, hipMemcpyHostToDevice, stream));
     hcheck(hipMemsetAsync(chain, 0, nb * 16 + 32, stream));
@@ -3018,8 +3065,10 @@ int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int m
     stats.last_gather_queries = n;
     stats.last_get_device_keys = n;
     const uint32_t *ro = (const uint32_t *)res, *rl = ro + n;
-    for (uint32_t i = 0; i < n; ++i) out_off[i] = (uint64_t)ro[i] * 16;
-    std::memcpy(out_len, rl, (size_t)n * 4);
+    parallel_ranges(n, n >= 65536 ? host_threads() : 1, [&](uint32_t lo, uint32_t hi) {
+        for (uint32_t i = lo; i < hi; ++i) out_off[i] = (uint64_t)ro[i] * 16;
+        std::memcpy(out_len + lo, rl + lo, (size_t)(hi - lo) * 4);
+    });
     int rc = PX_OK;
     if (hr[5]) {
         uint32_t *rs = (uint32_t *)dk_hres.get(o_end - o_ctl) + (o_ds - o_ctl) / 4;

@@ -15,6 +15,15 @@ constexpr uint32_t kSortTile = 4096;
 struct SegTile {
     uint32_t start, count, seg, first;
 };
+// The first sort's keys carry, above their symbols (bits kDlShift..+3), the suffix's doubling
+// reach: the number of doubling steps k (h = syms << k) with h < its distance to the doc
+// end, i.e. the steps whose key is a rank rather than 0 (<= 14: docs are < 65,536 bytes).
+// The sort passes never look at these bits; the first grouping reads them in suffix-array
+// order, so the doubling needs no scattered read of the distances.  Keys compare equal on
+// their low kKeyBits.
+constexpr uint32_t kDlShift = 58, kKeyBits = 54;
+constexpr uint64_t kKeyMask = (1ull << kKeyBits) - 1ull;
+
 // device scratch borrowed from the caller (px_psa.hip's Scratch / the runtime heap)
 struct SortAlloc {
     void *(*alloc)(void *self, uint64_t n);

@@ -53,7 +53,7 @@ typedef PX_GAS uint32_t gu32;
 
 // the first suffix sort's key of text position p (k_psa_key0's layout without the shard):
 // 8 text bytes by two aligned 8-byte loads and a funnel shift (G is 8-byte aligned and
-// padded), then `syms` symbols of 9 bits
+// padded), then `syms` symbols of 9 bits; the doubling reach above them (px_sort.h kDlShift)
 SD uint64_t text_key(const uint8_t *G, const uint16_t *dist, uint32_t p, uint32_t syms) {
     gcu64 *G8 = (gcu64 *)G;
     const uint32_t w = p >> 3, sh = (p & 7u) * 8u;
@@ -62,7 +62,9 @@ SD uint64_t text_key(const uint8_t *G, const uint16_t *dist, uint32_t p, uint32_
     const uint32_t left = ((gcu16 *)dist)[p];
     uint64_t k = 0;
     for (uint32_t s = 0; s < syms; ++s) k = k << 9 | (s < left ? ((x >> (8 * s)) & 0xffu) + 1u : 0u);
-    return k;
+    uint32_t dl = 0;
+    while (dl < 15u && (syms << dl) < left) ++dl;
+    return k | (uint64_t)dl << kDlShift;
 }
 
 // lanes (of `valid`) holding the same RB-bit digit as this lane
