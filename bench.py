@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group for N > 1 (nccl = RCCL over xGMI; gloo: CPU transport, for tests)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r04.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r05.json"),
                     help="per-kernel PMC summary (tools/pmc_summary.py); used only if its workload matches")
     return ap.parse_args()
 
@@ -795,7 +795,9 @@ def main():
         # instance, chunks rotated by its MemPool rule (suffix-array path with the pool
         # emulation), next to the oracle's single instance on the CPU
         torch.cuda.empty_cache()
-        r0 = run_config(a.config, a, rank, world, local, 1, 1, 0, None, checks=False)
+        # (checks: every record's compat getitem, compressed bytes and slot against the
+        # reference's own single instance, tests/golden/refdig_c3_r0.npz, outside the timing)
+        r0 = run_config(a.config, a, rank, world, local, 1, 1, 0, None, checks=not a.no_checks)
         s0 = summarize(a.config, r0, 0, world, a, None)
         line["single_instance"] = {
             "records_per_shard": 0, "setitem_MBps": s0["setitem_MBps"], "getitem_MBps": s0["getitem_MBps"],
@@ -806,6 +808,8 @@ def main():
             "psa_split_ms": s0["encode_stage"].get("psa_split_ms"), "reference_check": check_single(r0)}
         if "reference_check" in r0:  # every record's compat getitem / bytes / slot vs the reference's digests
             line["single_instance"]["reference_digests"] = r0["reference_check"]
+        if "parity_counts" in r0:
+            line["single_instance"]["parity_counts"] = r0["parity_counts"]
         if not a.no_cpu:
             c0 = cpu_single_instance(corpus, a.cpu_seconds)
             line["single_instance"]["cpu_baseline"] = {

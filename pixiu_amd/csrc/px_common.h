@@ -204,7 +204,7 @@ struct DecodeQuery {
     uint32_t out_cap;     // consumer stops pulling after this many bytes
     uint32_t mode;        // 0 compat, 1 exact
     uint32_t nrec;        // records in the chunk (record tokens are bounds-checked against it)
-    uint32_t pad;
+    uint32_t pad;         // compat: the top frame's ret cursor at `from` (a piece of a whole drain), else 0
 };
 
 // Span table (fast full-range getitem): a record's compat expansion
@@ -216,10 +216,14 @@ struct SpanEnt {
     uint32_t start;
 };
 constexpr int32_t kAddrNone = (int32_t)0x80000000;  // a source beyond +-2 GiB of the record
+// k_decode_addr writes a run's address at its first output byte only; the array starts filled
+// with kAddrMark (the byte continues the run before it: its address is the previous one + 1)
+constexpr int32_t kAddrMark = (int32_t)0x80000001;
 
-// span build work item: the address decode of one record (k_decode_addr's output)
+// span build work item: the address decode of one record (k_decode_addr's output), in one
+// piece (addr, len) or in the pieces first..last of a piece table (pq[k].out_off, pl[k])
 struct SpanJob {
-    const int32_t *addr;  // per output byte: source address relative to the record's comp
+    const int32_t *addr;  // per output run: source address relative to the record's comp (kAddrMark between)
     const uint8_t *base;  // the record's comp pointer
     const uint8_t *doc;   // the escaped doc (compat == exact test), or null
     SpanEnt *out;         // span entries (count pass: null)
@@ -227,6 +231,9 @@ struct SpanJob {
     uint32_t doc_len;
     uint32_t *count;      // count pass: spans | kSpanBad, eq flag in bit 30
     uint32_t *tix;        // write pass: tile index (kGatherTile bytes per tile), or null
+    const DecodeQuery *pq;  // pieces (null: one piece at addr)
+    const uint32_t *pl;
+    uint32_t first, last;
 };
 // span build source of one record: its escaped doc on the device (compat == exact test) or null
 struct SpanSrc {

@@ -1617,27 +1617,68 @@ PX_DEV uint32_t seg_find(const SlotV &s, int32_t from) {
 }
 
 // Output writers of the decoder.  Byte output (getitem) copies bytes; address output
-// (k_decode_addr, the span build) writes, per output byte, the address of the
-// compressed byte it is copied from, relative to the query record's comp pointer.
+// (k_decode_addr, the span build) writes, at the first output byte of each run copied from
+// consecutive compressed bytes, the address of its first source byte relative to the query
+// record's comp pointer (kAddrNone for a run reaching beyond +-2 GiB of it); the run's other
+// bytes keep the kAddrMark the array was filled with.  (One store per run: a lane writing its
+// run's addresses byte by byte was most of the span build's decode.)
 PX_DEV int32_t addr_of(const PX_GAS uint8_t *p, const PX_GAS uint8_t *qb) {
     const int64_t d = (int64_t)((uint64_t)p - (uint64_t)qb);
-    return (d == (int64_t)(int32_t)d && (int32_t)d != kAddrNone) ? (int32_t)d : kAddrNone;
+    return (d == (int64_t)(int32_t)d && (int32_t)d != kAddrNone && (int32_t)d != kAddrMark) ? (int32_t)d : kAddrNone;
+}
+PX_DEV int32_t run_addr(const PX_GAS uint8_t *p, uint32_t n, const PX_GAS uint8_t *qb) {
+    const int32_t a = addr_of(p, qb);
+    return a != kAddrNone && addr_of(p + (n - 1), qb) != kAddrNone ? a : kAddrNone;
 }
 PX_DEV void out_wave_copy(PX_GAS uint8_t *dst, const PX_GAS uint8_t *src, uint32_t n, const PX_GAS uint8_t *) {
     wave_copy(dst, src, n);
 }
 PX_DEV void out_wave_copy(PX_GAS int32_t *dst, const PX_GAS uint8_t *src, uint32_t n, const PX_GAS uint8_t *qb) {
-    for (uint32_t i = lane_id(); i < n; i += 64) dst[i] = addr_of(src + i, qb);
+    if (n && lane_id() == 0) dst[0] = run_addr(src, n, qb);
 }
 PX_DEV void out_lane_copy(PX_GAS uint8_t *dst, const PX_GAS uint8_t *src, uint32_t n, const PX_GAS uint8_t *) {
     lane_copy(dst, src, n);
 }
 PX_DEV void out_lane_copy(PX_GAS int32_t *dst, const PX_GAS uint8_t *src, uint32_t n, const PX_GAS uint8_t *qb) {
-    for (uint32_t i = 0; i < n; ++i) dst[i] = addr_of(src + i, qb);
+    if (n) dst[0] = run_addr(src, n, qb);
 }
 PX_DEV void out_one(PX_GAS uint8_t *dst, const PX_GAS uint8_t *src, const PX_GAS uint8_t *) { *dst = *src; }
 PX_DEV void out_one(PX_GAS int32_t *dst, const PX_GAS uint8_t *src, const PX_GAS uint8_t *qb) {
     *dst = addr_of(src, qb);
+}
+// A window stopped by a short or flagged segment redoes its output from `from`; address output
+// clears the run starts its abandoned lanes left in [from, to) (the redo may cut runs elsewhere)
+PX_DEV void out_clear(PX_GAS uint8_t *, uint32_t, uint32_t) {}
+PX_DEV void out_clear(PX_GAS int32_t *o, uint32_t from, uint32_t to) {
+    __threadfence_block();
+    for (uint32_t i = from + lane_id(); i < to; i += 64) o[i] = kAddrMark;
+    __threadfence_block();
+}
+// A periodic record token repeats its child's output [s, s + produced) to end (PiXiuStr.h:168-181).
+// Address output first writes every address of the child's output (the repeat copies them by
+// position); its first byte is a run start.
+PX_DEV void out_repeat(PX_GAS uint8_t *o, uint32_t s, uint32_t produced, uint32_t end) {
+    for (uint32_t k = produced + lane_id(); s + k < end; k += 64) o[s + k] = o[s + (k % produced)];
+}
+PX_DEV void out_repeat(PX_GAS int32_t *o, uint32_t s, uint32_t produced, uint32_t end) {
+    const uint32_t lane = lane_id();
+    int32_t carry = kAddrNone;  // the address of the byte before the window
+    for (uint32_t i0 = 0; i0 < produced; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        const bool in = i < produced;
+        const int32_t raw = in ? o[s + i] : kAddrMark;
+        const uint64_t sm = ballot(in && raw != kAddrMark);
+        const uint64_t le = sm & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));  // starts at or below the lane
+        const uint32_t sl = le ? 63u - (uint32_t)__clzll((long long)le) : 0u;
+        const int32_t sv = (int32_t)__shfl(raw, (int)sl);
+        const int32_t base = le ? sv : carry;
+        const int32_t dist = le ? (int32_t)(lane - sl) : (int32_t)lane + 1;
+        const int32_t v = base == kAddrNone ? kAddrNone : base + dist;
+        if (in && raw == kAddrMark) o[s + i] = v;
+        carry = (int32_t)__shfl(v, (int)(min(produced - i0, 64u) - 1u));
+    }
+    __threadfence_block();
+    for (uint32_t k = produced + lane; s + k < end; k += 64) o[s + k] = o[s + (k % produced)];
 }
 
 struct DecLds {
@@ -1684,6 +1725,10 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
         const PX_GAS uint8_t *qb =
             slots && uni(q.idx) < nrec ? (const PX_GAS uint8_t *)uni64((uint64_t)slot_at(slots, uni(q.idx)).comp) : nullptr;
         const uint32_t qcap = uni(q.out_cap);
+        // the top frame's ret cursor in record coordinates: a piece [from, to) of a compat drain
+        // cut at token starts continues the whole drain's cursor (the self-overlap test of a
+        // record token compares against it, PiXiuStr.h:163-170)
+        const int32_t qbase = unii((int32_t)q.pad);
         uint32_t outp = 0, err = 0, depth = 0;
         bool capped = false;
 
@@ -1724,6 +1769,7 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
         // f.seg must go through the serial path next.
         auto window = [&](Frame &f, const SlotV &sv) -> bool {
             if (!sv.lane) return true;  // no lane entries: the serial path takes every segment
+            const int32_t rbase = depth == 1 ? qbase : 0;
             const uint32_t outp0 = outp;
             const int32_t ret0 = f.ret;
             uint32_t next = f.seg;     // next unassigned segment
@@ -1798,7 +1844,7 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                             ++reqc;
                     } else if (active && enter) {
                         sub_to = min(rto, sub_from + need);
-                        const int32_t stp = compat ? ret_l : max(sx, f.from);
+                        const int32_t stp = compat ? ret_l + rbase : max(sx, f.from);
                         if (ridx >= nrec || (sub_from < stp && stp < sub_to && ridx == f.rec)) {
                             fl = true;
                             PX_FR(1);
@@ -2034,6 +2080,7 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
 #endif
             if (stop_key != 0xffffffffu && (stop_key >> 1) <= next) {
                 PX_CNT(P_D_COMMIT, (stop_key >> 1) - f.seg);
+                out_clear(o, stop_out, run_out);
                 f.seg = stop_key >> 1;
                 outp = stop_out;
                 f.ret = stop_ret;
@@ -2074,6 +2121,7 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
             f.sub_to = unii(f.sub_to);
             f.supply = unii(f.supply);
             const SlotV sv = slot_uniform(slots, f.rec);
+            const int32_t rbase = depth == 1 ? qbase : 0;
             bool pop = false;
 
             if (f.state != 0) {  // a child just returned
@@ -2090,8 +2138,7 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                         if (produced < n) {
                             uint32_t end = min(f.pstart + n, f.cap);
                             __threadfence_block();
-                            for (uint32_t k = produced + lane; f.pstart + k < end; k += 64)
-                                o[f.pstart + k] = o[f.pstart + (k % produced)];
+                            out_repeat(o, f.pstart, produced, end);
                             outp = end;
                             if (outp >= f.cap) pop = true;
                         }
@@ -2120,7 +2167,7 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                     if (sx - 1 + supply >= f.from) {
                         int32_t sub_from = rfrom + max(0, f.from - sx);
                         int32_t sub_to = min(rto, sub_from + (f.len - f.ret));
-                        int32_t stop = compat ? f.ret : max(sx, f.from);
+                        int32_t stop = compat ? f.ret + rbase : max(sx, f.from);
                         bool periodic = sub_from < stop && stop < sub_to && (uint32_t)ridx == f.rec;
                         f.state = periodic ? 2 : 1;
                         f.pstart = outp;
@@ -2202,44 +2249,65 @@ __global__ void __launch_bounds__(64 * kDecWaves) k_decode_addr(const DecodeQuer
 }
 
 // ====================================================================== spans
-// Span build: one wave per record scans its address decode.  A span starts where the
-// address is not the previous one + 1.  Count pass: spans (| kSpanBad for a source out
+// Span build: one wave per record scans its address decode (run starts, kAddrMark between:
+// each byte's address is expanded from its run's start).  A span starts where the address is
+// not the previous one + 1.  Count pass: spans (| kSpanBad for a source out
 // of the relative range, | kSpanEq when the expansion equals the doc, i.e. compat ==
 // exact).  Write pass: {rel, start} entries plus the {0, len} sentinel.
 PX_DEV void span_job(const SpanJob &jb) {
     const uint32_t lane = lane_id();
-    const PX_GAS int32_t *a = (const PX_GAS int32_t *)jb.addr;
     const PX_GAS uint8_t *base = (const PX_GAS uint8_t *)jb.base;
     const PX_GAS uint8_t *doc = (const PX_GAS uint8_t *)jb.doc;
     PX_GAS SpanEnt *out = (PX_GAS SpanEnt *)jb.out;
     const uint32_t len = uni(jb.len);
     uint32_t cnt = 0;
     bool bad = false, eq = doc && len == uni(jb.doc_len);
-    int32_t prev_last = kAddrNone;  // address of byte k0 - 1 (lane 63 of the last step)
-    for (uint32_t k0 = 0; k0 < len; k0 += 64) {
-        const uint32_t k = k0 + lane;
-        const bool in = k < len;
-        const int32_t v = in ? a[k] : 0;
-        int32_t pv = __shfl_up(v, 1);
-        if (lane == 0) pv = prev_last;
-        const bool start = in && (k == 0 || pv == kAddrNone || v != pv + 1);
-        bad = bad || (bool)ballot(in && v == kAddrNone);
-        if (eq) eq = !ballot(in && (v == kAddrNone || base[v] != doc[k]));
-        const uint64_t m = ballot(start);
-        if (out && !bad) {
-            const uint32_t rank =
-                __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-            if (start) {
-                PX_GAS uint32_t *e = (PX_GAS uint32_t *)(out + cnt + rank);
-                e[0] = (uint32_t)v;
-                e[1] = k;
-            }
-            // tile index: the span holding byte k, at every tile start
-            if (jb.tix && in && (k % kGatherTile) == 0)
-                ((PX_GAS uint32_t *)jb.tix)[k / kGatherTile] = cnt + rank + (start ? 1u : 0u) - 1u;
+    int32_t prev_last = kAddrNone;  // address of the byte before k0 (lane 63 of the last step)
+    // pieces: output bytes [o, o + pn) of the record are at a (a piece's bytes are contiguous)
+    const uint32_t np = jb.pq ? uni(jb.last) - uni(jb.first) : 1u;
+    uint32_t o = 0;
+    for (uint32_t pi = 0; pi < np; ++pi) {
+        const PX_GAS int32_t *a = (const PX_GAS int32_t *)jb.addr;
+        uint32_t pn = len;
+        if (jb.pq) {
+            const uint32_t j = uni(jb.first) + pi;
+            a += uni64(jb.pq[j].out_off);
+            pn = min(uni(jb.pl[j]), len - o);
         }
-        cnt += (uint32_t)__popcll(m);
-        prev_last = __shfl(v, 63);
+        for (uint32_t i0 = 0; i0 < pn; i0 += 64) {
+            const uint32_t i = i0 + lane, k = o + i;
+            const bool in = i < pn;
+            // the byte's address: its run's start address + its distance from the start (the
+            // latest start at or below the lane, else the previous window's last address + 1)
+            const int32_t raw = in ? a[i] : kAddrMark;
+            const uint64_t le = ballot(in && raw != kAddrMark) & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
+            const uint32_t sl = le ? 63u - (uint32_t)__clzll((long long)le) : 0u;
+            const int32_t sv = (int32_t)__shfl(raw, (int)sl);
+            const int32_t rb = le ? sv : prev_last;
+            const int32_t v = !in ? 0 : rb == kAddrNone ? kAddrNone : rb + (le ? (int32_t)(lane - sl) : (int32_t)lane + 1);
+            int32_t pv = __shfl_up(v, 1);
+            if (lane == 0) pv = prev_last;
+            const bool start = in && (k == 0 || pv == kAddrNone || v != pv + 1);
+            bad = bad || (bool)ballot(in && v == kAddrNone);
+            if (eq) eq = !ballot(in && (v == kAddrNone || base[v] != doc[k]));
+            const uint64_t m = ballot(start);
+            if (out && !bad) {
+                const uint32_t rank =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                if (start) {
+                    PX_GAS uint32_t *e = (PX_GAS uint32_t *)(out + cnt + rank);
+                    e[0] = (uint32_t)v;
+                    e[1] = k;
+                }
+                // tile index: the span holding byte k, at every tile start
+                if (jb.tix && in && (k % kGatherTile) == 0)
+                    ((PX_GAS uint32_t *)jb.tix)[k / kGatherTile] = cnt + rank + (start ? 1u : 0u) - 1u;
+            }
+            cnt += (uint32_t)__popcll(m);
+            const uint32_t nl = min(pn - i0, 64u);  // (the piece's last byte of this step)
+            prev_last = __shfl(v, (int)(nl - 1));
+        }
+        o += pn;
     }
     if (out && !bad && lane == 0) {
         PX_GAS uint32_t *e = (PX_GAS uint32_t *)(out + cnt);
@@ -2260,14 +2328,19 @@ __global__ void __launch_bounds__(256) k_span_jobs(uint32_t n, const DecodeQuery
                                                    const RecSlot *const *chunk_slots, const int32_t *addr,
                                                    uint32_t *cnt, uint32_t *ents, uint32_t *tiles,
                                                    const uint32_t *eoff_incl, const uint32_t *toff_incl, SpanEnt *tab,
-                                                   uint32_t *tixb) {
+                                                   uint32_t *tixb, const DecodeQuery *pq, const uint32_t *pl,
+                                                   const uint32_t *pfirst) {
     const uint32_t lane = lane_id();
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);
     for (uint32_t j = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); j < n; j += waves) {
         const DecodeQuery &q = dq[j];
         const uint32_t st = uni(ds[j]), len = uni(dl[j]);
         SpanJob jb;
-        jb.addr = addr + q.out_off;
+        jb.addr = pq ? addr : addr + q.out_off;
+        jb.pq = pq;
+        jb.pl = pl;
+        jb.first = pq ? pfirst[j] : 0u;
+        jb.last = pq ? pfirst[j + 1] : 0u;
         jb.base = chunk_slots[uni(q.chunk)][uni(q.idx)].comp;
         jb.doc = src[j].doc;
         jb.len = len;
@@ -2680,32 +2753,92 @@ hipError_t launch_slot_place(hipStream_t s, uint32_t n, const RecSlot *src, cons
 // A record decoded in pieces (the exact span build: exact parses of consecutive ranges are
 // the consecutive slices of the doc): its length = the pieces' sum, its status = the first
 // failing piece's.  first[k] .. first[k + 1] are record k's pieces.
+// A record's pieces that reach its whole decode's room (cap) report kErrSpace, as the whole
+// decode would.
 __global__ void __launch_bounds__(256) k_span_agg(uint32_t n, const uint32_t *first, const uint32_t *pl,
-                                                  const uint32_t *ps, uint32_t *dl, uint32_t *ds) {
+                                                  const uint32_t *ps, const DecodeQuery *dq, uint32_t *dl, uint32_t *ds) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
-    uint32_t len = 0, st = kOk;
+    uint64_t len = 0;
+    uint32_t st = kOk;
     for (uint32_t j = first[k]; j < first[k + 1]; ++j) {
         len += pl[j];
         if (st == kOk) st = ps[j];
     }
-    dl[k] = len;
+    if (st == kOk && len >= dq[k].out_cap) st = kErrSpace;
+    dl[k] = (uint32_t)min<uint64_t>(len, 0xffffffffu);
     ds[k] = st;
 }
 hipError_t launch_span_agg(hipStream_t s, uint32_t n, const uint32_t *first, const uint32_t *pl, const uint32_t *ps,
-                           uint32_t *dl, uint32_t *ds) {
+                           const DecodeQuery *dq, uint32_t *dl, uint32_t *ds) {
     if (!n) return hipSuccess;
-    k_span_agg<<<(n + 255) / 256, 256, 0, s>>>(n, first, pl, ps, dl, ds);
+    k_span_agg<<<(n + 255) / 256, 256, 0, s>>>(n, first, pl, ps, dq, dl, ds);
+    return hipGetLastError();
+}
+
+// Compat pieces cut at token starts (build_spans): sub-query j is piece m of its record, nominal
+// range [m * P, (m + 1) * P) of the record's source positions (from = m * P; out_off = the
+// record's output base + 64 * m).  Its bounds move to the first token starting at or after
+// each end (so a piece drains whole top-level tokens and the pieces' outputs, in order, are the
+// whole drain's: PXSGen's ret cursor only counts requested bytes, PiXiuStr.h:136-192), its
+// output to base + start + 64 * m with the piece's bytes + 64 of room, and `pad` carries the ret
+// cursor at its start.  A record without a position index (source positions not monotone) or
+// whose tokens cover more than its doc is drained whole by its piece 0.
+__global__ void __launch_bounds__(256) k_span_pieces(uint32_t ns, DecodeQuery *sq, const RecSlot *const *chunk_slots,
+                                                     uint32_t piece) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= ns) return;
+    DecodeQuery q = sq[j];
+    const uint32_t m = (uint32_t)q.from / piece, L = q.pad;  // (pad: the record's doc length, on the way in)
+    const uint64_t base = q.out_off - 64ull * m;
+    const RecSlot *sl = chunk_slots[q.chunk] + q.idx;
+    const uint32_t nseg = sl->nseg;
+    const uint4 *seg = (const uint4 *)sl->seg;
+    const uint16_t *pidx = (const uint16_t *)sl->pidx;
+    const uint32_t S = nseg ? seg[2 * nseg].x : 0u;  // (the end sentinel's position: the tokens' total)
+    const bool split = nseg && sl->pidx_n && sl->lane && S <= L;
+    auto bound = [&](uint32_t t) -> uint32_t {  // the first token start at or after t
+        if (t == 0) return 0;
+        if (t >= S) return S;
+        uint32_t k = (t >> 4) < sl->pidx_n ? min((uint32_t)pidx[t >> 4], nseg) : nseg;
+        while (k > 0 && seg[2 * k].x > t) --k;  // (a position index entry is the segment holding 16b)
+        while (k < nseg && seg[2 * k].y <= t) ++k;
+        return k >= nseg ? S : (seg[2 * k].x >= t ? seg[2 * k].x : seg[2 * k].y);
+    };
+    if (!split) {
+        q.from = 0;
+        q.to = m == 0 ? (int32_t)kMaxDoc : 0;
+        q.out_off = base;
+        q.out_cap = m == 0 ? q.out_cap : 16u;  // (piece 0 keeps the whole record's room)
+        q.pad = 0;
+    } else {
+        const uint32_t a = bound(m * piece), nominal_end = (m + 1) * piece;
+        const bool last = nominal_end >= L;
+        const uint32_t b = last ? S : bound(nominal_end);
+        q.from = (int32_t)a;
+        q.to = last ? (int32_t)kMaxDoc : (int32_t)b;
+        q.out_off = base + a + 64ull * m;
+        q.out_cap = b - a + 64u;
+        q.pad = a;
+    }
+    sq[j] = q;
+}
+hipError_t launch_span_pieces(hipStream_t s, uint32_t ns, DecodeQuery *sq, const RecSlot *const *chunk_slots,
+                              uint32_t piece) {
+    if (!ns) return hipSuccess;
+    k_span_pieces<<<(ns + 255) / 256, 256, 0, s>>>(ns, sq, chunk_slots, piece);
     return hipGetLastError();
 }
 
 hipError_t launch_span_jobs(hipStream_t s, uint32_t n, const DecodeQuery *dq, const uint32_t *dl, const uint32_t *ds,
                             const SpanSrc *src, const RecSlot *const *chunk_slots, const int32_t *addr, uint32_t *cnt,
                             uint32_t *ents, uint32_t *tiles, const uint32_t *eoff_incl, const uint32_t *toff_incl,
-                            SpanEnt *tab, uint32_t *tixb) {
+                            SpanEnt *tab, uint32_t *tixb, const DecodeQuery *pq, const uint32_t *pl,
+                            const uint32_t *pfirst) {
     if (!n) return hipSuccess;
     k_span_jobs<<<std::min<uint32_t>((n + 3) / 4, 16384), 256, 0, s>>>(n, dq, dl, ds, src, chunk_slots, addr, cnt, ents,
-                                                                       tiles, eoff_incl, toff_incl, tab, tixb);
+                                                                       tiles, eoff_incl, toff_incl, tab, tixb, pq, pl,
+                                                                       pfirst);
     return hipGetLastError();
 }
 

@@ -53,11 +53,13 @@ hipError_t launch_rehash(hipStream_t, const uint4 *, uint32_t, uint32_t, uint4 *
 hipError_t launch_decode_addr(hipStream_t, const DecodeQuery *, uint32_t, const RecSlot *const *, int32_t *,
                               uint32_t *, uint32_t *, Frame *, uint32_t, uint32_t);
 hipError_t launch_slot_place(hipStream_t, uint32_t, const RecSlot *, const uint32_t *, const SlotDst *, LinkJob *);
-hipError_t launch_span_agg(hipStream_t, uint32_t, const uint32_t *, const uint32_t *, const uint32_t *, uint32_t *,
-                           uint32_t *);
+hipError_t launch_span_agg(hipStream_t, uint32_t, const uint32_t *, const uint32_t *, const uint32_t *,
+                           const DecodeQuery *, uint32_t *, uint32_t *);
+hipError_t launch_span_pieces(hipStream_t, uint32_t, DecodeQuery *, const RecSlot *const *, uint32_t);
 hipError_t launch_span_jobs(hipStream_t, uint32_t, const DecodeQuery *, const uint32_t *, const uint32_t *,
                             const SpanSrc *, const RecSlot *const *, const int32_t *, uint32_t *, uint32_t *,
-                            uint32_t *, const uint32_t *, const uint32_t *, SpanEnt *, uint32_t *);
+                            uint32_t *, const uint32_t *, const uint32_t *, SpanEnt *, uint32_t *, const DecodeQuery *,
+                            const uint32_t *, const uint32_t *);
 uint64_t gather_task_bytes(uint32_t);
 hipError_t launch_gather(hipStream_t, uint32_t, const uint32_t *, uint64_t, void *, const GatherQuery *, uint32_t,
                          uint8_t *, uint32_t *, uint32_t *);
@@ -1013,10 +1015,9 @@ struct px_ctx {
     }
 
     // Runs decode queries; out_dev is a device buffer.  Returns per-query len/status.
-    // `addr` runs k_decode_addr instead (the span build: 4-byte address elements,
-    // out_off in elements); getitem batches (timed) send span-served queries to k_gather.
+    // getitem batches (timed) send span-served queries to k_gather.
     void run_decode(const std::vector<DecodeQuery> &q, uint8_t *out_dev, std::vector<uint32_t> &len,
-                    std::vector<uint32_t> &st, bool timed, int32_t *addr = nullptr) {
+                    std::vector<uint32_t> &st, bool timed) {
         uint32_t nq = (uint32_t)q.size();
         len.assign(nq, 0);
         st.assign(nq, 0);
@@ -1047,7 +1048,7 @@ struct px_ctx {
             qn[j].nrec = src.chunk == kNone ? 0 : chunks[src.chunk].n;
         }
         std::vector<GatherQuery> gq;
-        if (timed && !addr) gq = take_gathers(qn, 0, nq, 0);
+        if (timed) gq = take_gathers(qn, 0, nq, 0);
         stats.last_gather_queries = timed ? (uint32_t)gq.size() : stats.last_gather_queries;
         // every found key gathered: no walk launch (the host answers the missing keys)
         bool walk = false;
@@ -1061,9 +1062,6 @@ struct px_ctx {
             return !(e && e[0] == '0');
         }();
         if (!walk) {
-        } else if (addr) {
-            hcheck(launch_decode_addr(stream, dq, nq, (const RecSlot *const *)chunk_tab, addr, dl, ds, frames, depth,
-                                      waves | (xcd ? 0x80000000u : 0u)));
         } else {
             hcheck(launch_decode(stream, dq, nq, (const RecSlot *const *)chunk_tab, out_dev, dl, ds, frames, depth,
                                  waves | (xcd ? 0x80000000u : 0u), !timed));
@@ -1101,7 +1099,7 @@ struct px_ctx {
         uint32_t chunk, idx;
         const uint8_t *doc;
     };
-    void build_spans(const std::vector<SpanReq> &reqs_in, uint32_t mode = 0, bool exact_too = true) {
+    void build_spans(const std::vector<SpanReq> &reqs_in, uint32_t mode = 0, bool exact_too = true, bool split = true) {
         if (reqs_in.empty() || !spans_enabled()) return;
         std::vector<SpanReq> sorted_reqs;
         const std::vector<SpanReq> *rp = &reqs_in;
@@ -1118,18 +1116,35 @@ struct px_ctx {
         PhaseClock phase(mode ? "build_spans (exact)" : "build_spans", "PX_SET_VERBOSE");
         phase.mark("queries and sources");
         // queries (pinned) and sources
+        // Records are decoded in pieces of kPiece source bytes, one wave each (a config-3 batch
+        // has 10,000 records of 60 KB: whole, their waves kept the decode at 19 ms).
+        //  * exact: an exact parse of [a, b) of a record whose exact expansion is its doc is the
+        //    doc's slice, so the pieces' addresses land side by side; a record whose pieces do
+        //    not reassemble its doc (one near a length-251 alias token: its exact expansion is
+        //    not its doc, and its doc coordinates are not the decoder's) is decoded again whole;
+        //  * compat: pieces are cut at token starts (k_span_pieces) and carry the whole drain's
+        //    ret cursor, so each drains the same top-level tokens as the whole drain, to the
+        //    same bytes; each lands 64 bytes past the previous piece's nominal end (an
+        //    over-yield has room) and k_span_jobs reads the pieces in order.  A record whose
+        //    pieces fail or reach the whole decode's room is decoded again whole.
+        constexpr uint32_t kPiece = 4096;
+        const char *split_env = std::getenv("PX_SPAN_SPLIT");
+        const bool compat_split = !(split_env && split_env[0] == '0');
+        split = split && (mode == 1 || compat_split);
         auto *qn = (DecodeQuery *)hq_buf.get((uint64_t)n * sizeof(DecodeQuery));
         std::vector<SpanSrc> src(n);
         uint64_t tot = 0;
         for (uint32_t k = 0; k < n; ++k) {
             const SpanReq &r = reqs[k];
             const Chunk &ch = chunks[r.chunk];
-            const uint32_t cap = (uint32_t)round_up(ch.doc_len[r.idx] + 64, 16);
+            const uint32_t L = ch.doc_len[r.idx];
+            const uint32_t cap = (uint32_t)round_up(L + 64, 16);
             qn[k] = DecodeQuery{r.chunk, r.idx, 0, kMaxDoc, tot, cap, mode, ch.n, 0};
-            src[k] = SpanSrc{r.doc, ch.doc_len[r.idx], 0};
-            tot += cap;
+            src[k] = SpanSrc{r.doc, L, 0};
+            tot += cap + (split && mode == 0 ? 64ull * std::max<uint32_t>(1, (L + kPiece - 1) / kPiece) : 0ull);
         }
         auto *addr = (int32_t *)heap.alloc(tot * 4 + 64);
+        hcheck(hipMemsetD32Async((hipDeviceptr_t)addr, kAddrMark, tot, stream));  // (k_decode_addr writes run starts only)
         // device: queries, lengths + statuses, sources, counts / entries / tiles and their scans
         const uint64_t o_dl = round_up((uint64_t)n * sizeof(DecodeQuery), 256), o_src = o_dl + round_up((uint64_t)n * 8, 256),
                        o_u32 = o_src + round_up((uint64_t)n * sizeof(SpanSrc), 256), o_end = o_u32 + (uint64_t)n * 20 + 256;
@@ -1150,25 +1165,28 @@ struct px_ctx {
             return !(e && e[0] == '0');
         }();
         const auto *ctab = (const RecSlot *const *)chunk_tab;
-        // exact tables: every record decoded in pieces of kExactPiece bytes, one wave each (an exact
-        // parse of [a, b) is the doc's slice, so the pieces' addresses land side by side; the
-        // ~1,000 records of a config-3 batch with compat != exact kept 1,000 waves busy for 6.8 ms)
-        constexpr uint32_t kExactPiece = 4096;
         uint64_t sub_bytes = 0;
         uint8_t *sub_buf = nullptr;
-        if (mode == 1) {
+        DecodeQuery *sdq = nullptr;
+        uint32_t *dfirst = nullptr, *pl = nullptr;
+        if (split) {
             std::vector<DecodeQuery> sq;
             std::vector<uint32_t> first(n + 1, 0);
             for (uint32_t k = 0; k < n; ++k) {
                 first[k] = (uint32_t)sq.size();
                 const uint32_t L = src[k].doc_len;
-                for (uint32_t a = 0; a < L || (a == 0 && L == 0); a += kExactPiece) {
-                    const uint32_t b = std::min(L, a + kExactPiece);
+                for (uint32_t a = 0, m = 0; a < L || (a == 0 && L == 0); a += kPiece, ++m) {
+                    const uint32_t b = std::min(L, a + kPiece);
                     DecodeQuery d = qn[k];
                     d.from = (int32_t)a;
                     d.to = (int32_t)b;
-                    d.out_off = qn[k].out_off + a;
-                    d.out_cap = b - a + 16;  // (exactly b - a bytes come; room past them keeps the cap from firing)
+                    if (mode == 1) {
+                        d.out_off = qn[k].out_off + a;
+                        d.out_cap = b - a + 16;  // (exactly b - a bytes come; room past them keeps the cap from firing)
+                    } else {
+                        d.out_off = qn[k].out_off + 64ull * m;  // (k_span_pieces adds the piece's start)
+                        d.pad = L;
+                    }
                     sq.push_back(d);
                     if (L == 0) break;
                 }
@@ -1179,20 +1197,22 @@ struct px_ctx {
             const uint64_t o_pl = o_first + round_up((uint64_t)(n + 1) * 4, 256);
             sub_bytes = o_pl + (uint64_t)ns * 8 + 256;
             sub_buf = (uint8_t *)heap.alloc(sub_bytes);
-            auto *sdq = (DecodeQuery *)sub_buf;
-            auto *dfirst = (uint32_t *)(sub_buf + o_first);
-            auto *pl = (uint32_t *)(sub_buf + o_pl), *ps = pl + ns;
+            sdq = (DecodeQuery *)sub_buf;
+            dfirst = (uint32_t *)(sub_buf + o_first);
+            pl = (uint32_t *)(sub_buf + o_pl);
+            uint32_t *ps = pl + ns;
             h2d(sdq, sq.data(), (size_t)ns * sizeof(DecodeQuery));
             h2d(dfirst, first.data(), (size_t)(n + 1) * 4);
+            if (mode == 0) hcheck(launch_span_pieces(stream, ns, sdq, ctab, kPiece));
             const uint32_t sw = std::min<uint32_t>(opts.decode_waves ? opts.decode_waves : 16384, ns);
             auto *sframes = (Frame *)scratch_frames.get((uint64_t)sw * depth * sizeof(Frame));
             hcheck(launch_decode_addr(stream, sdq, ns, ctab, addr, pl, ps, sframes, depth, sw | (xcd ? 0x80000000u : 0u)));
-            hcheck(launch_span_agg(stream, n, dfirst, pl, ps, dl, ds));
+            hcheck(launch_span_agg(stream, n, dfirst, pl, ps, dq, dl, ds));
         } else {
             hcheck(launch_decode_addr(stream, dq, n, ctab, addr, dl, ds, frames, depth, waves | (xcd ? 0x80000000u : 0u)));
         }
         hcheck(launch_span_jobs(stream, n, dq, dl, ds, dsrc, ctab, addr, cnt, ents, tiles, nullptr, nullptr, nullptr,
-                                nullptr));
+                                nullptr, sdq, pl, dfirst));
         const SortAlloc SA{[](void *self, uint64_t bytes) -> void * { return static_cast<px_ctx *>(self)->heap.alloc(bytes); },
                            [](void *self, void *p, uint64_t bytes) { static_cast<px_ctx *>(self)->heap.release(p, bytes); },
                            this};
@@ -1223,6 +1243,18 @@ struct px_ctx {
             for (auto &w : why) fprintf(stderr, " status %u x%u", w.first, w.second);
             fprintf(stderr, "\n");
         }
+        // split decodes to do again whole: exact ones that are not the doc, compat ones that
+        // failed (the whole decode decides those records)
+        std::vector<SpanReq> redo;
+        std::vector<uint8_t> skip(n, 0);
+        if (split)
+            for (uint32_t j = 0; j < n; ++j) {
+                const bool bad = (hc[j] & kSpanBad) != 0;
+                if (mode == 0 ? bad : (!bad && (!(hc[j] & kSpanEq) || hl[j] != src[j].doc_len))) {
+                    redo.push_back(reqs[j]);
+                    skip[j] = 1;
+                }
+            }
         uint64_t nents = 0, ntiles = 0;
         for (uint32_t j = 0; j < n; ++j)
             if (!(hc[j] & kSpanBad)) {
@@ -1236,10 +1268,17 @@ struct px_ctx {
             auto *tab = (SpanEnt *)heap.alloc(tab_bytes);
             store_blocks.emplace_back(tab, tab_bytes);
             auto *tixb = (uint32_t *)((uint8_t *)tab + round_up(nents * sizeof(SpanEnt), 64));
-            hcheck(launch_span_jobs(stream, n, dq, dl, ds, dsrc, ctab, addr, cnt, ents, tiles, eoff, toff, tab, tixb));
+            hcheck(launch_span_jobs(stream, n, dq, dl, ds, dsrc, ctab, addr, cnt, ents, tiles, eoff, toff, tab, tixb, sdq,
+                                    pl, dfirst));
             uint64_t o = 0, to = 0;
             for (uint32_t j = 0; j < n; ++j) {
                 if (hc[j] & kSpanBad) continue;
+                const uint32_t ns0 = hc[j] & ~(kSpanBad | kSpanEq);
+                if (skip[j]) {  // (its entries are written but not used: the whole decode replaces them)
+                    o += ns0 + 1;
+                    to += (hl[j] + kGatherTile - 1) / kGatherTile;
+                    continue;
+                }
                 Chunk &ch = chunks[reqs[j].chunk];
                 if (ch.span.size() < ch.n) ch.span.resize(ch.n);
                 const uint32_t ns = hc[j] & ~(kSpanBad | kSpanEq);
@@ -1266,6 +1305,7 @@ struct px_ctx {
         if (sub_buf) heap.release(sub_buf, sub_bytes);
         heap.release(wb, o_end);
         heap.release(addr, tot * 4 + 64);
+        if (!redo.empty()) build_spans(redo, mode, false, false);
         phase.mark("exact tables");
         if (mode == 0 && exact_too) {  // exact tables for the records whose compat expansion is not the doc
             std::vector<SpanReq> x;
@@ -3019,14 +3059,24 @@ int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int m
     // keys up through pinned memory (one copy of the bytes and the rebased offsets)
     auto *hb = (uint8_t *)dk_hbuf.get(o_gq);
     auto *ho = (uint64_t *)(hb + o_off);
-    // (a million-key batch: 16 MB staged, on the host threads)
-    parallel_ranges(n + 1, n >= 65536 ? host_threads() : 1, [&](uint32_t lo, uint32_t hi) {
-        const uint64_t a = koff[lo] - k0, b = (hi > n ? koff[n] : koff[hi]) - k0;
-        std::memcpy(hb + a, keys + k0 + a, b - a);
-        for (uint32_t i = lo; i < hi; ++i) ho[i] = koff[i] - k0;
-    });
-    phase.mark("uploads and launches");
-    hcheck(hipMemcpyAsync(dkeys, hb, o_off + (uint64_t)(n + 1) * 8, hipMemcpyHostToDevice, stream));
+    // (a million-key batch: 16 MB staged on the host threads, in parts whose uploads start
+    // while the next part is staged)
+    const uint32_t parts = n >= 65536 ? 4u : 1u;
+    for (uint32_t part = 0; part < parts; ++part) {
+        const uint32_t r0 = (uint32_t)((uint64_t)(n + 1) * part / parts), r1 = (uint32_t)((uint64_t)(n + 1) * (part + 1) / parts);
+        parallel_ranges(r1 - r0, n >= 65536 ? host_threads() : 1, [&](uint32_t lo, uint32_t hi) {
+            lo += r0;
+            hi += r0;
+            const uint64_t a = koff[lo] - k0, b = (hi > n ? koff[n] : koff[hi]) - k0;
+            std::memcpy(hb + a, keys + k0 + a, b - a);
+            for (uint32_t i = lo; i < hi; ++i) ho[i] = koff[i] - k0;
+        });
+        // (part p uploads its key bytes and offsets; the last part also the bytes' tail to o_off)
+        const uint64_t ka = koff[r0] - k0, kb = part + 1 == parts ? o_off : (r1 > n ? koff[n] : koff[r1]) - k0;
+        hcheck(hipMemcpyAsync(dkeys + ka, hb + ka, kb - ka, hipMemcpyHostToDevice, stream));
+        hcheck(hipMemcpyAsync(doff + r0, ho + r0, (uint64_t)(r1 - r0) * 8, hipMemcpyHostToDevice, stream));
+    }
+    phase.mark("launches");
     hcheck(hipMemsetAsync(chain, 0, nb * 16 + 32, stream));
     flush_tab();
     hcheck(hipEventRecord(ev0, stream));
@@ -3065,21 +3115,27 @@ int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int m
     stats.last_gather_queries = n;
     stats.last_get_device_keys = n;
     const uint32_t *ro = (const uint32_t *)res, *rl = ro + n;
+    const uint32_t *rs = nullptr;
+    if (hr[5]) {  // (statuses only when some query ran past its room)
+        uint32_t *h = (uint32_t *)dk_hres.get(o_end - o_ctl) + (o_ds - o_ctl) / 4;
+        hcheck(hipMemcpy(h, ds, (size_t)n * 4, hipMemcpyDeviceToHost));
+        rs = h;
+    }
     parallel_ranges(n, n >= 65536 ? host_threads() : 1, [&](uint32_t lo, uint32_t hi) {
         for (uint32_t i = lo; i < hi; ++i) out_off[i] = (uint64_t)ro[i] * 16;
         std::memcpy(out_len + lo, rl + lo, (size_t)(hi - lo) * 4);
+        if (rs)
+            for (uint32_t i = lo; i < hi; ++i) status[i] = map_status(rs[i]);
+        else
+            std::fill(status + lo, status + hi, (uint32_t)PX_OK);
     });
     int rc = PX_OK;
-    if (hr[5]) {
-        uint32_t *rs = (uint32_t *)dk_hres.get(o_end - o_ctl) + (o_ds - o_ctl) / 4;
-        hcheck(hipMemcpy(rs, ds, (size_t)n * 4, hipMemcpyDeviceToHost));
-        for (uint32_t i = 0; i < n; ++i) {
-            status[i] = map_status(rs[i]);
-            if (status[i] != PX_OK && rc == PX_OK) rc = (int)status[i];
-        }
-    } else {
-        std::fill(status, status + n, (uint32_t)PX_OK);
-    }
+    if (rs)
+        for (uint32_t i = 0; i < n; ++i)
+            if (status[i] != PX_OK) {
+                rc = (int)status[i];
+                break;
+            }
     if (needed) *needed = total;
     return rc;
 }
@@ -3542,8 +3598,9 @@ int px_get_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *k
         rc = ctx->opts.decode_waves == 0
                  ? ctx->dki_get(n, keys, koff, mode, out, out_cap, out_on_device, out_off, out_len, status, needed)
                  : -1;
-        if (rc != -1) {
-            // (resolved on the device: no host lookups)
+        const bool on_device = rc != -1;
+        if (on_device) {
+            // (resolved on the device: no host lookups; rc is the first failing status)
         } else if (out_on_device && n >= 4096 && ctx->opts.decode_waves == 0) {
             rc = ctx->get_overlapped(n, keys, koff, mode, out, out_cap, out_off, out_len, status, needed, lookup_ms);
         } else {
@@ -3558,7 +3615,7 @@ int px_get_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *k
             lookup_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
             rc = ctx->expand(q, out, out_cap, out_on_device, out_off, out_len, status, needed, pre);
         }
-        if (rc == PX_OK)
+        if (rc == PX_OK && !on_device)
             for (uint32_t i = 0; i < n; ++i)
                 if (status[i] != PX_OK) {
                     rc = (int)status[i];

@@ -88,3 +88,80 @@ def test_gather_capped_output(store_factory):
     h = buf.cpu().numpy()
     got = [h[int(o):int(o) + int(l)].tobytes() for o, l in zip(off, ln)]
     assert got == st.get_batch(keys)
+
+
+def test_exact_tables_near_length_251_aliases(store_factory):
+    """Config 5 at the bench's shard size (126 records of 65,531 B): some records' streams
+    hold a length-251 run token, which the decoder reads as an escape (the reference's alias,
+    PiXiuStr.cpp:61-78), so their exact expansion is not their doc.  The exact span tables
+    (built from 4 KB pieces, and whole for records whose pieces do not reassemble the doc)
+    must serve what the walk decodes (PX_SPANS=0), record by record."""
+    from pixiu_amd import synth
+    n, rps = 252, 126
+    cp = synth.make(5, n)
+    keys = [cp.key(i) for i in range(n)]
+
+    def run():
+        st = store_factory(records_per_shard=rps)
+        st.set_batch((cp.keys, cp.koff.astype(np.uint64)), (cp.vals, cp.voff.astype(np.uint64)))
+        return st.get_batch(keys, mode=px.EXACT), st.get_batch(keys)
+
+    e1, g1 = _with_spans(True, run)
+    e0, g0 = _with_spans(False, run)
+    assert g1 == g0
+    assert e1 == e0
+    docs = [assemble(cp.key(i), cp.val(i)) for i in range(n)]
+    assert sum(e != d for e, d in zip(e1, docs)) < n  # (most exact expansions are their docs)
+
+
+def _small_alphabet_docs(seed, n, lo, hi):
+    """Docs over a few symbols with 251s and repeats of earlier material: self-referencing
+    record tokens (the periodic case), 251 pairs at token edges, long nesting."""
+    rng = np.random.default_rng(seed)
+    alpha = np.frombuffer(b"ab<\xfb", np.uint8)
+    keys, vals = [], []
+    for i in range(n):
+        L = int(rng.integers(lo, hi))
+        v = alpha[rng.integers(0, len(alpha), L)].copy()
+        for _ in range(int(rng.integers(1, 8))):  # copies of earlier parts, some overlapping
+            a = int(rng.integers(0, L // 2))
+            d = int(rng.integers(1, 64))
+            m = int(rng.integers(16, L // 3))
+            for k in range(m):
+                if a + d + k < L:
+                    v[a + d + k] = v[a + k]
+        keys.append(b"k%05d" % i)
+        vals.append(v.tobytes())
+    return keys, vals
+
+
+@pytest.mark.parametrize("rps", [0, 40])
+def test_compat_tables_in_pieces(rps, store_factory):
+    """Compat span tables decoded in 4 KB pieces cut at token starts (k_span_pieces) equal the
+    whole-record decode (PX_SPAN_SPLIT=0) and the walk (PX_SPANS=0), compat and exact, on docs
+    of 2-20 KB with self-referencing tokens and 251 runs."""
+    keys, vals = _small_alphabet_docs(7 + rps, 120, 2000, 20000)
+
+    def run():
+        st = store_factory(records_per_shard=rps)
+        r = st.set_batch(keys, vals)
+        assert int(r["status"].max()) == 0
+        g = st.get_batch(keys)
+        gq = st.stats()["last_gather_queries"]
+        return g, st.get_batch(keys, mode=px.EXACT), gq
+
+    old = os.environ.get("PX_SPAN_SPLIT")
+    try:
+        os.environ["PX_SPAN_SPLIT"] = "1"
+        g1, e1, q1 = _with_spans(True, run)
+        os.environ["PX_SPAN_SPLIT"] = "0"
+        g2, e2, q2 = _with_spans(True, run)
+    finally:
+        if old is None:
+            os.environ.pop("PX_SPAN_SPLIT", None)
+        else:
+            os.environ["PX_SPAN_SPLIT"] = old
+    g0, e0, _ = _with_spans(False, run)
+    assert q1 == q2 and q1 >= 0.5 * len(keys)
+    assert g1 == g2 == g0
+    assert e1 == e2 == e0
