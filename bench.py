@@ -379,9 +379,17 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
     gather_buf = [None]
     gathered = [None]
     st = px.Store(records_per_shard=rps, device=local, retain_mb=a.retain_mb)
-    # the getitem results land in host arrays reused every step (written once here: a fresh
-    # array's pages fault on first write, 4 K of them for config 4's million keys)
-    into = (np.ones(n, np.uint64), np.ones(n, np.uint32), np.ones(n, np.uint32))
+    # getitem takes the keys where setitem took them (HBM: kb / ko) and leaves its offsets,
+    # lengths and statuses in HBM (px_get_batch_dev); the pcie_inclusive leg times host keys
+    # and host results
+    r_off = torch.empty(n, dtype=torch.int64, device=dev)
+    r_len = torch.empty(n, dtype=torch.int32, device=dev)
+    r_sts = torch.empty(n, dtype=torch.int32, device=dev)
+
+    def get_dev(buf, mode):
+        rc, need = st.get_batch_dev(n, kb.data_ptr(), ko.data_ptr(), buf.data_ptr(), out_cap, r_off.data_ptr(),
+                                    r_len.data_ptr(), r_sts.data_ptr(), mode)
+        return rc, need
 
     def step():
         tr = time.perf_counter()
@@ -395,7 +403,7 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
                sst["last_psa_sort_ms"], sst["last_psa_lcp_ms"], sst["last_psa_msg_ms"], int(sst["last_psa_iters"]),
                int(sst["last_psa_rounds"]), int(sst["last_psa_rotations"]), sst["last_psa_pool_ms"], int(sst["chunks"]))
         t1 = time.perf_counter()  # (the set stats above are instrumentation, outside both timings)
-        rc, off, ln, sts, need = st.get_batch_device(keys_host, out.data_ptr(), out_cap, px.COMPAT, into=into)
+        rc, need = get_dev(out, px.COMPAT)
         t2 = time.perf_counter()
         gst = st.stats()
         dec_kms, look_ms, call_ms = gst["last_decode_kernel_ms"], gst["last_get_lookup_ms"], gst["last_get_call_ms"]
@@ -420,8 +428,8 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
         # setitem's one exchange (the compressed-blob gather to rank 0) counts as setitem time
         return {"set_s": t_set + g_ms * 1e-3, "get_s": t2 - t1, "reset_s": t0 - tr, "set_kms": set_kms, "walk_kms": walk_kms,
                 "emit_kms": emit_kms, "dec_kms": dec_kms, "gather_ms": g_ms, "look_ms": look_ms,
-                "call_ms": call_ms, "comp": int(res["comp_len"].sum()), "exp": int(ln.sum()), "res": res,
-                "off": off, "len": ln, "psa": psa, "spans": spans}
+                "call_ms": call_ms, "comp": int(res["comp_len"].sum()), "exp": int(r_len.sum(dtype=torch.int64)),
+                "res": res, "psa": psa, "spans": spans}
 
     for _ in range(warmup):
         step()
@@ -437,6 +445,8 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
     r = {"corpus": corpus, "st": st, "runs": runs, "elapsed": T1 - T0, "n": n, "raw": raw_bytes,
          "out": out, "out_cap": out_cap, "keys_host": keys_host, "gathered": gathered[0]}
     last = runs[-1]
+    last["off"] = r_off.cpu().numpy().astype(np.uint64)  # (the last step's results, for the checks)
+    last["len"] = r_len.cpu().numpy().astype(np.uint32)
     # every record against the reference's own output (per-record digests made from the
     # compiled reference over the same corpus part and shards, tests/_refdig.py); only the
     # canonical part 0 at full size has them (not in --no-checks runs: the profiling legs)
@@ -454,8 +464,9 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
     out2 = torch.empty(out_cap, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
     te = time.perf_counter()
-    rc, eoff, eln, ests, _ = st.get_batch_device(keys_host, out2.data_ptr(), out_cap, px.EXACT)
+    rc, _ = get_dev(out2, px.EXACT)
     r["exact_s"] = time.perf_counter() - te
+    eoff, eln = r_off.cpu().numpy().astype(np.uint64), r_len.cpu().numpy().astype(np.uint32)
     r["exact_dec_kms"] = st.stats()["last_decode_kernel_ms"]
     r["exact_gather"] = int(st.stats()["last_gather_queries"])
     r["exact_exp"] = int(eln.sum())

@@ -18,6 +18,7 @@
  *   px_set_docs ............... PiXiuCtrl::setitem(k, 0, NULL, 0, reinsert)  (PiXiuCtrl.cpp:26-40, ready docs)
  *   px_flush .................. (none: the write-behind queue of one-record setitem calls)
  *   px_get_batch .............. PiXiuCtrl::getitem + PXSGen drain   (PiXiuCtrl.cpp:59-61, PiXiuStr.h:129-198)
+ *   px_get_batch_dev .......... the same, keys and results in device memory
  *   px_contains_batch ......... PiXiuCtrl::contains                 (PiXiuCtrl.cpp:55-57)
  *   px_del_batch .............. PiXiuCtrl::delitem                  (PiXiuCtrl.cpp:63-69)
  *   px_iter ................... PiXiuCtrl::iter -> CBTGen           (PiXiuCtrl.cpp:71-75, CritBitTree.h:55-157)
@@ -178,6 +179,16 @@ int px_flush(px_ctx *ctx, px_set_result *last);
 int px_get_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff, int mode,
                  uint8_t *out, uint64_t out_cap, int out_on_device, uint64_t *out_off,
                  uint32_t *out_len, uint32_t *status, uint64_t *needed);
+
+/* Batch getitem with everything in device memory: keys + koff[n + 1] (CSR offsets into
+ * keys), out, out_off / out_len / status (n entries each) are device pointers; the results are
+ * written on the device and complete when the call returns.  Same results and return codes as
+ * px_get_batch, except that when out_cap is too small only *needed is defined (with
+ * PX_ESPACE).  Keys the device key index does not answer go the host path (keys copied down,
+ * results up). */
+int px_get_batch_dev(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff, int mode,
+                     uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint32_t *out_len,
+                     uint32_t *status, uint64_t *needed);
 
 /* Batch PiXiuStr::parse(from, to) of stored records (the kernel-level boundary). */
 int px_parse_batch(px_ctx *ctx, uint32_t n, const px_rec *recs, int mode, uint8_t *out,

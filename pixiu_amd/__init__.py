@@ -86,7 +86,7 @@ REC_DTYPE = np.dtype([("shard", "<u4"), ("chunk", "<u4"), ("idx", "<u4"), ("from
 EXPORTS = ["px_open", "px_close", "px_strerror", "px_set_batch", "px_get_batch", "px_parse_batch",
            "px_contains_batch", "px_del_batch", "px_export", "px_stats_get", "px_stream", "px_reset",
            "px_last_store", "px_import_chunk", "px_iter", "px_save", "px_load", "px_locate_batch", "px_reinsert",
-           "px_set_docs", "px_flush", "px_trim"]
+           "px_set_docs", "px_flush", "px_trim", "px_get_batch_dev"]
 
 _LIB = None
 
@@ -108,6 +108,7 @@ def load_library() -> C.CDLL:
     lib.px_strerror.argtypes = [i32]
     lib.px_set_batch.argtypes = [vp, u32, vp, vp, vp, vp, i32, vp]
     lib.px_get_batch.argtypes = [vp, u32, vp, vp, i32, vp, u64, i32, vp, vp, vp, vp]
+    lib.px_get_batch_dev.argtypes = [vp, u32, vp, vp, i32, vp, u64, vp, vp, vp, vp]
     lib.px_parse_batch.argtypes = [vp, u32, vp, i32, vp, u64, i32, vp, vp, vp, vp]
     lib.px_contains_batch.argtypes = [vp, u32, vp, vp, vp]
     lib.px_del_batch.argtypes = [vp, u32, vp, vp, vp]
@@ -280,6 +281,15 @@ class Store:
         rc, _, off, ln, st, need = self._expand(self._lib.px_get_batch, n, (_ptr(kb), _ptr(ko), mode),
                                                 out_ptr, out_cap, into)
         return rc, off, ln, st, need
+
+    def get_batch_dev(self, n: int, keys_ptr: int, koff_ptr: int, out_ptr: int, out_cap: int, off_ptr: int,
+                      len_ptr: int, status_ptr: int, mode: int = COMPAT):
+        """getitem with device-resident keys (CSR: bytes + n + 1 u64 offsets) and results (u64
+        offsets, u32 lengths, u32 statuses, n each): px_get_batch_dev.  Returns (rc, needed)."""
+        need = np.zeros(1, np.uint64)
+        rc = self._lib.px_get_batch_dev(self._h, n, keys_ptr, koff_ptr, mode, out_ptr, out_cap, off_ptr, len_ptr,
+                                        status_ptr, _ptr(need))
+        return rc, int(need[0])
 
     def get_batch_host(self, keys, out: np.ndarray, mode: int = COMPAT):
         """Expand into a caller-owned host buffer (one call, no retry); returns

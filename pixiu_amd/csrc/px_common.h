@@ -155,6 +155,16 @@ struct alignas(16) LaneEnt {
 static_assert(sizeof(LaneEnt) == 16, "LaneEnt is one 16-byte vector");
 constexpr int32_t kRelNone = (int32_t)0x80000000;
 
+// a record token as k_gst_emit wrote it: k_tok_segs builds the record's segment index from its
+// tokens (the plain segments lie between them) instead of parsing the compressed bytes again
+struct alignas(16) TokEnt {
+    uint32_t x;   // doc position of the run the token stands for (its source position)
+    uint32_t o;   // comp offset of the token
+    uint32_t w;   // idx | from << 16 (SegEnt::aux)
+    uint32_t rs;  // run length | token bytes << 16
+};
+constexpr uint32_t kTokBad = 1u << 31;  // a record's token count flag: parse its bytes (k_tokenize) instead
+
 // compressed-record slot: what a chunk table entry points at
 struct alignas(16) RecSlot {
     const uint8_t *comp;    // compressed bytes

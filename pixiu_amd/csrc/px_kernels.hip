@@ -1013,18 +1013,29 @@ __global__ void __launch_bounds__(64 * kGstWaves, 6) k_gst_encode(const GstShard
 //     and PASS messages are their doc bytes, literally.
 // Output offsets come from a wave prefix sum of the per-position output sizes; the
 // open run, the pair parity and the output cursor carry between steps.
+// toks (optional): every record token it writes, in order, at toks + tok_off[r] (room for
+// doc_len / 7 + 2), their count in ntok[r] (| kTokBad where the bytes must be parsed instead: a
+// run of length 251, whose length byte reads as an escape pair -- the reference's alias --, a
+// `from` that wraps below 0, a corrupt or failed record).
 __global__ void __launch_bounds__(256) k_gst_emit(uint32_t n, const uint8_t *const *doc_ptr, const uint32_t *doc_len,
                                                   uint8_t *const *comp_dst, const uint8_t *comp_base,
-                                                  const uint32_t *msgs, uint32_t *rec_status, uint32_t *comp_len) {
+                                                  const uint32_t *msgs, uint32_t *rec_status, uint32_t *comp_len,
+                                                  const uint64_t *tok_off, TokEnt *toks, uint32_t *ntok) {
     const uint32_t lane = lane_id();
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);
     const uint64_t below = (1ull << lane) - 1;
     for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < n; r += waves) {
         const uint32_t len = uni(doc_len[r]);
         if (len == 0xffffffffu || uni(rec_status[r]) != kOk) {
-            if (lane == 0) comp_len[r] = 0;
+            if (lane == 0) {
+                comp_len[r] = 0;
+                if (ntok) ntok[r] = kTokBad;
+            }
             continue;
         }
+        PX_GAS TokEnt *tk = toks ? (PX_GAS TokEnt *)toks + uni64(tok_off[r]) : nullptr;
+        uint32_t ntk = 0;
+        bool tbad = false;
         const PX_GAS uint8_t *doc = (const PX_GAS uint8_t *)doc_ptr[r];
         PX_GAS uint8_t *out = (PX_GAS uint8_t *)comp_dst[r];
         const PX_GAS uint32_t *msg = (const PX_GAS uint32_t *)msgs + (comp_dst[r] - comp_base);
@@ -1087,6 +1098,31 @@ __global__ void __launch_bounds__(256) k_gst_emit(uint32_t n, const uint8_t *con
             if (end) size += run_size(rl);
             const int32_t incl = wave_incl_scan_dpp((int32_t)size);
             uint32_t o = outp + (uint32_t)incl - size;
+            if (tk) {  // the step's record tokens, in output order (lane 0's flushed run comes first)
+                uint32_t tx = 0, tl = 0, tm = 0, tof = 0;
+                bool has = false;
+                if (flush_prev && ws - open_start > 6) {
+                    has = true;
+                    tx = open_start;
+                    tl = ws - open_start;
+                    tm = open_msg;
+                    tof = o;
+                } else if (end && rl > 6) {
+                    has = true;
+                    tx = start;
+                    tl = rl;
+                    tm = m;
+                    tof = o + pre;
+                }
+                const uint64_t hm = ballot(has);
+                if (has) {
+                    const uint32_t to = ((tm & 0xffffu) + 1u) & 0xffffu, from = (to - tl) & 0xffffu;
+                    tbad = tbad || tl == 251u || to < tl;
+                    *(PX_GAS u32x4 *)(tk + ntk + (uint32_t)__popcll(hm & below)) =
+                        mk4(tx, tof, (tm >> 16) | from << 16, tl | (tl > 255 ? 8u : 6u) << 16);
+                }
+                ntk += (uint32_t)__popcll(hm);
+            }
             if (flush_prev) {
                 run_out(o, ws - open_start, open_msg, open_start);
                 o += pre;
@@ -1099,9 +1135,11 @@ __global__ void __launch_bounds__(256) k_gst_emit(uint32_t n, const uint8_t *con
             open_start = ((em >> 63) & 1) ? uni(readlane(start, 63)) : ws + 64;
             open_msg = uni(readlane(m, 63));
         }
+        tbad = ballot(tbad) != 0;
         if (lane == 0) {
             comp_len[r] = outp;
             if (corrupt) rec_status[r] = kErrCorrupt;
+            if (ntok) ntok[r] = ntk | (tbad || corrupt ? kTokBad : 0u);
         }
     }
 }
@@ -1200,10 +1238,11 @@ PX_DEV void put_ent(PX_GAS SegEnt *seg, uint32_t k, u32x4 lo, uint64_t ptr) {
 }
 
 __global__ void __launch_bounds__(256) k_tokenize(uint32_t n, const RecSlot *slots_in, uint32_t *nseg_out,
-                                                  uint32_t *status) {
+                                                  uint32_t *status, const uint32_t *ntok) {
     const uint32_t lane = lane_id();
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);
     for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < n; r += waves) {
+        if (ntok && !(uni(ntok[r]) & kTokBad)) continue;  // (k_tok_segs built it from the encoder's tokens)
         const RecSlot sl = slots_in[r];
         const PX_GAS uint8_t *comp = (const PX_GAS uint8_t *)sl.comp;
         const uint64_t comp_addr = (uint64_t)sl.comp;
@@ -1325,6 +1364,99 @@ __global__ void __launch_bounds__(256) k_tokenize(uint32_t n, const RecSlot *slo
         if (lane == 0) {
             nseg_out[r] = err ? 0 : (ns | (mono && pidx_n ? 0u : kNoPidx));
             status[r] = err;
+        }
+    }
+}
+
+// The segment index of a record from the tokens k_gst_emit wrote (the same entries k_tokenize
+// parses out of the compressed bytes: plain segments between the record tokens, each token
+// covering its run's doc positions, then the end sentinel), 64 tokens per step, one wave per
+// record.  Records flagged kTokBad are left to k_tokenize (launched after it), and so is a
+// record whose stored bytes do not hold its tokens (a record not placed: comp_len 0).
+__global__ void __launch_bounds__(256) k_tok_segs(uint32_t n, const RecSlot *slots_in, const uint32_t *doc_len,
+                                                  const uint64_t *tok_off, const TokEnt *toks, uint32_t *ntok,
+                                                  uint32_t *nseg_out, uint32_t *status) {
+    const uint32_t lane = lane_id();
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < n; r += waves) {
+        const uint32_t nt = uni(ntok[r]);
+        if (nt & kTokBad) continue;
+        const RecSlot sl = slots_in[r];
+        const uint64_t comp_addr = uni64((uint64_t)sl.comp);
+        const uint32_t clen = uni(sl.comp_len), L = uni(doc_len[r]), pidx_n = uni(sl.pidx_n);
+        PX_GAS SegEnt *seg = (PX_GAS SegEnt *)uni64((uint64_t)sl.seg);
+        PX_GAS uint16_t *pidx = (PX_GAS uint16_t *)uni64((uint64_t)sl.pidx);
+        PX_GAS LaneEnt *lanes = (PX_GAS LaneEnt *)uni64((uint64_t)sl.lane);
+        const PX_GAS TokEnt *tk = (const PX_GAS TokEnt *)toks + uni64(tok_off[r]);
+        bool fits = clen > 0 && L <= 0xffffu;
+        if (fits && nt) {
+            const u32x4 t = *(const PX_GAS u32x4 *)(tk + nt - 1);  // (tokens come in comp order: x, o, w, rs)
+            fits = t.y + (t.w >> 16) <= clen && t.x + (t.w & 0xffffu) <= L;
+        }
+        if (!uni((uint32_t)fits)) {
+            if (lane == 0) ntok[r] = nt | kTokBad;
+            continue;
+        }
+        // one segment: its entry, its lane entry, its position-index blocks
+        auto put = [&](uint32_t k, uint32_t x, uint32_t ex, uint32_t kz, uint32_t w) {
+            const bool plain = (kz >> 30) == 0;
+            const uint64_t ptr = plain ? comp_addr + (kz & kSegMask) : 0;
+            put_ent(seg, k, mk4(x, ex, kz, w), ptr);
+            if (lanes) {
+                const int64_t d = (int64_t)comp_addr - (int64_t)(uint64_t)(lanes + k);
+                *(PX_GAS u32x4 *)(lanes + k) = mk4(x | ex << 16, kz, w, plain ? (uint32_t)(int32_t)(d >> 3) : (uint32_t)kRelNone);
+            }
+            if (pidx_n)
+                for (uint32_t b = (x + 15) >> 4, b1 = min((ex + 15) >> 4, pidx_n); b < b1; ++b) pidx[b] = (uint16_t)k;
+        };
+        uint32_t ns = 0, px = 0, po = 0;  // segments so far; doc position and comp offset after the last token
+        for (uint32_t i0 = 0; i0 < nt; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            const bool in = i < nt;
+            u32x4 tv = mk4(0, 0, 0, 0);
+            if (in) tv = *(const PX_GAS u32x4 *)(tk + i);
+            const TokEnt t{tv.x, tv.y, tv.z, tv.w};
+            const uint32_t rl = t.rs & 0xffffu, sz = t.rs >> 16;
+            // the doc position and comp offset after the previous token
+            uint32_t ex_prev = (uint32_t)__shfl_up((int)(t.x + rl), 1), eo_prev = (uint32_t)__shfl_up((int)(t.o + sz), 1);
+            if (lane == 0) {
+                ex_prev = px;
+                eo_prev = po;
+            }
+            const bool plain = in && t.o > eo_prev;
+            const uint32_t c = in ? (plain ? 2u : 1u) : 0u;
+            uint32_t incl = c;
+            for (uint32_t o = 1; o < 64; o <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+                if (lane >= o) incl += y;
+            }
+            const uint32_t k0 = ns + incl - c;
+            if (plain) put(k0, ex_prev, t.x, eo_prev, 0u);
+            if (in) put(k0 + (plain ? 1u : 0u), t.x, t.x + rl, t.o | kSegRecord, t.w);
+            const uint32_t last = min(nt - i0, 64u) - 1u;
+            ns += (uint32_t)__shfl((int)incl, (int)last);
+            px = (uint32_t)__shfl((int)(t.x + rl), (int)last);
+            po = (uint32_t)__shfl((int)(t.o + sz), (int)last);
+        }
+        if (lane == 0) {
+            if (po < clen) put(ns++, px, L, po, 0u);  // the doc's last plain bytes
+            put_ent(seg, ns, mk4(L, L, clen | kSegEnd, 0), 0);
+            if (lanes) *(PX_GAS u32x4 *)(lanes + ns) = mk4(L | L << 16, clen | kSegEnd, 0, 0);
+        }
+        ns = uni(readlane(ns, 0));
+        // blocks past the source end: no segment
+        if (pidx_n)
+            for (uint32_t b = (L + 15) / 16 + lane; b < pidx_n; b += 64) pidx[b] = (uint16_t)min(ns, 65535u);
+        // lane entries need 16-bit coordinates and a comp base within +-16 GiB (k_tokenize's rule)
+        bool mono = true;
+        if (lanes) {
+            const int64_t d0 = (int64_t)comp_addr - (int64_t)(uint64_t)lanes,
+                          d1 = (int64_t)comp_addr - (int64_t)(uint64_t)(lanes + ns);
+            mono = mono && (d0 >> 3) == (int64_t)(int32_t)(d0 >> 3) && (d1 >> 3) == (int64_t)(int32_t)(d1 >> 3);
+        }
+        if (lane == 0) {
+            nseg_out[r] = ns | (mono && pidx_n ? 0u : kNoPidx);
+            status[r] = kOk;
         }
     }
 }
@@ -2671,10 +2803,12 @@ hipError_t launch_gst_encode(hipStream_t s, const GstShard *shards, uint32_t n_s
 
 hipError_t launch_gst_emit(hipStream_t s, uint32_t n, const uint8_t *const *doc_ptr, const uint32_t *doc_len,
                            uint8_t *const *comp_dst, const uint8_t *comp_base, const uint32_t *msgs,
-                           uint32_t *rec_status, uint32_t *comp_len) {
+                           uint32_t *rec_status, uint32_t *comp_len, const uint64_t *tok_off, TokEnt *toks,
+                           uint32_t *ntok) {
     if (!n) return hipSuccess;
     const uint32_t blocks = min((n + 3) / 4, 8192u);
-    k_gst_emit<<<blocks, 256, 0, s>>>(n, doc_ptr, doc_len, comp_dst, comp_base, msgs, rec_status, comp_len);
+    k_gst_emit<<<blocks, 256, 0, s>>>(n, doc_ptr, doc_len, comp_dst, comp_base, msgs, rec_status, comp_len, tok_off,
+                                      toks, ntok);
     return hipGetLastError();
 }
 
@@ -2713,10 +2847,18 @@ hipError_t launch_link(hipStream_t s, uint32_t n, const LinkJob *jobs) {
     return hipGetLastError();
 }
 
-hipError_t launch_tokenize(hipStream_t s, uint32_t n, const RecSlot *slots, uint32_t *nseg_out, uint32_t *status) {
+hipError_t launch_tokenize(hipStream_t s, uint32_t n, const RecSlot *slots, uint32_t *nseg_out, uint32_t *status,
+                           const uint32_t *ntok) {
     if (!n) return hipSuccess;
     uint32_t blocks = min((n + 3) / 4, 8192u);
-    k_tokenize<<<blocks, 256, 0, s>>>(n, slots, nseg_out, status);
+    k_tokenize<<<blocks, 256, 0, s>>>(n, slots, nseg_out, status, ntok);
+    return hipGetLastError();
+}
+hipError_t launch_tok_segs(hipStream_t s, uint32_t n, const RecSlot *slots, const uint32_t *doc_len, const uint64_t *tok_off,
+                           const TokEnt *toks, uint32_t *ntok, uint32_t *nseg_out, uint32_t *status) {
+    if (!n) return hipSuccess;
+    uint32_t blocks = min((n + 3) / 4, 8192u);
+    k_tok_segs<<<blocks, 256, 0, s>>>(n, slots, doc_len, tok_off, toks, ntok, nseg_out, status);
     return hipGetLastError();
 }
 

@@ -229,7 +229,29 @@ __global__ void __launch_bounds__(256) k_dk_lookup(uint32_t nq, const uint8_t *q
     }
 }
 
+// A device-resident batch's results into the caller's device arrays: byte offsets, lengths and
+// statuses (px_status codes: the device codes 0..7 are the same numbers, anything else is
+// PX_ECORRUPT).  Nothing is written when a key missed (ctl[0]: the host path answers that
+// batch) or the output did not fit (nothing was gathered either).
+__global__ void __launch_bounds__(256) k_dk_results(uint32_t n, const uint32_t *ctl, uint64_t out_cap,
+                                                    const uint32_t *out_off16, const uint32_t *dl, const uint32_t *ds,
+                                                    uint64_t *out_off, uint32_t *out_len, uint32_t *status) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || ctl[0] || (uint64_t)ctl[1] * 16u > out_cap) return;
+    out_off[i] = (uint64_t)out_off16[i] * 16u;
+    out_len[i] = dl[i];
+    const uint32_t s = ctl[5] ? ds[i] : 0u;  // (statuses are only written when a query ran past its room)
+    status[i] = s <= 7u ? s : 4u;
+}
+
 }  // namespace
+
+hipError_t launch_dk_results(hipStream_t s, uint32_t n, const uint32_t *ctl, uint64_t out_cap, const uint32_t *out_off16,
+                             const uint32_t *dl, const uint32_t *ds, uint64_t *out_off, uint32_t *out_len, uint32_t *status) {
+    if (!n) return hipSuccess;
+    k_dk_results<<<(n + 255) / 256, 256, 0, s>>>(n, ctl, out_cap, out_off16, dl, ds, out_off, out_len, status);
+    return hipGetLastError();
+}
 
 hipError_t launch_dk_insert(hipStream_t s, uint32_t gid0, uint32_t n, const DkRec *rec, const uint8_t *keys, DkSlot *tab,
                             uint32_t mask, uint32_t *err) {

@@ -78,17 +78,6 @@ __global__ void __launch_bounds__(256) k_psa_gather(uint32_t ndocs, const PsaDoc
     }
 }
 
-// group heads of the first sort: a new group at a key change, and every suffix shorter
-// than `syms` symbols (its key holds its whole string, so its last symbol is 0: equal ones
-// are equal strings, kept in position order by the stable sort and resolved as they are)
-__global__ void __launch_bounds__(256) k_psa_head0(uint32_t N, const uint64_t *keys, uint32_t *hflag) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= N) return;
-    const uint64_t k = keys[r] & kKeyMask;
-    const bool complete = (k & 511u) == 0;
-    hflag[r] = (r == 0 || k != (keys[r - 1] & kKeyMask) || complete) ? r : 0u;
-}
-
 // ---------------------------------------------------------------- unsorted groups
 // Prefix doubling keeps the suffixes that still share their first h symbols with another
 // suffix in GROUPS: a group is a range [start, start + size) of the suffix array, and
@@ -369,29 +358,93 @@ PSA_DEV void push_long(const LongLists &L, bool valid, uint64_t ent) {
     }
 }
 
-// rank = group head index, sd = the doubling reach in suffix-array order (the sorted keys'
-// kDlShift bits: steps whose key is a rank), act / gsz of the first groups (tag 0: step 0
-// sorts them).  A group's size is written at its start by its last element; every other
-// slot writes its own gsz (0)
-__global__ void __launch_bounds__(256) k_psa_groups0(uint32_t N, const uint32_t *sa, const uint32_t *head,
-                                                     const uint64_t *skeys, uint32_t *rank, uint16_t *sd, uint8_t *act,
-                                                     uint32_t *gsz, StepStat ss) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t a = 0, mx = 0;
-    if (r < N) {
-        const uint32_t p = sa[r], hd = head[r];
+// The first groups, in one pass over the sorted keys (the group heads' max-scan by decoupled
+// look-back over workgroups in the order they start).  A group starts at a key change and at
+// every suffix shorter than `syms` symbols (its key holds its whole string, so its last symbol
+// is 0: equal ones are equal strings, kept in position order by the stable sort and resolved as
+// they are).  rank = group head index, sd = the doubling reach in suffix-array order (the
+// sorted keys' kDlShift bits: steps whose key is a rank), act / gsz of the first groups (tag 0:
+// step 0 sorts them).  A group's size is written at its start by its last element; every
+// other slot writes its own gsz (0).  chain: one word per workgroup and the ticket after them,
+// zeroed by the caller; a word is flag << 62 | (head + 1), the flag 1 for the workgroup's own
+// last head (0: none in it), 2 for the last head at or before its end.
+constexpr unsigned long long kG0Agg = 1ull << 62, kG0Incl = 2ull << 62, kG0Val = (1ull << 62) - 1ull;
+PSA_DEV bool head_at(const uint64_t *skeys, uint32_t N, uint32_t r) {
+    if (r == 0 || r >= N) return true;
+    const uint64_t k = skeys[r] & kKeyMask;
+    return k != (skeys[r - 1] & kKeyMask) || (k & 511u) == 0;
+}
+constexpr uint32_t kG0Rows = 16, kG0Slots = kG0Rows * 256;  // slots per workgroup: rows of 256
+__global__ void __launch_bounds__(256) k_psa_groups0(uint32_t N, const uint32_t *sa, const uint64_t *skeys,
+                                                     unsigned long long *chain, uint32_t *err, uint32_t *rank, uint16_t *sd,
+                                                     uint8_t *act, uint32_t *gsz, StepStat ss) {
+    __shared__ uint32_t s_bid, s_w[2][4], s_pre;
+    const uint32_t nb = gridDim.x;
+    if (threadIdx.x == 0) s_bid = atomicAdd((uint32_t *)(chain + nb), 1u);  // (tickets: look-back never waits on a later one)
+    __syncthreads();
+    const uint32_t bid = s_bid, base = bid * kG0Slots, lane = lane_id(), w = threadIdx.x >> 6;
+    // row i = slots base + 256 i + (0..255): inclusive max-scan of (head + 1) in slot order
+    uint32_t hv[kG0Rows], hnm = 0, carry = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kG0Rows; ++i) {
+        const uint32_t r = base + i * 256u + threadIdx.x;
+        const bool f = r < N && head_at(skeys, N, r);
+        if (r < N && head_at(skeys, N, r + 1)) hnm |= 1u << i;  // r + 1 starts the next group (or the end)
+        uint32_t v = f ? r + 1u : 0u;
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)v, o);
+            if (lane >= o) v = max(v, y);
+        }
+        if (lane == 63) s_w[i & 1][w] = v;
+        __syncthreads();  // (rows alternate between two exchange slots: one barrier per row)
+        for (uint32_t x = 0; x < w; ++x) v = max(v, s_w[i & 1][x]);
+        hv[i] = max(v, carry);
+        carry = max(carry, max(max(s_w[i & 1][0], s_w[i & 1][1]), max(s_w[i & 1][2], s_w[i & 1][3])));
+    }
+    if (threadIdx.x == 0) {
+        const uint32_t agg = carry;
+        // a workgroup holding a head knows its inclusive value at once
+        __hip_atomic_store(chain + bid, (agg || bid == 0 ? kG0Incl : kG0Agg) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t pre = 0, spins = 0;
+        if (bid > 0 && !head_at(skeys, N, base)) {  // (its first slot's head lies before it)
+            for (uint32_t j = bid - 1;;) {
+                const unsigned long long x = __hip_atomic_load(chain + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (!(x >> 62)) {
+                    if (++spins > (1u << 24)) {  // (cannot happen: the batch fails loudly)
+                        atomicOr(err, 1u);
+                        break;
+                    }
+                    continue;
+                }
+                pre = max(pre, (uint32_t)(x & kG0Val));
+                if ((x >> 62) == 2 || j == 0) break;
+                --j;
+            }
+            if (!agg) __hip_atomic_store(chain + bid, kG0Incl | pre, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_pre = pre;
+    }
+    __syncthreads();
+    const uint32_t pre = s_pre;
+    uint32_t a_all = 0, mx = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kG0Rows; ++i) {
+        const uint32_t r = base + i * 256u + threadIdx.x;
+        if (r >= N) break;
+        const bool hn = (hnm >> i) & 1u;
+        const uint32_t hd = max(hv[i], pre) - 1u, p = sa[r];
         rank[p] = hd;
-        const bool hn = r + 1 == N || head[r + 1] == r + 1;  // r + 1 starts the next group
-        a = (hd != r || !hn) ? 1u : 0u;                       // in a group of >= 2
+        const uint32_t a = (hd != r || !hn) ? 1u : 0u;  // in a group of >= 2
+        a_all += a;
         sd[r] = a ? (uint16_t)((skeys[r] >> kDlShift) & 15u) : (uint16_t)0;
         act[r] = (uint8_t)a;
         if (!(hd == r && !hn)) gsz[r] = 0;  // (not the start of a group of >= 2)
         if (hn && hd != r) {                // the last element of a group of >= 2
             gsz[hd] = r - hd + 1;
-            mx = r - hd + 1;
+            mx = max(mx, r - hd + 1);
         }
     }
-    block_stat(ss, 0, a, mx);
+    block_stat(ss, 0, a_all, mx);
 }
 
 // this step's keys: rank of the suffix h further on (+1), 0 past the doc end (step `it` of
@@ -1905,9 +1958,6 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         S.put(segs);
         S.put(va);
         S.put(vb);
-        uint32_t *hflag = (uint32_t *)keys, *head = (uint32_t *)keys + N;  // (the pass buffers are spent)
-        k_psa_head0<<<blocks(N), tb, 0, s>>>(N, keys2, hflag);
-        PSA_CHECK(scan_u32(s, SA, hflag, head, N, ScanOp::kMax, false));
     }
     // ---- the first groups, then prefix doubling over them
     auto *sd = S.get<uint16_t>(n64 * 2);
@@ -1920,7 +1970,12 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     PSA_CHECK(hipMemsetAsync(stat_sh, 0, (size_t)(kMaxSteps + 1) * kStatShards * kStatStride * 4, s));
     auto region = [&](uint32_t k) { return StepStat{stat_sh + (uint64_t)k * kStatShards * kStatStride}; };
     auto stats_of = [&](uint32_t k) { return region(k + 1); };
-    k_psa_groups0<<<blocks(N), tb, 0, s>>>(N, sa, (const uint32_t *)keys + N, keys2, rank, sd, act, gsz, region(0));
+    {
+        auto *chain = (unsigned long long *)keys;  // (the pass buffers are spent: the look-back chain and its ticket)
+        const uint32_t g0 = (uint32_t)((n64 + kG0Slots - 1) / kG0Slots);
+        PSA_CHECK(hipMemsetAsync(chain, 0, ((uint64_t)g0 + 1) * 8, s));
+        k_psa_groups0<<<g0, 256, 0, s>>>(N, sa, keys2, chain, cnt + kCntSortErr, rank, sd, act, gsz, region(0));
+    }
     k_stat_sum<<<1, 64, 0, s>>>(region(0).sh, cnt + kCntSorted + kMaxSteps, cnt + kCntActive, cnt + kCntMax);
     S.put(keys);
     S.put(keys2);

@@ -42,9 +42,11 @@ hipError_t psa_run(hipStream_t, const PsaAlloc &, uint32_t, const PsaDoc *, uint
                    uint32_t,
                    uint32_t *, uint32_t *, uint32_t *, uint32_t *, bool, PsaPoolOut *, PsaStats *);
 hipError_t launch_gst_emit(hipStream_t, uint32_t, const uint8_t *const *, const uint32_t *, uint8_t *const *,
-                           const uint8_t *, const uint32_t *, uint32_t *, uint32_t *);
+                           const uint8_t *, const uint32_t *, uint32_t *, uint32_t *, const uint64_t *, TokEnt *, uint32_t *);
 hipError_t launch_compact(hipStream_t, uint32_t, uint8_t *const *, const uint32_t *, uint8_t *, const uint64_t *);
-hipError_t launch_tokenize(hipStream_t, uint32_t, const RecSlot *, uint32_t *, uint32_t *);
+hipError_t launch_tokenize(hipStream_t, uint32_t, const RecSlot *, uint32_t *, uint32_t *, const uint32_t *);
+hipError_t launch_tok_segs(hipStream_t, uint32_t, const RecSlot *, const uint32_t *, const uint64_t *, const TokEnt *,
+                           uint32_t *, uint32_t *, uint32_t *);
 hipError_t launch_count_esc(hipStream_t, uint32_t, uint8_t *const *, const uint32_t *, uint32_t *);
 hipError_t launch_link(hipStream_t, uint32_t, const LinkJob *);
 hipError_t launch_decode(hipStream_t, const DecodeQuery *, uint32_t, const RecSlot *const *, uint8_t *,
@@ -66,6 +68,8 @@ hipError_t launch_gather(hipStream_t, uint32_t, const uint32_t *, uint64_t, void
 hipError_t launch_dk_insert(hipStream_t, uint32_t, uint32_t, const DkRec *, const uint8_t *, DkSlot *, uint32_t,
                             uint32_t *);
 hipError_t launch_dk_kill(hipStream_t, uint32_t, const uint32_t *, DkRec *);
+hipError_t launch_dk_results(hipStream_t, uint32_t, const uint32_t *, uint64_t, const uint32_t *, const uint32_t *,
+                             const uint32_t *, uint64_t *, uint32_t *, uint32_t *);
 hipError_t launch_dk_lookup(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, const DkSlot *, uint32_t,
                             const DkRec *, const uint8_t *, uint32_t, GatherQuery *, uint32_t *, uint32_t *,
                             unsigned long long *, const uint32_t *);
@@ -505,8 +509,10 @@ struct px_ctx {
         hcheck(launch_dk_kill(stream, (uint32_t)kills.size(), d, dki.rec));
     }
     DevBuf dk_kbuf;
+    // dev_io: keys, koff, out_off, out_len and status are device pointers (px_get_batch_dev)
     int dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int mode, uint8_t *out, uint64_t out_cap,
-                int out_on_device, uint64_t *out_off, uint32_t *out_len, uint32_t *status, uint64_t *needed);
+                int out_on_device, uint64_t *out_off, uint32_t *out_len, uint32_t *status, uint64_t *needed,
+                bool dev_io = false);
     DevBuf dk_qbuf, dk_obuf;
     HostBuf dk_hbuf, dk_hres;
 
@@ -2189,7 +2195,20 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
                                  d_idx, d_status, d_stout, sink));
     }
     hcheck(hipEventRecord(ev_mid, stream));
-    hcheck(launch_gst_emit(stream, n, d_dst, d_doclen, d_cdst, comp_scratch, msgs, d_status, d_complen));
+    // the encoder's record tokens (k_tok_segs builds the segment index from them): room for
+    // doc_len / 7 + 2 per record (a token stands for a run of 7 or more doc bytes)
+    uint64_t tok_n = 0;
+    std::vector<uint64_t> tok_off(n);
+    for (uint32_t r = 0; r < n; ++r) {
+        tok_off[r] = tok_n;
+        tok_n += doc_len[r] == 0xffffffffu ? 0 : doc_len[r] / 7 + 2;
+    }
+    auto *d_toks = (TokEnt *)heap.alloc(tok_n * sizeof(TokEnt) + 64);
+    auto *d_tokoff = (uint64_t *)heap.alloc((uint64_t)n * 12 + 64);
+    auto *d_ntok = (uint32_t *)(d_tokoff + n);
+    h2d(d_tokoff, tok_off.data(), (size_t)n * 8);
+    hcheck(launch_gst_emit(stream, n, d_dst, d_doclen, d_cdst, comp_scratch, msgs, d_status, d_complen, d_tokoff, d_toks,
+                           d_ntok));
     hcheck(hipEventRecord(ev1, stream));
     hcheck(launch_count_esc(stream, n, d_cdst, d_complen, d_nesc));
     std::vector<uint32_t> comp_len(n), rchunk(n), ridx(n), rstatus(n), nesc(n);
@@ -2293,11 +2312,51 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     auto *d_slots = (RecSlot *)heap.alloc((uint64_t)n * sizeof(RecSlot));
     h2d(d_slots, slots.data(), (size_t)n * sizeof(RecSlot));
     std::vector<uint32_t> tstat(n);
-    hcheck(launch_tokenize(stream, n, d_slots, d_nseg, d_status));
+    // segment index: from the encoder's tokens, then by parsing the bytes for the records that
+    // could not be (k_tok_segs flags them)
+    hcheck(launch_tok_segs(stream, n, d_slots, d_doclen, d_tokoff, d_toks, d_ntok, d_nseg, d_status));
+    hcheck(launch_tokenize(stream, n, d_slots, d_nseg, d_status, d_ntok));
     std::vector<uint32_t> nseg(n);
     d2h(nseg.data(), d_nseg, n * 4);
     d2h(tstat.data(), d_status, n * 4);
     sync();
+    if (const char *e = std::getenv("PX_DEBUG_TOKSEGS"); e && e[0] == '1') {  // test hook: the tokens' segment index == the bytes' parse
+        const uint64_t seg_bytes = soff[n] + poff[n], lane_bytes = soff[n] / 2;
+        std::vector<uint8_t> a(seg_bytes), al(lane_bytes), b(seg_bytes), bl(lane_bytes);
+        std::vector<uint32_t> nseg2(n), tstat2(n);
+        d2h(a.data(), segs, seg_bytes);
+        d2h(al.data(), store + lane_at, lane_bytes);
+        sync();
+        hcheck(launch_tokenize(stream, n, d_slots, d_nseg, d_status, nullptr));
+        d2h(b.data(), segs, seg_bytes);
+        d2h(bl.data(), store + lane_at, lane_bytes);
+        d2h(nseg2.data(), d_nseg, n * 4);
+        d2h(tstat2.data(), d_status, n * 4);
+        sync();
+        uint32_t ntok_recs = 0;
+        {
+            std::vector<uint32_t> nt(n);
+            d2h(nt.data(), d_ntok, n * 4);
+            sync();
+            for (uint32_t r = 0; r < n; ++r) ntok_recs += !(nt[r] & kTokBad);
+        }
+        for (uint32_t r = 0; r < n; ++r) {
+            const uint64_t e = (nseg2[r] & ~(1u << 31)) + 1;  // entries incl. the sentinel
+            const bool same = nseg[r] == nseg2[r] && tstat[r] == tstat2[r] &&
+                              (!placed[r] || (std::memcmp(a.data() + soff[r], b.data() + soff[r], e * sizeof(SegEnt)) == 0 &&
+                                              std::memcmp(al.data() + soff[r] / 2, bl.data() + soff[r] / 2, e * sizeof(LaneEnt)) == 0 &&
+                                              std::memcmp(a.data() + soff[n] + poff[r], b.data() + soff[n] + poff[r],
+                                                          pidx_blocks(doc_len[r]) * 2) == 0));
+            if (!same) {
+                fprintf(stderr, "pixiu_amd: record %u: segment index from tokens differs from the parse (nseg %u vs %u)\n", r,
+                        nseg[r], nseg2[r]);
+                throw PxFail{PX_ECORRUPT};
+            }
+        }
+        fprintf(stderr, "pixiu_amd: segment index from tokens == parse for %u records (%u from tokens)\n", n, ntok_recs);
+    }
+    heap.release(d_toks, tok_n * sizeof(TokEnt) + 64);
+    heap.release(d_tokoff, (uint64_t)n * 12 + 64);
     heap.release(comp_scratch, scratch_bytes + 256);
     heap.release(msgs, scratch_bytes * 4 + 256);
     heap.release(d_dst, (uint64_t)n * 8);
@@ -3024,7 +3083,8 @@ void px_ctx::dki_commit(uint32_t gid0, const std::vector<DkRec> &recs, const std
 // written, nothing reported) when any key is not one the index answers, or the output
 // does not fit: the caller then runs the host path, so results never depend on this.
 int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int mode, uint8_t *out, uint64_t out_cap,
-                    int out_on_device, uint64_t *out_off, uint32_t *out_len, uint32_t *status, uint64_t *needed) {
+                    int out_on_device, uint64_t *out_off, uint32_t *out_len, uint32_t *status, uint64_t *needed,
+                    bool dev_io) {
     if (!dki_enabled() || !dki.valid || !dki.tab || !n || !spans_enabled()) return -1;
     // a store whose batches keep missing (8 in a row: records the index does not hold, e.g. reinserted or
     // set as ready docs) tries it only every 16th batch until a set batch adds records
@@ -3032,7 +3092,7 @@ int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int m
     PhaseClock phase("dki_get", "PX_GET_VERBOSE");
     phase.mark("kills, scratch, keys to pinned");
     dki_apply_kills();  // (deletes since the last set batch)
-    const uint64_t k0 = koff[0], kbytes = koff[n] - k0;
+    const uint64_t k0 = dev_io ? 0 : koff[0], kbytes = dev_io ? 0 : koff[n] - k0;  // (device keys: read in place)
     // device scratch: keys, offsets, gather queries, the look-back chain, then what comes back
     // in one copy (ctl: misses, output / 16, tiles, insert error, ticket; offsets out; lengths;
     // statuses), then the gather's task table
@@ -3048,8 +3108,8 @@ int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int m
     const uint64_t cap_fit = std::min<uint64_t>(out_cap, out_on_device ? (1ull << 36) - 16 : 4ull << 30);
     const uint64_t ntask_max = std::min<uint64_t>(cap_fit / 1024 + 2, 0xffffffffull);
     auto *b = (uint8_t *)dk_qbuf.get(o_task + gather_task_bytes((uint32_t)ntask_max));
-    auto *dkeys = b;
-    auto *doff = (uint64_t *)(b + o_off);
+    auto *dkeys = dev_io ? const_cast<uint8_t *>(keys) : b;
+    auto *doff = dev_io ? const_cast<uint64_t *>(koff) : (uint64_t *)(b + o_off);
     auto *gq = (GatherQuery *)(b + o_gq);
     auto *chain = (unsigned long long *)(b + o_chain);
     auto *ctl = (uint32_t *)(b + o_ctl);
@@ -3061,7 +3121,7 @@ int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int m
     auto *ho = (uint64_t *)(hb + o_off);
     // (a million-key batch: 16 MB staged on the host threads, in parts whose uploads start
     // while the next part is staged)
-    const uint32_t parts = n >= 65536 ? 4u : 1u;
+    const uint32_t parts = dev_io ? 0u : n >= 65536 ? 4u : 1u;
     for (uint32_t part = 0; part < parts; ++part) {
         const uint32_t r0 = (uint32_t)((uint64_t)(n + 1) * part / parts), r1 = (uint32_t)((uint64_t)(n + 1) * (part + 1) / parts);
         parallel_ranges(r1 - r0, n >= 65536 ? host_threads() : 1, [&](uint32_t lo, uint32_t hi) {
@@ -3087,9 +3147,10 @@ int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int m
     hcheck(launch_gather(stream, (uint32_t)ntask_max, ctl, cap_fit, task, gq, n, dout, dl, ds));
     hcheck(hipEventRecord(ev1, stream));
     // one copy, one round trip: ctl, offsets and lengths (the statuses only when some query
-    // ran past its room, ctl[5])
+    // ran past its room, ctl[5]); device results: the results kernel, then ctl alone
     auto *hr = (uint32_t *)dk_hres.get(o_end - o_ctl);
-    hcheck(hipMemcpyAsync(hr, ctl, o_ds - o_ctl, hipMemcpyDeviceToHost, stream));
+    if (dev_io) hcheck(launch_dk_results(stream, n, ctl, cap_fit, oo, dl, ds, out_off, out_len, status));
+    hcheck(hipMemcpyAsync(hr, ctl, dev_io ? 32 : o_ds - o_ctl, hipMemcpyDeviceToHost, stream));
     phase.mark("wait for the device");
     hcheck(hipStreamSynchronize(stream));
     phase.mark("results");
@@ -3100,6 +3161,10 @@ int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int m
         return -1;
     }
     const uint64_t total = (uint64_t)hr[1] * 16;
+    if (dev_io && !hr[0] && total > out_cap) {  // (device results: too little room is the caller's answer)
+        if (needed) *needed = total;
+        return PX_ESPACE;
+    }
     if (hr[0] || total > cap_fit) {  // (nothing was gathered: the host path answers)
         dki.miss_streak += hr[0] ? 1 : 0;
         return -1;
@@ -3114,6 +3179,10 @@ int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int m
     stats.last_decode_kernel_ms = ms;
     stats.last_gather_queries = n;
     stats.last_get_device_keys = n;
+    if (dev_io) {  // (the results kernel wrote offsets, lengths and statuses)
+        if (needed) *needed = total;
+        return hr[5] ? PX_ESPACE : PX_OK;
+    }
     const uint32_t *ro = (const uint32_t *)res, *rl = ro + n;
     const uint32_t *rs = nullptr;
     if (hr[5]) {  // (statuses only when some query ran past its room)
@@ -3333,7 +3402,7 @@ int px_ctx::load(const uint8_t *src, uint64_t len, int src_on_device, uint32_t *
     auto *d_slots = (RecSlot *)heap.alloc((uint64_t)n * sizeof(RecSlot));
     auto *d_tmp = (uint32_t *)heap.alloc((uint64_t)n * 8);
     h2d(d_slots, slots.data(), (size_t)n * sizeof(RecSlot));
-    hcheck(launch_tokenize(stream, n, d_slots, d_tmp, d_tmp + n));
+    hcheck(launch_tokenize(stream, n, d_slots, d_tmp, d_tmp + n, nullptr));
     std::vector<uint32_t> nseg(n), tst(n);
     d2h(nseg.data(), d_tmp, (size_t)n * 4);
     d2h(tst.data(), d_tmp + n, (size_t)n * 4);
@@ -3585,43 +3654,88 @@ int px_flush(px_ctx *ctx, px_set_result *last) {
     })
 }
 
+static int get_batch_impl(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff, int mode, uint8_t *out,
+                          uint64_t out_cap, int out_on_device, uint64_t *out_off, uint32_t *out_len, uint32_t *status,
+                          uint64_t *needed, bool try_device) {
+    const auto t0 = std::chrono::steady_clock::now();
+    int rc;
+    double lookup_ms = 0;
+    ctx->stats.last_get_device_keys = 0;
+    rc = ctx->opts.decode_waves == 0 && try_device
+             ? ctx->dki_get(n, keys, koff, mode, out, out_cap, out_on_device, out_off, out_len, status, needed)
+             : -1;
+    const bool on_device = rc != -1;
+    if (on_device) {
+        // (resolved on the device: no host lookups; rc is the first failing status)
+    } else if (out_on_device && n >= 4096 && ctx->opts.decode_waves == 0) {
+        rc = ctx->get_overlapped(n, keys, koff, mode, out, out_cap, out_off, out_len, status, needed, lookup_ms);
+    } else {
+        std::vector<DecodeQuery> q(n);
+        std::vector<uint32_t> pre(n, PX_OK);
+        // key -> record lookups are read-only: host threads over key ranges
+        parallel_ranges(n, ctx->host_threads(), [&](uint32_t lo, uint32_t hi) {
+            std::string ek;
+            for (uint32_t i = lo; i < hi; ++i)
+                ctx->resolve_key(keys + koff[i], koff[i + 1] - koff[i], mode, ek, q[i], pre[i]);
+        });
+        lookup_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        rc = ctx->expand(q, out, out_cap, out_on_device, out_off, out_len, status, needed, pre);
+    }
+    if (rc == PX_OK && !on_device)
+        for (uint32_t i = 0; i < n; ++i)
+            if (status[i] != PX_OK) {
+                rc = (int)status[i];
+                break;
+            }
+    ctx->stats.last_get_lookup_ms = lookup_ms;
+    ctx->stats.last_get_call_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+}
+
 int px_get_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff, int mode, uint8_t *out,
                  uint64_t out_cap, int out_on_device, uint64_t *out_off, uint32_t *out_len, uint32_t *status,
                  uint64_t *needed) {
     if (!ctx || (n && (!keys || !koff || !out_off || !out_len || !status))) return PX_EINVAL;
     PX_GUARD({
         PX_FLUSHED(ctx);
+        return get_batch_impl(ctx, n, keys, koff, mode, out, out_cap, out_on_device, out_off, out_len, status, needed,
+                              true);
+    })
+}
+
+int px_get_batch_dev(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff, int mode, uint8_t *out,
+                     uint64_t out_cap, uint64_t *out_off, uint32_t *out_len, uint32_t *status, uint64_t *needed) {
+    if (!ctx || (n && (!keys || !koff || !out || !out_off || !out_len || !status))) return PX_EINVAL;
+    PX_GUARD({
+        PX_FLUSHED(ctx);
+        if (needed) *needed = 0;
+        if (!n) return PX_OK;
         const auto t0 = std::chrono::steady_clock::now();
-        int rc;
-        double lookup_ms = 0;
         ctx->stats.last_get_device_keys = 0;
-        rc = ctx->opts.decode_waves == 0
-                 ? ctx->dki_get(n, keys, koff, mode, out, out_cap, out_on_device, out_off, out_len, status, needed)
-                 : -1;
-        const bool on_device = rc != -1;
-        if (on_device) {
-            // (resolved on the device: no host lookups; rc is the first failing status)
-        } else if (out_on_device && n >= 4096 && ctx->opts.decode_waves == 0) {
-            rc = ctx->get_overlapped(n, keys, koff, mode, out, out_cap, out_off, out_len, status, needed, lookup_ms);
-        } else {
-            std::vector<DecodeQuery> q(n);
-            std::vector<uint32_t> pre(n, PX_OK);
-            // key -> record lookups are read-only: host threads over key ranges
-            parallel_ranges(n, ctx->host_threads(), [&](uint32_t lo, uint32_t hi) {
-                std::string ek;
-                for (uint32_t i = lo; i < hi; ++i)
-                    ctx->resolve_key(keys + koff[i], koff[i + 1] - koff[i], mode, ek, q[i], pre[i]);
-            });
-            lookup_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-            rc = ctx->expand(q, out, out_cap, out_on_device, out_off, out_len, status, needed, pre);
+        int rc = ctx->opts.decode_waves == 0 ? ctx->dki_get(n, keys, koff, mode, out, out_cap, 1, out_off, out_len,
+                                                             status, needed, true)
+                                             : -1;
+        if (rc == -1) {
+            // keys the device index does not answer: keys and offsets down, the host path, the
+            // results up (offsets rebased to the first key)
+            std::vector<uint64_t> ko(n + 1);
+            ctx->d2h(ko.data(), koff, (size_t)(n + 1) * 8);
+            ctx->sync();
+            const uint64_t k0 = ko[0];
+            std::vector<uint8_t> kb(ko[n] - k0 + 1);
+            if (ko[n] > k0) ctx->d2h(kb.data(), keys + k0, ko[n] - k0);
+            ctx->sync();
+            for (auto &x : ko) x -= k0;
+            std::vector<uint64_t> ho(n);
+            std::vector<uint32_t> hl(n), hs(n);
+            rc = get_batch_impl(ctx, n, kb.data(), ko.data(), mode, out, out_cap, 1, ho.data(), hl.data(), hs.data(),
+                                needed, false);
+            ctx->h2d(out_off, ho.data(), (size_t)n * 8);
+            ctx->h2d(out_len, hl.data(), (size_t)n * 4);
+            ctx->h2d(status, hs.data(), (size_t)n * 4);
+            ctx->sync();
         }
-        if (rc == PX_OK && !on_device)
-            for (uint32_t i = 0; i < n; ++i)
-                if (status[i] != PX_OK) {
-                    rc = (int)status[i];
-                    break;
-                }
-        ctx->stats.last_get_lookup_ms = lookup_ms;
         ctx->stats.last_get_call_ms =
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         return rc;
@@ -3815,7 +3929,7 @@ int px_import_chunk(px_ctx *ctx, uint32_t n, const uint8_t *comp, const uint64_t
         auto *d_slots = (RecSlot *)ctx->heap.alloc((uint64_t)n * sizeof(RecSlot));
         auto *d_tmp = (uint32_t *)ctx->heap.alloc((uint64_t)n * 8);
         ctx->h2d(d_slots, slots.data(), (size_t)n * sizeof(RecSlot));
-        hcheck(launch_tokenize(ctx->stream, n, d_slots, d_tmp, d_tmp + n));
+        hcheck(launch_tokenize(ctx->stream, n, d_slots, d_tmp, d_tmp + n, nullptr));
         std::vector<uint32_t> nseg(n), tst(n);
         ctx->d2h(nseg.data(), d_tmp, (size_t)n * 4);
         ctx->d2h(tst.data(), d_tmp + n, (size_t)n * 4);

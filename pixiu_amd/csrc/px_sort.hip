@@ -62,8 +62,9 @@ SD uint64_t text_key(const uint8_t *G, const uint16_t *dist, uint32_t p, uint32_
     const uint32_t left = ((gcu16 *)dist)[p];
     uint64_t k = 0;
     for (uint32_t s = 0; s < syms; ++s) k = k << 9 | (s < left ? ((x >> (8 * s)) & 0xffu) + 1u : 0u);
-    uint32_t dl = 0;
-    while (dl < 15u && (syms << dl) < left) ++dl;
+    // steps k < 15 with (syms << k) < left: 2^k <= (left - 1) / syms, i.e. that quotient's bit length
+    const uint32_t q = left > syms ? (left - 1u) / syms : 0u;
+    const uint32_t dl = min(15u, 32u - (uint32_t)__clz(q));
     return k | (uint64_t)dl << kDlShift;
 }
 

@@ -168,3 +168,48 @@ def test_after_set_docs(store_factory, oracle, rps):
     only_old = [k for k in live if k not in set(ks[500:])]
     assert st.get_batch(only_old) == [want[k] for k in only_old]
     assert st.stats()["last_get_device_keys"] == len(only_old)
+
+
+def test_device_keys_and_results(store_factory):
+    """px_get_batch_dev: keys and results in device memory.  Answered on the device it gives
+    the host-key call's bytes, lengths and statuses; keys the index cannot answer (a missing
+    key) go the host path and still land in the device arrays; too little room returns
+    PX_ESPACE with the needed size."""
+    import torch
+    from pixiu_amd import synth
+    cp = synth.make(4, 20000)
+    st = store_factory(records_per_shard=2000)
+    st.set_batch((cp.keys, cp.koff.astype(np.uint64)), (cp.vals, cp.voff.astype(np.uint64)))
+    dev = torch.device("cuda", 0)
+    keys = [cp.key(i) for i in range(0, cp.n, 3)]
+
+    def run(ks, cap):
+        kb, ko = px.csr(ks)
+        dkb = torch.from_numpy(kb.copy() if kb.size else np.zeros(1, np.uint8)).to(dev)
+        dko = torch.from_numpy(ko.astype(np.int64)).to(dev)
+        n = len(ks)
+        out = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
+        off = torch.full((n,), 7, dtype=torch.int64, device=dev)
+        ln = torch.full((n,), 7, dtype=torch.int32, device=dev)
+        sts = torch.full((n,), 7, dtype=torch.int32, device=dev)
+        rc, need = st.get_batch_dev(n, dkb.data_ptr(), dko.data_ptr(), out.data_ptr(), cap, off.data_ptr(),
+                                    ln.data_ptr(), sts.data_ptr())
+        return rc, need, out, off.cpu().numpy(), ln.cpu().numpy(), sts.cpu().numpy()
+
+    want = st.get_batch(keys)
+    rc, need, out, off, ln, sts = run(keys, 64 << 20)
+    assert rc == px.PX_OK and st.stats()["last_get_device_keys"] == len(keys)
+    h = out.cpu().numpy()
+    assert (sts == 0).all()
+    assert [h[o:o + l].tobytes() for o, l in zip(off, ln)] == want
+    # a missing key: the host path, results still in the device arrays
+    ks2 = keys[:100] + [b"no such key"] + keys[100:200]
+    rc, need, out, off, ln, sts = run(ks2, 64 << 20)
+    assert rc == px.PX_ENOTFOUND and st.stats()["last_get_device_keys"] == 0
+    h = out.cpu().numpy()
+    assert sts[100] == px.PX_ENOTFOUND and (np.delete(sts, 100) == 0).all()
+    got = [None if s else h[o:o + l].tobytes() for o, l, s in zip(off, ln, sts)]
+    assert got == st.get_batch(ks2)
+    # too little room
+    rc, need, *_ = run(keys, 4096)
+    assert rc == px.PX_ESPACE and need > 4096

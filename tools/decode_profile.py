@@ -23,8 +23,17 @@ out_cap = int(2 * cp.raw_bytes + 256 * n + (1 << 20))
 out = torch.empty(out_cap, dtype=torch.uint8, device="cuda")
 buf = (C.c_ulonglong * 128)()
 with px.Store(records_per_shard=rps, decode_waves=waves) as st:
+    lib.px_debug_prof_take(buf, 128)
     st.set_batch((cp.keys, cp.koff.astype(np.uint64)), (cp.vals, cp.voff.astype(np.uint64)))
     lib.px_debug_prof_take(buf, 128)
+    # the set batch's decodes: key prefixes and the span build (k_decode_addr)
+    v = {name: buf[IDX[name]] for name in NAMES}
+    print(f"config {cfg} n {n} rps {rps}: set batch decodes (key prefixes + span tables)")
+    for name in NAMES:
+        print(f"  {name:10s} {v[name]:16d}  per record {v[name] / n:12.1f}")
+    print(f"  lane iterations per batch {v['d_laneit'] / max(v['d_batch'], 1):.2f}, committed per batch {v['d_commit'] / max(v['d_batch'], 1):.2f}")
+    print(f"  lane-phase share of wave time {v['d_t_lane'] / max(v['d_t_total'], 1) * 100:.1f}%")
+    print(f"  assignment share of wave time {v['d_t_assign'] / max(v['d_t_total'], 1) * 100:.1f}%")
     rc, off, ln, sts, need = st.get_batch_device(keys_host, out.data_ptr(), out_cap, px.COMPAT)
     ms = st.stats()["last_decode_kernel_ms"]
 k = lib.px_debug_prof_take(buf, 128)
