@@ -1133,7 +1133,11 @@ struct px_ctx {
         //    same bytes; each lands 64 bytes past the previous piece's nominal end (an
         //    over-yield has room) and k_span_jobs reads the pieces in order.  A record whose
         //    pieces fail or reach the whole decode's room is decoded again whole.
-        constexpr uint32_t kPiece = 4096;
+        static const uint32_t kPiece = [] {  // (PX_SPAN_PIECE: experiments; a power of two >= 256)
+            const char *e = std::getenv("PX_SPAN_PIECE");
+            const uint32_t v = e ? (uint32_t)std::atoi(e) : 4096u;
+            return v >= 256 && (v & (v - 1)) == 0 ? v : 4096u;
+        }();
         const char *split_env = std::getenv("PX_SPAN_SPLIT");
         const bool compat_split = !(split_env && split_env[0] == '0');
         split = split && (mode == 1 || compat_split);
