@@ -1929,10 +1929,6 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
             // walk state
             const PX_GAS u32x4 *e = nullptr;  // the lane entry F was loaded from
             u32x4 F = mk4(0, 0, 0, 0);
-            // the two entries after e, loaded ahead (a walk mostly moves to the next entry: each
-            // of its loads then has two steps to arrive instead of one); gv: they belong to e
-            u32x4 G = F, H = F;
-            bool gv = false;
             uint32_t rec = 0, d = 0;
             int32_t from = 0, len = 0, ret = 0;
             PX_CNT(P_D_BATCH, 1);
@@ -2039,7 +2035,6 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                             // the first entry is loaded by the lane's first walk step
                             busy = true;
                             fresh = true;
-                            gv = false;
                             rec = ridx;
                             d = 0;
                             from = sub_from;
@@ -2144,21 +2139,9 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                             }
                         }
                         // next entry first (every entry a lane can reach is in bounds: a
-                        // record's entries end with a sentinel, which pops; the two read ahead
-                        // of it stay inside the allocation's 64 bytes of slack)
+                        // record's entries end with a sentinel, which pops)
                         u32x4 NF = F;
-                        if (busy && !pmode) {
-                            if (gv && ne == e + 1) {
-                                NF = G;
-                                G = H;
-                                H = ne[2];
-                            } else {
-                                NF = ne[0];
-                                G = ne[1];
-                                H = ne[2];
-                                gv = true;
-                            }
-                        }
+                        if (busy && !pmode) NF = ne[0];
                         if (nb) {
                             const PX_GAS uint8_t *cp = seg0 + poff;
                             const uint32_t last = ov ? cp[nb - 1] : 0u;

@@ -383,13 +383,29 @@ __global__ void __launch_bounds__(256) k_psa_groups0(uint32_t N, const uint32_t 
     if (threadIdx.x == 0) s_bid = atomicAdd((uint32_t *)(chain + nb), 1u);  // (tickets: look-back never waits on a later one)
     __syncthreads();
     const uint32_t bid = s_bid, base = bid * kG0Slots, lane = lane_id(), w = threadIdx.x >> 6;
+    // every load first (rows of 256 slots; a slot's neighbours come from the next lanes, the
+    // wave's edge lanes load theirs), so the block waits on memory once
+    uint64_t kc[kG0Rows], ke[kG0Rows];
+    uint32_t pp[kG0Rows];
+#pragma unroll
+    for (uint32_t i = 0; i < kG0Rows; ++i) {
+        const uint32_t r = base + i * 256u + threadIdx.x;
+        kc[i] = r < N ? skeys[r] : 0ull;
+        ke[i] = lane == 0 ? (r > 0 && r <= N ? skeys[r - 1] : 0ull) : lane == 63 ? (r + 1 < N ? skeys[r + 1] : 0ull) : 0ull;
+        pp[i] = r < N ? sa[r] : 0u;
+    }
     // row i = slots base + 256 i + (0..255): inclusive max-scan of (head + 1) in slot order
     uint32_t hv[kG0Rows], hnm = 0, carry = 0;
 #pragma unroll
     for (uint32_t i = 0; i < kG0Rows; ++i) {
         const uint32_t r = base + i * 256u + threadIdx.x;
-        const bool f = r < N && head_at(skeys, N, r);
-        if (r < N && head_at(skeys, N, r + 1)) hnm |= 1u << i;  // r + 1 starts the next group (or the end)
+        const uint64_t k = kc[i] & kKeyMask;
+        // (every lane shuffles: a lane left out of a shuffle hands its neighbour nothing)
+        const uint64_t sl = shfl64(kc[i], (lane + 63u) & 63u), sr = shfl64(kc[i], (lane + 1u) & 63u);
+        const uint64_t kl = (lane == 0 ? ke[i] : sl) & kKeyMask;
+        const uint64_t kr = (lane == 63 ? ke[i] : sr) & kKeyMask;
+        const bool f = r < N && (r == 0 || k != kl || (k & 511u) == 0);
+        if (r < N && (r + 1 >= N || kr != k || (kr & 511u) == 0)) hnm |= 1u << i;  // r + 1 starts the next group (or the end)
         uint32_t v = f ? r + 1u : 0u;
         for (uint32_t o = 1; o < 64; o <<= 1) {
             const uint32_t y = (uint32_t)__shfl_up((int)v, o);
@@ -432,11 +448,11 @@ __global__ void __launch_bounds__(256) k_psa_groups0(uint32_t N, const uint32_t 
         const uint32_t r = base + i * 256u + threadIdx.x;
         if (r >= N) break;
         const bool hn = (hnm >> i) & 1u;
-        const uint32_t hd = max(hv[i], pre) - 1u, p = sa[r];
-        rank[p] = hd;
+        const uint32_t hd = max(hv[i], pre) - 1u;
+        rank[pp[i]] = hd;
         const uint32_t a = (hd != r || !hn) ? 1u : 0u;  // in a group of >= 2
         a_all += a;
-        sd[r] = a ? (uint16_t)((skeys[r] >> kDlShift) & 15u) : (uint16_t)0;
+        sd[r] = a ? (uint16_t)((kc[i] >> kDlShift) & 15u) : (uint16_t)0;
         act[r] = (uint8_t)a;
         if (!(hd == r && !hn)) gsz[r] = 0;  // (not the start of a group of >= 2)
         if (hn && hd != r) {                // the last element of a group of >= 2

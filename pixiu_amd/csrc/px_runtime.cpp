@@ -1141,6 +1141,11 @@ struct px_ctx {
         const char *split_env = std::getenv("PX_SPAN_SPLIT");
         const bool compat_split = !(split_env && split_env[0] == '0');
         split = split && (mode == 1 || compat_split);
+        if (split) {  // (a batch whose records are all one piece long: whole decodes, no piece table)
+            bool longer = false;
+            for (uint32_t k = 0; k < n && !longer; ++k) longer = chunks[reqs[k].chunk].doc_len[reqs[k].idx] > kPiece;
+            split = longer;
+        }
         auto *qn = (DecodeQuery *)hq_buf.get((uint64_t)n * sizeof(DecodeQuery));
         std::vector<SpanSrc> src(n);
         uint64_t tot = 0;
