@@ -1065,14 +1065,21 @@ __global__ void __launch_bounds__(256) k_gst_emit(uint32_t n, const uint8_t *con
             }
         };
         auto run_size = [](uint32_t rl) -> uint32_t { return rl > 6 ? (rl > 255 ? 8u : 6u) : rl; };
+        // each window's doc bytes and messages are loaded two windows ahead (a step needs the
+        // next window's first message, and a step is shorter than a load's latency)
+        uint32_t bn = lane < len ? doc[lane] : 0u, mn = lane < len ? msg[lane] : kPassMsg;
+        uint32_t bn2 = 64 + lane < len ? doc[64 + lane] : 0u, mn2 = 64 + lane < len ? msg[64 + lane] : kPassMsg;
         for (uint32_t ws = 0; ws < len; ws += 64) {
             const uint32_t k = ws + lane;
             const bool live = k < len;
-            const uint32_t b = live ? doc[k] : 0u;
-            const uint32_t m = live ? msg[k] : kPassMsg;
+            const uint32_t b = bn, m = mn;
+            bn = bn2;
+            mn = mn2;
+            bn2 = ws + 128 + lane < len ? doc[ws + 128 + lane] : 0u;
+            mn2 = ws + 128 + lane < len ? msg[ws + 128 + lane] : kPassMsg;
             const bool isc = m != kPassMsg;
             const uint64_t cm = ballot(isc);
-            const bool nextc_63 = ws + 64 < len && uni(msg[ws + 64]) != kPassMsg;
+            const bool nextc_63 = ws + 64 < len && uni(readlane(mn, 0)) != kPassMsg;
             const bool isc_next = lane < 63 ? ((cm >> (lane + 1)) & 1) != 0 : nextc_63;
             const bool isc_prev = lane > 0 ? ((cm >> (lane - 1)) & 1) != 0 : prevc_in;
             // pair starts: within a run of 251 bytes they alternate from the run's start
@@ -2406,38 +2413,69 @@ PX_DEV void span_job(const SpanJob &jb) {
             a += uni64(jb.pq[j].out_off);
             pn = min(uni(jb.pl[j]), len - o);
         }
-        for (uint32_t i0 = 0; i0 < pn; i0 += 64) {
-            const uint32_t i = i0 + lane, k = o + i;
-            const bool in = i < pn;
-            // the byte's address: its run's start address + its distance from the start (the
-            // latest start at or below the lane, else the previous window's last address + 1)
-            const int32_t raw = in ? a[i] : kAddrMark;
-            const uint64_t le = ballot(in && raw != kAddrMark) & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
-            const uint32_t sl = le ? 63u - (uint32_t)__clzll((long long)le) : 0u;
-            const int32_t sv = (int32_t)__shfl(raw, (int)sl);
-            const int32_t rb = le ? sv : prev_last;
-            const int32_t v = !in ? 0 : rb == kAddrNone ? kAddrNone : rb + (le ? (int32_t)(lane - sl) : (int32_t)lane + 1);
-            int32_t pv = __shfl_up(v, 1);
-            if (lane == 0) pv = prev_last;
-            const bool start = in && (k == 0 || pv == kAddrNone || v != pv + 1);
-            bad = bad || (bool)ballot(in && v == kAddrNone);
-            if (eq) eq = !ballot(in && (v == kAddrNone || base[v] != doc[k]));
-            const uint64_t m = ballot(start);
-            if (out && !bad) {
-                const uint32_t rank =
-                    __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-                if (start) {
-                    PX_GAS uint32_t *e = (PX_GAS uint32_t *)(out + cnt + rank);
-                    e[0] = (uint32_t)v;
-                    e[1] = k;
-                }
-                // tile index: the span holding byte k, at every tile start
-                if (jb.tix && in && (k % kGatherTile) == 0)
-                    ((PX_GAS uint32_t *)jb.tix)[k / kGatherTile] = cnt + rank + (start ? 1u : 0u) - 1u;
+        // four 64-byte steps per group: their address loads, then their doc / comp byte loads
+        // for the compat == exact test, each issued together (one wave walks a record: its
+        // dependent loads were the pass's time)
+        for (uint32_t g0 = 0; g0 < pn; g0 += 256) {
+            int32_t raw[4], vv[4];
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u) {
+                const uint32_t i = g0 + 64u * u + lane;
+                raw[u] = i < pn ? a[i] : kAddrMark;
             }
-            cnt += (uint32_t)__popcll(m);
-            const uint32_t nl = min(pn - i0, 64u);  // (the piece's last byte of this step)
-            prev_last = __shfl(v, (int)(nl - 1));
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u) {
+                const uint32_t i0 = g0 + 64u * u;
+                vv[u] = kAddrNone;
+                if (i0 >= pn) break;  // (wave-uniform)
+                const uint32_t i = i0 + lane, k = o + i;
+                const bool in = i < pn;
+                // the byte's address: its run's start address + its distance from the start (the
+                // latest start at or below the lane, else the previous window's last address + 1)
+                const uint64_t le = ballot(in && raw[u] != kAddrMark) & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
+                const uint32_t sl = le ? 63u - (uint32_t)__clzll((long long)le) : 0u;
+                const int32_t sv = (int32_t)__shfl(raw[u], (int)sl);
+                const int32_t rb = le ? sv : prev_last;
+                const int32_t v = !in ? 0 : rb == kAddrNone ? kAddrNone : rb + (le ? (int32_t)(lane - sl) : (int32_t)lane + 1);
+                vv[u] = in ? v : kAddrNone;
+                int32_t pv = __shfl_up(v, 1);
+                if (lane == 0) pv = prev_last;
+                const bool start = in && (k == 0 || pv == kAddrNone || v != pv + 1);
+                bad = bad || (bool)ballot(in && v == kAddrNone);
+                const uint64_t m = ballot(start);
+                if (out && !bad) {
+                    const uint32_t rank =
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                    if (start) {
+                        PX_GAS uint32_t *e = (PX_GAS uint32_t *)(out + cnt + rank);
+                        e[0] = (uint32_t)v;
+                        e[1] = k;
+                    }
+                    // tile index: the span holding byte k, at every tile start
+                    if (jb.tix && in && (k % kGatherTile) == 0)
+                        ((PX_GAS uint32_t *)jb.tix)[k / kGatherTile] = cnt + rank + (start ? 1u : 0u) - 1u;
+                }
+                cnt += (uint32_t)__popcll(m);
+                const uint32_t nl = min(pn - i0, 64u);  // (the piece's last byte of this step)
+                prev_last = __shfl(v, (int)(nl - 1));
+            }
+            if (eq) {
+                uint32_t bb[4], dd[4];
+#pragma unroll
+                for (uint32_t u = 0; u < 4; ++u) {
+                    const uint32_t i = g0 + 64u * u + lane;
+                    const bool ok = i < pn && vv[u] != kAddrNone;
+                    bb[u] = ok ? base[vv[u]] : 0u;
+                    dd[u] = ok ? doc[o + i] : 0u;
+                }
+                bool mis = false;
+#pragma unroll
+                for (uint32_t u = 0; u < 4; ++u) {
+                    const uint32_t i = g0 + 64u * u + lane;
+                    mis = mis || (i < pn && (vv[u] == kAddrNone || bb[u] != dd[u]));
+                }
+                eq = !ballot(mis);
+            }
         }
         o += pn;
     }

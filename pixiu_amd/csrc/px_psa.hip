@@ -584,8 +584,13 @@ __global__ void __launch_bounds__(256) k_dbl_win(uint32_t N, uint32_t tag, uint3
         const uint32_t w = lobit(todo) * nch + c;
         todo &= todo - 1;
         const uint32_t b = w * 64, sA = b + lane, sB = b + 64 + lane;
-        const bool inA = sA < N;
+        const bool inA = sA < N, inB = sB < N;
         const uint32_t g = inA ? gsz[sA] : 0u;
+        // every load the window may need, issued with its group sizes (one memory round trip per
+        // window instead of three; lanes outside the window's groups discard theirs)
+        const uint32_t kA = inA ? key[sA] : 0u, kB = inB ? key[sB] : 0u;
+        const uint32_t pA0 = inA ? sa[sA] : 0u, pB0 = inB ? sa[sB] : 0u;
+        const uint32_t dA0 = inA ? sd[sA] : 0u, dB0 = inB ? sd[sB] : 0u;
         const bool start = (g & kTag) == tag && (g & kSizeMask) >= 2;
         const uint32_t gs = g & kSizeMask;
         const uint64_t S = __ballot(start && gs <= kWinMax);
@@ -606,8 +611,8 @@ __global__ void __launch_bounds__(256) k_dbl_win(uint32_t N, uint32_t tag, uint3
         const uint32_t zA = (uint32_t)__shfl((int)gs, (int)(cA & 63u)), zB = (uint32_t)__shfl((int)gs, (int)cB);
         WinElem A{cA < 64 && lane < cA + zA, cA & 63u, zA, lane - cA, 0, 0, 0};
         WinElem B{64 + lane < cB + zB, cB, zB, 64 + lane - cB, 0, 0, 0};
-        if (A.mem) A.key = key[sA];
-        if (B.mem) B.key = key[sB];
+        if (A.mem) A.key = kA;
+        if (B.mem) B.key = kB;
         {
             // every group keeps one key (a repeat longer than 2h): the groups stay as they are,
             // only their sizes move to the next step's tag
@@ -629,12 +634,12 @@ __global__ void __launch_bounds__(256) k_dbl_win(uint32_t N, uint32_t tag, uint3
                 uint32_t pA = 0;
                 if (rA) {
                     act[sA] = 0;
-                    pA = sa[sA];
+                    pA = pA0;
                     rank[pA] = idA | kRetired;
                 }
                 if (rB) {
                     act[sB] = 0;
-                    rank[sa[sB]] = idB | kRetired;
+                    rank[pB0] = idB | kRetired;
                 }
                 if ((S >> lane) & 1ull) {
                     if ((Rm >> lane) & 1ull) {
@@ -653,12 +658,12 @@ __global__ void __launch_bounds__(256) k_dbl_win(uint32_t N, uint32_t tag, uint3
             }
         }
         if (A.mem) {
-            A.p = sa[sA];
-            A.d = sd[sA];
+            A.p = pA0;
+            A.d = dA0;
         }
         if (B.mem) {
-            B.p = sa[sB];
-            B.d = sd[sB];
+            B.p = pB0;
+            B.d = dB0;
         }
         lk[lane] = A.key;
         lk[64 + lane] = B.key;
