@@ -720,12 +720,15 @@ __global__ void __launch_bounds__(256) k_dbl_reg(const uint64_t *list, const uin
         const uint64_t ent = list[gi];
         const uint32_t start = (uint32_t)ent, size = (uint32_t)(ent >> 32);
         uint64_t x[E];
+        uint32_t pv[E], dv[E];  // (payloads loaded with the keys: one memory round trip per group)
         const uint32_t key0 = key[start];
         bool split = false;
 #pragma unroll
         for (uint32_t r = 0; r < E; ++r) {
             const uint32_t i = lane * E + r;
             const uint32_t k = i < size ? key[start + i] : key0;
+            pv[r] = i < size ? sa[start + i] : 0u;
+            dv[r] = i < size ? sd[start + i] : 0u;
             x[r] = i < size ? (uint64_t)k << 11 | i : ~0ull;
             split = split || k != key0 || k == 0;
         }
@@ -744,7 +747,7 @@ __global__ void __launch_bounds__(256) k_dbl_reg(const uint64_t *list, const uin
                     const uint32_t i = lane * E + r;
                     if (i < size) {
                         act[start + i] = 0;
-                        const uint32_t p = sa[start + i];
+                        const uint32_t p = pv[r];
                         rank[p] = id | kRetired;
                         if (i == 0) p0 = p;
                     }
@@ -764,8 +767,8 @@ __global__ void __launch_bounds__(256) k_dbl_reg(const uint64_t *list, const uin
         for (uint32_t r = 0; r < E; ++r) {
             const uint32_t i = lane * E + r;
             if (i < size) {
-                lp[wv][i] = sa[start + i];
-                ld[wv][i] = sd[start + i];
+                lp[wv][i] = pv[r];
+                ld[wv][i] = (uint16_t)dv[r];
             }
         }
 #pragma unroll
@@ -843,6 +846,8 @@ __global__ void __launch_bounds__(256) k_dbl_blk(const uint64_t *list, const uin
                                                  uint32_t *sa, uint16_t *sd, uint8_t *act, uint32_t *gsz, const uint32_t *key,
                                                  uint32_t *rank, StepStat ss, RetList R) {
     __shared__ uint64_t sk[kMedMax];
+    __shared__ uint32_t sp_[kMedMax];  // (the payloads, loaded with the keys: read back after the sort)
+    __shared__ uint16_t sdd[kMedMax];
     __shared__ uint32_t sl[256], sf[256];
     constexpr uint32_t kC = kMedMax / 256;
     const uint32_t cnt = __hip_atomic_load(cnt_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -859,6 +864,10 @@ __global__ void __launch_bounds__(256) k_dbl_blk(const uint64_t *list, const uin
             const uint32_t k = i < size ? key[start + i] : key0;
             split = split || k != key0 || k == 0;
             sk[i] = i < size ? (uint64_t)k << 12 | i : ~0ull;
+            if (i < size) {
+                sp_[i] = sa[start + i];
+                sdd[i] = sd[start + i];
+            }
         }
         if (!__syncthreads_or(split)) {  // one key: the group stays as it is (see k_dbl_win) or retires
             __shared__ uint32_t s_id;
@@ -878,7 +887,7 @@ __global__ void __launch_bounds__(256) k_dbl_blk(const uint64_t *list, const uin
                 uint32_t p0 = 0;
                 for (uint32_t i = tid; i < size; i += 256) {
                     act[start + i] = 0;
-                    const uint32_t p = sa[start + i];
+                    const uint32_t p = sp_[i];
                     rank[p] = id | kRetired;
                     if (i == 0) p0 = p;
                 }
@@ -921,8 +930,8 @@ __global__ void __launch_bounds__(256) k_dbl_blk(const uint64_t *list, const uin
                 const uint32_t k = (uint32_t)(x >> 12);
                 if (i == 0 || k != (uint32_t)(sk[i - 1] >> 12) || k == 0) hm |= 1u << c;
                 const uint32_t o = (uint32_t)(x & 4095u);
-                pv[c] = sa[start + o];
-                dv[c] = sd[start + o];
+                pv[c] = sp_[o];
+                dv[c] = sdd[o];
             }
         }
         sl[tid] = hm ? i0 + (31u - (uint32_t)__clz(hm)) + 1u : 0u;
