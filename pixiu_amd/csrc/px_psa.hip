@@ -584,13 +584,8 @@ __global__ void __launch_bounds__(256) k_dbl_win(uint32_t N, uint32_t tag, uint3
         const uint32_t w = lobit(todo) * nch + c;
         todo &= todo - 1;
         const uint32_t b = w * 64, sA = b + lane, sB = b + 64 + lane;
-        const bool inA = sA < N, inB = sB < N;
+        const bool inA = sA < N;
         const uint32_t g = inA ? gsz[sA] : 0u;
-        // every load the window may need, issued with its group sizes (one memory round trip per
-        // window instead of three; lanes outside the window's groups discard theirs)
-        const uint32_t kA = inA ? key[sA] : 0u, kB = inB ? key[sB] : 0u;
-        const uint32_t pA0 = inA ? sa[sA] : 0u, pB0 = inB ? sa[sB] : 0u;
-        const uint32_t dA0 = inA ? sd[sA] : 0u, dB0 = inB ? sd[sB] : 0u;
         const bool start = (g & kTag) == tag && (g & kSizeMask) >= 2;
         const uint32_t gs = g & kSizeMask;
         const uint64_t S = __ballot(start && gs <= kWinMax);
@@ -611,8 +606,8 @@ __global__ void __launch_bounds__(256) k_dbl_win(uint32_t N, uint32_t tag, uint3
         const uint32_t zA = (uint32_t)__shfl((int)gs, (int)(cA & 63u)), zB = (uint32_t)__shfl((int)gs, (int)cB);
         WinElem A{cA < 64 && lane < cA + zA, cA & 63u, zA, lane - cA, 0, 0, 0};
         WinElem B{64 + lane < cB + zB, cB, zB, 64 + lane - cB, 0, 0, 0};
-        if (A.mem) A.key = kA;
-        if (B.mem) B.key = kB;
+        if (A.mem) A.key = key[sA];
+        if (B.mem) B.key = key[sB];
         {
             // every group keeps one key (a repeat longer than 2h): the groups stay as they are,
             // only their sizes move to the next step's tag
@@ -634,12 +629,12 @@ __global__ void __launch_bounds__(256) k_dbl_win(uint32_t N, uint32_t tag, uint3
                 uint32_t pA = 0;
                 if (rA) {
                     act[sA] = 0;
-                    pA = pA0;
+                    pA = sa[sA];
                     rank[pA] = idA | kRetired;
                 }
                 if (rB) {
                     act[sB] = 0;
-                    rank[pB0] = idB | kRetired;
+                    rank[sa[sB]] = idB | kRetired;
                 }
                 if ((S >> lane) & 1ull) {
                     if ((Rm >> lane) & 1ull) {
@@ -658,12 +653,12 @@ __global__ void __launch_bounds__(256) k_dbl_win(uint32_t N, uint32_t tag, uint3
             }
         }
         if (A.mem) {
-            A.p = pA0;
-            A.d = dA0;
+            A.p = sa[sA];
+            A.d = sd[sA];
         }
         if (B.mem) {
-            B.p = pB0;
-            B.d = dB0;
+            B.p = sa[sB];
+            B.d = sd[sB];
         }
         lk[lane] = A.key;
         lk[64 + lane] = B.key;
@@ -720,15 +715,12 @@ __global__ void __launch_bounds__(256) k_dbl_reg(const uint64_t *list, const uin
         const uint64_t ent = list[gi];
         const uint32_t start = (uint32_t)ent, size = (uint32_t)(ent >> 32);
         uint64_t x[E];
-        uint32_t pv[E], dv[E];  // (payloads loaded with the keys: one memory round trip per group)
         const uint32_t key0 = key[start];
         bool split = false;
 #pragma unroll
         for (uint32_t r = 0; r < E; ++r) {
             const uint32_t i = lane * E + r;
             const uint32_t k = i < size ? key[start + i] : key0;
-            pv[r] = i < size ? sa[start + i] : 0u;
-            dv[r] = i < size ? sd[start + i] : 0u;
             x[r] = i < size ? (uint64_t)k << 11 | i : ~0ull;
             split = split || k != key0 || k == 0;
         }
@@ -747,7 +739,7 @@ __global__ void __launch_bounds__(256) k_dbl_reg(const uint64_t *list, const uin
                     const uint32_t i = lane * E + r;
                     if (i < size) {
                         act[start + i] = 0;
-                        const uint32_t p = pv[r];
+                        const uint32_t p = sa[start + i];
                         rank[p] = id | kRetired;
                         if (i == 0) p0 = p;
                     }
@@ -767,8 +759,8 @@ __global__ void __launch_bounds__(256) k_dbl_reg(const uint64_t *list, const uin
         for (uint32_t r = 0; r < E; ++r) {
             const uint32_t i = lane * E + r;
             if (i < size) {
-                lp[wv][i] = pv[r];
-                ld[wv][i] = (uint16_t)dv[r];
+                lp[wv][i] = sa[start + i];
+                ld[wv][i] = sd[start + i];
             }
         }
 #pragma unroll
@@ -846,8 +838,6 @@ __global__ void __launch_bounds__(256) k_dbl_blk(const uint64_t *list, const uin
                                                  uint32_t *sa, uint16_t *sd, uint8_t *act, uint32_t *gsz, const uint32_t *key,
                                                  uint32_t *rank, StepStat ss, RetList R) {
     __shared__ uint64_t sk[kMedMax];
-    __shared__ uint32_t sp_[kMedMax];  // (the payloads, loaded with the keys: read back after the sort)
-    __shared__ uint16_t sdd[kMedMax];
     __shared__ uint32_t sl[256], sf[256];
     constexpr uint32_t kC = kMedMax / 256;
     const uint32_t cnt = __hip_atomic_load(cnt_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -864,10 +854,6 @@ __global__ void __launch_bounds__(256) k_dbl_blk(const uint64_t *list, const uin
             const uint32_t k = i < size ? key[start + i] : key0;
             split = split || k != key0 || k == 0;
             sk[i] = i < size ? (uint64_t)k << 12 | i : ~0ull;
-            if (i < size) {
-                sp_[i] = sa[start + i];
-                sdd[i] = sd[start + i];
-            }
         }
         if (!__syncthreads_or(split)) {  // one key: the group stays as it is (see k_dbl_win) or retires
             __shared__ uint32_t s_id;
@@ -887,7 +873,7 @@ __global__ void __launch_bounds__(256) k_dbl_blk(const uint64_t *list, const uin
                 uint32_t p0 = 0;
                 for (uint32_t i = tid; i < size; i += 256) {
                     act[start + i] = 0;
-                    const uint32_t p = sp_[i];
+                    const uint32_t p = sa[start + i];
                     rank[p] = id | kRetired;
                     if (i == 0) p0 = p;
                 }
@@ -930,8 +916,8 @@ __global__ void __launch_bounds__(256) k_dbl_blk(const uint64_t *list, const uin
                 const uint32_t k = (uint32_t)(x >> 12);
                 if (i == 0 || k != (uint32_t)(sk[i - 1] >> 12) || k == 0) hm |= 1u << c;
                 const uint32_t o = (uint32_t)(x & 4095u);
-                pv[c] = sp_[o];
-                dv[c] = sdd[o];
+                pv[c] = sa[start + o];
+                dv[c] = sd[start + o];
             }
         }
         sl[tid] = hm ? i0 + (31u - (uint32_t)__clz(hm)) + 1u : 0u;
