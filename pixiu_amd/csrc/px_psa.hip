@@ -470,41 +470,44 @@ __global__ void __launch_bounds__(256) k_psa_groups0(uint32_t N, const uint32_t 
 __global__ void __launch_bounds__(256) k_dbl_key(uint32_t N, uint32_t h, uint32_t it, const uint8_t *act, const uint32_t *sa,
                                                  const uint16_t *sd, const uint32_t *rank, uint32_t *key,
                                                  uint32_t *long_cnt, RetList R) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < 8) long_cnt[t] = 0;  // (the step's long-group lists start empty: k_dbl_win fills them)
-    const uint32_t s0 = t * 16;
-    if (s0 >= N) return;
-    if (s0 + 16 <= N) {
-        const uint4 av = *(const uint4 *)(act + s0);
-        if ((av.x | av.y | av.z | av.w) == 0) return;
-        uint32_t p[16], k[16];
-        uint16_t d[16];
-        for (int q = 0; q < 4; ++q) *(uint4 *)(p + 4 * q) = *(const uint4 *)(sa + s0 + 4 * q);
-        for (int q = 0; q < 2; ++q) *(uint4 *)(d + 8 * q) = *(const uint4 *)(sd + s0 + 8 * q);
-        const uint32_t aw[4] = {av.x, av.y, av.z, av.w};
-        bool any_ret = false;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {  // (slots outside groups get a key nobody reads)
-            k[i] = ((aw[i >> 2] >> (8 * (i & 3))) & 0xffu) && it < d[i] ? rank[p[i] + h] + 1u : 0u;
-            any_ret = any_ret || (k[i] != 0 && ((k[i] - 1u) & kRetired) != 0);
-        }
-        if (any_ret) {  // (ranks of retired groups: through their links)
-#pragma unroll
-            for (int i = 0; i < 16; ++i)
-                if (k[i] != 0 && ((k[i] - 1u) & kRetired)) k[i] = live_rank(R, rank, p[i] + h, k[i] - 1u) + 1u;
-        }
-        for (int q = 0; q < 4; ++q) *(uint4 *)(key + s0 + 4 * q) = *(const uint4 *)(k + 4 * q);
-    } else {
-        for (uint32_t s = s0; s < N; ++s)
-            if (act[s]) {
-                uint32_t r = 0;
-                if (it < sd[s]) {
-                    r = rank[sa[s] + h];
-                    if (r & kRetired) r = live_rank(R, rank, sa[s] + h, r);
-                    ++r;
-                }
-                key[s] = r;
+    const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t0 < 8) long_cnt[t0] = 0;  // (the step's long-group lists start empty: k_dbl_win fills them)
+    // grid-stride over 16-slot pieces: late steps leave most pieces without an active slot, and
+    // a workgroup per 4,096 slots spent those steps dispatching workgroups that found nothing
+    for (uint32_t t = t0; (uint64_t)t * 16 < N; t += gridDim.x * blockDim.x) {
+        const uint32_t s0 = t * 16;
+        if (s0 + 16 <= N) {
+            const uint4 av = *(const uint4 *)(act + s0);
+            if ((av.x | av.y | av.z | av.w) == 0) continue;
+            uint32_t p[16], k[16];
+            uint16_t d[16];
+            for (int q = 0; q < 4; ++q) *(uint4 *)(p + 4 * q) = *(const uint4 *)(sa + s0 + 4 * q);
+            for (int q = 0; q < 2; ++q) *(uint4 *)(d + 8 * q) = *(const uint4 *)(sd + s0 + 8 * q);
+            const uint32_t aw[4] = {av.x, av.y, av.z, av.w};
+            bool any_ret = false;
+    #pragma unroll
+            for (int i = 0; i < 16; ++i) {  // (slots outside groups get a key nobody reads)
+                k[i] = ((aw[i >> 2] >> (8 * (i & 3))) & 0xffu) && it < d[i] ? rank[p[i] + h] + 1u : 0u;
+                any_ret = any_ret || (k[i] != 0 && ((k[i] - 1u) & kRetired) != 0);
             }
+            if (any_ret) {  // (ranks of retired groups: through their links)
+    #pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    if (k[i] != 0 && ((k[i] - 1u) & kRetired)) k[i] = live_rank(R, rank, p[i] + h, k[i] - 1u) + 1u;
+            }
+            for (int q = 0; q < 4; ++q) *(uint4 *)(key + s0 + 4 * q) = *(const uint4 *)(k + 4 * q);
+        } else {
+            for (uint32_t s = s0; s < N; ++s)
+                if (act[s]) {
+                    uint32_t r = 0;
+                    if (it < sd[s]) {
+                        r = rank[sa[s] + h];
+                        if (r & kRetired) r = live_rank(R, rank, sa[s] + h, r);
+                        ++r;
+                    }
+                    key[s] = r;
+                }
+        }
     }
 }
 
@@ -1030,6 +1033,106 @@ __global__ void __launch_bounds__(256) k_big_put(uint32_t T, const uint64_t *lis
     }
     block_stat(ss, 0, ac, mx);
 }
+// The big groups placed back in one pass (what k_big_head, k_big_next, their two scans and
+// k_big_put did): a subgroup starts at a group's first member, at a key change and at every key
+// 0; the head at or before each member comes from a max-scan by decoupled look-back over
+// workgroups of kG0Slots members (k_psa_groups0's scheme); a subgroup's size is written at its
+// head by its last member.  chain: one word per workgroup and the ticket, zeroed by the caller.
+template <bool PACKED>
+__global__ void __launch_bounds__(256) k_big_place(uint32_t T, const uint64_t *list, const uint32_t *boff, const uint64_t *ck2,
+                                                   const uint32_t *cv2, const uint32_t *gp, const uint16_t *gd, uint32_t tag,
+                                                   unsigned long long *chain, uint32_t *err, uint32_t *sa, uint16_t *sd,
+                                                   uint8_t *act, uint32_t *gsz, uint32_t *rank, StepStat ss) {
+    __shared__ uint32_t s_bid, s_w[2][4], s_pre;
+    const uint32_t nb = gridDim.x;
+    if (threadIdx.x == 0) s_bid = atomicAdd((uint32_t *)(chain + nb), 1u);
+    __syncthreads();
+    const uint32_t bid = s_bid, base = bid * kG0Slots, lane = lane_id(), w = threadIdx.x >> 6;
+    const uint32_t gmask = PACKED ? 0xffffu : 0xffffffffu;
+    uint64_t kc[kG0Rows], ke[kG0Rows];
+    uint32_t vv[kG0Rows];
+#pragma unroll
+    for (uint32_t i = 0; i < kG0Rows; ++i) {
+        const uint32_t k = base + i * 256u + threadIdx.x;
+        kc[i] = k < T ? ck2[k] : 0ull;
+        ke[i] = lane == 0 ? (k > 0 && k <= T ? ck2[k - 1] : 0ull) : lane == 63 ? (k + 1 < T ? ck2[k + 1] : 0ull) : 0ull;
+        vv[i] = k < T ? cv2[k] : 0u;
+    }
+    // (a member's group is (c >> 32) & gmask, its key the low word)
+    auto head_of = [&](uint64_t c, uint64_t cl, uint32_t k) {
+        return k == 0 || (((c >> 32) ^ (cl >> 32)) & gmask) != 0 || (uint32_t)c != (uint32_t)cl || (uint32_t)c == 0;
+    };
+    uint32_t hv[kG0Rows], hnm = 0, carry = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kG0Rows; ++i) {
+        const uint32_t k = base + i * 256u + threadIdx.x;
+        const uint64_t sl = shfl64(kc[i], (lane + 63u) & 63u), sr = shfl64(kc[i], (lane + 1u) & 63u);
+        const uint64_t cl = lane == 0 ? ke[i] : sl, cr = lane == 63 ? ke[i] : sr;
+        const bool f = k < T && head_of(kc[i], cl, k);
+        if (k < T && (k + 1 >= T || head_of(cr, kc[i], k + 1))) hnm |= 1u << i;
+        uint32_t v = f ? k + 1u : 0u;
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)v, o);
+            if (lane >= o) v = max(v, y);
+        }
+        if (lane == 63) s_w[i & 1][w] = v;
+        __syncthreads();
+        for (uint32_t x = 0; x < w; ++x) v = max(v, s_w[i & 1][x]);
+        hv[i] = max(v, carry);
+        carry = max(carry, max(max(s_w[i & 1][0], s_w[i & 1][1]), max(s_w[i & 1][2], s_w[i & 1][3])));
+    }
+    if (threadIdx.x == 0) {
+        const uint32_t agg = carry;
+        __hip_atomic_store(chain + bid, (agg || bid == 0 ? kG0Incl : kG0Agg) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t pre = 0, spins = 0;
+        const bool first_head = base == 0 || head_of(ck2[base], ck2[base - 1], base);
+        if (bid > 0 && !first_head) {
+            for (uint32_t j = bid - 1;;) {
+                const unsigned long long x = __hip_atomic_load(chain + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (!(x >> 62)) {
+                    if (++spins > (1u << 24)) {
+                        atomicOr(err, 1u);
+                        break;
+                    }
+                    continue;
+                }
+                pre = max(pre, (uint32_t)(x & kG0Val));
+                if ((x >> 62) == 2 || j == 0) break;
+                --j;
+            }
+            if (!agg) __hip_atomic_store(chain + bid, kG0Incl | pre, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_pre = pre;
+    }
+    __syncthreads();
+    const uint32_t pre = s_pre;
+    uint32_t ac = 0, mx = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kG0Rows; ++i) {
+        const uint32_t k = base + i * 256u + threadIdx.x;
+        if (k >= T) break;
+        const uint64_t c = kc[i];
+        const uint32_t b = (uint32_t)(c >> 32) & gmask, key = (uint32_t)c, o = boff[b], start = (uint32_t)list[b];
+        const uint32_t hg = max(hv[i], pre) - 1u;  // the head at or before k (T coordinates)
+        const bool f = hg == k, hn = (hnm >> i) & 1u;
+        const uint32_t v = vv[i], p = PACKED ? v : gp[v], d = PACKED ? (uint32_t)(c >> 48) : gd[v];
+        const uint32_t q = k - o, dst = start + q, hd = hg - o;
+        sa[dst] = p;
+        sd[dst] = (uint16_t)d;
+        const bool grp = key != 0 && !(f && hn);  // (a head followed by a head: a subgroup of one)
+        act[dst] = grp ? 1 : 0;
+        if (!(f && grp)) gsz[dst] = 0;  // (a subgroup's size is written at its head by its last member)
+        if (hd != 0) rank[p] = start + hd;
+        ac += grp;
+        if (hn && grp) {  // the last member of a subgroup of >= 2
+            const uint32_t size = k - hg + 1u;
+            gsz[start + hd] = size | (tag ^ kTag);
+            mx = max(mx, size);
+        }
+    }
+    block_stat(ss, 0, ac, mx);
+}
+
 // nk[k] = the next head position after k (T past the last), from the head flags
 __global__ void __launch_bounds__(256) k_big_next(uint32_t T, const uint32_t *hf, uint32_t *nf) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1913,7 +2016,7 @@ bool env_on(const char *name) {
 constexpr uint32_t kMaxSteps = 20;  // h doubles from >= 5 past 65,535 (the longest doc) in 15
 // persistent grids of the doubling kernels (grid-stride over windows, and over lists whose
 // sizes only the device knows)
-constexpr uint32_t kGridWin = 16384, kGridReg = 2048, kGridBlk = 1024;
+constexpr uint32_t kGridWin = 16384, kGridReg = 2048, kGridBlk = 1024, kGridKey = 16384;
 // the cnt words of psa_run
 constexpr uint32_t kCntLong = 0, kCntSorted = 16, kCntActive = 48, kCntMax = 96, kCntCand = 200, kCntSortErr = 250,
                    kCntRet = 252, kCntWords = 256;
@@ -2035,7 +2138,8 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         const uint32_t tag = (it & 1u) ? kTag : 0u;
         const StepStat ss = stats_of(it);
         hipError_t e = hipSuccess;
-        k_dbl_key<<<blocks((n64 + 15) / 16), tb, 0, s>>>(N, h, it, act, sa, sd, rank, key, cnt + kCntLong, R);
+        k_dbl_key<<<std::min<uint32_t>(blocks((n64 + 15) / 16), kGridKey), tb, 0, s>>>(N, h, it, act, sa, sd, rank, key,
+                                                                                     cnt + kCntLong, R);
         k_dbl_win<<<gwin, 256, 0, s>>>(N, tag, h, sa, sd, act, gsz, key, rank, LL, ss, R);
         k_dbl_reg<2><<<kGridReg, 256, 0, s>>>(LL.lst[0], LL.cnt + 0, tag, h, sa, sd, act, gsz, key, rank, ss, R);
         k_dbl_reg<4><<<kGridReg, 256, 0, s>>>(LL.lst[1], LL.cnt + 1, tag, h, sa, sd, act, gsz, key, rank, ss, R);
@@ -2083,17 +2187,18 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
                                    nullptr, 0, cka, cva, nullptr, nullptr, ck2, cv2, cnt + kCntSortErr);
                 S.put(d_glen);
                 if (e != hipSuccess) return e;
-                k_big_head<<<blocks(T), tb, 0, s>>>((uint32_t)T, d_boff, ck2, packed ? 0xffffu : 0xffffffffu, hf);
-                k_big_next<<<blocks(T), tb, 0, s>>>((uint32_t)T, hf, nf);
-                e = scan_u32(s, SA, hf, hk, T, ScanOp::kMax, false);
-                if (e == hipSuccess) e = scan_u32(s, SA, nf, nk, T, ScanOp::kMin, true);
-                if (e != hipSuccess) return e;
-                if (packed)
-                    k_big_put<true><<<blocks(T), tb, 0, s>>>((uint32_t)T, LL.lst[4], d_boff, ck2, cv2, gp, gd, hf, hk, nk,
-                                                             tag, sa, sd, act, gsz, rank, ss);
-                else
-                    k_big_put<false><<<blocks(T), tb, 0, s>>>((uint32_t)T, LL.lst[4], d_boff, ck2, cv2, gp, gd, hf, hk, nk,
-                                                              tag, sa, sd, act, gsz, rank, ss);
+                {
+                    const uint32_t gb = (uint32_t)((T + kG0Slots - 1) / kG0Slots);
+                    auto *chain = (unsigned long long *)hf;  // (hf: 4 T bytes, the chain needs 8 (gb + 1))
+                    e = hipMemsetAsync(chain, 0, ((uint64_t)gb + 1) * 8, s);
+                    if (e != hipSuccess) return e;
+                    if (packed)
+                        k_big_place<true><<<gb, 256, 0, s>>>((uint32_t)T, LL.lst[4], d_boff, ck2, cv2, gp, gd, tag, chain,
+                                                             cnt + kCntSortErr, sa, sd, act, gsz, rank, ss);
+                    else
+                        k_big_place<false><<<gb, 256, 0, s>>>((uint32_t)T, LL.lst[4], d_boff, ck2, cv2, gp, gd, tag, chain,
+                                                              cnt + kCntSortErr, sa, sd, act, gsz, rank, ss);
+                }
                 for (const void *q : {(const void *)d_boff, (const void *)ck, (const void *)ck2, (const void *)cv,
                                       (const void *)cv2, (const void *)gp, (const void *)hf, (const void *)hk,
                                       (const void *)nf, (const void *)nk, (const void *)gd, (const void *)cka,

@@ -400,6 +400,7 @@ struct px_ctx {
     HostBuf hq_buf, hres_buf;  // pinned: decode queries up, lengths + statuses down
     HostBuf hg_buf[2];         // pinned: gather queries up (a head and a tail launch)
     HostBuf psa_pin;           // pinned: px_psa.hip's count read-backs
+    HostBuf kp_hbuf;           // pinned: decoded key prefixes down
     DevBuf sink_buf;           // k_gst_encode's message sink for replayed docs
     PsaStats psa_stats{};      // the last set batch's suffix-array pass
     // PX_PSA=0 sends every shard through k_gst_encode (A/B comparisons, tests)
@@ -1607,10 +1608,10 @@ struct px_ctx {
             std::vector<uint32_t> ql, qs;
             run_decode(q, kbuf, ql, qs, false);
             phase.mark("copy down");
-            // (uninitialised: 1 M key prefixes are ~80 MB, which a zero fill would write twice)
-            std::unique_ptr<uint8_t[]> hk_store(new uint8_t[qo + 1]);
-            uint8_t *hk = hk_store.get();
-            d2h(hk, kbuf, qo);
+            // (through a pinned buffer kept across batches: a million key prefixes are ~60 MB,
+            // which a pageable copy moved at a fifth of the rate)
+            auto *hk = (uint8_t *)kp_hbuf.get(qo + 1);
+            hcheck(hipMemcpyAsync(hk, kbuf, qo, hipMemcpyDeviceToHost, stream));
             sync();
             heap.release(kbuf, qo + 64);
             phase.mark("append to the chunks' prefix stores");
