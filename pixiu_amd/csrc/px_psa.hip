@@ -472,8 +472,8 @@ __global__ void __launch_bounds__(256) k_dbl_key(uint32_t N, uint32_t h, uint32_
                                                  uint32_t *long_cnt, RetList R) {
     const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x;
     if (t0 < 8) long_cnt[t0] = 0;  // (the step's long-group lists start empty: k_dbl_win fills them)
-    // grid-stride over 16-slot pieces: late steps leave most pieces without an active slot, and
-    // a workgroup per 4,096 slots spent those steps dispatching workgroups that found nothing
+    // (one thread per 16-slot piece: a bounded grid striding over the pieces kept fewer of the
+    // dense early steps' scattered reads in flight, 29.4 -> 34.1 ms over a batch's 12 steps)
     for (uint32_t t = t0; (uint64_t)t * 16 < N; t += gridDim.x * blockDim.x) {
         const uint32_t s0 = t * 16;
         if (s0 + 16 <= N) {
@@ -1007,32 +1007,6 @@ __global__ void __launch_bounds__(256) k_big_segs(uint32_t nb, const uint64_t *l
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < nb) len[i] = (uint32_t)(list[i] >> 32);
 }
-__global__ void __launch_bounds__(256) k_big_head(uint32_t T, const uint32_t *boff, const uint64_t *ck2, uint32_t bmask,
-                                                  uint32_t *hf) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= T) return;
-    const uint64_t c = ck2[k];
-    const uint32_t b = (uint32_t)(c >> 32) & bmask, key = (uint32_t)c;
-    hf[k] = (k == boff[b] || key != (uint32_t)ck2[k - 1] || key == 0) ? k : 0u;
-}
-template <bool PACKED>
-__global__ void __launch_bounds__(256) k_big_put(uint32_t T, const uint64_t *list, const uint32_t *boff, const uint64_t *ck2,
-                                                 const uint32_t *cv2, const uint32_t *gp, const uint16_t *gd,
-                                                 const uint32_t *hf, const uint32_t *hk, const uint32_t *nk, uint32_t tag,
-                                                 uint32_t *sa, uint16_t *sd, uint8_t *act, uint32_t *gsz, uint32_t *rank,
-                                                 StepStat ss) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t ac = 0, mx = 0;
-    if (k < T) {
-        const uint64_t c = ck2[k];
-        const uint32_t b = PACKED ? (uint32_t)(c >> 32) & 0xffffu : (uint32_t)(c >> 32), key = (uint32_t)c, o = boff[b];
-        const uint32_t size = (uint32_t)(list[b] >> 32), q = k - o, v = cv2[k];
-        const uint32_t nxt = min(nk[k] - o, size);
-        const uint32_t p = PACKED ? v : gp[v], d = PACKED ? (uint32_t)(c >> 48) : gd[v];
-        put_sorted((uint32_t)list[b], q, p, d, key, hf[k] == k, hk[k] - o, nxt, tag, sa, sd, act, gsz, rank, ac, mx);
-    }
-    block_stat(ss, 0, ac, mx);
-}
 // The big groups placed back in one pass (what k_big_head, k_big_next, their two scans and
 // k_big_put did): a subgroup starts at a group's first member, at a key change and at every key
 // 0; the head at or before each member comes from a max-scan by decoupled look-back over
@@ -1131,13 +1105,6 @@ __global__ void __launch_bounds__(256) k_big_place(uint32_t T, const uint64_t *l
         }
     }
     block_stat(ss, 0, ac, mx);
-}
-
-// nk[k] = the next head position after k (T past the last), from the head flags
-__global__ void __launch_bounds__(256) k_big_next(uint32_t T, const uint32_t *hf, uint32_t *nf) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= T) return;
-    nf[k] = k + 1 == T ? T : (hf[k + 1] == k + 1 ? k + 1 : 0xffffffffu);
 }
 
 // ---------------------------------------------------------------- nearest smaller positions
@@ -2016,7 +1983,7 @@ bool env_on(const char *name) {
 constexpr uint32_t kMaxSteps = 20;  // h doubles from >= 5 past 65,535 (the longest doc) in 15
 // persistent grids of the doubling kernels (grid-stride over windows, and over lists whose
 // sizes only the device knows)
-constexpr uint32_t kGridWin = 16384, kGridReg = 2048, kGridBlk = 1024, kGridKey = 16384;
+constexpr uint32_t kGridWin = 16384, kGridReg = 2048, kGridBlk = 1024;
 // the cnt words of psa_run
 constexpr uint32_t kCntLong = 0, kCntSorted = 16, kCntActive = 48, kCntMax = 96, kCntCand = 200, kCntSortErr = 250,
                    kCntRet = 252, kCntWords = 256;
@@ -2138,8 +2105,7 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         const uint32_t tag = (it & 1u) ? kTag : 0u;
         const StepStat ss = stats_of(it);
         hipError_t e = hipSuccess;
-        k_dbl_key<<<std::min<uint32_t>(blocks((n64 + 15) / 16), kGridKey), tb, 0, s>>>(N, h, it, act, sa, sd, rank, key,
-                                                                                     cnt + kCntLong, R);
+        k_dbl_key<<<blocks((n64 + 15) / 16), tb, 0, s>>>(N, h, it, act, sa, sd, rank, key, cnt + kCntLong, R);
         k_dbl_win<<<gwin, 256, 0, s>>>(N, tag, h, sa, sd, act, gsz, key, rank, LL, ss, R);
         k_dbl_reg<2><<<kGridReg, 256, 0, s>>>(LL.lst[0], LL.cnt + 0, tag, h, sa, sd, act, gsz, key, rank, ss, R);
         k_dbl_reg<4><<<kGridReg, 256, 0, s>>>(LL.lst[1], LL.cnt + 1, tag, h, sa, sd, act, gsz, key, rank, ss, R);
@@ -2168,8 +2134,7 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
                 if (e != hipSuccess) return e;
                 auto *ck = S.get<uint64_t>(T * 8), *ck2 = S.get<uint64_t>(T * 8), *cka = S.get<uint64_t>(T * 8);
                 auto *cv = S.get<uint32_t>(T * 4), *cv2 = S.get<uint32_t>(T * 4), *cva = S.get<uint32_t>(T * 4);
-                auto *gp = S.get<uint32_t>(T * 4), *hf = S.get<uint32_t>(T * 4), *hk = S.get<uint32_t>(T * 4);
-                auto *nf = S.get<uint32_t>(T * 4), *nk = S.get<uint32_t>(T * 4);
+                auto *gp = S.get<uint32_t>(T * 4), *hf = S.get<uint32_t>(T * 4);
                 auto *gd = S.get<uint16_t>(T * 2 + 64);
                 const bool packed = nbig <= 0x10000u;
                 if (packed)
@@ -2200,9 +2165,8 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
                                                               cnt + kCntSortErr, sa, sd, act, gsz, rank, ss);
                 }
                 for (const void *q : {(const void *)d_boff, (const void *)ck, (const void *)ck2, (const void *)cv,
-                                      (const void *)cv2, (const void *)gp, (const void *)hf, (const void *)hk,
-                                      (const void *)nf, (const void *)nk, (const void *)gd, (const void *)cka,
-                                      (const void *)cva})
+                                      (const void *)cv2, (const void *)gp, (const void *)hf, (const void *)gd,
+                                      (const void *)cka, (const void *)cva})
                     S.put(q);
             }
         }
