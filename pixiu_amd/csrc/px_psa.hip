@@ -472,8 +472,7 @@ __global__ void __launch_bounds__(256) k_dbl_key(uint32_t N, uint32_t h, uint32_
                                                  uint32_t *long_cnt, RetList R) {
     const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x;
     if (t0 < 8) long_cnt[t0] = 0;  // (the step's long-group lists start empty: k_dbl_win fills them)
-    // (a full grid in dense steps -- one piece per thread --, a bounded grid striding over the
-    // pieces in sparse ones; see the step driver)
+    // (launched with one thread per piece: the loop runs once; see the step driver)
     for (uint32_t t = t0; (uint64_t)t * 16 < N; t += gridDim.x * blockDim.x) {
         const uint32_t s0 = t * 16;
         if (s0 + 16 <= N) {
@@ -1983,7 +1982,7 @@ bool env_on(const char *name) {
 constexpr uint32_t kMaxSteps = 20;  // h doubles from >= 5 past 65,535 (the longest doc) in 15
 // persistent grids of the doubling kernels (grid-stride over windows, and over lists whose
 // sizes only the device knows)
-constexpr uint32_t kGridWin = 16384, kGridReg = 2048, kGridBlk = 1024, kGridKey = 16384;
+constexpr uint32_t kGridWin = 16384, kGridReg = 2048, kGridBlk = 1024;
 // the cnt words of psa_run
 constexpr uint32_t kCntLong = 0, kCntSorted = 16, kCntActive = 48, kCntMax = 96, kCntCand = 200, kCntSortErr = 250,
                    kCntRet = 252, kCntWords = 256;
@@ -2101,17 +2100,13 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     const uint32_t gwin = std::min<uint32_t>((uint32_t)((n64 + 255) / 256), kGridWin);
     // one step: every group's keys (flat), then every group sorted by them (windows, then
     // the long-group lists the window kernel filled); big groups need their count on the host
-    uint32_t known_active = active;  // (slots in groups after the last step whose count came back)
     auto step = [&](bool big) -> hipError_t {
         const uint32_t tag = (it & 1u) ? kTag : 0u;
         const StepStat ss = stats_of(it);
         hipError_t e = hipSuccess;
-        // (dense steps: one thread per 16-slot piece, every scattered read in flight at once;
-        // once fewer than an eighth of the slots are in groups -- the count the host last saw --
-        // a bounded grid strides over the pieces instead of dispatching workgroups that find
-        // nothing)
-        const uint32_t kb = blocks((n64 + 15) / 16), kg = known_active < N / 8 ? std::min(kb, kGridKey) : kb;
-        k_dbl_key<<<kg, tb, 0, s>>>(N, h, it, act, sa, sd, rank, key, cnt + kCntLong, R);
+        // (one thread per 16-slot piece; a bounded grid striding over the pieces measured slower
+        // in the dense steps (29.4 -> 34.1 ms) and no faster when used only in the sparse ones)
+        k_dbl_key<<<blocks((n64 + 15) / 16), tb, 0, s>>>(N, h, it, act, sa, sd, rank, key, cnt + kCntLong, R);
         k_dbl_win<<<gwin, 256, 0, s>>>(N, tag, h, sa, sd, act, gsz, key, rank, LL, ss, R);
         k_dbl_reg<2><<<kGridReg, 256, 0, s>>>(LL.lst[0], LL.cnt + 0, tag, h, sa, sd, act, gsz, key, rank, ss, R);
         k_dbl_reg<4><<<kGridReg, 256, 0, s>>>(LL.lst[1], LL.cnt + 1, tag, h, sa, sd, act, gsz, key, rank, ss, R);
@@ -2190,7 +2185,6 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         PSA_CHECK(read_words(0, kCntWords));
         active = pin[kCntActive + it];
         maxsz = pin[kCntMax + it];
-        known_active = active;
         if (verbose)
             fprintf(stderr, "psa: step %u (host) sorted %u (long groups %u %u %u %u %u) -> %u in groups, largest %u\n",
                     it - 1, pin[kCntSorted + it - 1], pin[kCntLong], pin[kCntLong + 1], pin[kCntLong + 2],
@@ -2209,7 +2203,6 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
             if (k >= it0 + 1) {
                 PSA_CHECK(hipEventSynchronize(sev.e[k - 1]));
                 done = pin[256 + k - 1] == 0;
-                known_active = pin[256 + k - 1];
             }
         }
     }
