@@ -1570,6 +1570,10 @@ __global__ void __launch_bounds__(256) k_link(uint32_t n, const LinkJob *jobs) {
 #define PX_DEC_WAVES 4
 #endif
 constexpr uint32_t kLaneDepth = PX_LANE_DEPTH;  // 10: 10 KB of LDS per wave, 4 blocks (16 waves) per CU
+#ifndef PX_LANE_SPILL
+#define PX_LANE_SPILL 24
+#endif
+constexpr uint32_t kLaneSpill = PX_LANE_SPILL;  // lane frames past kLaneDepth, in scratch memory
 constexpr uint32_t kLaneCopyMax = 512;  // plain pieces up to this size are copied by one lane
 constexpr uint32_t kAssignMin = 24;      // idle lanes that trigger an assignment round
 
@@ -1909,6 +1913,10 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
         auto window = [&](Frame &f, const SlotV &sv) -> bool {
             if (!sv.lane) return true;  // no lane entries: the serial path takes every segment
             const int32_t rbase = depth == 1 ? qbase : 0;
+            // lane frames past the LDS stack spill to this wave's unused serial frames
+            // (stk[depth, depth_cap) are free while the window runs): 1 KB per level
+            PX_GAS u32x4 *spill = (PX_GAS u32x4 *)(stk + depth);
+            const uint32_t dmax = kLaneDepth + min(kLaneSpill, (depth_cap - depth) * 3u / 64u);
             const uint32_t outp0 = outp;
             const int32_t ret0 = f.ret;
             uint32_t next = f.seg;     // next unassigned segment
@@ -2093,13 +2101,17 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                                 done = true;
                             } else {
                                 --d;
-                                const uint32_t w0 = lds.stk[d * 4 + 0][lane], w1 = lds.stk[d * 4 + 1][lane];
-                                const uint32_t w2 = lds.stk[d * 4 + 2][lane];
-                                ne = (const PX_GAS u32x4 *)((uint64_t)w0 | (uint64_t)(w1 & 0xffffu) << 32);
-                                rec = w1 >> 16;
-                                from = (int32_t)(w2 & 0xffffu);
-                                len = (int32_t)(w2 >> 16);
-                                ret = (int32_t)lds.stk[d * 4 + 3][lane];
+                                u32x4 W;
+                                if (d < kLaneDepth)
+                                    W = mk4(lds.stk[d * 4 + 0][lane], lds.stk[d * 4 + 1][lane], lds.stk[d * 4 + 2][lane],
+                                            lds.stk[d * 4 + 3][lane]);
+                                else
+                                    W = spill[(d - kLaneDepth) * 64 + lane];
+                                ne = (const PX_GAS u32x4 *)((uint64_t)W.x | (uint64_t)(W.y & 0xffffu) << 32);
+                                rec = W.y >> 16;
+                                from = (int32_t)(W.z & 0xffffu);
+                                len = (int32_t)(W.z >> 16);
+                                ret = (int32_t)W.w;
                             }
                         } else if (kd == 0) {
                             const int32_t q0 = max(x, from);
@@ -2126,16 +2138,22 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                                 const int32_t stp = compat ? ret : max(x, from);
                                 const PX_GAS u32x4 *t = (int32_t)F.w == kRelNone ? nullptr : e + (int32_t)F.w;
                                 const uint64_t nx = (uint64_t)(e + 1);
-                                if (!t || ri >= nrec || (ri == rec && sf < stp && stp < st) || d + 1 >= kLaneDepth ||
+                                if (!t || ri >= nrec || (ri == rec && sf < stp && stp < st) || d + 1 >= dmax ||
                                     (uint32_t)from > 0xffffu || (uint32_t)len > 0xffffu || (nx >> 48) != 0) {
-                                    PX_FR(!t ? 3 : ri >= nrec ? 8 : (ri == rec && sf < stp && stp < st) ? 5 : d + 1 >= kLaneDepth ? 6 : 7);
+                                    PX_FR(!t ? 3 : ri >= nrec ? 8 : (ri == rec && sf < stp && stp < st) ? 5 : d + 1 >= dmax ? 6 : 7);
                                     flag = true;  // leaves the lane path: serial machine
                                     busy = false;
                                 } else {
-                                    lds.stk[d * 4 + 0][lane] = (uint32_t)nx;
-                                    lds.stk[d * 4 + 1][lane] = (uint32_t)(nx >> 32) | rec << 16;
-                                    lds.stk[d * 4 + 2][lane] = (uint32_t)from | (uint32_t)len << 16;
-                                    lds.stk[d * 4 + 3][lane] = (uint32_t)(ret + (st - sf));
+                                    const u32x4 W = mk4((uint32_t)nx, (uint32_t)(nx >> 32) | rec << 16,
+                                                        (uint32_t)from | (uint32_t)len << 16, (uint32_t)(ret + (st - sf)));
+                                    if (d < kLaneDepth) {
+                                        lds.stk[d * 4 + 0][lane] = W.x;
+                                        lds.stk[d * 4 + 1][lane] = W.y;
+                                        lds.stk[d * 4 + 2][lane] = W.z;
+                                        lds.stk[d * 4 + 3][lane] = W.w;
+                                    } else {
+                                        spill[(d - kLaneDepth) * 64 + lane] = W;
+                                    }
                                     ++d;
                                     ne = t;  // the target's entry holding rf; entries before sf are passed over
                                     rec = ri;
