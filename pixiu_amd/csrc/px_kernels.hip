@@ -1557,21 +1557,22 @@ __global__ void __launch_bounds__(256) k_link(uint32_t n, const LinkJob *jobs) {
 // consumed 64 segments at a time: lane l takes segment f.seg + l, a prefix scan of
 // the requested sizes gives every lane its ret cursor and its output offset, and
 // each lane expands its own record reference depth-first, walking the linked
-// segment entries by address with a small per-lane stack in LDS and writing
-// straight to the output.  A lane whose work leaves the simple case (a periodic
-// self reference, deeper nesting, an output that would reach the consumer's cap or
+// segment entries by address with a small per-lane stack in LDS (deeper frames
+// spill to the wave's free serial frames) and writing straight to the output.  A
+// lane whose work leaves the simple case (a periodic self reference, nesting past
+// the spill, an output that would reach the consumer's cap or
 // exceed what it asked for, an unlinked token) ends the batch; that one segment
 // then goes through the serial frame machine (a stack of Frames in scratch memory),
 // which is the reference's generator nesting restated.
 #ifndef PX_LANE_DEPTH
-#define PX_LANE_DEPTH 10
+#define PX_LANE_DEPTH 4
 #endif
 #ifndef PX_DEC_WAVES
 #define PX_DEC_WAVES 4
 #endif
-constexpr uint32_t kLaneDepth = PX_LANE_DEPTH;  // 10: 10 KB of LDS per wave, 4 blocks (16 waves) per CU
+constexpr uint32_t kLaneDepth = PX_LANE_DEPTH;  // 4: 4 KB of LDS per wave; registers then bound occupancy (28 waves/CU)
 #ifndef PX_LANE_SPILL
-#define PX_LANE_SPILL 24
+#define PX_LANE_SPILL 32
 #endif
 constexpr uint32_t kLaneSpill = PX_LANE_SPILL;  // lane frames past kLaneDepth, in scratch memory
 constexpr uint32_t kLaneCopyMax = 512;  // plain pieces up to this size are copied by one lane
