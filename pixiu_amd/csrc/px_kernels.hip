@@ -98,7 +98,7 @@ enum { P_BYTES, P_FF_CALLS, P_FF_BYTES, P_PASS, P_ITERS, P_LOOKUPS, P_PROBES, P_
        P_G_NOSPLIT, P_G_T_LEAF, P_G_T_SPLIT, P_G_T_ADD,
        P_E_LOOK, P_E_OFF1, P_E_OFF2, P_E_OFF3, P_E_OFF4P, P_K_CACHED, P_K_LOAD1, P_K_LOADN,
        P_DF_NONE, P_DF_TOPREF, P_DF_CAP, P_DF_NOLINK, P_DF_OVER, P_DF_LPER, P_DF_DEPTH, P_DF_RANGE, P_DF_BADREC,
-       P_D_TOPB, P_D_SUBB, P_D_TOPC, P_D_MAXIT, P_D_T_ASSIGN, P_D_ROUNDS, P_N };
+       P_D_TOPB, P_D_SUBB, P_D_TOPC, P_D_MAXIT, P_D_T_ASSIGN, P_D_ROUNDS, P_D_SPILL, P_N };
 __device__ unsigned long long g_prof[P_N];
 #define PX_CNT(k, v) (prof[k] += (v))
 #define PX_T0() uint64_t _t0 = __builtin_amdgcn_s_memtime()
@@ -1940,7 +1940,7 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
             const PX_GAS uint8_t *psrc = nullptr;
 #ifdef PX_PROFILE
             uint32_t freason = 0, freason_first = 0;
-            uint32_t lane_it = 0;
+            uint32_t lane_it = 0, nspill = 0;  // (nspill: this lane's frames stored past the LDS stack)
 #endif
             // walk state
             const PX_GAS u32x4 *e = nullptr;  // the lane entry F was loaded from
@@ -2154,6 +2154,9 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                                         lds.stk[d * 4 + 3][lane] = W.w;
                                     } else {
                                         spill[(d - kLaneDepth) * 64 + lane] = W;
+#ifdef PX_PROFILE
+                                        ++nspill;
+#endif
                                     }
                                     ++d;
                                     ne = t;  // the target's entry holding rf; entries before sf are passed over
@@ -2231,6 +2234,8 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
             }
 #ifdef PX_PROFILE
             prof[P_D_T_LANE] += __builtin_amdgcn_s_memtime() - t_lane0;
+            for (int ofs = 32; ofs >= 1; ofs >>= 1) nspill += (uint32_t)__shfl_xor((int)nspill, ofs);
+            prof[P_D_SPILL] += nspill;
             {
                 uint32_t mx = lane_it;
                 prof[P_D_MAXIT] += uni(mx);

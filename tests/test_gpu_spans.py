@@ -165,3 +165,39 @@ def test_compat_tables_in_pieces(rps, store_factory):
     assert q1 == q2 and q1 >= 0.5 * len(keys)
     assert g1 == g2 == g0
     assert e1 == e2 == e0
+
+
+def _chain_docs(seed, n, size):
+    """Each doc is the previous one with one random byte inserted: the text around the latest
+    insertions occurs only in the previous doc, so a record's tokens reference the record
+    before it, whose range references the one before that — nesting as deep as the shard."""
+    rng = np.random.default_rng(seed)
+    v = rng.integers(0, 256, size, dtype=np.uint8)
+    vals = [v.tobytes()]
+    for _ in range(n - 1):
+        v = np.insert(v, int(rng.integers(0, len(v) + 1)), np.uint8(rng.integers(0, 256)))
+        vals.append(v.tobytes())
+    return [b"c%04d" % i for i in range(n)], vals
+
+
+def test_deep_reference_chains(store_factory, oracle):
+    """Walks nested past the decoder's LDS lane stack (frames spilled to scratch) and past the
+    spill (the serial frame machine): gathered and walked compat bytes equal the oracle's
+    PXSGen restatement record by record, and exact getitem is the doc."""
+    n, rps = 96, 48
+    keys, vals = _chain_docs(11, n, 1500)
+
+    def run():
+        st = store_factory(records_per_shard=rps)
+        r = st.set_batch(keys, vals)
+        assert int(r["status"].max()) == 0
+        return st.get_batch(keys), st.get_batch(keys, mode=px.EXACT)
+
+    g1, e1 = _with_spans(True, run)
+    g0, e0 = _with_spans(False, run)
+    want = []
+    for a in range(0, n, rps):
+        want += oracle.run(keys[a:a + rps], vals[a:a + rps])["get"]
+    assert g1 == g0 == want
+    docs = [assemble(k, v) for k, v in zip(keys, vals)]
+    assert e1 == e0 == docs

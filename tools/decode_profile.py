@@ -7,12 +7,10 @@ import torch
 import pixiu_amd as px
 from pixiu_amd import synth
 import re
-_src = open(os.path.join(os.path.dirname(__file__), "..", "pixiu_amd", "csrc", "px_kernels.hip")).read()
-_enum = re.search(r"enum \{ (P_BYTES.*?) P_N \};", _src, re.S).group(1)
-IDX = {n.strip()[2:].lower(): i for i, n in enumerate(_enum.replace("\n", " ").split(",")) if n.strip()}
+from decode_profile_names import IDX
 NAMES = ["d_batch", "d_laneit", "d_serial", "d_commit", "d_flagged", "d_short", "d_push", "d_t_total", "d_t_lane",
          "df_none", "df_topref", "df_cap", "df_nolink", "df_over", "df_lper", "df_depth", "df_range", "df_badrec",
-         "d_topb", "d_subb", "d_topc", "d_maxit", "d_t_assign", "d_rounds"]
+         "d_topb", "d_subb", "d_topc", "d_maxit", "d_t_assign", "d_rounds", "d_spill"]
 lib = px.load_library()
 lib.px_debug_prof_take.argtypes = [C.c_void_p, C.c_uint32]
 cfg, n, rps = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
