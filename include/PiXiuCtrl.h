@@ -235,16 +235,19 @@ struct PiXiuCtrl {
             uint8_t dummy = 0;
             rc = px_set_batch(ctx, 1, k, koff, v ? v : &dummy, voff, 0, &r);
         }
-        if (rc == PX_OK && flush_rc != PX_OK) {  // an earlier queued record failed to store
-            rc = flush_rc;
-            flush_rc = PX_OK;
-        }
         if (rc != PX_OK) return -rc;
+        // this record is accepted (stored or queued): its bookkeeping first, then an earlier
+        // queued record's failure, if one is still unreported, is returned in its place
         if (r.chunk == PX_PENDING) {
             pending = true;
         } else {
             pending = false;
             apply(r);
+        }
+        if (flush_rc != PX_OK) {
+            const int f = flush_rc;
+            flush_rc = PX_OK;
+            return -f;
         }
         return (int)r.replaced;
     }

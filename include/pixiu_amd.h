@@ -54,7 +54,11 @@ typedef enum px_status {
 
 typedef enum px_mode {
     PX_COMPAT = 0, /* byte-exact with the reference PXSGen, bugs included */
-    PX_EXACT = 1   /* correct LZ expansion: equals the original escaped doc */
+    PX_EXACT = 1   /* correct LZ expansion: equals the original escaped doc, except in a record
+                      holding a small reference token of length 251 (the reference encoder writes
+                      its length byte as 251, which every decoder reads as an escape pair:
+                      PiXiuStr.cpp:61-78) -- those bytes are lost at setitem, in the reference
+                      too, and such a record's exact expansion is shorter than its doc */
 } px_mode;
 
 typedef struct px_opts {
@@ -70,7 +74,9 @@ typedef struct px_opts {
     uint32_t retain_mb;         /* device memory the heap keeps cached in wholly free slabs after a
                                    set batch (the rest goes back to the driver); 0 = what that
                                    batch needed at its peak beyond what stays live (similar
-                                   batches then never re-allocate), 0xffffffff = keep everything.
+                                   batches then never re-allocate), capped at half of the device
+                                   memory free to the process (free + cached); 0xffffffff = keep
+                                   everything.
                                    px_trim returns cached memory on request. */
 } px_opts;
 
@@ -185,7 +191,8 @@ int px_get_batch(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *k
  * written on the device and complete when the call returns.  Same results and return codes as
  * px_get_batch, except that when out_cap is too small only *needed is defined (with
  * PX_ESPACE).  Keys the device key index does not answer go the host path (keys copied down,
- * results up). */
+ * results up).  The keys are read in place and never past keys + koff[n]: no padding is
+ * needed after the last key (its tail is read byte by byte). */
 int px_get_batch_dev(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff, int mode,
                      uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint32_t *out_len,
                      uint32_t *status, uint64_t *needed);

@@ -26,8 +26,10 @@ namespace {
 
 #define DK_DEV __device__ __forceinline__
 
-// keys are read 16 bytes at a time (unaligned loads; both key buffers keep >= 16 bytes of
-// slack past their last key), the bytes past a key's end masked off
+// keys are read 16 bytes at a time (unaligned loads), the bytes past a key's end masked off.
+// The index's own key arena keeps >= 16 bytes of slack past its last key; a query key may sit
+// at the very end of a caller's allocation (px_get_batch_dev reads the caller's device keys in
+// place), so its last partial chunk is read byte by byte (SAFE) and nothing past it is touched.
 #define DK_GAS __attribute__((address_space(1)))
 typedef uint32_t dk_u4 __attribute__((ext_vector_type(4), aligned(1)));
 DK_DEV uint32_t dk_word(const dk_u4 &v, int j, uint32_t left) {  // word j of v, bytes past `left` zeroed
@@ -35,12 +37,25 @@ DK_DEV uint32_t dk_word(const dk_u4 &v, int j, uint32_t left) {  // word j of v,
     const uint32_t lo = 4u * (uint32_t)j;
     return left >= lo + 4u ? x : left <= lo ? 0u : x & ((1u << (8u * (left - lo))) - 1u);
 }
+template <bool SAFE>
+DK_DEV dk_u4 dk_load(const DK_GAS uint8_t *p, uint32_t left) {
+    if (!SAFE || left >= 16u) return *(const DK_GAS dk_u4 *)p;
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    for (uint32_t b = 0; b < left; ++b) w[b >> 2] |= (uint32_t)p[b] << (8u * (b & 3u));
+    dk_u4 v;
+    v.x = w[0];
+    v.y = w[1];
+    v.z = w[2];
+    v.w = w[3];
+    return v;
+}
 
+template <bool SAFE>
 DK_DEV unsigned long long dk_hash(const uint8_t *k_, uint32_t n) {
     const DK_GAS uint8_t *k = (const DK_GAS uint8_t *)k_;
     unsigned long long h = 0x9E3779B97F4A7C15ull ^ n;
     for (uint32_t i = 0; i < n; i += 16) {
-        const dk_u4 v = *(const DK_GAS dk_u4 *)(k + i);
+        const dk_u4 v = dk_load<SAFE>(k + i, n - i);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             h ^= dk_word(v, j, n - i);
@@ -53,10 +68,11 @@ DK_DEV unsigned long long dk_hash(const uint8_t *k_, uint32_t n) {
     return h | 1ull;
 }
 
+// a: the index's key arena (slack past its end), b: a query key (read safely)
 DK_DEV bool bytes_eq(const uint8_t *a_, const uint8_t *b_, uint32_t n) {
     const DK_GAS uint8_t *a = (const DK_GAS uint8_t *)a_, *b = (const DK_GAS uint8_t *)b_;
     for (uint32_t i = 0; i < n; i += 16) {
-        const dk_u4 x = *(const DK_GAS dk_u4 *)(a + i), y = *(const DK_GAS dk_u4 *)(b + i);
+        const dk_u4 x = dk_load<false>(a + i, n - i), y = dk_load<true>(b + i, n - i);
         uint32_t d = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) d |= dk_word(x, j, n - i) ^ dk_word(y, j, n - i);
@@ -72,7 +88,7 @@ __global__ void __launch_bounds__(256) k_dk_insert(uint32_t gid0, uint32_t n, co
     const uint32_t gid = gid0 + j;
     const DkRec r = rec[gid];
     const uint8_t *k = keys + r.key_off;
-    const unsigned long long h = dk_hash(k, r.key_len);
+    const unsigned long long h = dk_hash<false>(k, r.key_len);
     uint32_t i = (uint32_t)h & mask;
     for (uint32_t probes = 0; probes <= mask; ++probes, i = (i + 1) & mask) {
         // the slot of this hash: claimed by the first inserter, then every record with the
@@ -117,7 +133,7 @@ __global__ void __launch_bounds__(256) k_dk_lookup(uint32_t nq, const uint8_t *q
     if (q < nq && !*ins_err) {  // (an insert that gave up: every key goes to the host)
         const uint8_t *k = qkeys + qoff[q];
         const uint32_t n = (uint32_t)(qoff[q + 1] - qoff[q]);
-        const unsigned long long h = dk_hash(k, n);
+        const unsigned long long h = dk_hash<true>(k, n);
         uint32_t i = (uint32_t)h & mask, g = kNone;
         for (uint32_t probes = 0; probes <= mask; ++probes, i = (i + 1) & mask) {
             const unsigned long long x = tab[i].h;

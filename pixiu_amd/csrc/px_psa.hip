@@ -469,7 +469,9 @@ __global__ void __launch_bounds__(256) k_psa_groups0(uint32_t N, const uint32_t 
 // flight at once
 __global__ void __launch_bounds__(256) k_dbl_key(uint32_t N, uint32_t h, uint32_t it, const uint8_t *act, const uint32_t *sa,
                                                  const uint16_t *sd, const uint32_t *rank, uint32_t *key,
-                                                 uint32_t *long_cnt, RetList R) {
+                                                 uint32_t *long_cnt, RetList R, uint32_t *err) {
+    // (a rank read past the text -- a reach that overstates the doc, as corrupted sort keys
+    // once gave -- is refused and fails the batch instead of faulting)
     const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x;
     if (t0 < 8) long_cnt[t0] = 0;  // (the step's long-group lists start empty: k_dbl_win fills them)
     // (launched with one thread per piece: the loop runs once; see the step driver)
@@ -483,12 +485,16 @@ __global__ void __launch_bounds__(256) k_dbl_key(uint32_t N, uint32_t h, uint32_
             for (int q = 0; q < 4; ++q) *(uint4 *)(p + 4 * q) = *(const uint4 *)(sa + s0 + 4 * q);
             for (int q = 0; q < 2; ++q) *(uint4 *)(d + 8 * q) = *(const uint4 *)(sd + s0 + 8 * q);
             const uint32_t aw[4] = {av.x, av.y, av.z, av.w};
-            bool any_ret = false;
+            bool any_ret = false, bad = false;
     #pragma unroll
             for (int i = 0; i < 16; ++i) {  // (slots outside groups get a key nobody reads)
-                k[i] = ((aw[i >> 2] >> (8 * (i & 3))) & 0xffu) && it < d[i] ? rank[p[i] + h] + 1u : 0u;
+                const bool want = ((aw[i >> 2] >> (8 * (i & 3))) & 0xffu) && it < d[i];
+                const uint32_t q = p[i] + h;
+                k[i] = want && q < N ? rank[q] + 1u : 0u;
+                bad = bad || (want && q >= N);
                 any_ret = any_ret || (k[i] != 0 && ((k[i] - 1u) & kRetired) != 0);
             }
+            if (bad) atomicOr(err, 2u);
             if (any_ret) {  // (ranks of retired groups: through their links)
     #pragma unroll
                 for (int i = 0; i < 16; ++i)
@@ -499,7 +505,9 @@ __global__ void __launch_bounds__(256) k_dbl_key(uint32_t N, uint32_t h, uint32_
             for (uint32_t s = s0; s < N; ++s)
                 if (act[s]) {
                     uint32_t r = 0;
-                    if (it < sd[s]) {
+                    if (it < sd[s] && sa[s] + h >= N) {
+                        atomicOr(err, 2u);
+                    } else if (it < sd[s]) {
                         r = rank[sa[s] + h];
                         if (r & kRetired) r = live_rank(R, rank, sa[s] + h, r);
                         ++r;
@@ -2019,10 +2027,13 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     PSA_CHECK(hipMemsetAsync(G + N, 0, 64, s));  // (ld8 reads up to 15 bytes past the text)
     PSA_CHECK(hipMemsetAsync(cnt, 0, kCntWords * 4, s));
 
-    // ---- first sort: 6 symbols of 9 bits per suffix, inside each shard (px_sort.hip: the
+    // ---- first sort: `syms` (6) symbols of 9 bits per suffix, inside each shard (px_sort.hip: the
     // shards are contiguous in position space and their suffix-array ranges are the same
     // ranges, so each shard sorts on its own and no key carries the shard)
-    const uint32_t syms = 6;
+    // (PX_PSA_SYMS = 2..6 for tests and measurements: fewer symbols give odd pass counts,
+    // which px_route.h routes; more do not fit below the reach bits, kDlShift)
+    uint32_t syms = 6;
+    if (const char *ev_syms = std::getenv("PX_PSA_SYMS")) syms = (uint32_t)std::min(6, std::max(2, std::atoi(ev_syms)));
     {
         const uint32_t slices = std::max<uint32_t>(1, std::min<uint32_t>(64, 16384 / ndocs));
         const uint64_t nw = (uint64_t)ndocs * slices;
@@ -2106,7 +2117,8 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         hipError_t e = hipSuccess;
         // (one thread per 16-slot piece; a bounded grid striding over the pieces measured slower
         // in the dense steps (29.4 -> 34.1 ms) and no faster when used only in the sparse ones)
-        k_dbl_key<<<blocks((n64 + 15) / 16), tb, 0, s>>>(N, h, it, act, sa, sd, rank, key, cnt + kCntLong, R);
+        k_dbl_key<<<blocks((n64 + 15) / 16), tb, 0, s>>>(N, h, it, act, sa, sd, rank, key, cnt + kCntLong, R,
+                                                          cnt + kCntSortErr);
         k_dbl_win<<<gwin, 256, 0, s>>>(N, tag, h, sa, sd, act, gsz, key, rank, LL, ss, R);
         k_dbl_reg<2><<<kGridReg, 256, 0, s>>>(LL.lst[0], LL.cnt + 0, tag, h, sa, sd, act, gsz, key, rank, ss, R);
         k_dbl_reg<4><<<kGridReg, 256, 0, s>>>(LL.lst[1], LL.cnt + 1, tag, h, sa, sd, act, gsz, key, rank, ss, R);

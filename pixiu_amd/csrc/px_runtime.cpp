@@ -94,6 +94,14 @@ struct PxFail {
 };
 
 inline uint64_t round_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+// the fault-injecting test hooks (PX_DEBUG_SET_THROW, PX_DEBUG_FAIL_REC, PX_DEBUG_POISON) act
+// only when PX_TEST_HOOKS=1 arms them as well, so a stray variable cannot break production
+// batches
+inline const char *test_hook(const char *name) {
+    const char *armed = std::getenv("PX_TEST_HOOKS");
+    if (!armed || armed[0] != '1') return nullptr;
+    return std::getenv(name);
+}
 // position-index blocks for a record of `src_len` source bytes (k_tokenize)
 inline uint32_t pidx_blocks(uint32_t src_len) { return src_len / 16 + 2; }
 constexpr uint32_t kNoPidxBit = 1u << 31;  // k_tokenize: record has no position index
@@ -521,13 +529,18 @@ struct px_ctx {
     // what the batch itself needed at its peak beyond what stays live, so a workload of
     // similar batches never hands memory back to the driver and maps it again (round 4
     // freed ~25 GB after every config-3 batch and re-allocated it inside the next one);
-    // memory beyond that (a batch larger than the ones after it) goes back.  px_trim()
-    // returns cached memory on request.
+    // memory beyond that (a batch larger than the ones after it) goes back.  The adaptive
+    // amount is capped at half of what the device could give this process now (its free
+    // memory plus what the heap caches), so other allocators in the process (torch's) keep
+    // at least as much as the cache.  px_trim() returns cached memory on request.
     void trim_heap() {
         if (opts.retain_mb == 0xffffffffu) return;
         const uint64_t live = heap.live_bytes();
-        const uint64_t keep = opts.retain_mb ? (uint64_t)opts.retain_mb << 20
-                                             : heap.live_peak() - std::min(heap.live_peak(), live);
+        uint64_t keep = opts.retain_mb ? (uint64_t)opts.retain_mb << 20 : heap.live_peak() - std::min(heap.live_peak(), live);
+        if (!opts.retain_mb) {
+            size_t fr = 0, tot = 0;
+            if (hipMemGetInfo(&fr, &tot) == hipSuccess) keep = std::min<uint64_t>(keep, ((uint64_t)fr + heap.cached_free()) / 2);
+        }
         heap.trim(keep);
     }
 
@@ -1685,7 +1698,7 @@ struct px_ctx {
     // PX_DEBUG_POISON=1: fill the batch scratch with garbage before each set batch (tests
     // that no per-record result depends on what an earlier batch left there)
     static bool debug_poison() {
-        const char *e = std::getenv("PX_DEBUG_POISON");
+        const char *e = test_hook("PX_DEBUG_POISON");
         return e && *e && *e != '0';
     }
     ~px_ctx() {
@@ -1792,7 +1805,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         }
     }
     PhaseClock phase("set_batch", "PX_SET_VERBOSE");
-    if (std::getenv("PX_DEBUG_SET_THROW")) throw std::bad_alloc();  // (test hook: a failing batch)
+    if (test_hook("PX_DEBUG_SET_THROW")) throw std::bad_alloc();  // (test hook: a failing batch)
     heap.mark_peak();  // (this batch's scratch peak: trim_heap keeps that much cached)
     phase.mark("inputs on device; raw keys also on host ");
     // ---- inputs on device; raw keys also on host (the CritBit needs them)
@@ -2250,7 +2263,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             corrupt = PX_ECORRUPT;
         }
     }
-    if (const char *e = std::getenv("PX_DEBUG_FAIL_REC")) {  // test hook: fail one placed record
+    if (const char *e = test_hook("PX_DEBUG_FAIL_REC")) {  // test hook: fail one placed record
         const uint32_t r = (uint32_t)std::atoi(e);
         if (r < n && rstatus[r] == kOk) rstatus[r] = kErrCorrupt;
     }
@@ -3655,13 +3668,18 @@ int px_set_docs(px_ctx *ctx, uint32_t n, const uint8_t *docs, const uint64_t *do
 
 int px_flush(px_ctx *ctx, px_set_result *last) {
     if (!ctx) return PX_EINVAL;
-    PX_GUARD({
-        ctx->flush_queue();
-        if (last && ctx->have_last) *last = ctx->last_res;
-        const int rc = ctx->dq_rc;
-        ctx->dq_rc = PX_OK;
-        return rc;
-    })
+    // the failure is handed out once: dq_rc is cleared whether the flush itself threw or not
+    // (a failed flush_queue() records its code there too)
+    const int rc = [&]() -> int {
+        PX_GUARD({
+            ctx->flush_queue();
+            if (last && ctx->have_last) *last = ctx->last_res;
+            return PX_OK;
+        })
+    }();
+    const int dq = ctx->dq_rc;
+    ctx->dq_rc = PX_OK;
+    return rc != PX_OK ? rc : dq;
 }
 
 static int get_batch_impl(px_ctx *ctx, uint32_t n, const uint8_t *keys, const uint64_t *koff, int mode, uint8_t *out,

@@ -42,7 +42,9 @@ uint32_t seg_tile_count(const uint32_t *len, uint32_t nseg);
 // Pass 0 reads (k0, v0), or -- with G / dist set -- computes each position's key from the
 // text: `syms` 9-bit symbols (byte + 1, 0 past the doc end; value = the position).  The
 // last pass writes (kout, vout).  Scratch pairs: (ka, va) always; (kb, vb) when pass 0 reads
-// the text and there are >= 3 passes (otherwise k0 / v0 are reused).  kout may alias kb.
+// the text (otherwise k0 / v0 are reused).  Any pass count is routed so that no pass writes a
+// buffer it reads (px_route.h); kout / vout may alias kb / vb or k0 / v0.  A pass count that
+// cannot be routed returns hipErrorInvalidValue.
 // *err (device word, zeroed by the caller) is set if a tile's look-back outlasted its bound
 // (cannot happen; the sort is then wrong and the caller must fail).
 hipError_t seg_sort_pairs(hipStream_t s, const SortAlloc &A, uint32_t nseg, uint32_t ntiles, const uint32_t *d_start,

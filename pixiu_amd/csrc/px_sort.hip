@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <vector>
 
+#include "px_route.h"
 #include "px_sort.h"
 
 namespace px {
@@ -33,7 +34,7 @@ namespace {
 #define SD __device__ __forceinline__
 constexpr uint32_t kThreads = 256, kItems = 16, kWaves = kThreads / 64;
 static_assert(kThreads * kItems == kSortTile, "tile = threads x items");
-constexpr uint32_t kMaxPasses = 8;
+constexpr uint32_t kMaxPasses = kRouteMaxPasses;
 constexpr uint32_t kHistTiles = 16;       // tiles per histogram workgroup, at most (fewer for small sorts)
 constexpr uint32_t kHistGroups = 1024;    // histogram workgroups a sort aims for
 constexpr uint32_t kFlagAgg = 1u << 30, kFlagIncl = 2u << 30, kCountMask = (1u << 30) - 1u;
@@ -578,6 +579,15 @@ hipError_t seg_sort_pairs(hipStream_t s, const SortAlloc &A, uint32_t nseg, uint
     // 16 tiles per workgroup left ~30 workgroups, each walking 64 K elements alone)
     const uint32_t tpw = std::max<uint32_t>(1, std::min<uint32_t>(kHistTiles, (nt + kHistGroups - 1) / kHistGroups));
     const uint32_t hb = (nt + tpw - 1) / tpw;
+    // every pass's output pair (px_route.h: no pass writes a buffer it reads, for any pass count)
+    BufPair route[kRouteMaxPasses];
+    {
+        const BufPair scratch[4] = {{ka, va}, {kb, vb}, {text ? nullptr : k0, text ? nullptr : v0}, {kout, vout}};
+        if (!sort_route(passes, BufPair{text ? nullptr : k0, text ? nullptr : v0}, scratch, BufPair{kout, vout}, route)) {
+            A.release(A.self, mem, total);
+            return hipErrorInvalidValue;
+        }
+    }
 #define PX_SORT_RB(RB_)                                                                                            \
     do {                                                                                                           \
         if (text && RB_ == 9 && passes == syms)                                                                    \
@@ -590,18 +600,8 @@ hipError_t seg_sort_pairs(hipStream_t s, const SortAlloc &A, uint32_t nseg, uint
         const uint64_t *ki = k0;                                                                                   \
         const uint32_t *vi = v0;                                                                                   \
         for (uint32_t p = 0; p < passes && e == hipSuccess; ++p) {                                                 \
-            uint64_t *ko;                                                                                          \
-            uint32_t *vo;                                                                                          \
-            if (p + 1 == passes) {                                                                                 \
-                ko = kout;                                                                                         \
-                vo = vout;                                                                                         \
-            } else if (p % 2 == 0) {                                                                               \
-                ko = ka;                                                                                           \
-                vo = va;                                                                                           \
-            } else {                                                                                               \
-                ko = text ? kb : k0;                                                                               \
-                vo = text ? vb : v0;                                                                               \
-            }                                                                                                      \
+            uint64_t *ko = (uint64_t *)route[p].k;                                                                 \
+            uint32_t *vo = (uint32_t *)route[p].v;                                                                 \
             e = hipMemsetAsync(d_status, 0, b_status, s);                                                          \
             if (e != hipSuccess) break;                                                                            \
             if (text && p == 0)                                                                                    \

@@ -9,6 +9,9 @@ if ROOT not in sys.path:
 HERE = os.path.dirname(os.path.abspath(__file__))
 if HERE not in sys.path:
     sys.path.insert(0, HERE)
+# arms the runtime's fault-injecting test hooks (PX_DEBUG_SET_THROW, _FAIL_REC, _POISON): they
+# still act only while a test sets their own variable
+os.environ["PX_TEST_HOOKS"] = "1"
 
 
 def pytest_configure(config):

@@ -248,6 +248,7 @@ int main() {
         // a queued record whose store fails is reported, not lost silently (PX_DEBUG_SET_THROW:
         // the batch throws bad_alloc inside the flush a read triggers)
         CHECK(ctrl.setitem((uint8_t *)"FAILKEY", 7, (uint8_t *)"v", 1) == 0);
+        setenv("PX_TEST_HOOKS", "1", 1);  // (arms the runtime's fault-injecting hooks)
         setenv("PX_DEBUG_SET_THROW", "1", 1);
         CHECK(!ctrl.contains((uint8_t *)"FAILKEY", 7));
         unsetenv("PX_DEBUG_SET_THROW");
@@ -255,6 +256,20 @@ int main() {
         CHECK(ctrl.flush() == PX_OK);
         CHECK(ctrl.setitem((uint8_t *)"FAILKEY", 7, (uint8_t *)"v", 1) == 0);
         CHECK(ctrl.flush() == PX_OK && ctrl.contains((uint8_t *)"FAILKEY", 7));
+
+        // the failure surfacing inside sync_pending (a live-chunk read), then a setitem: the new
+        // record is kept (queued) and the earlier failure is returned in its place, once
+        CHECK(ctrl.setitem((uint8_t *)"LOSTKEY", 7, (uint8_t *)"w", 1) == 0);
+        setenv("PX_DEBUG_SET_THROW", "1", 1);
+        const uint16_t un = ctrl.st.local_chunk.used_num;  // (sync_pending: the flush throws)
+        (void)un;
+        unsetenv("PX_DEBUG_SET_THROW");
+        CHECK(ctrl.setitem((uint8_t *)"NEXTKEY", 7, (uint8_t *)"x", 1) == -PX_ENOMEM);
+        CHECK(ctrl.flush() == PX_OK);
+        CHECK(ctrl.flush() == PX_OK);
+        CHECK(ctrl.contains((uint8_t *)"NEXTKEY", 7) && !ctrl.contains((uint8_t *)"LOSTKEY", 7));
+        PiXiuStr *nl = ctrl.st.cbt_chunk->getitem(ctrl.st.local_chunk.used_num - 1);
+        CHECK(nl != NULL && nl->len > 0);
 
         // a generator that outlives free_prop yields nothing and says why
         PXSGen *late = ctrl.getitem((uint8_t *)"RAWKEY", 6);

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "px_host.h"
+#include "px_route.h"
 
 static int fails = 0;
 #define CHECK(c)                                                        \
@@ -269,7 +270,76 @@ static void test_parallel_ranges() {
     printf("parallel_ranges: ok\n");
 }
 
+// seg_sort_pairs' pass routing (px_route.h): for 1..8 passes and the callers' aliasings, every
+// pass writes buffers it does not read and the last writes the final pair; simulated on host
+// arrays the routed passes (stable copies standing in for the scatter) deliver the input intact
+static void test_sort_route() {
+    int bufk[6], bufv[6];  // distinct addresses: ka, kb, k0, out, out2 ...
+    const void *K[6], *V[6];
+    for (int i = 0; i < 6; ++i) K[i] = &bufk[i], V[i] = &bufv[i];
+    struct Case {
+        bool text;
+        int kb, out_k, out_v;  // kb: index or -1 (absent); out: indices of the final pair
+    };
+    // ka = 0, kb = 1, k0 = 2, separate outputs 3 / 4
+    const Case cases[] = {
+        {true, 1, 1, 4},   // the first suffix sort: kout = kb, vout = sa
+        {true, 1, 3, 4},   // separate outputs
+        {false, -1, 3, 4}, // the big groups' sort: k0 reused, outputs apart
+        {false, -1, 2, 2}, // in place over the input
+        {false, 1, 1, 1},  // output = kb
+    };
+    for (const Case &c : cases) {
+        for (uint32_t passes = 1; passes <= px::kRouteMaxPasses; ++passes) {
+            const px::BufPair in0 = c.text ? px::BufPair{nullptr, nullptr} : px::BufPair{K[2], V[2]};
+            const px::BufPair scratch[4] = {{K[0], V[0]},
+                                            {c.kb >= 0 ? K[c.kb] : nullptr, c.kb >= 0 ? V[c.kb] : nullptr},
+                                            {c.text ? nullptr : K[2], c.text ? nullptr : V[2]},
+                                            {K[c.out_k], V[c.out_v]}};
+            const px::BufPair fin{K[c.out_k], V[c.out_v]};
+            px::BufPair out[px::kRouteMaxPasses];
+            const bool ok = px::sort_route(passes, in0, scratch, fin, out);
+            // in place over its input with one scratch pair the passes alternate between two
+            // buffers, so only an even count ends in the input: odd counts must be refused
+            const bool expect = !(!c.text && c.kb < 0 && px::pair_overlap(in0, fin) && passes % 2 == 1);
+            if (ok != expect) fprintf(stderr, "case text=%d kb=%d out=%d/%d passes=%u ok=%d\n", c.text, c.kb, c.out_k, c.out_v, passes, ok);
+            CHECK(ok == expect);
+            if (!ok) continue;
+            CHECK(out[passes - 1].k == fin.k && out[passes - 1].v == fin.v);
+            for (uint32_t p = 0; p < passes; ++p) {
+                const px::BufPair in = p == 0 ? in0 : out[p - 1];
+                CHECK(!px::pair_overlap(out[p], in));
+                CHECK(out[p].k && out[p].v);
+            }
+            // the data survives the chain (every buffer holds the label of the pass that wrote it)
+            int val = 100;
+            for (int i = 0; i < 6; ++i) bufk[i] = bufv[i] = -1;
+            if (!c.text) bufk[2] = bufv[2] = val;
+            for (uint32_t p = 0; p < passes; ++p) {
+                const px::BufPair in = p == 0 ? in0 : out[p - 1];
+                const int ink = in.k ? *(const int *)in.k : val, inv = in.v ? *(const int *)in.v : val;
+                CHECK(ink == val && inv == val);
+                *(int *)out[p].k = val + 1;
+                *(int *)out[p].v = val + 1;
+                ++val;
+            }
+            CHECK(*(const int *)fin.k == val && *(const int *)fin.v == val);
+        }
+    }
+    // the parity routing that faulted: 7 and 5 passes from the text with kout == kb
+    for (uint32_t passes : {5u, 7u}) {
+        const px::BufPair scratch[4] = {{K[0], V[0]}, {K[1], V[1]}, {nullptr, nullptr}, {K[1], V[4]}};
+        px::BufPair out[px::kRouteMaxPasses];
+        CHECK(px::sort_route(passes, px::BufPair{nullptr, nullptr}, scratch, px::BufPair{K[1], V[4]}, out));
+        CHECK(out[passes - 2].k == K[0]);  // the pass before the last must not write kb
+    }
+    CHECK(!px::sort_route(0, px::BufPair{nullptr, nullptr}, nullptr, px::BufPair{K[0], V[0]}, nullptr));
+    CHECK(!px::sort_route(9, px::BufPair{nullptr, nullptr}, nullptr, px::BufPair{K[0], V[0]}, nullptr));
+    printf("sort_route: ok\n");
+}
+
 int main() {
+    test_sort_route();
     test_critbit();
     test_keymaps();
     test_heap();

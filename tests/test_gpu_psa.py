@@ -162,3 +162,25 @@ def test_segmented_sort_equals_radix(cfg, n, rps, store_factory):
             else:
                 os.environ["PX_PSA_SEGSORT"] = old
     assert out[0] == out[1]
+
+
+@pytest.mark.parametrize("syms", [5, 3, 4])
+@pytest.mark.parametrize("cfg,n,rps", [(3, 64, 32), (5, 400, 200), (4, 20000, 0)])
+def test_odd_pass_first_sort(syms, cfg, n, rps, store_factory, monkeypatch):
+    """The first suffix sort with 5 / 3 passes (odd: its last pass used to read and write the
+    same key buffer, px_route.h) and 4: the same bytes and placement as the default 6-symbol
+    sort.  (5, 400, 200) is config 5 across MemPool rotations, the shape of round 5's second
+    fault; (4, 20000, 0) the 251-heavy single instance."""
+    from pixiu_amd import synth
+    cp = synth.make(cfg, n)
+    out = []
+    for s in (None, str(syms)):
+        if s is None:
+            monkeypatch.delenv("PX_PSA_SYMS", raising=False)
+        else:
+            monkeypatch.setenv("PX_PSA_SYMS", s)
+        st = store_factory(records_per_shard=rps)
+        r = st.set_batch((cp.keys, cp.koff.astype(np.uint64)), (cp.vals, cp.voff.astype(np.uint64)))
+        assert int(r["status"].max()) == 0 and st.stats()["last_psa_shards"] >= 1
+        out.append((st.export(px.records_of(r)), r["chunk"].tolist(), r["idx"].tolist()))
+    assert out[0] == out[1]
