@@ -429,7 +429,8 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
         return {"set_s": t_set + g_ms * 1e-3, "get_s": t2 - t1, "reset_s": t0 - tr, "set_kms": set_kms, "walk_kms": walk_kms,
                 "emit_kms": emit_kms, "dec_kms": dec_kms, "gather_ms": g_ms, "look_ms": look_ms,
                 "call_ms": call_ms, "comp": int(res["comp_len"].sum()), "exp": int(r_len.sum(dtype=torch.int64)),
-                "res": res, "psa": psa, "spans": spans}
+                "res": res, "psa": psa, "spans": spans,
+                "mem": {k[4:-6]: int(sst[k]) for k in sst if k.startswith("mem_") and k.endswith("_bytes")}}
 
     for _ in range(warmup):
         step()
@@ -680,6 +681,12 @@ def summarize(cfg, r, rps, world, a, pmc_path):
     out["per_step"]["device_bytes_after_set"] = _mmm([x["spans"][3] for x in runs], 0)
     out["per_step"]["device_peak_bytes_in_set"] = _mmm([x["spans"][4] for x in runs], 0)
     out["per_step"]["device_live_bytes"] = runs[-1]["spans"][5]
+    # the stored data's device bytes by structure (px_stats mem_*), and per raw byte
+    mem = runs[-1].get("mem", {})
+    if mem:
+        raw = max(1, int(r["raw"]))
+        out["per_step"]["device_mem_bytes"] = mem
+        out["per_step"]["device_mem_per_raw_byte"] = {k: round(v / raw, 3) for k, v in mem.items()}
     if "parity_counts" in r:
         out["parity_counts"] = r["parity_counts"]
     return out

@@ -145,6 +145,18 @@ typedef struct px_stats {
                                      (0: the batch resolved its keys on the host) */
     uint64_t last_set_peak_bytes;  /* device memory in use at the peak of the last px_set_batch
                                      (heap live bytes incl. scratch, plus the mapped store arena) */
+    /* device memory held for stored data, by structure (allocated bytes; DESIGN.md §2 has the
+       per-record and per-text-byte table).  Their sum is device_live_bytes less small control
+       blocks and the write-behind queue. */
+    uint64_t mem_text_bytes;    /* suffix-array shards' live-chunk text (the next batch sorts it) */
+    uint64_t mem_tree_bytes;    /* walked shards' arenas: nodes, child hash, live-chunk text */
+    uint64_t mem_comp_bytes;    /* compressed records (8-byte aligned) */
+    uint64_t mem_lane_bytes;    /* lane-walk entries, 16 B per segment */
+    uint64_t mem_seg_bytes;     /* segment index, 16 B per segment */
+    uint64_t mem_pidx_bytes;    /* position index, 2 B per 16 doc bytes */
+    uint64_t mem_span_bytes;    /* span tables (8 B per span) and their tile index (4 B per 32 B out) */
+    uint64_t mem_slot_bytes;    /* chunk slot tables (48 B per slot of capacity) */
+    uint64_t mem_keyidx_bytes;  /* device key index: records (80 B), raw keys, hash slots (16 B) */
 } px_stats;
 
 px_ctx *px_open(const px_opts *opts);

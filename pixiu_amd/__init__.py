@@ -75,7 +75,10 @@ class PxStats(C.Structure):
                 ("device_live_bytes", C.c_uint64), ("device_peak_bytes", C.c_uint64),
                 ("deferred_records", C.c_uint64), ("deferred_flushes", C.c_uint64),
                 ("deferred_mismatch", C.c_uint64), ("last_get_device_keys", C.c_uint64),
-                ("last_set_peak_bytes", C.c_uint64)]
+                ("last_set_peak_bytes", C.c_uint64),
+                ("mem_text_bytes", C.c_uint64), ("mem_tree_bytes", C.c_uint64), ("mem_comp_bytes", C.c_uint64),
+                ("mem_lane_bytes", C.c_uint64), ("mem_seg_bytes", C.c_uint64), ("mem_pidx_bytes", C.c_uint64),
+                ("mem_span_bytes", C.c_uint64), ("mem_slot_bytes", C.c_uint64), ("mem_keyidx_bytes", C.c_uint64)]
 
 
 SET_RESULT_DTYPE = np.dtype([("status", "<u4"), ("replaced", "<u4"), ("shard", "<u4"), ("chunk", "<u4"),

@@ -127,16 +127,16 @@ constexpr uint64_t kPsaBytesPerPos = 96;
 constexpr uint32_t kPsaShardBits = 19;
 constexpr uint32_t kPsaMaxShards = 1u << kPsaShardBits;
 
-// segment index entry (k_tokenize fills it, k_link sets a record token's target)
+// segment index entry (k_tokenize / k_tok_segs fill it).  (Through round 5 it carried a
+// second 16-byte half with an address per entry -- a plain segment's first byte, a record
+// token's target entry -- that k_link wrote and no kernel read: the lane entries below carry
+// the relative form the decoder uses.)
 struct alignas(16) SegEnt {
     uint32_t x, ex;  // source range [x, ex) of the segment
     uint32_t kz;     // comp offset | kind << 30: 0 plain, 1 skip, 2 record, 3 end (sentinel)
     uint32_t aux;    // record token: idx | from << 16 (its to = from + ex - x)
-    uint64_t ptr;    // plain: address of its first comp byte; record: address of the entry
-                     // of record idx holding source position `from` (0: none)
-    uint64_t pad;
 };
-static_assert(sizeof(SegEnt) == 32, "SegEnt is two 16-byte vectors");
+static_assert(sizeof(SegEnt) == 16, "SegEnt is one 16-byte vector");
 
 // lane-walk entry (k_decode's lanes), parallel to SegEnt k of the same record: one
 // 16-byte load per step.  Only records whose source coordinates fit 16 bits (every
@@ -173,7 +173,8 @@ struct alignas(16) RecSlot {
     uint32_t comp_len;
     uint32_t nseg;
     uint32_t pidx_n;        // blocks in pidx (0: no position index, serial decode only)
-    uint32_t pad;
+    uint32_t seg_cap;       // segment entries the index has room for, sentinel included (0: sized by
+                            // seg_entries of its 251 bytes); k_tokenize fails a record that needs more
     const LaneEnt *lane;    // lane-walk entries (null: serial decode only); 48 bytes in all
 };
 static_assert(sizeof(RecSlot) == 48, "RecSlot is loaded as three 16-byte vectors");

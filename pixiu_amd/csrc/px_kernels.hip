@@ -1238,11 +1238,7 @@ __global__ void __launch_bounds__(256) k_count_esc(uint32_t n, uint8_t *const *s
 constexpr uint32_t kSegRecord = 2u << 30, kSegSkip = 1u << 30, kSegEnd = 3u << 30, kSegMask = (1u << 30) - 1;
 constexpr uint32_t kNoPidx = 1u << 31;
 
-PX_DEV void put_ent(PX_GAS SegEnt *seg, uint32_t k, u32x4 lo, uint64_t ptr) {
-    PX_GAS u32x4 *e = (PX_GAS u32x4 *)(seg + k);
-    e[0] = lo;
-    e[1] = mk4((uint32_t)ptr, (uint32_t)(ptr >> 32), 0, 0);
-}
+PX_DEV void put_ent(PX_GAS SegEnt *seg, uint32_t k, u32x4 lo) { *(PX_GAS u32x4 *)(seg + k) = lo; }
 
 __global__ void __launch_bounds__(256) k_tokenize(uint32_t n, const RecSlot *slots_in, uint32_t *nseg_out,
                                                   uint32_t *status, const uint32_t *ntok) {
@@ -1251,23 +1247,37 @@ __global__ void __launch_bounds__(256) k_tokenize(uint32_t n, const RecSlot *slo
     for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < n; r += waves) {
         if (ntok && !(uni(ntok[r]) & kTokBad)) continue;  // (k_tok_segs built it from the encoder's tokens)
         const RecSlot sl = slots_in[r];
+        if (!sl.seg) {  // (room for lane entries only: k_tok_segs had to take it -- cannot happen)
+            if (lane_id() == 0) {
+                nseg_out[r] = 0;
+                status[r] = kErrCorrupt;
+            }
+            continue;
+        }
         const PX_GAS uint8_t *comp = (const PX_GAS uint8_t *)sl.comp;
         const uint64_t comp_addr = (uint64_t)sl.comp;
         const uint32_t len = sl.comp_len;
         PX_GAS SegEnt *seg = (PX_GAS SegEnt *)sl.seg;
         PX_GAS uint16_t *pidx = (PX_GAS uint16_t *)sl.pidx;
         PX_GAS LaneEnt *lanes = (PX_GAS LaneEnt *)sl.lane;
-        const uint32_t pidx_n = sl.pidx_n;
+        const uint32_t pidx_n = sl.pidx_n, cap = sl.seg_cap ? sl.seg_cap : 0xffffffffu;
         uint32_t ns = 0, p = 0, wb = 0, err = 0, plain_start = 0;
         int32_t src = 0, plain_src = 0;
-        bool plain_open = false, mono = true, have = false;
+        bool plain_open = false, mono = true, have = false, over = false;
         uint32_t pend_x = 0, pend_z = 0, pend_w = 0;
         // the pending segment is written once the next one starts (its end is then known)
         auto emit = [&](int32_t x, uint32_t z, uint32_t w) {
             if (have) {
-                uint64_t ptr = (pend_z >> 30) == 0 ? comp_addr + (pend_z & kSegMask) : 0;
+                if (ns + 1u >= cap) {  // (no room for it and the sentinel: the record fails)
+                    over = true;
+                    ++ns;
+                    pend_x = (uint32_t)x;
+                    pend_z = z;
+                    pend_w = w;
+                    return;
+                }
                 if (lane == 0) {
-                    put_ent(seg, ns, mk4(pend_x, (uint32_t)x, pend_z, pend_w), ptr);
+                    put_ent(seg, ns, mk4(pend_x, (uint32_t)x, pend_z, pend_w));
                     if (lanes) {
                         const int64_t d = (int64_t)comp_addr - (int64_t)(uint64_t)(lanes + ns);
                         const int32_t rel = (pend_z >> 30) == 0 ? (int32_t)(d >> 3) : kRelNone;
@@ -1359,8 +1369,11 @@ __global__ void __launch_bounds__(256) k_tokenize(uint32_t n, const RecSlot *slo
         if (!err) {
             if (plain_open && plain_start < len) emit(plain_src, plain_start, 0);
             emit(src, len | kSegEnd, 0);  // closes the last segment; the sentinel stays pending
+            if (over) err = kErrCorrupt;
+        }
+        if (!err) {
             if (lane == 0) {
-                put_ent(seg, ns, mk4((uint32_t)src, (uint32_t)src, len | kSegEnd, 0), 0);
+                put_ent(seg, ns, mk4((uint32_t)src, (uint32_t)src, len | kSegEnd, 0));
                 if (lanes) *(PX_GAS u32x4 *)(lanes + ns) = mk4((uint32_t)src | (uint32_t)src << 16, len | kSegEnd, 0, 0);
             }
             // blocks past the source end: no segment
@@ -1395,7 +1408,7 @@ __global__ void __launch_bounds__(256) k_tok_segs(uint32_t n, const RecSlot *slo
         PX_GAS uint16_t *pidx = (PX_GAS uint16_t *)uni64((uint64_t)sl.pidx);
         PX_GAS LaneEnt *lanes = (PX_GAS LaneEnt *)uni64((uint64_t)sl.lane);
         const PX_GAS TokEnt *tk = (const PX_GAS TokEnt *)toks + uni64(tok_off[r]);
-        bool fits = clen > 0 && L <= 0xffffu;
+        bool fits = clen > 0 && L <= 0xffffu && (!sl.seg_cap || 2u * nt + 2u <= sl.seg_cap);
         if (fits && nt) {
             const u32x4 t = *(const PX_GAS u32x4 *)(tk + nt - 1);  // (tokens come in comp order: x, o, w, rs)
             fits = t.y + (t.w >> 16) <= clen && t.x + (t.w & 0xffffu) <= L;
@@ -1407,8 +1420,7 @@ __global__ void __launch_bounds__(256) k_tok_segs(uint32_t n, const RecSlot *slo
         // one segment: its entry, its lane entry, its position-index blocks
         auto put = [&](uint32_t k, uint32_t x, uint32_t ex, uint32_t kz, uint32_t w) {
             const bool plain = (kz >> 30) == 0;
-            const uint64_t ptr = plain ? comp_addr + (kz & kSegMask) : 0;
-            put_ent(seg, k, mk4(x, ex, kz, w), ptr);
+            if (seg) put_ent(seg, k, mk4(x, ex, kz, w));
             if (lanes) {
                 const int64_t d = (int64_t)comp_addr - (int64_t)(uint64_t)(lanes + k);
                 *(PX_GAS u32x4 *)(lanes + k) = mk4(x | ex << 16, kz, w, plain ? (uint32_t)(int32_t)(d >> 3) : (uint32_t)kRelNone);
@@ -1447,7 +1459,7 @@ __global__ void __launch_bounds__(256) k_tok_segs(uint32_t n, const RecSlot *slo
         }
         if (lane == 0) {
             if (po < clen) put(ns++, px, L, po, 0u);  // the doc's last plain bytes
-            put_ent(seg, ns, mk4(L, L, clen | kSegEnd, 0), 0);
+            if (seg) put_ent(seg, ns, mk4(L, L, clen | kSegEnd, 0));
             if (lanes) *(PX_GAS u32x4 *)(lanes + ns) = mk4(L | L << 16, clen | kSegEnd, 0, 0);
         }
         ns = uni(readlane(ns, 0));
@@ -1463,7 +1475,8 @@ __global__ void __launch_bounds__(256) k_tok_segs(uint32_t n, const RecSlot *slo
         }
         if (lane == 0) {
             nseg_out[r] = ns | (mono && pidx_n ? 0u : kNoPidx);
-            status[r] = kOk;
+            // (no lane entries and no segment entries: nothing could decode it -- cannot happen)
+            status[r] = !seg && !(mono && pidx_n && lanes) ? kErrCorrupt : kOk;
         }
     }
 }
@@ -1490,7 +1503,7 @@ PX_DEV void store48(PX_GAS T *p, const T &t) {
 
 struct SlotV {
     const PX_GAS uint8_t *comp;
-    const PX_GAS u32x4 *seg;  // entry k: seg[2k] = {x, ex, kz, aux}, seg[2k + 1] = {ptr lo, ptr hi, 0, 0}
+    const PX_GAS u32x4 *seg;  // entry k: seg[k] = {x, ex, kz, aux}
     const PX_GAS uint16_t *pidx;
     const PX_GAS u32x4 *lane;  // LaneEnt k = lane[k] (null: serial decode only)
     uint32_t nseg, pidx_n;
@@ -1518,6 +1531,16 @@ PX_DEV SlotV slot_uniform(const PX_GAS RecSlot *slots, uint32_t r) {
     return v;
 }
 
+// Segment entry k as {x, ex, kz, aux}.  A record built from the encoder's tokens keeps only
+// its lane entries (16-bit x / ex, the same kz / aux): its seg pointer is null.  A record
+// parsed by k_tokenize (source positions may wrap: 32-bit x) keeps both.
+PX_DEV u32x4 seg_ent(const PX_GAS u32x4 *seg, const PX_GAS u32x4 *lane, uint32_t k) {
+    if (seg) return seg[k];
+    const u32x4 l = lane[k];
+    return mk4(l.x & 0xffffu, l.x >> 16, l.y, l.z);
+}
+PX_DEV u32x4 seg_ent(const SlotV &s, uint32_t k) { return seg_ent(s.seg, s.lane, k); }
+
 // Resolve every record token of the new records to the entry of its target record
 // that holds the token's `from` (the decoder's lanes then walk entries by address).
 __global__ void __launch_bounds__(256) k_link(uint32_t n, const LinkJob *jobs) {
@@ -1528,26 +1551,22 @@ __global__ void __launch_bounds__(256) k_link(uint32_t n, const LinkJob *jobs) {
         PX_GAS u32x4 *seg = (PX_GAS u32x4 *)job.seg;
         PX_GAS u32x4 *lanes = (PX_GAS u32x4 *)job.lane;
         const PX_GAS RecSlot *slots = (const PX_GAS RecSlot *)job.slots;
+        if (!lanes) continue;
         for (uint32_t k = lane; k < job.nseg; k += 64) {
-            const u32x4 e = seg[2 * k];
+            const u32x4 e = seg_ent(seg, lanes, k);
             if ((e.z >> 30) != 2) continue;
             const uint32_t ridx = e.w & 0xffffu, rfrom = e.w >> 16;
-            uint64_t ptr = 0;
             int32_t rel = kRelNone;
             if (ridx < job.nrec) {
                 const SlotV t = slot_at(slots, ridx);
-                if (t.pidx_n && (rfrom >> 4) < t.pidx_n) {
+                if (t.pidx_n && (rfrom >> 4) < t.pidx_n && t.lane) {
                     uint32_t k2 = min((uint32_t)t.pidx[rfrom >> 4], t.nseg);
-                    while (k2 < t.nseg && t.seg[2 * k2].y <= rfrom) ++k2;
-                    ptr = (uint64_t)(t.seg + 2 * k2);
-                    if (lanes && t.lane) {
-                        const int64_t d = ((int64_t)(uint64_t)(t.lane + k2) - (int64_t)(uint64_t)(lanes + k)) / 16;
-                        if (d > INT32_MIN && d <= INT32_MAX) rel = (int32_t)d;
-                    }
+                    while (k2 < t.nseg && seg_ent(t, k2).y <= rfrom) ++k2;
+                    const int64_t d = ((int64_t)(uint64_t)(t.lane + k2) - (int64_t)(uint64_t)(lanes + k)) / 16;
+                    if (d > INT32_MIN && d <= INT32_MAX) rel = (int32_t)d;
                 }
             }
-            seg[2 * k + 1] = mk4((uint32_t)ptr, (uint32_t)(ptr >> 32), 0, 0);
-            if (lanes) lanes[k].w = (uint32_t)rel;
+            lanes[k].w = (uint32_t)rel;
         }
     }
 }
@@ -1738,7 +1757,7 @@ PX_DEV uint32_t seg_find(const SlotV &s, int32_t from) {
         lo = min((uint32_t)uni(s.pidx[(uint32_t)from >> 4]), hi);
         for (;;) {  // at most 16 source bytes past a segment start: one probe, almost always
             uint32_t k = lo + lane;
-            uint64_t m = ballot(k < hi && (int32_t)s.seg[2 * k].y > from);
+            uint64_t m = ballot(k < hi && (int32_t)seg_ent(s, k).y > from);
             if (m) return lo + ffs64(m);
             if (hi - lo <= 64) return hi;
             lo += 64;
@@ -1747,7 +1766,7 @@ PX_DEV uint32_t seg_find(const SlotV &s, int32_t from) {
     while (hi - lo > 64) {
         uint32_t step = (hi - lo + 63) / 64;
         uint32_t k = lo + lane * step;
-        bool le = k < hi && (int32_t)s.seg[2 * k].y <= from;  // segment k ends at or before from
+        bool le = k < hi && (int32_t)seg_ent(s, k).y <= from;  // segment k ends at or before from
         uint64_t m = ballot(le);
         uint32_t cnt = (uint32_t)__popcll(m);  // prefix of lanes with le (monotone)
         uint32_t nlo = cnt ? lo + (cnt - 1) * step + 1 : lo;
@@ -1756,7 +1775,7 @@ PX_DEV uint32_t seg_find(const SlotV &s, int32_t from) {
         hi = uni(nhi);
     }
     uint32_t k = lo + lane;
-    bool le = k < hi && (int32_t)s.seg[2 * k].y <= from;
+    bool le = k < hi && (int32_t)seg_ent(s, k).y <= from;
     return uni(lo + (uint32_t)__popcll(ballot(le)));
 }
 
@@ -2318,7 +2337,7 @@ PX_DEV void decode_body(const DecodeQuery *qs, uint32_t nq, const RecSlot *const
                 if (!window(f, sv)) continue;
                 PX_CNT(P_D_SERIAL, 1);
                 // one segment through the serial machine
-                const u32x4 E = sv.seg[2 * f.seg];
+                const u32x4 E = seg_ent(sv, f.seg);
                 const int32_t sx = (int32_t)uni(E.x), ex = (int32_t)uni(E.y);
                 const uint32_t sz = uni(E.z), sw = uni(E.w);
                 const uint32_t cs = sz & kSegMask;
@@ -2997,17 +3016,19 @@ __global__ void __launch_bounds__(256) k_span_pieces(uint32_t ns, DecodeQuery *s
     const uint64_t base = q.out_off - 64ull * m;
     const RecSlot *sl = chunk_slots[q.chunk] + q.idx;
     const uint32_t nseg = sl->nseg;
-    const uint4 *seg = (const uint4 *)sl->seg;
+    const PX_GAS u32x4 *sg = (const PX_GAS u32x4 *)sl->seg, *ln = (const PX_GAS u32x4 *)sl->lane;
+    auto seg_x = [&](uint32_t k) { return seg_ent(sg, ln, k).x; };
+    auto seg_y = [&](uint32_t k) { return seg_ent(sg, ln, k).y; };
     const uint16_t *pidx = (const uint16_t *)sl->pidx;
-    const uint32_t S = nseg ? seg[2 * nseg].x : 0u;  // (the end sentinel's position: the tokens' total)
+    const uint32_t S = nseg && (sg || ln) ? seg_x(nseg) : 0u;  // (the end sentinel's position: the tokens' total)
     const bool split = nseg && sl->pidx_n && sl->lane && S <= L;
     auto bound = [&](uint32_t t) -> uint32_t {  // the first token start at or after t
         if (t == 0) return 0;
         if (t >= S) return S;
         uint32_t k = (t >> 4) < sl->pidx_n ? min((uint32_t)pidx[t >> 4], nseg) : nseg;
-        while (k > 0 && seg[2 * k].x > t) --k;  // (a position index entry is the segment holding 16b)
-        while (k < nseg && seg[2 * k].y <= t) ++k;
-        return k >= nseg ? S : (seg[2 * k].x >= t ? seg[2 * k].x : seg[2 * k].y);
+        while (k > 0 && seg_x(k) > t) --k;  // (a position index entry is the segment holding 16b)
+        while (k < nseg && seg_y(k) <= t) ++k;
+        return k >= nseg ? S : (seg_x(k) >= t ? seg_x(k) : seg_y(k));
     };
     if (!split) {
         q.from = 0;

@@ -92,16 +92,17 @@ __global__ void __launch_bounds__(256) k_psa_gather(uint32_t ndocs, const PsaDoc
 // Sorting by group size: <= 64 where they lie (k_dbl_win: one wave per 64-slot window sorts
 // the groups starting in it), 65..kRegMax by one wave in registers, up to kMedMax by one
 // workgroup in LDS, larger ones by a gathered radix sort (host-driven: only early steps).
-constexpr uint32_t kWinMax = 64, kRegMax = 512, kMedMax = 4096;
+constexpr uint32_t kWinMax = 64, kRegMax = 1024, kMedMax = 4096;
 constexpr uint32_t kTag = 1u << 31, kSizeMask = kTag - 1u;
-constexpr int kLongClasses = 5;  // E = 2, 4, 8 (registers), LDS, big
+constexpr int kLongClasses = 6;  // E = 2, 4, 8, 16 (registers), LDS, big
+constexpr int kBigClass = kLongClasses - 1;
 struct LongLists {
     uint64_t *lst[kLongClasses];  // entry: start | size << 32
     uint32_t *cnt;                // [0..4] entries, [5] overflow flag
     uint32_t cap[kLongClasses];
 };
 PSA_DEV uint32_t long_class(uint32_t size) {
-    return size <= 128 ? 0u : size <= 256 ? 1u : size <= kRegMax ? 2u : size <= kMedMax ? 3u : 4u;
+    return size <= 128 ? 0u : size <= 256 ? 1u : size <= 512 ? 2u : size <= kRegMax ? 3u : size <= kMedMax ? 4u : 5u;
 }
 
 // ---------------------------------------------------------------- retired groups
@@ -2078,7 +2079,7 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     auto *key = S.get<uint32_t>(n64 * 4 + 64);
     LongLists LL;
     {
-        const uint32_t lo[kLongClasses] = {kWinMax + 1, 129, 257, kRegMax + 1, kMedMax + 1};
+        const uint32_t lo[kLongClasses] = {kWinMax + 1, 129, 257, 513, kRegMax + 1, kMedMax + 1};
         for (int c = 0; c < kLongClasses; ++c) {
             LL.cap[c] = (uint32_t)(n64 / lo[c] + 64);
             LL.lst[c] = S.get<uint64_t>((uint64_t)LL.cap[c] * 8);
@@ -2087,7 +2088,7 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     }
     // retired groups (see RetList; off unless PX_PSA_RETIRE=1: measured on config 3 they take
     // 6 ms off the window sorter but add 4 ms of link walks to the key gathers and 11 ms of
-    // resolution): list capped at N / 32 (groups past it stay in the doubling)
+    // resolution, CHANGELOG.md round 5): list capped at N / 32 (groups past it stay in the doubling)
     RetList R{};
     if (env_on("PX_PSA_RETIRE")) {
         R.per = (uint32_t)std::min<uint64_t>((n64 / 32 + 4096) / kRetShards + 1, 0x7fffffffull / kRetShards);
@@ -2109,6 +2110,8 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     uint32_t active = pin[kCntActive], maxsz = pin[kCntMax];
     uint32_t h = syms, it = 0;
     const uint32_t gwin = std::min<uint32_t>((uint32_t)((n64 + 255) / 256), kGridWin);
+    const char *r16 = std::getenv("PX_PSA_REG16");  // (A/B: 0 sends the 513..1024 class to the LDS sorter)
+    const bool reg16 = !(r16 && r16[0] == '0');
     // one step: every group's keys (flat), then every group sorted by them (windows, then
     // the long-group lists the window kernel filled); big groups need their count on the host
     auto step = [&](bool big) -> hipError_t {
@@ -2123,18 +2126,24 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         k_dbl_reg<2><<<kGridReg, 256, 0, s>>>(LL.lst[0], LL.cnt + 0, tag, h, sa, sd, act, gsz, key, rank, ss, R);
         k_dbl_reg<4><<<kGridReg, 256, 0, s>>>(LL.lst[1], LL.cnt + 1, tag, h, sa, sd, act, gsz, key, rank, ss, R);
         k_dbl_reg<8><<<kGridReg, 256, 0, s>>>(LL.lst[2], LL.cnt + 2, tag, h, sa, sd, act, gsz, key, rank, ss, R);
-        k_dbl_blk<<<kGridBlk, 256, 0, s>>>(LL.lst[3], LL.cnt + 3, tag, h, sa, sd, act, gsz, key, rank, ss, R);
+        // (513..1024: one wave in registers, E = 16 -- in the LDS sorter's 256-thread bitonic network these
+        // groups waited on a barrier per stage)
+        if (reg16)
+            k_dbl_reg<16><<<kGridReg, 256, 0, s>>>(LL.lst[3], LL.cnt + 3, tag, h, sa, sd, act, gsz, key, rank, ss, R);
+        else
+            k_dbl_blk<<<kGridBlk, 256, 0, s>>>(LL.lst[3], LL.cnt + 3, tag, h, sa, sd, act, gsz, key, rank, ss, R);
+        k_dbl_blk<<<kGridBlk, 256, 0, s>>>(LL.lst[4], LL.cnt + 4, tag, h, sa, sd, act, gsz, key, rank, ss, R);
         auto sum = [&]() {
             k_stat_sum<<<1, 64, 0, s>>>(ss.sh, cnt + kCntSorted + it, cnt + kCntActive + 1 + it, cnt + kCntMax + 1 + it);
         };
         if (big) {
             e = read_words(kCntLong, 8);
             if (e != hipSuccess) return e;
-            const uint32_t nbig = pin[kCntLong + 4];
+            const uint32_t nbig = pin[kCntLong + kBigClass];
             if (pin[kCntLong + kLongClasses]) return hipErrorUnknown;  // (list overflow: cannot happen)
             if (nbig) {
                 std::vector<uint64_t> bl(nbig);
-                e = hipMemcpy(bl.data(), LL.lst[4], (size_t)nbig * 8, hipMemcpyDeviceToHost);  // (synchronous)
+                e = hipMemcpy(bl.data(), LL.lst[kBigClass], (size_t)nbig * 8, hipMemcpyDeviceToHost);  // (synchronous)
                 if (e != hipSuccess) return e;
                 std::vector<uint32_t> boff(nbig);
                 uint64_t T = 0;
@@ -2151,16 +2160,16 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
                 auto *gd = S.get<uint16_t>(T * 2 + 64);
                 const bool packed = nbig <= 0x10000u;
                 if (packed)
-                    k_big_gather<true><<<blocks(T), tb, 0, s>>>((uint32_t)T, nbig, LL.lst[4], d_boff, sa, sd, key, ck, cv,
+                    k_big_gather<true><<<blocks(T), tb, 0, s>>>((uint32_t)T, nbig, LL.lst[kBigClass], d_boff, sa, sd, key, ck, cv,
                                                                 gp, gd, ss);
                 else
-                    k_big_gather<false><<<blocks(T), tb, 0, s>>>((uint32_t)T, nbig, LL.lst[4], d_boff, sa, sd, key, ck, cv,
+                    k_big_gather<false><<<blocks(T), tb, 0, s>>>((uint32_t)T, nbig, LL.lst[kBigClass], d_boff, sa, sd, key, ck, cv,
                                                                  gp, gd, ss);
                 // every group sorted by its 32-bit keys on its own (px_sort.hip): segments = groups
                 std::vector<uint32_t> glen(nbig);
                 for (uint32_t b = 0; b < nbig; ++b) glen[b] = (uint32_t)(bl[b] >> 32);
                 auto *d_glen = S.get<uint32_t>((uint64_t)nbig * 4 + 64);
-                k_big_segs<<<(nbig + 255) / 256, 256, 0, s>>>(nbig, LL.lst[4], d_glen);
+                k_big_segs<<<(nbig + 255) / 256, 256, 0, s>>>(nbig, LL.lst[kBigClass], d_glen);
                 e = seg_sort_pairs(s, SA, nbig, seg_tile_count(glen.data(), nbig), d_boff, d_glen, 32, 8, ck, cv, nullptr,
                                    nullptr, 0, cka, cva, nullptr, nullptr, ck2, cv2, cnt + kCntSortErr);
                 S.put(d_glen);
@@ -2171,10 +2180,10 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
                     e = hipMemsetAsync(chain, 0, ((uint64_t)gb + 1) * 8, s);
                     if (e != hipSuccess) return e;
                     if (packed)
-                        k_big_place<true><<<gb, 256, 0, s>>>((uint32_t)T, LL.lst[4], d_boff, ck2, cv2, gp, gd, tag, chain,
+                        k_big_place<true><<<gb, 256, 0, s>>>((uint32_t)T, LL.lst[kBigClass], d_boff, ck2, cv2, gp, gd, tag, chain,
                                                              cnt + kCntSortErr, sa, sd, act, gsz, rank, ss);
                     else
-                        k_big_place<false><<<gb, 256, 0, s>>>((uint32_t)T, LL.lst[4], d_boff, ck2, cv2, gp, gd, tag, chain,
+                        k_big_place<false><<<gb, 256, 0, s>>>((uint32_t)T, LL.lst[kBigClass], d_boff, ck2, cv2, gp, gd, tag, chain,
                                                               cnt + kCntSortErr, sa, sd, act, gsz, rank, ss);
                 }
                 for (const void *q : {(const void *)d_boff, (const void *)ck, (const void *)ck2, (const void *)cv,
@@ -2198,9 +2207,9 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         active = pin[kCntActive + it];
         maxsz = pin[kCntMax + it];
         if (verbose)
-            fprintf(stderr, "psa: step %u (host) sorted %u (long groups %u %u %u %u %u) -> %u in groups, largest %u\n",
+            fprintf(stderr, "psa: step %u (host) sorted %u (long groups %u %u %u %u %u %u) -> %u in groups, largest %u\n",
                     it - 1, pin[kCntSorted + it - 1], pin[kCntLong], pin[kCntLong + 1], pin[kCntLong + 2],
-                    pin[kCntLong + 3], pin[kCntLong + 4], active, maxsz);
+                    pin[kCntLong + 3], pin[kCntLong + 4], pin[kCntLong + 5], active, maxsz);
     }
     if (active > 0) {
         PSA_CHECK(sev.make(kMaxSteps, hipEventDisableTiming));

@@ -6,6 +6,7 @@
 // produced by the HIP kernels in px_kernels.hip; the host only moves metadata
 // (lengths, statuses, key prefixes) and runs the CritBit walk.
 #include <hip/hip_runtime.h>
+#include <malloc.h>
 
 #include <algorithm>
 #include <atomic>
@@ -396,6 +397,10 @@ struct px_ctx {
     std::vector<std::pair<ShardState *, ShardState>> pending_state;  // states set after the zeroing (loaded shards)
     PartKeyMap keymap;  // raw key -> shard (multi-shard only)
     std::vector<std::pair<void *, uint64_t>> store_blocks;  // packed record stores + segment indexes
+    // stored-data bytes by structure (px_stats mem_*; only px_reset frees stored data)
+    struct MemAcct {
+        uint64_t comp = 0, lane = 0, seg = 0, pidx = 0, span = 0;
+    } macct;
     StoreArena arena;                                        // (record stores: StoreArena above)
     void *store_alloc(uint64_t bytes) {
         if (void *p = arena.alloc(bytes)) return p;
@@ -542,6 +547,22 @@ struct px_ctx {
             if (hipMemGetInfo(&fr, &tot) == hipSuccess) keep = std::min<uint64_t>(keep, ((uint64_t)fr + heap.cached_free()) / 2);
         }
         heap.trim(keep);
+    }
+
+    // stored-data device bytes by structure (px_stats mem_*)
+    void mem_stats(px_stats *st) const {
+        st->mem_text_bytes = st->mem_tree_bytes = 0;
+        for (const auto &sp : shards)
+            if (sp->arena) (sp->text_only ? st->mem_text_bytes : st->mem_tree_bytes) += sp->arena_bytes;
+        st->mem_comp_bytes = macct.comp;
+        st->mem_lane_bytes = macct.lane;
+        st->mem_seg_bytes = macct.seg;
+        st->mem_pidx_bytes = macct.pidx;
+        st->mem_span_bytes = macct.span;
+        uint64_t sl = (uint64_t)chunk_tab_cap * sizeof(RecSlot *);
+        for (const auto &c : chunks) sl += (uint64_t)c.dev_cap * sizeof(RecSlot);
+        st->mem_slot_bytes = sl;
+        st->mem_keyidx_bytes = dki.rec_cap * sizeof(DkRec) + dki.keys_cap + (uint64_t)dki.tab_cap * sizeof(DkSlot);
     }
 
     // ------------------------------------------------------------ helpers
@@ -1162,16 +1183,24 @@ struct px_ctx {
         }
         auto *qn = (DecodeQuery *)hq_buf.get((uint64_t)n * sizeof(DecodeQuery));
         std::vector<SpanSrc> src(n);
-        uint64_t tot = 0;
+        std::vector<uint64_t> qoff(n + 1, 0);
         for (uint32_t k = 0; k < n; ++k) {
-            const SpanReq &r = reqs[k];
-            const Chunk &ch = chunks[r.chunk];
-            const uint32_t L = ch.doc_len[r.idx];
-            const uint32_t cap = (uint32_t)round_up(L + 64, 16);
-            qn[k] = DecodeQuery{r.chunk, r.idx, 0, kMaxDoc, tot, cap, mode, ch.n, 0};
-            src[k] = SpanSrc{r.doc, L, 0};
-            tot += cap + (split && mode == 0 ? 64ull * std::max<uint32_t>(1, (L + kPiece - 1) / kPiece) : 0ull);
+            const uint32_t L = chunks[reqs[k].chunk].doc_len[reqs[k].idx];
+            qoff[k + 1] = qoff[k] + round_up(L + 64, 16) +
+                          (split && mode == 0 ? 64ull * std::max<uint32_t>(1, (L + kPiece - 1) / kPiece) : 0ull);
         }
+        const uint64_t tot = qoff[n];
+        const uint32_t pthr = n >= 65536 ? host_threads() : 1;
+        parallel_ranges(n, pthr, [&](uint32_t lo, uint32_t hi) {
+            for (uint32_t k = lo; k < hi; ++k) {
+                const SpanReq &r = reqs[k];
+                const Chunk &ch = chunks[r.chunk];
+                const uint32_t L = ch.doc_len[r.idx];
+                const uint32_t cap = (uint32_t)round_up(L + 64, 16);
+                qn[k] = DecodeQuery{r.chunk, r.idx, 0, kMaxDoc, qoff[k], cap, mode, ch.n, 0};
+                src[k] = SpanSrc{r.doc, L, 0};
+            }
+        });
         auto *addr = (int32_t *)heap.alloc(tot * 4 + 64);
         hcheck(hipMemsetD32Async((hipDeviceptr_t)addr, kAddrMark, tot, stream));  // (k_decode_addr writes run starts only)
         // device: queries, lengths + statuses, sources, counts / entries / tiles and their scans
@@ -1296,38 +1325,48 @@ struct px_ctx {
             const uint64_t tab_bytes = round_up(nents * sizeof(SpanEnt), 64) + ntiles * 4 + 64;
             auto *tab = (SpanEnt *)heap.alloc(tab_bytes);
             store_blocks.emplace_back(tab, tab_bytes);
+            macct.span += tab_bytes;
             auto *tixb = (uint32_t *)((uint8_t *)tab + round_up(nents * sizeof(SpanEnt), 64));
             hcheck(launch_span_jobs(stream, n, dq, dl, ds, dsrc, ctab, addr, cnt, ents, tiles, eoff, toff, tab, tixb, sdq,
                                     pl, dfirst));
-            uint64_t o = 0, to = 0;
+            // every record's entry and tile offsets (the device scans' running sums), the
+            // chunks' view tables sized, then the views filled on host threads
+            std::vector<uint64_t> eo(n + 1, 0), tofs(n + 1, 0);
+            uint64_t used = 0;
             for (uint32_t j = 0; j < n; ++j) {
-                if (hc[j] & kSpanBad) continue;
-                const uint32_t ns0 = hc[j] & ~(kSpanBad | kSpanEq);
-                if (skip[j]) {  // (its entries are written but not used: the whole decode replaces them)
-                    o += ns0 + 1;
-                    to += (hl[j] + kGatherTile - 1) / kGatherTile;
-                    continue;
-                }
-                Chunk &ch = chunks[reqs[j].chunk];
-                if (ch.span.size() < ch.n) ch.span.resize(ch.n);
+                const bool has = !(hc[j] & kSpanBad);
                 const uint32_t ns = hc[j] & ~(kSpanBad | kSpanEq);
-                Chunk::Span &sp = ch.span[reqs[j].idx];
-                if (mode == 0) {
-                    sp.p = tab + o;
-                    sp.t = tixb + to;
-                    sp.n = ns;
-                    sp.len = hl[j];
-                    sp.eq = (hc[j] & kSpanEq) != 0;
-                } else {
-                    sp.xp = tab + o;
-                    sp.xt = tixb + to;
-                    sp.xn = ns;
-                    sp.xlen = hl[j];
+                eo[j + 1] = eo[j] + (has ? ns + 1 : 0);
+                tofs[j + 1] = tofs[j] + (has ? (hl[j] + kGatherTile - 1) / kGatherTile : 0);
+                if (has && !skip[j]) {
+                    used += ns + 1;
+                    Chunk &ch = chunks[reqs[j].chunk];
+                    if (ch.span.size() < ch.n) ch.span.resize(ch.n);
                 }
-                o += ns + 1;
-                to += (hl[j] + kGatherTile - 1) / kGatherTile;
-                stats.span_entries += ns + 1;
             }
+            stats.span_entries += used;
+            parallel_ranges(n, pthr, [&](uint32_t lo, uint32_t hi) {
+                for (uint32_t j = lo; j < hi; ++j) {
+                    // (a skipped record's entries are written but not used: the whole decode
+                    // replaces them)
+                    if ((hc[j] & kSpanBad) || skip[j]) continue;
+                    Chunk &ch = chunks[reqs[j].chunk];
+                    const uint32_t ns = hc[j] & ~(kSpanBad | kSpanEq);
+                    Chunk::Span &sp = ch.span[reqs[j].idx];
+                    if (mode == 0) {
+                        sp.p = tab + eo[j];
+                        sp.t = tixb + tofs[j];
+                        sp.n = ns;
+                        sp.len = hl[j];
+                        sp.eq = (hc[j] & kSpanEq) != 0;
+                    } else {
+                        sp.xp = tab + eo[j];
+                        sp.xt = tixb + tofs[j];
+                        sp.xn = ns;
+                        sp.xlen = hl[j];
+                    }
+                }
+            });
         }
         phase.mark("wait (write pass)");
         sync();
@@ -1577,6 +1616,7 @@ struct px_ctx {
         for (auto &b : store_blocks)
             if (!arena.owns(b.first)) heap.release(b.first, b.second);
         store_blocks.clear();
+        macct = MemAcct{};
         arena.reset();
         last_store = nullptr;
         last_store_bytes = 0;
@@ -1605,16 +1645,18 @@ struct px_ctx {
         PhaseClock phase("decode_key_prefixes", "PX_SET_VERBOSE");
         phase.mark("queries");
         st.assign(jobs.size(), kOk);
-        std::vector<DecodeQuery> q;
-        std::vector<uint32_t> qj;
-        q.reserve(jobs.size());
-        qj.reserve(jobs.size());
-        uint64_t qo = 0;
-        for (size_t i = 0; i < jobs.size(); ++i) {
-            q.push_back(DecodeQuery{jobs[i].chunk, jobs[i].idx, 0, kMaxDoc, qo, jobs[i].cap, 0});
-            qj.push_back((uint32_t)i);
-            qo += round_up(jobs[i].cap, 16);
-        }
+        const uint32_t nj = (uint32_t)jobs.size();
+        std::vector<DecodeQuery> q(nj);
+        std::vector<uint32_t> qj(nj);
+        std::vector<uint64_t> qoff(nj + 1, 0);
+        for (uint32_t i = 0; i < nj; ++i) qoff[i + 1] = qoff[i] + round_up(jobs[i].cap, 16);
+        parallel_ranges(nj, nj >= 65536 ? host_threads() : 1, [&](uint32_t lo, uint32_t hi) {
+            for (uint32_t i = lo; i < hi; ++i) {
+                q[i] = DecodeQuery{jobs[i].chunk, jobs[i].idx, 0, kMaxDoc, qoff[i], jobs[i].cap, 0};
+                qj[i] = i;
+            }
+        });
+        uint64_t qo = qoff[nj];
         for (int pass = 0; pass < 2 && !q.empty(); ++pass) {
             phase.mark(pass ? "decode (again)" : "decode");
             auto *kbuf = (uint8_t *)heap.alloc(qo + 64);
@@ -2234,8 +2276,9 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
                            d_ntok));
     hcheck(hipEventRecord(ev1, stream));
     hcheck(launch_count_esc(stream, n, d_cdst, d_complen, d_nesc));
-    std::vector<uint32_t> comp_len(n), rchunk(n), ridx(n), rstatus(n), nesc(n);
+    std::vector<uint32_t> comp_len(n), rchunk(n), ridx(n), rstatus(n), nesc(n), ntok(n);
     d2h(nesc.data(), d_nesc, n * 4);
+    d2h(ntok.data(), d_ntok, n * 4);  // (sizes the segment index: k_tok_segs writes 2 ntok + 2 entries at most)
     d2h(comp_len.data(), d_complen, n * 4);
     d2h(rchunk.data(), d_chunk, n * 4);
     d2h(ridx.data(), d_idx, n * 4);
@@ -2299,39 +2342,62 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     for (uint32_t r = 0; r < n; ++r)
         placed[r] = rchunk[r] != 0xffffffffu && ridx[r] != 0xffffffffu && doc_len[r] != 0xffffffffu &&
                     comp_len[r] <= 2 * doc_len[r] + 8;
-    std::vector<uint64_t> coff(n + 1, 0), soff(n + 1, 0), poff(n + 1, 0);
+    std::vector<uint64_t> coff(n + 1, 0), soff(n + 1, 0), loff(n + 1, 0), poff(n + 1, 0);
+    std::vector<uint32_t> scap(n);
+    const char *tsh = std::getenv("PX_DEBUG_TOKSEGS");
+    const bool toksegs_check = tsh && tsh[0] == '1';
     for (uint32_t r = 0; r < n; ++r) {
         bool ok = placed[r];
         coff[r + 1] = coff[r] + (ok ? round_up(comp_len[r], 8) : 0);
-        // a failed record still gets one entry: k_tokenize writes its end sentinel
-        soff[r + 1] = soff[r] + (ok ? seg_entries(nesc[r]) : 1) * sizeof(SegEnt);
+        // room for the segment index: the encoder's tokens give it exactly (a plain segment
+        // before each token, the tokens, the last plain bytes, the end sentinel); a record
+        // whose tokens k_tok_segs cannot use is parsed by k_tokenize, which needs room for
+        // every 251 of its bytes starting a token (seg_entries).  A failed record still gets
+        // one entry: k_tokenize writes its end sentinel.  (Sizing every record by its 251
+        // bytes gave config 4's records ~100 entries for the ~3 they use: 4.5 GB.)
+        const bool parsed = !ok || (ntok[r] & kTokBad);
+        const uint64_t ents = parsed ? (ok ? seg_entries(nesc[r]) : 1)
+                                     : std::min<uint64_t>(seg_entries(nesc[r]), 2ull * ntok[r] + 2);
+        scap[r] = (uint32_t)ents;
+        // the lane entries hold everything a segment entry does for a record k_tok_segs
+        // builds (16-bit source coordinates): such a record keeps no segment entries
+        // (k_tokenize's records, whose coordinates may wrap, keep both)
+        soff[r + 1] = soff[r] + (parsed || toksegs_check ? ents : 0) * sizeof(SegEnt);
+        loff[r + 1] = loff[r] + ents * sizeof(LaneEnt);
         poff[r + 1] = poff[r] + (ok ? round_up(pidx_blocks(doc_len[r]) * 2, 16) : 0);
     }
     // compressed bytes and the lane entries share one allocation: a plain lane entry
     // reaches its record's bytes by a 32-bit relative offset (LaneEnt::rel)
     const uint64_t lane_at = round_up(coff[n] + 64, 16);
-    const uint64_t store_bytes = lane_at + soff[n] / 2 + 64;  // LaneEnt is half a SegEnt
+    const uint64_t store_bytes = lane_at + loff[n] + 64;
     auto *store = (uint8_t *)store_alloc(store_bytes);
     auto *segs = (uint8_t *)heap.alloc(soff[n] + poff[n] + 64);
     store_blocks.emplace_back(store, store_bytes);
     last_store = store;
     last_store_bytes = coff[n];
     store_blocks.emplace_back(segs, soff[n] + poff[n] + 64);
+    macct.comp += lane_at;
+    macct.lane += loff[n] + 64;
+    macct.seg += soff[n];
+    macct.pidx += poff[n] + 64;
     auto *d_coff = (uint64_t *)heap.alloc((uint64_t)n * 8);
     h2d(d_coff, coff.data(), (size_t)n * 8);
     hcheck(launch_compact(stream, n, d_cdst, d_complen, store, d_coff));
     std::vector<RecSlot> slots(n);
-    for (uint32_t r = 0; r < n; ++r) {
+    const uint32_t pthr = n >= 65536 ? host_threads() : 1;  // (per-record host loops of big batches)
+    parallel_ranges(n, pthr, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t r = lo; r < hi; ++r) {
         bool ok = placed[r];
         slots[r].comp = store + coff[r];
-        slots[r].seg = (const SegEnt *)(segs + soff[r]);
+        slots[r].seg = soff[r + 1] > soff[r] ? (const SegEnt *)(segs + soff[r]) : nullptr;
         slots[r].pidx = (const uint16_t *)(segs + soff[n] + poff[r]);
         slots[r].comp_len = ok ? comp_len[r] : 0;
         slots[r].nseg = 0;
         slots[r].pidx_n = ok ? pidx_blocks(doc_len[r]) : 0;
-        slots[r].pad = 0;
-        slots[r].lane = (const LaneEnt *)(store + lane_at + soff[r] / 2);
+        slots[r].seg_cap = scap[r];
+        slots[r].lane = (const LaneEnt *)(store + lane_at + loff[r]);
     }
+    });
     auto *d_slots = (RecSlot *)heap.alloc((uint64_t)n * sizeof(RecSlot));
     h2d(d_slots, slots.data(), (size_t)n * sizeof(RecSlot));
     std::vector<uint32_t> tstat(n);
@@ -2343,8 +2409,8 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     d2h(nseg.data(), d_nseg, n * 4);
     d2h(tstat.data(), d_status, n * 4);
     sync();
-    if (const char *e = std::getenv("PX_DEBUG_TOKSEGS"); e && e[0] == '1') {  // test hook: the tokens' segment index == the bytes' parse
-        const uint64_t seg_bytes = soff[n] + poff[n], lane_bytes = soff[n] / 2;
+    if (toksegs_check) {  // test hook: the tokens' segment index == the bytes' parse
+        const uint64_t seg_bytes = soff[n] + poff[n], lane_bytes = loff[n];
         std::vector<uint8_t> a(seg_bytes), al(lane_bytes), b(seg_bytes), bl(lane_bytes);
         std::vector<uint32_t> nseg2(n), tstat2(n);
         d2h(a.data(), segs, seg_bytes);
@@ -2367,7 +2433,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             const uint64_t e = (nseg2[r] & ~(1u << 31)) + 1;  // entries incl. the sentinel
             const bool same = nseg[r] == nseg2[r] && tstat[r] == tstat2[r] &&
                               (!placed[r] || (std::memcmp(a.data() + soff[r], b.data() + soff[r], e * sizeof(SegEnt)) == 0 &&
-                                              std::memcmp(al.data() + soff[r] / 2, bl.data() + soff[r] / 2, e * sizeof(LaneEnt)) == 0 &&
+                                              std::memcmp(al.data() + loff[r], bl.data() + loff[r], e * sizeof(LaneEnt)) == 0 &&
                                               std::memcmp(a.data() + soff[n] + poff[r], b.data() + soff[n] + poff[r],
                                                           pidx_blocks(doc_len[r]) * 2) == 0));
             if (!same) {
@@ -2390,40 +2456,73 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     // ---- register records in their chunks
     std::vector<uint32_t> rgchunk(n, kNone);  // chunk of every placed record
     std::vector<uint8_t> live(n, 0);          // placed, OK and indexed
-    for (uint32_t r = 0; r < n; ++r) {
-        if (doc_len[r] == 0xffffffffu) rstatus[r] = kErrInval;
-        if (!placed[r]) continue;
-        if (rstatus[r] == kOk && tstat[r] != kOk) rstatus[r] = tstat[r];
-        Shard &s = *shards[rec_shard[r]];
-        while (s.chunks.size() <= rchunk[r]) {
-            if (!s.chunks.empty()) chunks[s.chunks.back()].total = chunks[s.chunks.back()].n;  // closed
-            s.chunks.push_back(new_chunk(s.id));
+    // the chunks the batch opens, created in record order (global chunk ids as the serial
+    // registration gave them); a chunk closed by a newer one gets its total once its records
+    // are in.  Then every shard's records on host threads: a shard's chunks are its own.
+    std::vector<uint32_t> closing;
+    for (const Work &w : work) {
+        Shard &s = *w.s;
+        for (uint32_t r = w.r0; r < w.r1; ++r) {
+            if (!placed[r]) continue;
+            while (s.chunks.size() <= rchunk[r]) {
+                if (!s.chunks.empty()) closing.push_back(s.chunks.back());
+                s.chunks.push_back(new_chunk(s.id));
+            }
         }
-        uint32_t c = s.chunks[rchunk[r]];
-        Chunk &ch = chunks[c];
-        if (ridx[r] != ch.n) {  // the device numbered slots differently: fail loudly
-            fprintf(stderr, "pixiu_amd: internal error: record %u placed at slot %u of chunk %u holding %u\n", r,
-                    ridx[r], rchunk[r], ch.n);
-            rstatus[r] = kErrCorrupt;
-            corrupt = PX_ECORRUPT;
-            continue;
+    }
+    struct RegAcc {
+        uint64_t records = 0, raw = 0, doc = 0, comp = 0;
+        int corrupt = 0;
+    };
+    std::vector<RegAcc> racc(work.size());
+    auto register_work = [&](uint32_t k) {
+        const Work &w = work[k];
+        Shard &s = *w.s;
+        RegAcc &a = racc[k];
+        for (uint32_t r = w.r0; r < w.r1; ++r) {
+            if (doc_len[r] == 0xffffffffu) rstatus[r] = kErrInval;
+            if (!placed[r]) continue;
+            if (rstatus[r] == kOk && tstat[r] != kOk) rstatus[r] = tstat[r];
+            uint32_t c = s.chunks[rchunk[r]];
+            Chunk &ch = chunks[c];
+            if (ridx[r] != ch.n) {  // the device numbered slots differently: fail loudly
+                fprintf(stderr, "pixiu_amd: internal error: record %u placed at slot %u of chunk %u holding %u\n", r,
+                        ridx[r], rchunk[r], ch.n);
+                rstatus[r] = kErrCorrupt;
+                a.corrupt = PX_ECORRUPT;
+                continue;
+            }
+            const bool ok = rstatus[r] == kOk;
+            set_nseg(slots[r], nseg[r]);
+            ch.slots.push_back(slots[r]);
+            ch.doc_len.push_back(doc_len[r]);
+            ch.dead.push_back(ok ? 0 : 1);
+            ch.kp_off.push_back(0);
+            ch.kp_len.push_back(0);
+            ch.n++;
+            ch.used += ok ? 1 : 0;
+            rgchunk[r] = c;
+            live[r] = ok;
+            if (!ok) continue;
+            a.records++;
+            a.raw += (hkoff[r + 1] - hkoff[r]) + (hvoff[r + 1] - hvoff[r]);
+            a.doc += doc_len[r];
+            a.comp += comp_len[r];
         }
-        const bool ok = rstatus[r] == kOk;
-        set_nseg(slots[r], nseg[r]);
-        ch.slots.push_back(slots[r]);
-        ch.doc_len.push_back(doc_len[r]);
-        ch.dead.push_back(ok ? 0 : 1);
-        ch.kp_off.push_back(0);
-        ch.kp_len.push_back(0);
-        ch.n++;
-        ch.used += ok ? 1 : 0;
-        rgchunk[r] = c;
-        live[r] = ok;
-        if (!ok) continue;
-        stats.records++;
-        stats.raw_bytes += (hkoff[r + 1] - hkoff[r]) + (hvoff[r + 1] - hvoff[r]);
-        stats.doc_bytes += doc_len[r];
-        stats.comp_bytes += comp_len[r];
+    };
+    if (work.size() > 1 && n >= 65536) {
+        const std::function<void(uint32_t)> job = [&](uint32_t k) { register_work(k); };
+        WorkerPool::get().run((uint32_t)work.size(), job);
+    } else {
+        for (uint32_t k = 0; k < (uint32_t)work.size(); ++k) register_work(k);
+    }
+    for (uint32_t c : closing) chunks[c].total = chunks[c].n;  // closed
+    for (const RegAcc &a : racc) {
+        stats.records += a.records;
+        stats.raw_bytes += a.raw;
+        stats.doc_bytes += a.doc;
+        stats.comp_bytes += a.comp;
+        if (a.corrupt) corrupt = a.corrupt;
     }
     phase.mark("register: slot tables and link jobs");
     // push new slot entries to the device tables and resolve the new records' tokens to
@@ -2500,6 +2599,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         stats.last_span_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts).count();
     }
 
+    phase.mark("device key index entries");
     // ---- device key index: ids for this batch's live records, in record order (before the
     // CritBit inserts, whose replaces kill ids -- older ones and this batch's own)
     const bool dk = dki_enabled() && dki.valid && !raw_docs;
@@ -2679,10 +2779,11 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     for (auto &b : deferred_release) heap.release(b.first, b.second);
     deferred_release.clear();
 
-    phase.mark("results");
+    phase.mark("wait for the device");
     // ---- results (the batch's device work is done when the call returns: slot scatters
     // and span builds are not left running into the caller's next call)
     hcheck(hipStreamSynchronize(stream));
+    phase.mark("results");
     int rc = corrupt;
     uint64_t ub = 0;
     for (auto &sp : shards) ub += sp->hs.ub_reads;
@@ -2690,21 +2791,22 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     stats.last_set_peak_bytes = heap.live_peak() + arena.mapped;
     trim_heap();
     stats.device_bytes = heap.held() + arena.mapped;
-    for (uint32_t r = 0; r < n; ++r) {
-        px_status st = map_status(rstatus[r]);
-        if (st != PX_OK && rc == PX_OK) rc = st;
-        if (res) {
-            px_set_result &o = res[r];
-            o.status = st;
-            o.replaced = replaced[r];
-            o.shard = rec_shard[r];
-            o.chunk = rchunk[r];
-            o.idx = ridx[r];
-            o.comp_len = st == PX_OK ? comp_len[r] : 0;
-            o.doc_len = doc_len[r] == 0xffffffffu ? 0 : doc_len[r];
-            o.pad = 0;
-        }
-    }
+    for (uint32_t r = 0; r < n && rc == PX_OK; ++r) rc = map_status(rstatus[r]);
+    if (res)
+        parallel_ranges(n, n >= 65536 ? host_threads() : 1, [&](uint32_t lo, uint32_t hi) {
+            for (uint32_t r = lo; r < hi; ++r) {
+                const px_status st = map_status(rstatus[r]);
+                px_set_result &o = res[r];
+                o.status = st;
+                o.replaced = replaced[r];
+                o.shard = rec_shard[r];
+                o.chunk = rchunk[r];
+                o.idx = ridx[r];
+                o.comp_len = st == PX_OK ? comp_len[r] : 0;
+                o.doc_len = doc_len[r] == 0xffffffffu ? 0 : doc_len[r];
+                o.pad = 0;
+            }
+        });
     return rc;
 }
 
@@ -3409,18 +3511,22 @@ int px_ctx::load(const uint8_t *src, uint64_t len, int src_on_device, uint32_t *
         poff[i + 1] = poff[i] + round_up(pidx_blocks(dl) * 2, 16);
     }
     // the store keeps data and lane entries in one allocation (LaneEnt::rel is relative)
-    const uint64_t lane_at = data_cap, store_bytes = lane_at + soff[n] / 2 + 64;
+    const uint64_t lane_at = data_cap, store_bytes = lane_at + soff[n] + 64;  // (LaneEnt: the size of a SegEnt)
     auto *store = (uint8_t *)store_alloc(store_bytes);
     hcheck(hipMemcpyAsync(store, data, h.data_bytes, hipMemcpyDeviceToDevice, stream));
     auto *segs = (uint8_t *)heap.alloc(soff[n] + poff[n] + 64);
     store_blocks.emplace_back(store, store_bytes);
     store_blocks.emplace_back(segs, soff[n] + poff[n] + 64);
+    macct.comp += lane_at;
+    macct.lane += soff[n] + 64;
+    macct.seg += soff[n];
+    macct.pidx += poff[n] + 64;
     std::vector<RecSlot> slots(n);
     for (uint32_t i = 0; i < n; ++i) {
         const uint32_t dl = br[i].doc_len & ~kBlobDead;
         slots[i] = RecSlot{store + br[i].off, (const SegEnt *)(segs + soff[i]),
                            (const uint16_t *)(segs + soff[n] + poff[i]), br[i].comp_len, 0, pidx_blocks(dl), 0,
-                           (const LaneEnt *)(store + lane_at + soff[i] / 2)};
+                           (const LaneEnt *)(store + lane_at + soff[i])};
     }
     auto *d_slots = (RecSlot *)heap.alloc((uint64_t)n * sizeof(RecSlot));
     auto *d_tmp = (uint32_t *)heap.alloc((uint64_t)n * 8);
@@ -3539,8 +3645,26 @@ int px_ctx::load(const uint8_t *src, uint64_t len, int src_on_device, uint32_t *
 // ====================================================================== C ABI
 extern "C" {
 
+// Host heap policy (once per process, PX_NO_MALLOPT=1 leaves glibc's defaults): a set batch
+// of a million records builds ~1 GB of per-record host arrays, and glibc serves each array
+// over 32 MB -- and, past its dynamic threshold, smaller ones -- by a fresh mmap that it
+// unmaps at free, so every batch paid first-touch page faults on all of them again (config 4:
+// 244 -> 177 ms per set batch with the policy, profiles/r06c_*phases.log).  With mmap off and
+// the trim threshold out of reach, freed blocks stay in the heap and the next batch reuses
+// pages already mapped.  The cost: the process keeps its host heap's high-water mark.
+static void host_heap_policy() {
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const char *e = std::getenv("PX_NO_MALLOPT");
+        if (e && e[0] == '1') return;
+        mallopt(M_MMAP_MAX, 0);
+        mallopt(M_TRIM_THRESHOLD, 0x7fffffff);
+    });
+}
+
 px_ctx *px_open(const px_opts *opts) {
     try {
+        host_heap_policy();
         auto *c = new px_ctx();
         if (opts) c->opts = *opts;
         hcheck(hipSetDevice(c->opts.device));
@@ -4022,6 +4146,7 @@ int px_stats_get(px_ctx *ctx, px_stats *st) {
         st->device_bytes = ctx->heap.held() + ctx->arena.mapped;
         st->device_live_bytes = ctx->heap.live_bytes() + ctx->arena.top;
         st->device_peak_bytes = ctx->heap.peak();
+        ctx->mem_stats(st);
         return PX_OK;
     })
 }

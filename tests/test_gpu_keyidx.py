@@ -112,7 +112,7 @@ def test_pieces_keep_span_tables(store_factory):
     """A batch over 512 MB raw into one shard is stored in pieces; every record keeps its
     span table (its chunk's records stay within the span entries' 2 GiB reach: the record
     stores share one reserved address range) and every key resolves on the device, also
-    after resets that reuse the memory."""
+    after resets that reuse the memory (CHANGELOG.md round 4)."""
     import numpy as np
     import torch
     from pixiu_amd import synth

@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <stdexcept>
 #include <vector>
+#include <algorithm>
 
 typedef std::vector<uint8_t> Bytes;
 typedef std::vector<uint32_t> Addr;
@@ -116,6 +117,33 @@ static size_t segments(const Bytes &d) {
     return n + plain + 1;
 }
 
+// 32-byte output tiles (the gather's unit): source loads as k_gather issues them (one
+// unaligned 16-byte load per span piece inside the tile, a second for a piece over 16 bytes)
+// against 16-byte windows covering the tile's source bytes greedily (one load serving every
+// span whose bytes fall inside it)
+static void tile_loads(const Addr &a, size_t &pieces, size_t &windows, size_t &tiles) {
+    for (size_t t0 = 0; t0 < a.size(); t0 += 32) {
+        const size_t t1 = std::min(a.size(), t0 + 32);
+        ++tiles;
+        size_t k = t0;
+        std::vector<uint32_t> src;
+        while (k < t1) {
+            size_t e = k + 1;
+            while (e < t1 && a[e] == a[e - 1] + 1) ++e;
+            pieces += (e - k) > 16 ? 2 : 1;
+            for (size_t q = k; q < e; ++q) src.push_back(a[q]);
+            k = e;
+        }
+        std::sort(src.begin(), src.end());
+        size_t i = 0;
+        while (i < src.size()) {
+            const uint32_t w = src[i];
+            ++windows;
+            while (i < src.size() && src[i] < w + 16) ++i;
+        }
+    }
+}
+
 static size_t spans(const Addr &a) {
     size_t n = 0;
     for (size_t k = 0; k < a.size(); ++k) n += (k == 0 || a[k] != a[k - 1] + 1);
@@ -125,6 +153,7 @@ static size_t spans(const Addr &a) {
 int main(int argc, char **argv) {
     FILE *f = fopen(argv[1], "rb");
     size_t segs = 0, chunks = 0, recs = 0, comp = 0, out_e = 0, out_c = 0, sp_e = 0, sp_c = 0, differ = 0, maxsp = 0;
+    size_t t_pieces = 0, t_windows = 0, t_tiles = 0;
     uint32_t nrec;
     while (fread(&nrec, 4, 1, f) == 1) {
         Chunk ch;
@@ -146,6 +175,7 @@ int main(int argc, char **argv) {
             s.limit = 65535;
             compat(ch, (int)r, 0, 65535, s, (size_t)-1, 0);
             size_t a = spans(e), b = spans(s.out);
+            tile_loads(s.out, t_pieces, t_windows, t_tiles);
             sp_e += a; sp_c += b; out_e += e.size(); out_c += s.out.size();
             differ += s.out != e;
             maxsp = std::max(maxsp, b);
@@ -157,4 +187,6 @@ int main(int argc, char **argv) {
            "(%.1f B/span, max %zu/rec) | compat!=exact %zu | span table @8B = %.1f%% of comp | segments %zu (@48B = %.1f%%)\n",
            argv[1], chunks, recs, comp, out_e, sp_e, (double)out_e / sp_e, out_c, sp_c, (double)out_c / sp_c, maxsp,
            differ, 100.0 * 8 * sp_c / comp, segs, 100.0 * 48 * segs / comp);
+    printf("compat tiles %zu: span-piece loads %zu (%.2f per tile), 16-byte window loads %zu (%.2f per tile, %.1f%% of the pieces)\n",
+           t_tiles, t_pieces, (double)t_pieces / t_tiles, t_windows, (double)t_windows / t_tiles, 100.0 * t_windows / t_pieces);
 }
