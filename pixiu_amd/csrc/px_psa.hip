@@ -92,9 +92,9 @@ __global__ void __launch_bounds__(256) k_psa_gather(uint32_t ndocs, const PsaDoc
 // Sorting by group size: <= 64 where they lie (k_dbl_win: one wave per 64-slot window sorts
 // the groups starting in it), 65..kRegMax by one wave in registers, up to kMedMax by one
 // workgroup in LDS, larger ones by a gathered radix sort (host-driven: only early steps).
-constexpr uint32_t kWinMax = 64, kRegMax = 1024, kMedMax = 4096;
+constexpr uint32_t kWinMax = 64, kRegMax = 512, kMedMax = 4096;
 constexpr uint32_t kTag = 1u << 31, kSizeMask = kTag - 1u;
-constexpr int kLongClasses = 6;  // E = 2, 4, 8, 16 (registers), LDS, big
+constexpr int kLongClasses = 5;  // E = 2, 4, 8 (registers), LDS, big
 constexpr int kBigClass = kLongClasses - 1;
 struct LongLists {
     uint64_t *lst[kLongClasses];  // entry: start | size << 32
@@ -102,7 +102,7 @@ struct LongLists {
     uint32_t cap[kLongClasses];
 };
 PSA_DEV uint32_t long_class(uint32_t size) {
-    return size <= 128 ? 0u : size <= 256 ? 1u : size <= 512 ? 2u : size <= kRegMax ? 3u : size <= kMedMax ? 4u : 5u;
+    return size <= 128 ? 0u : size <= 256 ? 1u : size <= kRegMax ? 2u : size <= kMedMax ? 3u : 4u;
 }
 
 // ---------------------------------------------------------------- retired groups
@@ -841,6 +841,50 @@ __global__ void __launch_bounds__(256) k_dbl_reg(const uint64_t *list, const uin
     if (lane == 0) stat_put(ss, blockIdx.x * 4 + wv, sorted, active, mx);
 }
 
+// bitonic network over sk[0 .. P) in LDS (256 threads; PMAX >= P, both powers of two >= 512):
+// stage (kk, j) compares pair q's elements i = q with a 0 bit inserted at j, and i | j
+template <uint32_t P>
+PSA_DEV void blk_bitonic(uint64_t *sk) {
+    const uint32_t tid = threadIdx.x;
+#pragma unroll
+    for (uint32_t kk = 2; kk <= P; kk <<= 1) {
+#pragma unroll
+        for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+#pragma unroll
+            for (uint32_t m = 0; m < P / 512; ++m) {
+                const uint32_t q = tid + m * 256;
+                const uint32_t i = ((q & ~(j - 1u)) << 1) | (q & (j - 1u)), l = i | j;
+                const bool up = (i & kk) == 0;
+                const uint64_t x = sk[i], y = sk[l];
+                if (up ? x > y : x < y) {
+                    sk[i] = y;
+                    sk[l] = x;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+// any power-of-two P (256 .. kMedMax): the runtime-sized network
+PSA_DEV void blk_bitonic_any(uint64_t *sk, uint32_t P) {
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t kk = 2; kk <= P; kk <<= 1)
+        for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = tid; i < P; i += 256) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const bool up = (i & kk) == 0;
+                    const uint64_t x = sk[i], y = sk[l];
+                    if (up ? x > y : x < y) {
+                        sk[i] = y;
+                        sk[l] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+}
+
 // one workgroup per group of kRegMax+1 .. kMedMax: bitonic sort of the keys in LDS; then
 // each thread takes C = P / 256 consecutive positions: their heads as a mask, their payloads
 // gathered before any slot of the group is rewritten, and the subgroup bounds across threads
@@ -902,21 +946,12 @@ __global__ void __launch_bounds__(256) k_dbl_blk(const uint64_t *list, const uin
             __syncthreads();  // (s_id is rewritten by the next group)
             continue;  // (the barrier above: nobody reads sk any more)
         }
-        for (uint32_t kk = 2; kk <= P; kk <<= 1)
-            for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
-                for (uint32_t i = tid; i < P; i += 256) {
-                    const uint32_t l = i ^ j;
-                    if (l > i) {
-                        const bool up = (i & kk) == 0;
-                        const uint64_t x = sk[i], y = sk[l];
-                        if (up ? x > y : x < y) {
-                            sk[i] = y;
-                            sk[l] = x;
-                        }
-                    }
-                }
-                __syncthreads();
-            }
+        // (the network at compile-time sizes: every thread takes P / 512 pairs per stage; the
+        // runtime-sized loops spent more scalar than vector instructions, profiles/r05ze_sq_summary.txt)
+        if (P == 1024) blk_bitonic<1024>(sk);
+        else if (P == 2048) blk_bitonic<2048>(sk);
+        else if (P == 4096) blk_bitonic<4096>(sk);
+        else blk_bitonic_any(sk, P);
         const uint32_t C = P / 256, i0 = tid * C;
         uint32_t hm = 0, pv[kC], dv[kC];
 #pragma unroll
@@ -1369,13 +1404,60 @@ PSA_DEV uint32_t lce(const uint64_t *G8, uint32_t p, uint32_t q, uint32_t k, uin
 // bytes per step alone.  Here 8 lanes share a comparison, 64 bytes per step; a wave runs
 // 8 comparisons (4 span starts, each with both neighbours).  seed[2 t] / seed[2 t + 1] =
 // lcp with the previous / next smaller neighbour of span t's first position.
+//
+// Most span starts need no comparison (round 6): where a neighbour chain continues through the
+// whole span before (q = q' + 1 at every position) the shifted-pair identity k_psa_lce uses
+// (lcp(p - 1, q') = L >= 2 gives lcp(p, q' + 1) = L - 1 exactly) carries the last computed
+// seed S of the chain's run forward: S - span * (t - s) for span t of a run started at span s,
+// valid while it stays >= 1 (then every position between had L >= 2).  brk[t] (k_psa_seed_brk)
+// is t + 1 where side `side` of span t does not continue span t - 1's chain, else 0; its
+// max-scan gives each span its run start.  Launched twice: `derive` 0 compares the runs' first
+// spans; `derive` 1 carries their seeds along the runs and compares where that is not valid.
+__global__ void __launch_bounds__(256) k_psa_seed_brk(uint32_t N, uint32_t nspan, const uint32_t *psvp,
+                                                      const uint32_t *nsvp, uint32_t span, uint32_t *brk_p,
+                                                      uint32_t *brk_n) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nspan) return;
+    bool cp = t > 0, cn = t > 0;
+    if (t > 0) {
+        const uint32_t p0 = t * span, a = p0 - span;
+        uint32_t qp = psvp[a], qn = nsvp[a];
+        cp = qp != kNoPos;
+        cn = qn != kNoPos;
+        for (uint32_t p = a + 1; p <= p0 && (cp || cn); ++p) {
+            const uint32_t xp = psvp[p], xn = nsvp[p];
+            cp = cp && xp != kNoPos && xp == qp + 1;
+            cn = cn && xn != kNoPos && xn == qn + 1;
+            qp = xp;
+            qn = xn;
+        }
+    }
+    brk_p[t] = cp ? 0u : t + 1u;
+    brk_n[t] = cn ? 0u : t + 1u;
+}
 __global__ void __launch_bounds__(256) k_psa_lce_seed(uint32_t N, uint32_t nspan, const uint64_t *G8,
                                                       const uint16_t *dist, const uint32_t *psvp,
-                                                      const uint32_t *nsvp, uint32_t span, uint16_t *seed) {
+                                                      const uint32_t *nsvp, uint32_t span, uint16_t *seed,
+                                                      const uint32_t *run_p, const uint32_t *run_n, uint32_t derive) {
     const uint32_t lane = lane_id(), grp = lane >> 3, sub = lane & 7u;
     const uint32_t c = (blockIdx.x * blockDim.x + threadIdx.x) >> 3;  // comparison index
     const uint32_t t = c >> 1;
     bool live = t < nspan;
+    if (live && run_p) {  // (run_p null: every span compares)
+        const uint32_t s = ((c & 1u) ? run_n[t] : run_p[t]) - 1u;  // the run's first span
+        if (!derive) {
+            live = s == t;
+        } else if (s == t) {
+            live = false;  // (compared by the first launch)
+        } else {
+            const uint32_t S = seed[2 * s + (c & 1u)];
+            const uint64_t d = (uint64_t)span * (t - s);
+            if ((uint64_t)S >= d + 1) {
+                if (sub == 0) seed[c] = (uint16_t)(S - d);
+                live = false;
+            }
+        }
+    }
     uint32_t p = 0, q = kNoPos, lim = 0;
     if (live) {
         p = t * span;
@@ -2079,7 +2161,7 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     auto *key = S.get<uint32_t>(n64 * 4 + 64);
     LongLists LL;
     {
-        const uint32_t lo[kLongClasses] = {kWinMax + 1, 129, 257, 513, kRegMax + 1, kMedMax + 1};
+        const uint32_t lo[kLongClasses] = {kWinMax + 1, 129, 257, kRegMax + 1, kMedMax + 1};
         for (int c = 0; c < kLongClasses; ++c) {
             LL.cap[c] = (uint32_t)(n64 / lo[c] + 64);
             LL.lst[c] = S.get<uint64_t>((uint64_t)LL.cap[c] * 8);
@@ -2110,8 +2192,6 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     uint32_t active = pin[kCntActive], maxsz = pin[kCntMax];
     uint32_t h = syms, it = 0;
     const uint32_t gwin = std::min<uint32_t>((uint32_t)((n64 + 255) / 256), kGridWin);
-    const char *r16 = std::getenv("PX_PSA_REG16");  // (A/B: 0 sends the 513..1024 class to the LDS sorter)
-    const bool reg16 = !(r16 && r16[0] == '0');
     // one step: every group's keys (flat), then every group sorted by them (windows, then
     // the long-group lists the window kernel filled); big groups need their count on the host
     auto step = [&](bool big) -> hipError_t {
@@ -2126,13 +2206,10 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         k_dbl_reg<2><<<kGridReg, 256, 0, s>>>(LL.lst[0], LL.cnt + 0, tag, h, sa, sd, act, gsz, key, rank, ss, R);
         k_dbl_reg<4><<<kGridReg, 256, 0, s>>>(LL.lst[1], LL.cnt + 1, tag, h, sa, sd, act, gsz, key, rank, ss, R);
         k_dbl_reg<8><<<kGridReg, 256, 0, s>>>(LL.lst[2], LL.cnt + 2, tag, h, sa, sd, act, gsz, key, rank, ss, R);
-        // (513..1024: one wave in registers, E = 16 -- in the LDS sorter's 256-thread bitonic network these
-        // groups waited on a barrier per stage)
-        if (reg16)
-            k_dbl_reg<16><<<kGridReg, 256, 0, s>>>(LL.lst[3], LL.cnt + 3, tag, h, sa, sd, act, gsz, key, rank, ss, R);
-        else
-            k_dbl_blk<<<kGridBlk, 256, 0, s>>>(LL.lst[3], LL.cnt + 3, tag, h, sa, sd, act, gsz, key, rank, ss, R);
-        k_dbl_blk<<<kGridBlk, 256, 0, s>>>(LL.lst[4], LL.cnt + 4, tag, h, sa, sd, act, gsz, key, rank, ss, R);
+        // (513..4096: the LDS sorter.  A 16-per-lane register sorter for 513..1024 measured slower:
+        // 253 VGPRs, one wave per SIMD -- k_dbl_reg + k_dbl_blk 39.0 against 29.6 ms on config 3,
+        // profiles/r06d_reg16_ab.txt)
+        k_dbl_blk<<<kGridBlk, 256, 0, s>>>(LL.lst[3], LL.cnt + 3, tag, h, sa, sd, act, gsz, key, rank, ss, R);
         auto sum = [&]() {
             k_stat_sum<<<1, 64, 0, s>>>(ss.sh, cnt + kCntSorted + it, cnt + kCntActive + 1 + it, cnt + kCntMax + 1 + it);
         };
@@ -2207,9 +2284,9 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         active = pin[kCntActive + it];
         maxsz = pin[kCntMax + it];
         if (verbose)
-            fprintf(stderr, "psa: step %u (host) sorted %u (long groups %u %u %u %u %u %u) -> %u in groups, largest %u\n",
+            fprintf(stderr, "psa: step %u (host) sorted %u (long groups %u %u %u %u %u) -> %u in groups, largest %u\n",
                     it - 1, pin[kCntSorted + it - 1], pin[kCntLong], pin[kCntLong + 1], pin[kCntLong + 2],
-                    pin[kCntLong + 3], pin[kCntLong + 4], pin[kCntLong + 5], active, maxsz);
+                    pin[kCntLong + 3], pin[kCntLong + 4], active, maxsz);
     }
     if (active > 0) {
         PSA_CHECK(sev.make(kMaxSteps, hipEventDisableTiming));
@@ -2291,8 +2368,21 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     {
         const uint32_t nspan = (uint32_t)((n64 + lsp - 1) / lsp);
         auto *seed = S.get<uint16_t>((uint64_t)nspan * 4 + 64);
-        k_psa_lce_seed<<<(uint32_t)(((uint64_t)nspan * 16 + 255) / 256), 256, 0, s>>>(N, nspan, (const uint64_t *)G, dist,
-                                                                                       psvp, nsvp, lsp, seed);
+        const uint32_t gseed = (uint32_t)(((uint64_t)nspan * 16 + 255) / 256);
+        if (env_on("PX_LCE_SEED_ALL")) {  // (A/B: every span start compared)
+            k_psa_lce_seed<<<gseed, 256, 0, s>>>(N, nspan, (const uint64_t *)G, dist, psvp, nsvp, lsp, seed, nullptr,
+                                                 nullptr, 0);
+        } else {
+            auto *brk = S.get<uint32_t>((uint64_t)nspan * 8 + 64);
+            uint32_t *brk_p = brk, *brk_n = brk + nspan;
+            k_psa_seed_brk<<<blocks(nspan), tb, 0, s>>>(N, nspan, psvp, nsvp, lsp, brk_p, brk_n);
+            PSA_CHECK(scan_u32(s, SA, brk_p, brk_p, nspan, ScanOp::kMax, false));
+            PSA_CHECK(scan_u32(s, SA, brk_n, brk_n, nspan, ScanOp::kMax, false));
+            for (uint32_t derive = 0; derive < 2; ++derive)
+                k_psa_lce_seed<<<gseed, 256, 0, s>>>(N, nspan, (const uint64_t *)G, dist, psvp, nsvp, lsp, seed, brk_p,
+                                                     brk_n, derive);
+            S.put(brk);
+        }
         k_psa_lce<<<blocks(nspan), tb, 0, s>>>(N, (const uint64_t *)G, dist, psvp, nsvp, lcp_p, lcp_n, lsp, seed);
         S.put(seed);
     }

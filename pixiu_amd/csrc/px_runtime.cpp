@@ -512,7 +512,9 @@ struct px_ctx {
         dki.kills.clear();
         for (auto &c : chunks) c.gid.clear();
     }
-    void dki_commit(uint32_t gid0, const std::vector<DkRec> &recs, const std::vector<uint8_t> &kb);
+    void dki_commit(uint32_t gid0, const DkRec *recs, uint32_t nn, const uint8_t *kb, uint64_t kbn);
+    std::vector<DkRec> dk_rec_buf;      // a set batch's new index entries (kept: no re-initialisation per batch)
+    std::vector<uint8_t> dk_key_buf;    // and their raw key bytes
     // the live bit of every record killed since (replaces, deletes, reinsert), on the device
     void dki_apply_kills() {
         std::vector<uint32_t> kills;
@@ -2613,12 +2615,17 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         }
     } dk_txn{this, !dk};
     const uint32_t dk_gid0 = dki.nrec;
-    std::vector<DkRec> dk_new;
+    // (the entries and key bytes are written into buffers kept across batches: value-
+    // initialising a fresh 80 MB vector for a million records cost ~8 ms)
+    DkRec *dk_new = nullptr;
+    uint32_t dk_m = 0;
     std::vector<uint32_t> dk_r;  // the batch record of each entry
-    std::vector<uint8_t> dk_kb;
+    uint8_t *dk_kb = nullptr;
+    uint64_t dk_kbn = 0;
     if (dk) {
         // live records in order: their ids and key-arena places by prefix sums, then the
         // entries on host threads (a batch of 1 M records spent ~45 ms here on one)
+        dk_r.reserve(n);
         for (uint32_t r = 0; r < n; ++r)
             if (live[r]) dk_r.push_back(r);
         const uint32_t m = (uint32_t)dk_r.size();
@@ -2626,11 +2633,18 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         for (uint32_t j = 0; j < m; ++j) {
             const uint32_t r = dk_r[j];
             kbo[j + 1] = kbo[j] + (hkoff[r + 1] - hkoff[r]);
-            Chunk &ch = chunks[rgchunk[r]];
-            if (ch.gid.size() <= ridx[r]) ch.gid.resize(ridx[r] + 1, kNone);  // (sized before the threads)
         }
-        dk_new.resize(m);
-        dk_kb.resize(kbo[m]);
+        for (const Work &w : work)  // (every chunk's id table sized before the threads)
+            for (uint32_t c : w.s->chunks) {
+                Chunk &ch = chunks[c];
+                if (ch.gid.size() < ch.n) ch.gid.resize(ch.n, kNone);
+            }
+        if (dk_rec_buf.size() < m) dk_rec_buf.resize(m);
+        if (dk_key_buf.size() < kbo[m]) dk_key_buf.resize(kbo[m]);
+        dk_new = dk_rec_buf.data();
+        dk_m = m;
+        dk_kb = dk_key_buf.data();
+        dk_kbn = kbo[m];
         const uint32_t gid0 = dki.nrec;
         dki.nrec += m;
         parallel_ranges(m, m >= 4096 ? host_threads() : 1, [&](uint32_t lo, uint32_t hi) {
@@ -2645,7 +2659,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             DkRec d{};
             d.key_off = dki.keys_len + kbo[j];
             d.key_len = (uint32_t)kl;
-            if (kl) std::memcpy(dk_kb.data() + kbo[j], k, kl);
+            if (kl) std::memcpy(dk_kb + kbo[j], k, kl);
             if (i < ch.span.size() && ch.span[i].p) {
                 const Chunk::Span &sp = ch.span[i];
                 d.sp = sp.p;
@@ -2681,10 +2695,15 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     // shard's, so this is the order the sequential loop would have used)
     std::vector<uint32_t> replaced(n, 0);
     std::vector<std::pair<uint32_t, uint32_t>> moved;  // (record, older shard)
+    // the key -> shard map's partitions (multi-shard stores) and the shards' tries are
+    // independent: one pool run takes both (partitions first: the longer tasks)
+    std::function<void(uint32_t)> keymap_job;
+    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> mv;
+    std::vector<std::string> rawk;
+    std::vector<uint8_t> part;  // (key-map partition of each record; outlives the block: keymap_job reads it)
     if (opts.records_per_shard != 0) {
         // key -> shard upserts, one key-map partition per task (keys in record order); the
         // map holds raw keys: a ready doc's is its key prefix unescaped
-        std::vector<std::string> rawk;
         if (raw_docs) {
             rawk.resize(n);
             for (uint32_t r = 0; r < n; ++r) {
@@ -2706,15 +2725,17 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             *len = hkoff[r + 1] - hkoff[r];
             return hkeys.data() + hkoff[r];
         };
-        std::vector<uint8_t> part(n);
-        for (uint32_t r = 0; r < n; ++r)
-            if (live[r]) {
-                uint64_t kl;
-                const uint8_t *kp = raw_key(r, &kl);
-                part[r] = (uint8_t)PartKeyMap::part_of(kp, kl);
-            }
-        std::vector<std::vector<std::pair<uint32_t, uint32_t>>> mv(PartKeyMap::kParts);
-        const std::function<void(uint32_t)> job = [&](uint32_t pi) {
+        part.resize(n);
+        parallel_ranges(n, n >= 65536 ? host_threads() : 1, [&](uint32_t lo, uint32_t hi) {
+            for (uint32_t r = lo; r < hi; ++r)
+                if (live[r]) {
+                    uint64_t kl;
+                    const uint8_t *kp = raw_key(r, &kl);
+                    part[r] = (uint8_t)PartKeyMap::part_of(kp, kl);
+                }
+        });
+        mv.resize(PartKeyMap::kParts);
+        keymap_job = [&, raw_key](uint32_t pi) {
             KeyMap &m = keymap.part(pi);
             m.reserve(n / PartKeyMap::kParts + 64);
             for (uint32_t r = 0; r < n; ++r) {
@@ -2725,13 +2746,6 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
                 if (prev >= 0 && (uint32_t)prev != rec_shard[r]) mv[pi].emplace_back(r, (uint32_t)prev);
             }
         };
-        if (n >= 4096) {
-            WorkerPool::get().run(PartKeyMap::kParts, job);
-        } else {
-            for (uint32_t pi = 0; pi < PartKeyMap::kParts; ++pi) job(pi);
-        }
-        for (auto &v : mv) moved.insert(moved.end(), v.begin(), v.end());
-        std::sort(moved.begin(), moved.end());  // record order
     }
     auto insert_work = [&](size_t k) {
         const Work &w = work[k];
@@ -2748,13 +2762,19 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             replaced[r] |= cbt_insert(s, q, Leaf{rgchunk[r], ridx[r]}) == 1 ? 1u : 0u;
         }
     };
-    const uint32_t nthr = std::min<uint32_t>(host_threads(), (uint32_t)work.size());
+    const uint32_t nk = keymap_job ? PartKeyMap::kParts : 0u;
+    const uint32_t nthr = std::min<uint32_t>(host_threads(), (uint32_t)work.size() + nk);
+    const std::function<void(uint32_t)> job = [&](uint32_t t) {
+        if (t < nk) keymap_job(t);
+        else insert_work(t - nk);
+    };
     if (nthr <= 1 || n < 2048) {
-        for (size_t k = 0; k < work.size(); ++k) insert_work(k);
+        for (uint32_t t = 0; t < nk + (uint32_t)work.size(); ++t) job(t);
     } else {
-        const std::function<void(uint32_t)> job = [&](uint32_t k) { insert_work(k); };
-        WorkerPool::get().run((uint32_t)work.size(), job);
+        WorkerPool::get().run(nk + (uint32_t)work.size(), job);
     }
+    for (auto &v : mv) moved.insert(moved.end(), v.begin(), v.end());
+    std::sort(moved.begin(), moved.end());  // record order
     for (const auto &mv : moved) {  // cross-shard replace
         const uint32_t r = mv.first;
         cbt_delete(*shards[mv.second], crit_key(hkeys.data() + hkoff[r], hkoff[r + 1] - hkoff[r]));
@@ -2764,12 +2784,12 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     phase.mark("device key index");
     // a record the reference's CritBit skipped is answered by no walk: not by the index
     // either; a shard whose trie took an unclean prefix walks every lookup from now on
-    for (size_t j = 0; j < dk_new.size(); ++j)
+    for (uint32_t j = 0; j < dk_m; ++j)
         if (!chunks[rgchunk[dk_r[j]]].in_tree(ridx[dk_r[j]])) dk_new[j].flags &= ~kDkClean;
     for (const Work &w : work)
         if (w.s->unclean) dki.valid = false;
     if (dki.valid && dki_enabled()) {
-        if (dk) dki_commit(dk_gid0, dk_new, dk_kb);
+        if (dk) dki_commit(dk_gid0, dk_new, dk_m, dk_kb, dk_kbn);
         dki_apply_kills();
     } else if (dki.nrec) {
         dki_clear();
@@ -3157,8 +3177,7 @@ int px_ctx::flush_queue() {
 }
 
 // ====================================================================== device key index
-void px_ctx::dki_commit(uint32_t gid0, const std::vector<DkRec> &recs, const std::vector<uint8_t> &kb) {
-    const uint32_t nn = (uint32_t)recs.size();
+void px_ctx::dki_commit(uint32_t gid0, const DkRec *recs, uint32_t nn, const uint8_t *kb, uint64_t kbn) {
     if (!nn) return;
     dki.miss_streak = 0;
     if (!dki.err) {
@@ -3176,9 +3195,9 @@ void px_ctx::dki_commit(uint32_t gid0, const std::vector<DkRec> &recs, const std
         dki.rec = nr;
         dki.rec_cap = cap;
     }
-    if (dki.keys_len + kb.size() + 16 > dki.keys_cap) {  // (16 bytes of slack: the index reads 16 at a time)
+    if (dki.keys_len + kbn + 16 > dki.keys_cap) {  // (16 bytes of slack: the index reads 16 at a time)
         const uint64_t cap =
-            std::max<uint64_t>(dki.keys_len + kb.size() + 16, std::max<uint64_t>(1 << 16, dki.keys_cap * 2));
+            std::max<uint64_t>(dki.keys_len + kbn + 16, std::max<uint64_t>(1 << 16, dki.keys_cap * 2));
         auto *nk = (uint8_t *)heap.alloc(cap);
         if (dki.keys) {
             hcheck(hipMemcpyAsync(nk, dki.keys, dki.keys_len, hipMemcpyDeviceToDevice, stream));
@@ -3187,9 +3206,9 @@ void px_ctx::dki_commit(uint32_t gid0, const std::vector<DkRec> &recs, const std
         dki.keys = nk;
         dki.keys_cap = cap;
     }
-    h2d(dki.rec + gid0, recs.data(), (size_t)nn * sizeof(DkRec));
-    if (!kb.empty()) h2d(dki.keys + dki.keys_len, kb.data(), kb.size());
-    dki.keys_len += kb.size();
+    h2d(dki.rec + gid0, recs, (size_t)nn * sizeof(DkRec));
+    if (kbn) h2d(dki.keys + dki.keys_len, kb, kbn);
+    dki.keys_len += kbn;
     uint32_t first = gid0, count = nn;
     if ((uint64_t)dki.nrec * 2 > dki.tab_cap) {  // a new table: every record again (newest id wins)
         uint32_t cap = 1024;

@@ -11,7 +11,10 @@ namespace px {
 
 // A tile is kSortTile consecutive elements of ONE segment; a segment's tiles are
 // consecutive in the tile table and the first one carries first = 1.
-constexpr uint32_t kSortTile = 4096;
+#ifndef PX_SORT_ITEMS
+#define PX_SORT_ITEMS 16
+#endif
+constexpr uint32_t kSortTile = 256 * PX_SORT_ITEMS;
 struct SegTile {
     uint32_t start, count, seg, first;
 };

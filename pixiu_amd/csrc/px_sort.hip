@@ -32,7 +32,7 @@ namespace px {
 namespace {
 
 #define SD __device__ __forceinline__
-constexpr uint32_t kThreads = 256, kItems = 16, kWaves = kThreads / 64;
+constexpr uint32_t kThreads = 256, kItems = PX_SORT_ITEMS, kWaves = kThreads / 64;
 static_assert(kThreads * kItems == kSortTile, "tile = threads x items");
 constexpr uint32_t kMaxPasses = kRouteMaxPasses;
 constexpr uint32_t kHistTiles = 16;       // tiles per histogram workgroup, at most (fewer for small sorts)
@@ -294,19 +294,24 @@ __global__ void __launch_bounds__(kThreads) k_seg_base(const uint32_t *ghist, co
 
 // ---------------------------------------------------------------- one radix pass
 template <int RB, bool TEXT>
-__global__ void __launch_bounds__(kThreads) k_seg_pass(const SegTile *tiles, uint32_t *tile_ctr, const uint64_t *kin_,
+#ifndef PX_SORT_WPE
+#define PX_SORT_WPE 1
+#endif
+__global__ void __launch_bounds__(kThreads, PX_SORT_WPE) k_seg_pass(const SegTile *tiles, uint32_t *tile_ctr, const uint64_t *kin_,
                                                        const uint32_t *vin_, uint64_t *kout_, uint32_t *vout_,
                                                        uint32_t pass, uint32_t passes, const uint32_t *base,
                                                        uint32_t *status, const uint8_t *G, const uint16_t *dist,
                                                        uint32_t syms, uint32_t *err) {
     constexpr uint32_t BINS = 1u << RB, BPT = BINS / kThreads;
-    __shared__ uint32_t s_tile;
+    // (the tile number and the scan's partials live in s_dst's first words, which are written only
+    // after both are spent)
     __shared__ uint16_t wh[kWaves][BINS];  // per wave: running count, then the wave's offset in the tile
     __shared__ uint32_t s_excl[BINS];      // tile-local start of each digit's run
     __shared__ uint32_t s_dst[BINS];       // global position of that run's first element
-    __shared__ uint32_t red[kWaves];
     __shared__ uint64_t stage[kSortTile];  // the tile in digit order: keys, then values
     __shared__ uint16_t sdig[kSortTile];   // and each staged element's digit
+    uint32_t &s_tile = s_dst[0];
+    uint32_t *red = s_dst + 4;
     gcu64 *kin = (gcu64 *)kin_;
     gcu32 *vin = (gcu32 *)vin_;
     gu64 *kout = (gu64 *)kout_;
@@ -425,6 +430,9 @@ __global__ void __launch_bounds__(kThreads) k_seg_pass(const SegTile *tiles, uin
     __syncthreads();
     // ---- stage the keys in digit order, write each digit's run to its place
     // (consecutive lanes, consecutive addresses); then the values the same way
+    // (staging the values as value | digit << 32 instead of keeping sdig measured slower: the first
+    // sort 43.3 -> 45.7 ms, profiles/r06e_*; without sdig the LDS would allow a fourth workgroup
+    // per CU, but the registers (166 VGPRs) keep it at three)
     uint16_t at[kItems];
 #pragma unroll
     for (uint32_t it = 0; it < kItems; ++it) {
@@ -461,7 +469,8 @@ template <ScanOp OP>
 SD uint32_t op_do(uint32_t a, uint32_t b) {
     return OP == ScanOp::kMax ? max(a, b) : OP == ScanOp::kMin ? min(a, b) : a + b;
 }
-constexpr uint32_t kScanBlock = 4096;  // elements per workgroup (16 per thread)
+constexpr uint32_t kScanItems = 16, kScanBlock = kThreads * kScanItems;  // elements per workgroup (16 per
+                                                                          // thread, whatever the sort tile)
 
 template <ScanOp OP, bool REV>
 SD uint64_t scan_at(uint64_t i, uint64_t n) { return REV ? n - 1 - i : i; }
@@ -530,10 +539,10 @@ __global__ void __launch_bounds__(kThreads) k_scan_apply(const uint32_t *in, uin
     __shared__ uint32_t red[kWaves];
     const uint64_t b0 = (uint64_t)blockIdx.x * kScanBlock;
     // each thread: 16 consecutive elements (in scan order)
-    const uint64_t i0 = b0 + (uint64_t)threadIdx.x * kItems;
-    uint32_t x[kItems], acc = op_id<OP>();
+    const uint64_t i0 = b0 + (uint64_t)threadIdx.x * kScanItems;
+    uint32_t x[kScanItems], acc = op_id<OP>();
 #pragma unroll
-    for (uint32_t j = 0; j < kItems; ++j) {
+    for (uint32_t j = 0; j < kScanItems; ++j) {
         const uint64_t i = i0 + j;
         x[j] = i < n ? in[scan_at<OP, REV>(i, n)] : op_id<OP>();
         acc = op_do<OP>(acc, x[j]);
@@ -547,7 +556,7 @@ __global__ void __launch_bounds__(kThreads) k_scan_apply(const uint32_t *in, uin
     if (lane_id() == 0) run = threadIdx.x ? last[(threadIdx.x >> 6) - 1] : op_id<OP>();
     run = op_do<OP>(part[blockIdx.x], run);
 #pragma unroll
-    for (uint32_t j = 0; j < kItems; ++j) {
+    for (uint32_t j = 0; j < kScanItems; ++j) {
         const uint64_t i = i0 + j;
         run = op_do<OP>(run, x[j]);
         if (i < n) out[scan_at<OP, REV>(i, n)] = run;
