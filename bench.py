@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group for N > 1 (nccl = RCCL over xGMI; gloo: CPU transport, for tests)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r05.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r06.json"),
                     help="per-kernel PMC summary (tools/pmc_summary.py); used only if its workload matches")
     return ap.parse_args()
 

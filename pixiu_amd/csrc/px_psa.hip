@@ -843,6 +843,11 @@ __global__ void __launch_bounds__(256) k_dbl_reg(const uint64_t *list, const uin
 
 // bitonic network over sk[0 .. P) in LDS (256 threads; PMAX >= P, both powers of two >= 512):
 // stage (kk, j) compares pair q's elements i = q with a 0 bit inserted at j, and i | j
+// A stage with j <= 32 stays inside each wave's own elements (wave w takes pairs 64 w .. 64 w + 63
+// of every 256, i.e. elements 128 w .. 128 w + 127 of every 512), so it needs no workgroup barrier:
+// only the stages with j >= 64 and the last stage of each kk (the next kk starts at j = kk / 2)
+// wait for the other waves.  (LDS operations of one wave complete in order; the wave barrier keeps
+// the compiler from moving them across stages.)
 template <uint32_t P>
 PSA_DEV void blk_bitonic(uint64_t *sk) {
     const uint32_t tid = threadIdx.x;
@@ -861,7 +866,13 @@ PSA_DEV void blk_bitonic(uint64_t *sk) {
                     sk[l] = x;
                 }
             }
-            __syncthreads();
+            if (j >= 64 || j == 1) {
+                __syncthreads();
+            } else {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
         }
     }
 }
@@ -1380,13 +1391,12 @@ inline uint32_t lce_span(uint64_t n) {
     return (uint32_t)sp;
 }
 
-// 8 text bytes from any offset: two aligned 8-byte loads and a funnel shift
+// 8 text bytes from any offset: one unaligned 8-byte load (gfx950 runs in unaligned access
+// mode; G is padded by 64 bytes).  (Two aligned loads and a funnel shift doubled the lane
+// addresses of the LCE's scattered neighbour reads, which are what bounds it on random text.)
+typedef uint64_t u64_ua __attribute__((aligned(1)));
 PSA_DEV uint64_t ld8(const uint64_t *G8, uint32_t off) {
-    const uint32_t w = off >> 3, sh = (off & 7u) * 8u;
-    const uint64_t a = G8[w];
-    if (!sh) return a;
-    const uint64_t b = G8[w + 1];
-    return (a >> sh) | (b << (64u - sh));
+    return *(const PX_GAS u64_ua *)((const PX_GAS uint8_t *)G8 + off);
 }
 
 PSA_DEV uint32_t lce(const uint64_t *G8, uint32_t p, uint32_t q, uint32_t k, uint32_t lim) {

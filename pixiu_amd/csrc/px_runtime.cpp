@@ -1315,6 +1315,7 @@ struct px_ctx {
                     skip[j] = 1;
                 }
             }
+        std::vector<uint8_t> need_x(n, 0);  // compat tables that are not the doc: an exact table too
         uint64_t nents = 0, ntiles = 0;
         for (uint32_t j = 0; j < n; ++j)
             if (!(hc[j] & kSpanBad)) {
@@ -1340,12 +1341,13 @@ struct px_ctx {
                 const uint32_t ns = hc[j] & ~(kSpanBad | kSpanEq);
                 eo[j + 1] = eo[j] + (has ? ns + 1 : 0);
                 tofs[j + 1] = tofs[j] + (has ? (hl[j] + kGatherTile - 1) / kGatherTile : 0);
-                if (has && !skip[j]) {
-                    used += ns + 1;
+                used += has && !skip[j] ? ns + 1 : 0;
+            }
+            for (uint32_t j = 0; j < n; ++j)  // (the requests come in chunk order: one check per chunk)
+                if (j == 0 || reqs[j].chunk != reqs[j - 1].chunk) {
                     Chunk &ch = chunks[reqs[j].chunk];
                     if (ch.span.size() < ch.n) ch.span.resize(ch.n);
                 }
-            }
             stats.span_entries += used;
             parallel_ranges(n, pthr, [&](uint32_t lo, uint32_t hi) {
                 for (uint32_t j = lo; j < hi; ++j) {
@@ -1361,6 +1363,7 @@ struct px_ctx {
                         sp.n = ns;
                         sp.len = hl[j];
                         sp.eq = (hc[j] & kSpanEq) != 0;
+                        if (!sp.eq) need_x[j] = 1;
                     } else {
                         sp.xp = tab + eo[j];
                         sp.xt = tixb + tofs[j];
@@ -1378,8 +1381,11 @@ struct px_ctx {
         if (!redo.empty()) build_spans(redo, mode, false, false);
         phase.mark("exact tables");
         if (mode == 0 && exact_too) {  // exact tables for the records whose compat expansion is not the doc
+            // (marked while the views were filled; a record the whole decode redid is checked here)
             std::vector<SpanReq> x;
-            for (const SpanReq &r : reqs) {
+            for (uint32_t j = 0; j < n; ++j) {
+                if (!need_x[j] && !skip[j]) continue;
+                const SpanReq &r = reqs[j];
                 const Chunk &ch = chunks[r.chunk];
                 if (r.idx < ch.span.size() && ch.span[r.idx].p && !ch.span[r.idx].eq) x.push_back(r);
             }
@@ -1643,12 +1649,16 @@ struct px_ctx {
     // GPU-decode each record's key prefix (up to the spec-aware 251,0) into its chunk's
     // kp table; a prefix that overran `cap` is decoded again with the whole doc's room.
     // st[i] = kOk or the decode's failure status.
+    std::vector<DecodeQuery> kp_queries;
     void decode_key_prefixes(const std::vector<KpJob> &jobs, std::vector<uint32_t> &st) {
         PhaseClock phase("decode_key_prefixes", "PX_SET_VERBOSE");
         phase.mark("queries");
         st.assign(jobs.size(), kOk);
         const uint32_t nj = (uint32_t)jobs.size();
-        std::vector<DecodeQuery> q(nj);
+        // (the query table is kept across batches: value-initialising 40 MB of fresh queries for
+        // a million records was most of this phase)
+        std::vector<DecodeQuery> &q = kp_queries;
+        q.resize(nj);
         std::vector<uint32_t> qj(nj);
         std::vector<uint64_t> qoff(nj + 1, 0);
         for (uint32_t i = 0; i < nj; ++i) qoff[i + 1] = qoff[i] + round_up(jobs[i].cap, 16);
@@ -1722,7 +1732,7 @@ struct px_ctx {
             } else {
                 for (uint32_t k = 0; k + 1 < runs.size(); ++k) append_run(k);
             }
-            q.swap(again);
+            q.assign(again.begin(), again.end());
             qj.swap(again_j);
             qo = ao;
         }
