@@ -2201,10 +2201,16 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     PSA_CHECK(read_words(0, kCntWords));
     uint32_t active = pin[kCntActive], maxsz = pin[kCntMax];
     uint32_t h = syms, it = 0;
-    const uint32_t gwin = std::min<uint32_t>((uint32_t)((n64 + 255) / 256), kGridWin);
+    // (k_dbl_win: one wave per 64-window chunk at most -- a single-instance round of 12 M positions
+    // has 3,076 chunks, and 16,384 workgroups of which 15,600 had nothing to do cost each of its
+    // 636 launches their dispatch)
+    const uint64_t nchunk = ((n64 + 63) / 64 + 63) / 64;
+    const uint32_t gwin = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nchunk + 3) / 4, kGridWin));
     // one step: every group's keys (flat), then every group sorted by them (windows, then
     // the long-group lists the window kernel filled); big groups need their count on the host
-    auto step = [&](bool big) -> hipError_t {
+    // lists: launch the register and LDS sorters (false once every group fits a window: groups
+    // only split, so a step whose input's largest group is <= kWinMax fills no list)
+    auto step = [&](bool big, bool lists = true) -> hipError_t {
         const uint32_t tag = (it & 1u) ? kTag : 0u;
         const StepStat ss = stats_of(it);
         hipError_t e = hipSuccess;
@@ -2213,13 +2219,15 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         k_dbl_key<<<blocks((n64 + 15) / 16), tb, 0, s>>>(N, h, it, act, sa, sd, rank, key, cnt + kCntLong, R,
                                                           cnt + kCntSortErr);
         k_dbl_win<<<gwin, 256, 0, s>>>(N, tag, h, sa, sd, act, gsz, key, rank, LL, ss, R);
-        k_dbl_reg<2><<<kGridReg, 256, 0, s>>>(LL.lst[0], LL.cnt + 0, tag, h, sa, sd, act, gsz, key, rank, ss, R);
-        k_dbl_reg<4><<<kGridReg, 256, 0, s>>>(LL.lst[1], LL.cnt + 1, tag, h, sa, sd, act, gsz, key, rank, ss, R);
-        k_dbl_reg<8><<<kGridReg, 256, 0, s>>>(LL.lst[2], LL.cnt + 2, tag, h, sa, sd, act, gsz, key, rank, ss, R);
-        // (513..4096: the LDS sorter.  A 16-per-lane register sorter for 513..1024 measured slower:
-        // 253 VGPRs, one wave per SIMD -- k_dbl_reg + k_dbl_blk 39.0 against 29.6 ms on config 3,
-        // profiles/r06d_reg16_ab.txt)
-        k_dbl_blk<<<kGridBlk, 256, 0, s>>>(LL.lst[3], LL.cnt + 3, tag, h, sa, sd, act, gsz, key, rank, ss, R);
+        if (lists || big) {
+            k_dbl_reg<2><<<kGridReg, 256, 0, s>>>(LL.lst[0], LL.cnt + 0, tag, h, sa, sd, act, gsz, key, rank, ss, R);
+            k_dbl_reg<4><<<kGridReg, 256, 0, s>>>(LL.lst[1], LL.cnt + 1, tag, h, sa, sd, act, gsz, key, rank, ss, R);
+            k_dbl_reg<8><<<kGridReg, 256, 0, s>>>(LL.lst[2], LL.cnt + 2, tag, h, sa, sd, act, gsz, key, rank, ss, R);
+            // (513..4096: the LDS sorter.  A 16-per-lane register sorter for 513..1024 measured slower:
+            // 253 VGPRs, one wave per SIMD -- k_dbl_reg + k_dbl_blk 39.0 against 29.6 ms on config 3,
+            // profiles/r06d_reg16_ab.txt)
+            k_dbl_blk<<<kGridBlk, 256, 0, s>>>(LL.lst[3], LL.cnt + 3, tag, h, sa, sd, act, gsz, key, rank, ss, R);
+        }
         auto sum = [&]() {
             k_stat_sum<<<1, 64, 0, s>>>(ss.sh, cnt + kCntSorted + it, cnt + kCntActive + 1 + it, cnt + kCntMax + 1 + it);
         };
@@ -2302,15 +2310,20 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         PSA_CHECK(sev.make(kMaxSteps, hipEventDisableTiming));
         const uint32_t it0 = it;
         bool done = false;
+        // (pin[256 + k] / pin[288 + k]: slots in groups / the largest group after step k, known on the
+        // host once step k's event has passed -- two steps behind the step being enqueued)
+        uint32_t known_max = maxsz;  // the largest group after the last step whose counts are back
         while (!done) {
             if (it >= kMaxSteps) return hipErrorUnknown;
-            PSA_CHECK(step(false));
+            PSA_CHECK(step(false, known_max > kWinMax));
             const uint32_t k = it - 1;
             PSA_CHECK(hipMemcpyAsync(pin + 256 + k, cnt + kCntActive + 1 + k, 4, hipMemcpyDeviceToHost, s));
+            PSA_CHECK(hipMemcpyAsync(pin + 288 + k, cnt + kCntMax + 1 + k, 4, hipMemcpyDeviceToHost, s));
             PSA_CHECK(hipEventRecord(sev.e[k], s));
             if (k >= it0 + 1) {
                 PSA_CHECK(hipEventSynchronize(sev.e[k - 1]));
                 done = pin[256 + k - 1] == 0;
+                known_max = pin[288 + k - 1];
             }
         }
     }
