@@ -1400,11 +1400,26 @@ PSA_DEV uint64_t ld8(const uint64_t *G8, uint32_t off) {
 }
 
 PSA_DEV uint32_t lce(const uint64_t *G8, uint32_t p, uint32_t q, uint32_t k, uint32_t lim) {
-    // bytes equal from offset k on, up to lim (both suffixes stay inside their docs)
-    while (k < lim) {
+    // bytes equal from offset k on, up to lim (both suffixes stay inside their docs).  Most
+    // comparisons end in their first 8 bytes; one that does not runs on 32 bytes per step with
+    // the four loads issued together (a thread comparing a template copy from 0 was the tail of
+    // a single-instance round's launch: ~1,000 dependent 8-byte steps).  Reads stay below
+    // p + lim + 32 <= N + 32, inside G's 64 bytes of padding.
+    if (k >= lim) return lim;
+    {
         const uint64_t x = ld8(G8, p + k) ^ ld8(G8, q + k);
         if (x) return min(lim, k + (uint32_t)(__builtin_ctzll(x) >> 3));
         k += 8;
+    }
+    while (k < lim) {
+        const uint64_t a = ld8(G8, p + k) ^ ld8(G8, q + k), b = ld8(G8, p + k + 8) ^ ld8(G8, q + k + 8),
+                       c = ld8(G8, p + k + 16) ^ ld8(G8, q + k + 16), d = ld8(G8, p + k + 24) ^ ld8(G8, q + k + 24);
+        if (a | b | c | d) {
+            const uint32_t o = a ? 0u : b ? 8u : c ? 16u : 24u;
+            const uint64_t x = a ? a : b ? b : c ? c : d;
+            return min(lim, k + o + (uint32_t)(__builtin_ctzll(x) >> 3));
+        }
+        k += 32;
     }
     return lim;
 }

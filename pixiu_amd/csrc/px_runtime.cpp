@@ -3678,7 +3678,7 @@ extern "C" {
 // of a million records builds ~1 GB of per-record host arrays, and glibc serves each array
 // over 32 MB -- and, past its dynamic threshold, smaller ones -- by a fresh mmap that it
 // unmaps at free, so every batch paid first-touch page faults on all of them again (config 4:
-// 244 -> 177 ms per set batch with the policy, profiles/r06c_*phases.log).  With mmap off and
+// 244 -> 177 ms per set batch with the policy, profiles/r06c_cfg4_set_phases_*.log).  With mmap off and
 // the trim threshold out of reach, freed blocks stay in the heap and the next batch reuses
 // pages already mapped.  The cost: the process keeps its host heap's high-water mark.
 static void host_heap_policy() {
