@@ -276,7 +276,10 @@ PSA_DEV void stat_put(const StepStat &ss, uint32_t slot, uint32_t sorted, uint32
     if (active) atomicAdd(c + 1, active);
     if (mx) atomicMax(c + 2, mx);
 }
-__global__ void k_stat_sum(const uint32_t *sh, uint32_t *sorted, uint32_t *active, uint32_t *maxsz) {
+// (h_active / h_max: pinned host words also written, so the late doubling steps read their
+// counts back without a copy each)
+__global__ void k_stat_sum(const uint32_t *sh, uint32_t *sorted, uint32_t *active, uint32_t *maxsz,
+                           uint32_t *h_active = nullptr, uint32_t *h_max = nullptr) {
     const uint32_t l = threadIdx.x;  // one wave
     uint32_t a = sh[l * kStatStride], b = sh[l * kStatStride + 1], c = sh[l * kStatStride + 2];
     for (int o = 32; o > 0; o >>= 1) {
@@ -288,6 +291,10 @@ __global__ void k_stat_sum(const uint32_t *sh, uint32_t *sorted, uint32_t *activ
         *sorted = a;
         *active = b;
         *maxsz = c;
+        if (h_active) {  // (system scope: visible to the host once the step's event has passed)
+            __hip_atomic_store(h_active, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(h_max, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
@@ -559,7 +566,7 @@ PSA_DEV void win_put(const WinElem &e, uint32_t b, uint32_t lt, uint32_t eqb, ui
 }
 __global__ void __launch_bounds__(256) k_dbl_win(uint32_t N, uint32_t tag, uint32_t h, uint32_t *sa, uint16_t *sd, uint8_t *act,
                                                  uint32_t *gsz, const uint32_t *key, uint32_t *rank, LongLists L,
-                                                 StepStat ss, RetList R) {
+                                                 StepStat ss, RetList R, uint32_t split) {
     __shared__ uint32_t lks[4][128];
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
     uint32_t *lk = lks[wv];
@@ -573,8 +580,13 @@ __global__ void __launch_bounds__(256) k_dbl_win(uint32_t N, uint32_t tag, uint3
     // testing them one by one was a dependent load per window)
     // (lane l of chunk c tests window l * nch + c: a run of busy windows -- a template's
     // copies -- is dealt over many waves instead of queueing on one)
+    // (split > 1, small rounds: `split` waves share a chunk, each taking every split-th of its
+    // busy windows -- a single-instance round of 12 M positions has ~2,900 chunks, under 3 waves
+    // per SIMD for a kernel that waits on scattered loads)
     const uint32_t nch = (nwin + 63) / 64;
-    for (uint32_t c = blockIdx.x * (blockDim.x >> 6) + wv; c < nch; c += waves) {
+    const uint32_t units = nch * split;
+    for (uint32_t un = blockIdx.x * (blockDim.x >> 6) + wv; un < units; un += waves) {
+      const uint32_t c = un / split, sub = un - c * split;
       uint64_t todo;
       {
         const uint32_t wl = lane * nch + c, s0 = wl * 64;
@@ -589,7 +601,10 @@ __global__ void __launch_bounds__(256) k_dbl_win(uint32_t N, uint32_t tag, uint3
                 for (uint32_t q = s0; q < N; ++q) any |= act[q] != 0;
             }
         }
-        todo = __ballot(any);
+        // (a shared chunk: this wave's windows are its lanes l with l % split == sub -- a fixed
+        // owner per window.  Dealing the busy windows by their rank instead hangs: act changes
+        // while the chunk's waves run, so their busy masks, and ranks, differ)
+        todo = __ballot(any && lane % split == sub);
       }
       while (todo) {
         const uint32_t w = lobit(todo) * nch + c;
@@ -1399,18 +1414,29 @@ PSA_DEV uint64_t ld8(const uint64_t *G8, uint32_t off) {
     return *(const PX_GAS u64_ua *)((const PX_GAS uint8_t *)G8 + off);
 }
 
+#ifndef PX_LCE_STEP
+#define PX_LCE_STEP 64
+#endif
+// 16 text bytes from any offset: one unaligned 16-byte load
+typedef uint64_t u64x2_ua __attribute__((ext_vector_type(2), aligned(1)));
+PSA_DEV u64x2_ua ld16(const uint64_t *G8, uint32_t off) {
+    return *(const PX_GAS u64x2_ua *)((const PX_GAS uint8_t *)G8 + off);
+}
+
 PSA_DEV uint32_t lce(const uint64_t *G8, uint32_t p, uint32_t q, uint32_t k, uint32_t lim) {
     // bytes equal from offset k on, up to lim (both suffixes stay inside their docs).  Most
-    // comparisons end in their first 8 bytes; one that does not runs on 32 bytes per step with
-    // the four loads issued together (a thread comparing a template copy from 0 was the tail of
-    // a single-instance round's launch: ~1,000 dependent 8-byte steps).  Reads stay below
-    // p + lim + 32 <= N + 32, inside G's 64 bytes of padding.
+    // comparisons end in their first 8 bytes; one that does not runs on 64 bytes per step, four
+    // 16-byte loads per side issued together (a thread entering a template copy compares the
+    // copy's length alone, a dependent round trip per step: at 8 and then 32 bytes per step
+    // such threads were the tail of a single-instance round's launch).  Reads stay below
+    // p + lim + 64 <= N + 64, inside G's 64 bytes of padding.
     if (k >= lim) return lim;
     {
         const uint64_t x = ld8(G8, p + k) ^ ld8(G8, q + k);
         if (x) return min(lim, k + (uint32_t)(__builtin_ctzll(x) >> 3));
         k += 8;
     }
+#if PX_LCE_STEP == 32  // (A/B: 32 bytes per step, eight 8-byte loads)
     while (k < lim) {
         const uint64_t a = ld8(G8, p + k) ^ ld8(G8, q + k), b = ld8(G8, p + k + 8) ^ ld8(G8, q + k + 8),
                        c = ld8(G8, p + k + 16) ^ ld8(G8, q + k + 16), d = ld8(G8, p + k + 24) ^ ld8(G8, q + k + 24);
@@ -1422,6 +1448,28 @@ PSA_DEV uint32_t lce(const uint64_t *G8, uint32_t p, uint32_t q, uint32_t k, uin
         k += 32;
     }
     return lim;
+#else
+    while (k < lim) {
+        const u64x2_ua a = ld16(G8, p + k) ^ ld16(G8, q + k), b = ld16(G8, p + k + 16) ^ ld16(G8, q + k + 16),
+                       c = ld16(G8, p + k + 32) ^ ld16(G8, q + k + 32), d = ld16(G8, p + k + 48) ^ ld16(G8, q + k + 48);
+        const uint64_t w[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
+        if (w[0] | w[1] | w[2] | w[3] | w[4] | w[5] | w[6] | w[7]) {
+            uint32_t o = 0;
+            uint64_t x = 0;
+            bool f = false;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)  // (the first nonzero word)
+                if (!f && w[i]) {
+                    f = true;
+                    o = 8u * (uint32_t)i;
+                    x = w[i];
+                }
+            return min(lim, k + o + (uint32_t)(__builtin_ctzll(x) >> 3));
+        }
+        k += 64;
+    }
+    return lim;
+#endif
 }
 
 // The lcp values at every span's first position, where k_psa_lce would start from zero: a
@@ -1778,6 +1826,35 @@ __global__ void __launch_bounds__(256) k_pool_blocks(uint32_t N, uint8_t *code, 
         c = tab[h].min == p ? 3 : 1;
         code[p] = (uint8_t)c;
     }
+    blk[p] = c == 1 ? 8u : c == 3 ? 16u : 0u;
+}
+
+// The same decision without the hash table (default; PX_POOL_HASH=1 selects the table above):
+// the candidates in position order (a flag scan), stably sorted by (E, l) -- so each key's run
+// starts with its smallest position, the one that splits.  The table's two fabric atomics per
+// candidate (device-scope atomics bypass the XCD's L2) were most of a single-instance round's
+// pool emulation: k_pool_insert 0.6 ms of its ~1.2 ms.
+__global__ void __launch_bounds__(256) k_pool_cflag(uint32_t N, const uint8_t *code, uint32_t *f) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < N) f[p] = code[p] == 2 ? 1u : 0u;
+}
+__global__ void __launch_bounds__(256) k_pool_cpack(uint32_t N, const uint8_t *code, const uint32_t *E, const uint16_t *lp,
+                                                    const uint16_t *ln, const uint32_t *incl, uint64_t *ck, uint32_t *cv) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= N || code[p] != 2) return;
+    const uint32_t i = incl[p] - 1u;
+    ck[i] = (uint64_t)E[p] << 16 | max(lp[p], ln[p]);
+    cv[i] = p;
+}
+__global__ void __launch_bounds__(256) k_pool_cmark(uint32_t nc, const uint64_t *ck, const uint32_t *cv, uint8_t *code) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nc) return;
+    code[cv[i]] = (i == 0 || ck[i - 1] != ck[i]) ? 3 : 1;
+}
+__global__ void __launch_bounds__(256) k_pool_cblk(uint32_t N, const uint8_t *code, uint32_t *blk) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= N) return;
+    const uint32_t c = code[p];
     blk[p] = c == 1 ? 8u : c == 3 ? 16u : 0u;
 }
 
@@ -2220,12 +2297,15 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     // has 3,076 chunks, and 16,384 workgroups of which 15,600 had nothing to do cost each of its
     // 636 launches their dispatch)
     const uint64_t nchunk = ((n64 + 63) / 64 + 63) / 64;
-    const uint32_t gwin = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nchunk + 3) / 4, kGridWin));
+    // (chunks shared by up to 8 waves while there are fewer than 16,384 of them)
+    uint32_t wsplit = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8, 16384 / std::max<uint64_t>(1, nchunk)));
+    if (const char *e = std::getenv("PX_WIN_SPLIT")) wsplit = (uint32_t)std::min(8, std::max(1, std::atoi(e)));  // (A/B)
+    const uint32_t gwin = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nchunk * wsplit + 3) / 4, kGridWin));
     // one step: every group's keys (flat), then every group sorted by them (windows, then
     // the long-group lists the window kernel filled); big groups need their count on the host
     // lists: launch the register and LDS sorters (false once every group fits a window: groups
     // only split, so a step whose input's largest group is <= kWinMax fills no list)
-    auto step = [&](bool big, bool lists = true) -> hipError_t {
+    auto step = [&](bool big, bool lists = true, uint32_t *h_active = nullptr, uint32_t *h_max = nullptr) -> hipError_t {
         const uint32_t tag = (it & 1u) ? kTag : 0u;
         const StepStat ss = stats_of(it);
         hipError_t e = hipSuccess;
@@ -2233,7 +2313,7 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         // in the dense steps (29.4 -> 34.1 ms) and no faster when used only in the sparse ones)
         k_dbl_key<<<blocks((n64 + 15) / 16), tb, 0, s>>>(N, h, it, act, sa, sd, rank, key, cnt + kCntLong, R,
                                                           cnt + kCntSortErr);
-        k_dbl_win<<<gwin, 256, 0, s>>>(N, tag, h, sa, sd, act, gsz, key, rank, LL, ss, R);
+        k_dbl_win<<<gwin, 256, 0, s>>>(N, tag, h, sa, sd, act, gsz, key, rank, LL, ss, R, wsplit);
         if (lists || big) {
             k_dbl_reg<2><<<kGridReg, 256, 0, s>>>(LL.lst[0], LL.cnt + 0, tag, h, sa, sd, act, gsz, key, rank, ss, R);
             k_dbl_reg<4><<<kGridReg, 256, 0, s>>>(LL.lst[1], LL.cnt + 1, tag, h, sa, sd, act, gsz, key, rank, ss, R);
@@ -2244,7 +2324,8 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
             k_dbl_blk<<<kGridBlk, 256, 0, s>>>(LL.lst[3], LL.cnt + 3, tag, h, sa, sd, act, gsz, key, rank, ss, R);
         }
         auto sum = [&]() {
-            k_stat_sum<<<1, 64, 0, s>>>(ss.sh, cnt + kCntSorted + it, cnt + kCntActive + 1 + it, cnt + kCntMax + 1 + it);
+            k_stat_sum<<<1, 64, 0, s>>>(ss.sh, cnt + kCntSorted + it, cnt + kCntActive + 1 + it, cnt + kCntMax + 1 + it,
+                                        h_active, h_max);
         };
         if (big) {
             e = read_words(kCntLong, 8);
@@ -2330,10 +2411,14 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         uint32_t known_max = maxsz;  // the largest group after the last step whose counts are back
         while (!done) {
             if (it >= kMaxSteps) return hipErrorUnknown;
-            PSA_CHECK(step(false, known_max > kWinMax));
+            // (k_stat_sum writes step k's counts into pin[256 + k] / pin[288 + k] itself)
+            static const bool pin_copy = env_on("PX_PIN_COPY");  // (A/B: the counts copied back)
+            PSA_CHECK(step(false, known_max > kWinMax, pin_copy ? nullptr : pin + 256 + it, pin_copy ? nullptr : pin + 288 + it));
             const uint32_t k = it - 1;
-            PSA_CHECK(hipMemcpyAsync(pin + 256 + k, cnt + kCntActive + 1 + k, 4, hipMemcpyDeviceToHost, s));
-            PSA_CHECK(hipMemcpyAsync(pin + 288 + k, cnt + kCntMax + 1 + k, 4, hipMemcpyDeviceToHost, s));
+            if (pin_copy) {
+                PSA_CHECK(hipMemcpyAsync(pin + 256 + k, cnt + kCntActive + 1 + k, 4, hipMemcpyDeviceToHost, s));
+                PSA_CHECK(hipMemcpyAsync(pin + 288 + k, cnt + kCntMax + 1 + k, 4, hipMemcpyDeviceToHost, s));
+            }
             PSA_CHECK(hipEventRecord(sev.e[k], s));
             if (k >= it0 + 1) {
                 PSA_CHECK(hipEventSynchronize(sev.e[k - 1]));
@@ -2452,12 +2537,36 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         PSA_CHECK(hipStreamSynchronize(s));
         nc = pin[0];
         if (verbose) fprintf(stderr, "psa pools: %u split candidates\n", nc);
-        while (cap < 2ull * nc) cap <<= 1;
-        auto *tab = S.get<PoolSlot>(cap * sizeof(PoolSlot));
-        PSA_CHECK(hipMemsetAsync(tab, 0xff, cap * sizeof(PoolSlot), s));
-        const uint32_t mask = (uint32_t)(cap - 1);
-        k_pool_insert<<<blocks(N), tb, 0, s>>>(N, code, E, lcp_p, lcp_n, tab, mask);
-        k_pool_blocks<<<blocks(N), tb, 0, s>>>(N, code, E, lcp_p, lcp_n, tab, mask, blk);
+        if (env_on("PX_POOL_HASH")) {  // (the hash-table version, for A/B)
+            while (cap < 2ull * nc) cap <<= 1;
+            auto *tab = S.get<PoolSlot>(cap * sizeof(PoolSlot));
+            PSA_CHECK(hipMemsetAsync(tab, 0xff, cap * sizeof(PoolSlot), s));
+            const uint32_t mask = (uint32_t)(cap - 1);
+            k_pool_insert<<<blocks(N), tb, 0, s>>>(N, code, E, lcp_p, lcp_n, tab, mask);
+            k_pool_blocks<<<blocks(N), tb, 0, s>>>(N, code, E, lcp_p, lcp_n, tab, mask, blk);
+        } else {
+            if (nc) {
+                k_pool_cflag<<<blocks(N), tb, 0, s>>>(N, code, blk);
+                PSA_CHECK(scan_u32(s, SA, blk, P, N, ScanOp::kPlus, false));
+                auto *ck = S.get<uint64_t>((uint64_t)nc * 8), *ck2 = S.get<uint64_t>((uint64_t)nc * 8),
+                     *cka = S.get<uint64_t>((uint64_t)nc * 8);
+                auto *cv = S.get<uint32_t>((uint64_t)nc * 4), *cv2 = S.get<uint32_t>((uint64_t)nc * 4),
+                     *cva = S.get<uint32_t>((uint64_t)nc * 4);
+                k_pool_cpack<<<blocks(N), tb, 0, s>>>(N, code, E, lcp_p, lcp_n, P, ck, cv);
+                // one segment [0, nc); keys E << 16 | l below 16 + bit length of N - 1
+                auto *seg = S.get<uint32_t>(64);
+                PSA_CHECK(hipMemsetAsync(seg, 0, 4, s));
+                PSA_CHECK(hipMemcpyAsync(seg + 1, ncand, 4, hipMemcpyDeviceToDevice, s));
+                const uint32_t kbits = 16u + (N > 1 ? 32u - (uint32_t)__builtin_clz(N - 1u) : 1u);
+                PSA_CHECK(seg_sort_pairs(s, SA, 1, seg_tile_count(&nc, 1), seg, seg + 1, kbits, 8, ck, cv, nullptr, nullptr,
+                                         0, cka, cva, nullptr, nullptr, ck2, cv2, cnt + kCntSortErr));
+                k_pool_cmark<<<blocks(nc), tb, 0, s>>>(nc, ck2, cv2, code);
+                for (const void *q : {(const void *)ck, (const void *)ck2, (const void *)cka, (const void *)cv,
+                                      (const void *)cv2, (const void *)cva, (const void *)seg})
+                    S.put(q);
+            }
+            k_pool_cblk<<<blocks(N), tb, 0, s>>>(N, code, blk);
+        }
         PSA_CHECK(scan_u32(s, SA, blk, P, N, ScanOp::kPlus, false));
         auto *C = S.get<uint32_t>(n64 / kPoolCoarse * 4 + 256);
         k_pool_coarse<<<blocks((N + kPoolCoarse - 1) / kPoolCoarse), tb, 0, s>>>(N, P, C);

@@ -2774,14 +2774,25 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     };
     const uint32_t nk = keymap_job ? PartKeyMap::kParts : 0u;
     const uint32_t nthr = std::min<uint32_t>(host_threads(), (uint32_t)work.size() + nk);
+    // (PX_SET_VERBOSE: every task's time, to see which kind sets the phase's length)
+    std::vector<float> task_ms(phase.on ? nk + work.size() : 0);
     const std::function<void(uint32_t)> job = [&](uint32_t t) {
+        const auto t0 = std::chrono::steady_clock::now();
         if (t < nk) keymap_job(t);
         else insert_work(t - nk);
+        if (phase.on) task_ms[t] = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
     };
     if (nthr <= 1 || n < 2048) {
         for (uint32_t t = 0; t < nk + (uint32_t)work.size(); ++t) job(t);
     } else {
         WorkerPool::get().run(nk + (uint32_t)work.size(), job);
+    }
+    if (phase.on) {
+        float km = 0, ks = 0, im = 0, is = 0;
+        for (uint32_t t = 0; t < nk; ++t) km = std::max(km, task_ms[t]), ks += task_ms[t];
+        for (uint32_t t = nk; t < task_ms.size(); ++t) im = std::max(im, task_ms[t]), is += task_ms[t];
+        fprintf(stderr, "set_batch: key map tasks %u (max %.2f ms, sum %.2f), trie tasks %zu (max %.2f ms, sum %.2f), %u threads\n",
+                nk, km, ks, work.size(), im, is, nthr);
     }
     for (auto &v : mv) moved.insert(moved.end(), v.begin(), v.end());
     std::sort(moved.begin(), moved.end());  // record order

@@ -301,7 +301,7 @@ __global__ void __launch_bounds__(kThreads, PX_SORT_WPE) k_seg_pass(const SegTil
                                                        const uint32_t *vin_, uint64_t *kout_, uint32_t *vout_,
                                                        uint32_t pass, uint32_t passes, const uint32_t *base,
                                                        uint32_t *status, const uint8_t *G, const uint16_t *dist,
-                                                       uint32_t syms, uint32_t *err) {
+                                                       uint32_t syms, uint32_t *err, uint32_t *status_next) {
     constexpr uint32_t BINS = 1u << RB, BPT = BINS / kThreads;
     // (the tile number and the scan's partials live in s_dst's first words, which are written only
     // after both are spent)
@@ -322,6 +322,10 @@ __global__ void __launch_bounds__(kThreads, PX_SORT_WPE) k_seg_pass(const SegTil
     __syncthreads();
     const uint32_t t = s_tile;
     const SegTile T = tiles[t];
+    // the next pass's look-back words of this tile cleared here (that buffer was the previous
+    // pass's, which is complete): one memset per sort instead of one per pass
+    if (status_next)
+        for (uint32_t i = threadIdx.x; i < BINS; i += kThreads) ((gu32 *)status_next)[(uint64_t)t * BINS + i] = 0;
     // (the first pass: the tile's text in LDS, in the stage buffer's room until the ranking)
     const uint32_t tw0 = T.start >> 3;
     if (TEXT) {
@@ -600,7 +604,8 @@ hipError_t seg_sort_pairs(hipStream_t s, const SortAlloc &A, uint32_t nseg, uint
                    b_hist = (uint64_t)nseg * passes * bins * 4, b_status = (uint64_t)nt * bins * 4;
     const uint64_t o_pre = (b_tiles + 255) / 256 * 256, o_hist = o_pre + (b_pre + 255) / 256 * 256,
                    o_base = o_hist + (b_hist + 255) / 256 * 256, o_ctr = o_base + (b_hist + 255) / 256 * 256,
-                   o_status = o_ctr + 256, total = o_status + b_status + 256;
+                   o_status = o_ctr + 256, o_status2 = o_status + (b_status + 255) / 256 * 256,
+                   total = o_status2 + b_status + 256;
     auto *mem = (uint8_t *)A.alloc(A.self, total);
     if (!mem) return hipErrorOutOfMemory;
     auto *d_tiles = (SegTile *)mem;
@@ -608,9 +613,15 @@ hipError_t seg_sort_pairs(hipStream_t s, const SortAlloc &A, uint32_t nseg, uint
     auto *d_hist = (uint32_t *)(mem + o_hist);
     auto *d_base = (uint32_t *)(mem + o_base);
     auto *d_ctr = (uint32_t *)(mem + o_ctr);
-    auto *d_status = (uint32_t *)(mem + o_status);
-    hipError_t e = hipMemsetAsync(d_hist, 0, b_hist, s);
-    if (e == hipSuccess) e = hipMemsetAsync(d_ctr, 0, 256, s);
+    // two look-back buffers, alternating by pass: pass p clears the one pass p + 1 uses
+    uint32_t *d_status2[2] = {(uint32_t *)(mem + o_status), (uint32_t *)(mem + o_status2)};
+    // one memset: the digit counts, (the bases, written whole later), the tile counters and the
+    // first pass's look-back words
+    hipError_t e = hipMemsetAsync(d_hist, 0, o_status + b_status - o_hist, s);
+    static const bool per_pass_memset = [] {  // (A/B: one memset per pass, as before)
+        const char *v = std::getenv("PX_SORT_PASS_MEMSET");
+        return v && *v == '1';
+    }();
     if (e != hipSuccess) {
         A.release(A.self, mem, total);
         return e;
@@ -644,14 +655,18 @@ hipError_t seg_sort_pairs(hipStream_t s, const SortAlloc &A, uint32_t nseg, uint
         for (uint32_t p = 0; p < passes && e == hipSuccess; ++p) {                                                 \
             uint64_t *ko = (uint64_t *)route[p].k;                                                                 \
             uint32_t *vo = (uint32_t *)route[p].v;                                                                 \
-            e = hipMemsetAsync(d_status, 0, b_status, s);                                                          \
-            if (e != hipSuccess) break;                                                                            \
+            uint32_t *st = d_status2[p & 1u], *sn = p + 1 < passes ? d_status2[(p + 1) & 1u] : nullptr;          \
+            if (per_pass_memset) {                                                                                 \
+                st = d_status2[0];                                                                                 \
+                sn = nullptr;                                                                                      \
+                if (p > 0) e = hipMemsetAsync(st, 0, b_status, s);                                                 \
+            }                                                                                                      \
             if (text && p == 0)                                                                                    \
                 k_seg_pass<RB_, true><<<nt, kThreads, 0, s>>>(d_tiles, d_ctr + p, nullptr, nullptr, ko, vo, p,     \
-                                                              passes, d_base, d_status, G, dist, syms, err);       \
+                                                              passes, d_base, st, G, dist, syms, err, sn);         \
             else                                                                                                   \
                 k_seg_pass<RB_, false><<<nt, kThreads, 0, s>>>(d_tiles, d_ctr + p, ki, vi, ko, vo, p, passes,      \
-                                                               d_base, d_status, nullptr, nullptr, 0, err);        \
+                                                               d_base, st, nullptr, nullptr, 0, err, sn);          \
             ki = ko;                                                                                               \
             vi = vo;                                                                                               \
             e = hipGetLastError();                                                                                 \
