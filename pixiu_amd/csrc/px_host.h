@@ -180,8 +180,8 @@ class KeyMap {
             if (e.h == h && e.len == n && (n == 0 || std::memcmp(bytes_.data() + e.off, k, n) == 0)) return i;
         }
     }
-    void grow() {
-        std::vector<Slot> old(std::max<size_t>(tab_.size() * 2, 1024), Slot{0, 0, kFree, 0, ~0u, 0});
+    void grow(size_t want = 0) {
+        std::vector<Slot> old(std::max<size_t>({tab_.size() * 2, want, 1024}), Slot{0, 0, kFree, 0, ~0u, 0});
         old.swap(tab_);
         const size_t m = tab_.size() - 1;
         for (const Slot &e : old)
@@ -234,9 +234,33 @@ class KeyMap {
         *idx = e.idx;
         return true;
     }
-    // room for `more` keys without rehashing on the way
-    void reserve(size_t more) {
-        while ((n_ + more) * 2 > tab_.size()) grow();
+    // room for `more` keys (of `bytes` key bytes) without rehashing on the way: one table of
+    // the final size, not a doubling per step
+    void reserve(size_t more, size_t bytes = 0) {
+        if ((n_ + more) * 2 > tab_.size()) {
+            size_t want = 1024;
+            while ((n_ + more) * 2 > want) want <<= 1;
+            grow(want);
+        }
+        if (bytes) bytes_.reserve(bytes_.size() + bytes);
+    }
+    // the slot a hash starts probing at (prefetch ahead of upsert_h)
+    const void *probe_addr(uint64_t h) const { return tab_.empty() ? nullptr : &tab_[h & (tab_.size() - 1)]; }
+    // upsert with the hash already computed (KeyMap::hash(k, n))
+    int64_t upsert_h(uint64_t h, const uint8_t *k, size_t n, uint32_t shard, uint32_t chunk, uint32_t idx) {
+        if ((n_ + 1) * 2 > tab_.size()) grow();
+        Slot &e = tab_[probe(h, k, n)];
+        if (e.len == kFree) {
+            e = Slot{h, bytes_.size(), (uint32_t)n, shard, chunk, idx};
+            bytes_.insert(bytes_.end(), k, k + n);
+            ++n_;
+            return -1;
+        }
+        const int64_t prev = e.shard;
+        e.shard = shard;
+        e.chunk = chunk;
+        e.idx = idx;
+        return prev;
     }
     // put, returning the shard k was stored under before (-1: new key)
     int64_t upsert(const uint8_t *k, size_t n, uint32_t shard, uint32_t chunk, uint32_t idx) {
@@ -419,6 +443,35 @@ void parallel_ranges(uint32_t n, uint32_t threads, F fn) {
         if (lo < hi) fn(lo, hi);
     };
     WorkerPool::get().run(tasks, job);
+}
+
+// out[0] = 0, out[i + 1] = out[i] + val(i) for i < n (uint64), on `threads` host threads: block
+// sums, their prefix, then each block's running sum (a million-element prefix was ~2 ms serial)
+template <class V>
+void parallel_prefix(uint32_t n, uint32_t threads, uint64_t *out, V val) {
+    out[0] = 0;
+    if (threads <= 1 || n < 65536) {
+        for (uint32_t i = 0; i < n; ++i) out[i + 1] = out[i] + val(i);
+        return;
+    }
+    constexpr uint32_t kBlk = 16384;
+    const uint32_t nb = (n + kBlk - 1) / kBlk;
+    std::vector<uint64_t> bs(nb + 1, 0);
+    const std::function<void(uint32_t)> sum = [&](uint32_t b) {
+        uint64_t t = 0;
+        for (uint32_t i = b * kBlk, e = std::min(n, i + kBlk); i < e; ++i) t += val(i);
+        bs[b + 1] = t;
+    };
+    WorkerPool::get().run(nb, sum);
+    for (uint32_t b = 0; b < nb; ++b) bs[b + 1] += bs[b];
+    const std::function<void(uint32_t)> put = [&](uint32_t b) {
+        uint64_t t = bs[b];
+        for (uint32_t i = b * kBlk, e = std::min(n, i + kBlk); i < e; ++i) {
+            t += val(i);
+            out[i + 1] = t;
+        }
+    };
+    WorkerPool::get().run(nb, put);
 }
 
 // ---------------------------------------------------------------- crit-bit index

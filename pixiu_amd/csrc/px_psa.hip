@@ -1834,15 +1834,28 @@ __global__ void __launch_bounds__(256) k_pool_blocks(uint32_t N, uint8_t *code, 
 // starts with its smallest position, the one that splits.  The table's two fabric atomics per
 // candidate (device-scope atomics bypass the XCD's L2) were most of a single-instance round's
 // pool emulation: k_pool_insert 0.6 ms of its ~1.2 ms.
-__global__ void __launch_bounds__(256) k_pool_cflag(uint32_t N, const uint8_t *code, uint32_t *f) {
+// candidates per 256 positions (the compaction's scan runs over these, not over every position)
+__global__ void __launch_bounds__(256) k_pool_ccount(uint32_t N, const uint8_t *code, uint32_t *bc) {
+    __shared__ uint32_t wc[4];
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p < N) f[p] = code[p] == 2 ? 1u : 0u;
+    const uint64_t m = __ballot(p < N && code[p] == 2);
+    if (lane_id() == 0) wc[threadIdx.x >> 6] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) bc[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
 }
+// candidate p -> slot (candidates before its block, from the inclusive scan) + its rank in the block
 __global__ void __launch_bounds__(256) k_pool_cpack(uint32_t N, const uint8_t *code, const uint32_t *E, const uint16_t *lp,
-                                                    const uint16_t *ln, const uint32_t *incl, uint64_t *ck, uint32_t *cv) {
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= N || code[p] != 2) return;
-    const uint32_t i = incl[p] - 1u;
+                                                    const uint16_t *ln, const uint32_t *bincl, uint64_t *ck, uint32_t *cv) {
+    __shared__ uint32_t wc[4];
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x, w = threadIdx.x >> 6;
+    const bool c = p < N && code[p] == 2;
+    const uint64_t m = __ballot(c);
+    if (lane_id() == 0) wc[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (!c) return;
+    uint32_t i = blockIdx.x ? bincl[blockIdx.x - 1] : 0u;
+    for (uint32_t x = 0; x < w; ++x) i += wc[x];
+    i += (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull));
     ck[i] = (uint64_t)E[p] << 16 | max(lp[p], ln[p]);
     cv[i] = p;
 }
@@ -2546,13 +2559,13 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
             k_pool_blocks<<<blocks(N), tb, 0, s>>>(N, code, E, lcp_p, lcp_n, tab, mask, blk);
         } else {
             if (nc) {
-                k_pool_cflag<<<blocks(N), tb, 0, s>>>(N, code, blk);
-                PSA_CHECK(scan_u32(s, SA, blk, P, N, ScanOp::kPlus, false));
+                k_pool_ccount<<<blocks(N), tb, 0, s>>>(N, code, blk);
+                PSA_CHECK(scan_u32(s, SA, blk, blk, blocks(N), ScanOp::kPlus, false));
                 auto *ck = S.get<uint64_t>((uint64_t)nc * 8), *ck2 = S.get<uint64_t>((uint64_t)nc * 8),
                      *cka = S.get<uint64_t>((uint64_t)nc * 8);
                 auto *cv = S.get<uint32_t>((uint64_t)nc * 4), *cv2 = S.get<uint32_t>((uint64_t)nc * 4),
                      *cva = S.get<uint32_t>((uint64_t)nc * 4);
-                k_pool_cpack<<<blocks(N), tb, 0, s>>>(N, code, E, lcp_p, lcp_n, P, ck, cv);
+                k_pool_cpack<<<blocks(N), tb, 0, s>>>(N, code, E, lcp_p, lcp_n, blk, ck, cv);
                 // one segment [0, nc); keys E << 16 | l below 16 + bit length of N - 1
                 auto *seg = S.get<uint32_t>(64);
                 PSA_CHECK(hipMemsetAsync(seg, 0, 4, s));

@@ -7,6 +7,7 @@
 // (lengths, statuses, key prefixes) and runs the CritBit walk.
 #include <hip/hip_runtime.h>
 #include <malloc.h>
+#include <array>
 
 #include <algorithm>
 #include <atomic>
@@ -412,7 +413,8 @@ struct px_ctx {
         slotput_buf;
     HostBuf hq_buf, hres_buf;  // pinned: decode queries up, lengths + statuses down
     HostBuf hg_buf[2];         // pinned: gather queries up (a head and a tail launch)
-    HostBuf psa_pin;           // pinned: px_psa.hip's count read-backs
+    HostBuf psa_pin;
+    HostBuf slot_pin;          // pinned: set_batch's slot entries on their way to the device           // pinned: px_psa.hip's count read-backs
     HostBuf kp_hbuf;           // pinned: decoded key prefixes down
     DevBuf sink_buf;           // k_gst_encode's message sink for replayed docs
     PsaStats psa_stats{};      // the last set batch's suffix-array pass
@@ -513,8 +515,10 @@ struct px_ctx {
         for (auto &c : chunks) c.gid.clear();
     }
     void dki_commit(uint32_t gid0, const DkRec *recs, uint32_t nn, const uint8_t *kb, uint64_t kbn);
-    std::vector<DkRec> dk_rec_buf;      // a set batch's new index entries (kept: no re-initialisation per batch)
-    std::vector<uint8_t> dk_key_buf;    // and their raw key bytes
+    // a set batch's new index entries and their raw key bytes, in pinned memory kept across
+    // batches: copied to the device straight from here (80 MB for a million records went
+    // through the bulk ring's staging copy)
+    HostBuf dk_rec_pin, dk_key_pin;
     // the live bit of every record killed since (replaces, deletes, reinsert), on the device
     void dki_apply_kills() {
         std::vector<uint32_t> kills;
@@ -650,7 +654,9 @@ struct px_ctx {
     }
     void d2h(void *h, const void *d, size_t n) {
         if (!n) return;
-        if (n <= kPinBlock / 4) {
+        // (async through kept pinned blocks up to 32 MB: a million-record batch reads back six
+        // 4 MB arrays after its encode, which the synchronous bounce path took one by one)
+        if (n <= (32u << 20)) {
             uint8_t *p = pin_alloc(n);
             std::memset(p, 0xff, n);
             hcheck(hipMemcpyAsync(p, d, n, hipMemcpyDeviceToHost, stream));
@@ -1317,11 +1323,23 @@ struct px_ctx {
             }
         std::vector<uint8_t> need_x(n, 0);  // compat tables that are not the doc: an exact table too
         uint64_t nents = 0, ntiles = 0;
-        for (uint32_t j = 0; j < n; ++j)
-            if (!(hc[j] & kSpanBad)) {
-                nents += (hc[j] & ~(kSpanBad | kSpanEq)) + 1;
-                ntiles += (hl[j] + kGatherTile - 1) / kGatherTile;
-            }
+        {
+            std::vector<uint64_t> part_e(pthr > 1 ? 64 : 1, 0), part_t(part_e.size(), 0);
+            const uint32_t np = (uint32_t)part_e.size(), per = (n + np - 1) / np;
+            const std::function<void(uint32_t)> cnt_job = [&](uint32_t t) {
+                uint64_t ce = 0, ct = 0;
+                for (uint32_t j = t * per, e = std::min(n, j + per); j < e; ++j)
+                    if (!(hc[j] & kSpanBad)) {
+                        ce += (hc[j] & ~(kSpanBad | kSpanEq)) + 1;
+                        ct += (hl[j] + kGatherTile - 1) / kGatherTile;
+                    }
+                part_e[t] = ce;
+                part_t[t] = ct;
+            };
+            if (np > 1) WorkerPool::get().run(np, cnt_job);
+            else cnt_job(0);
+            for (uint32_t t = 0; t < np; ++t) nents += part_e[t], ntiles += part_t[t];
+        }
         if (nents) {
             // entries, then every record's tile index (4 B per kGatherTile output bytes); the
             // host's running offsets are the device scans' (same counts, same order)
@@ -1334,20 +1352,29 @@ struct px_ctx {
                                     pl, dfirst));
             // every record's entry and tile offsets (the device scans' running sums), the
             // chunks' view tables sized, then the views filled on host threads
-            std::vector<uint64_t> eo(n + 1, 0), tofs(n + 1, 0);
-            uint64_t used = 0;
-            for (uint32_t j = 0; j < n; ++j) {
-                const bool has = !(hc[j] & kSpanBad);
-                const uint32_t ns = hc[j] & ~(kSpanBad | kSpanEq);
-                eo[j + 1] = eo[j] + (has ? ns + 1 : 0);
-                tofs[j + 1] = tofs[j] + (has ? (hl[j] + kGatherTile - 1) / kGatherTile : 0);
-                used += has && !skip[j] ? ns + 1 : 0;
-            }
-            for (uint32_t j = 0; j < n; ++j)  // (the requests come in chunk order: one check per chunk)
-                if (j == 0 || reqs[j].chunk != reqs[j - 1].chunk) {
-                    Chunk &ch = chunks[reqs[j].chunk];
+            std::vector<uint64_t> eo(n + 1), tofs(n + 1);
+            pxh::parallel_prefix(n, pthr, eo.data(), [&](uint32_t j) -> uint64_t {
+                return (hc[j] & kSpanBad) ? 0u : (hc[j] & ~(kSpanBad | kSpanEq)) + 1u;
+            });
+            pxh::parallel_prefix(n, pthr, tofs.data(), [&](uint32_t j) -> uint64_t {
+                return (hc[j] & kSpanBad) ? 0u : (hl[j] + kGatherTile - 1) / kGatherTile;
+            });
+            uint64_t used = eo[n];
+            for (uint32_t j = 0; j < n; ++j)
+                if (skip[j]) used -= eo[j + 1] - eo[j];
+            {
+                // (the requests come in chunk order: one check per chunk; the chunks' view tables
+                // sized on host threads -- value-initialising a new chunk's table is page faults)
+                std::vector<uint32_t> cs;
+                for (uint32_t j = 0; j < n; ++j)
+                    if (j == 0 || reqs[j].chunk != reqs[j - 1].chunk) cs.push_back(reqs[j].chunk);
+                const std::function<void(uint32_t)> rs = [&](uint32_t i) {
+                    Chunk &ch = chunks[cs[i]];
                     if (ch.span.size() < ch.n) ch.span.resize(ch.n);
-                }
+                };
+                if (cs.size() > 4 && n >= 65536) WorkerPool::get().run((uint32_t)cs.size(), rs);
+                else for (uint32_t i = 0; i < (uint32_t)cs.size(); ++i) rs(i);
+            }
             stats.span_entries += used;
             parallel_ranges(n, pthr, [&](uint32_t lo, uint32_t hi) {
                 for (uint32_t j = lo; j < hi; ++j) {
@@ -1650,6 +1677,15 @@ struct px_ctx {
     // kp table; a prefix that overran `cap` is decoded again with the whole doc's room.
     // st[i] = kOk or the decode's failure status.
     std::vector<DecodeQuery> kp_queries;
+    // set_batch's key-map work, kept across batches: each live key's hash, each partition's records
+    std::vector<uint64_t> khash;
+    struct KEnt {
+        uint64_t h;
+        const uint8_t *k;
+        uint32_t klen, r, shard, chunk, idx;
+    };
+    std::vector<KEnt> kents;                          // every partition's entries, partitions in order
+    std::array<uint64_t, PartKeyMap::kParts + 1> pstart{};  // partition pi: kents[pstart[pi], pstart[pi + 1])
     void decode_key_prefixes(const std::vector<KpJob> &jobs, std::vector<uint32_t> &st) {
         PhaseClock phase("decode_key_prefixes", "PX_SET_VERBOSE");
         phase.mark("queries");
@@ -1660,8 +1696,9 @@ struct px_ctx {
         std::vector<DecodeQuery> &q = kp_queries;
         q.resize(nj);
         std::vector<uint32_t> qj(nj);
-        std::vector<uint64_t> qoff(nj + 1, 0);
-        for (uint32_t i = 0; i < nj; ++i) qoff[i + 1] = qoff[i] + round_up(jobs[i].cap, 16);
+        std::vector<uint64_t> qoff(nj + 1);
+        pxh::parallel_prefix(nj, nj >= 65536 ? host_threads() : 1, qoff.data(),
+                             [&](uint32_t i) -> uint64_t { return round_up(jobs[i].cap, 16); });
         parallel_ranges(nj, nj >= 65536 ? host_threads() : 1, [&](uint32_t lo, uint32_t hi) {
             for (uint32_t i = lo; i < hi; ++i) {
                 q[i] = DecodeQuery{jobs[i].chunk, jobs[i].idx, 0, kMaxDoc, qoff[i], jobs[i].cap, 0};
@@ -1688,20 +1725,25 @@ struct px_ctx {
             // the first pass's overruns go again with room; everything else is appended to
             // its chunk's prefix store, chunks in parallel (a chunk's queries are contiguous)
             std::vector<uint8_t> redo(q.size(), 0);
-            for (size_t i = 0; i < q.size(); ++i) {
-                if (qs[i] != kOk && qs[i] != kErrSpace) {
-                    st[qj[i]] = qs[i];
-                    redo[i] = 2;
-                    continue;
+            // (failures and overruns marked on host threads; the few overruns collected in order)
+            parallel_ranges((uint32_t)q.size(), q.size() >= 65536 ? host_threads() : 1, [&](uint32_t lo, uint32_t hi) {
+                for (uint32_t i = lo; i < hi; ++i) {
+                    if (qs[i] != kOk && qs[i] != kErrSpace) {
+                        st[qj[i]] = qs[i];
+                        redo[i] = 2;
+                    } else if (pass == 0 && qs[i] == kErrSpace && key_end(hk + q[i].out_off, ql[i]) == 0) {
+                        redo[i] = 1;
+                    }
                 }
-                if (pass == 0 && qs[i] == kErrSpace && key_end(hk + q[i].out_off, ql[i]) == 0) {
+            });
+            for (size_t i = 0; i < q.size(); ++i) {
+                if (redo[i] == 1) {
                     DecodeQuery d = q[i];
                     d.out_off = ao;
                     d.out_cap = jobs[qj[i]].doc_len + 256;
                     ao += round_up(d.out_cap, 16);
                     again.push_back(d);
                     again_j.push_back(qj[i]);
-                    redo[i] = 1;
                 }
             }
             std::vector<uint32_t> runs;  // [runs[k], runs[k+1]): one chunk's queries
@@ -2274,12 +2316,10 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     hcheck(hipEventRecord(ev_mid, stream));
     // the encoder's record tokens (k_tok_segs builds the segment index from them): room for
     // doc_len / 7 + 2 per record (a token stands for a run of 7 or more doc bytes)
-    uint64_t tok_n = 0;
-    std::vector<uint64_t> tok_off(n);
-    for (uint32_t r = 0; r < n; ++r) {
-        tok_off[r] = tok_n;
-        tok_n += doc_len[r] == 0xffffffffu ? 0 : doc_len[r] / 7 + 2;
-    }
+    std::vector<uint64_t> tok_off(n + 1);
+    pxh::parallel_prefix(n, n >= 65536 ? host_threads() : 1, tok_off.data(),
+                         [&](uint32_t r) -> uint64_t { return doc_len[r] == 0xffffffffu ? 0 : doc_len[r] / 7 + 2; });
+    const uint64_t tok_n = tok_off[n];
     auto *d_toks = (TokEnt *)heap.alloc(tok_n * sizeof(TokEnt) + 64);
     auto *d_tokoff = (uint64_t *)heap.alloc((uint64_t)n * 12 + 64);
     auto *d_ntok = (uint32_t *)(d_tokoff + n);
@@ -2358,6 +2398,24 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     std::vector<uint32_t> scap(n);
     const char *tsh = std::getenv("PX_DEBUG_TOKSEGS");
     const bool toksegs_check = tsh && tsh[0] == '1';
+    if (n >= 65536) {  // (a million records: the four prefix sums on host threads)
+        const uint32_t th = host_threads();
+        parallel_ranges(n, th, [&](uint32_t lo, uint32_t hi) {
+            for (uint32_t r = lo; r < hi; ++r) {
+                const bool ok = placed[r], parsed = !ok || (ntok[r] & kTokBad);
+                scap[r] = (uint32_t)(parsed ? (ok ? seg_entries(nesc[r]) : 1)
+                                            : std::min<uint64_t>(seg_entries(nesc[r]), 2ull * ntok[r] + 2));
+            }
+        });
+        pxh::parallel_prefix(n, th, coff.data(), [&](uint32_t r) -> uint64_t { return placed[r] ? round_up(comp_len[r], 8) : 0; });
+        pxh::parallel_prefix(n, th, soff.data(), [&](uint32_t r) -> uint64_t {
+            const bool parsed = !placed[r] || (ntok[r] & kTokBad);
+            return (parsed || toksegs_check ? scap[r] : 0) * sizeof(SegEnt);
+        });
+        pxh::parallel_prefix(n, th, loff.data(), [&](uint32_t r) -> uint64_t { return (uint64_t)scap[r] * sizeof(LaneEnt); });
+        pxh::parallel_prefix(n, th, poff.data(),
+                             [&](uint32_t r) -> uint64_t { return placed[r] ? round_up(pidx_blocks(doc_len[r]) * 2, 16) : 0; });
+    } else
     for (uint32_t r = 0; r < n; ++r) {
         bool ok = placed[r];
         coff[r + 1] = coff[r] + (ok ? round_up(comp_len[r], 8) : 0);
@@ -2395,7 +2453,9 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     auto *d_coff = (uint64_t *)heap.alloc((uint64_t)n * 8);
     h2d(d_coff, coff.data(), (size_t)n * 8);
     hcheck(launch_compact(stream, n, d_cdst, d_complen, store, d_coff));
-    std::vector<RecSlot> slots(n);
+    // (the batch's slot entries in pinned memory kept across batches: copied to the device
+    // straight from here, not through the bulk ring's staging copy -- 48 MB for a million records)
+    auto *slots = static_cast<RecSlot *>(slot_pin.get((uint64_t)n * sizeof(RecSlot)));
     const uint32_t pthr = n >= 65536 ? host_threads() : 1;  // (per-record host loops of big batches)
     parallel_ranges(n, pthr, [&](uint32_t lo, uint32_t hi) {
     for (uint32_t r = lo; r < hi; ++r) {
@@ -2411,7 +2471,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     }
     });
     auto *d_slots = (RecSlot *)heap.alloc((uint64_t)n * sizeof(RecSlot));
-    h2d(d_slots, slots.data(), (size_t)n * sizeof(RecSlot));
+    hcheck(hipMemcpyAsync(d_slots, slots, (size_t)n * sizeof(RecSlot), hipMemcpyHostToDevice, stream));
     std::vector<uint32_t> tstat(n);
     // segment index: from the encoder's tokens, then by parsing the bytes for the records that
     // could not be (k_tok_segs flags them)
@@ -2639,21 +2699,17 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         for (uint32_t r = 0; r < n; ++r)
             if (live[r]) dk_r.push_back(r);
         const uint32_t m = (uint32_t)dk_r.size();
-        std::vector<uint64_t> kbo(m + 1, 0);
-        for (uint32_t j = 0; j < m; ++j) {
-            const uint32_t r = dk_r[j];
-            kbo[j + 1] = kbo[j] + (hkoff[r + 1] - hkoff[r]);
-        }
+        std::vector<uint64_t> kbo(m + 1);
+        pxh::parallel_prefix(m, m >= 65536 ? host_threads() : 1, kbo.data(),
+                             [&](uint32_t j) -> uint64_t { return hkoff[dk_r[j] + 1] - hkoff[dk_r[j]]; });
         for (const Work &w : work)  // (every chunk's id table sized before the threads)
             for (uint32_t c : w.s->chunks) {
                 Chunk &ch = chunks[c];
                 if (ch.gid.size() < ch.n) ch.gid.resize(ch.n, kNone);
             }
-        if (dk_rec_buf.size() < m) dk_rec_buf.resize(m);
-        if (dk_key_buf.size() < kbo[m]) dk_key_buf.resize(kbo[m]);
-        dk_new = dk_rec_buf.data();
+        dk_new = static_cast<DkRec *>(dk_rec_pin.get((uint64_t)m * sizeof(DkRec) + 64));
         dk_m = m;
-        dk_kb = dk_key_buf.data();
+        dk_kb = static_cast<uint8_t *>(dk_key_pin.get(kbo[m] + 64));
         dk_kbn = kbo[m];
         const uint32_t gid0 = dki.nrec;
         dki.nrec += m;
@@ -2710,7 +2766,6 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     std::function<void(uint32_t)> keymap_job;
     std::vector<std::vector<std::pair<uint32_t, uint32_t>>> mv;
     std::vector<std::string> rawk;
-    std::vector<uint8_t> part;  // (key-map partition of each record; outlives the block: keymap_job reads it)
     if (opts.records_per_shard != 0) {
         // key -> shard upserts, one key-map partition per task (keys in record order); the
         // map holds raw keys: a ready doc's is its key prefix unescaped
@@ -2735,25 +2790,68 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             *len = hkoff[r + 1] - hkoff[r];
             return hkeys.data() + hkoff[r];
         };
-        part.resize(n);
-        parallel_ranges(n, n >= 65536 ? host_threads() : 1, [&](uint32_t lo, uint32_t hi) {
-            for (uint32_t r = lo; r < hi; ++r)
+        // every live key's hash (its partition is the top 4 bits), then each partition's
+        // records in order as packed entries (hash, key, destination), so a task reads its
+        // list sequentially and prefetches the slot and key bytes a few entries ahead (the
+        // strided reads of per-record arrays, not the probes, were most of ~190 ns a key).
+        // Both passes on host threads: per range of records, counts per partition, then the
+        // entries scattered to (partition, range) offsets -- record order within a partition.
+        constexpr uint32_t kRanges = 64;
+        const uint32_t per = (n + kRanges - 1) / kRanges;
+        std::vector<uint32_t> rcnt((size_t)kRanges * PartKeyMap::kParts, 0);
+        khash.resize(n);
+        const bool par = n >= 65536;
+        const std::function<void(uint32_t)> count_job = [&](uint32_t t) {
+            uint32_t *c = rcnt.data() + (size_t)t * PartKeyMap::kParts;
+            for (uint32_t r = t * per, e = std::min(n, r + per); r < e; ++r)
                 if (live[r]) {
                     uint64_t kl;
                     const uint8_t *kp = raw_key(r, &kl);
-                    part[r] = (uint8_t)PartKeyMap::part_of(kp, kl);
+                    khash[r] = KeyMap::hash(kp, kl);
+                    ++c[khash[r] >> 60];
                 }
-        });
+        };
+        if (par) WorkerPool::get().run(kRanges, count_job);
+        else for (uint32_t t = 0; t < kRanges; ++t) count_job(t);
+        std::vector<uint64_t> roff((size_t)kRanges * PartKeyMap::kParts);  // (range, part) -> first entry
+        uint64_t at = 0;
+        for (uint32_t pi = 0; pi < PartKeyMap::kParts; ++pi) {
+            pstart[pi] = at;
+            for (uint32_t t = 0; t < kRanges; ++t) {
+                roff[(size_t)t * PartKeyMap::kParts + pi] = at;
+                at += rcnt[(size_t)t * PartKeyMap::kParts + pi];
+            }
+        }
+        pstart[PartKeyMap::kParts] = at;
+        if (kents.size() < at) kents.resize(at);
+        const std::function<void(uint32_t)> fill_job = [&](uint32_t t) {
+            uint64_t *o = roff.data() + (size_t)t * PartKeyMap::kParts;
+            for (uint32_t r = t * per, e = std::min(n, r + per); r < e; ++r)
+                if (live[r]) {
+                    uint64_t kl;
+                    const uint8_t *kp = raw_key(r, &kl);
+                    kents[o[khash[r] >> 60]++] = KEnt{khash[r], kp, (uint32_t)kl, r, rec_shard[r], rgchunk[r], ridx[r]};
+                }
+        };
+        if (par) WorkerPool::get().run(kRanges, fill_job);
+        else for (uint32_t t = 0; t < kRanges; ++t) fill_job(t);
         mv.resize(PartKeyMap::kParts);
-        keymap_job = [&, raw_key](uint32_t pi) {
+        keymap_job = [&](uint32_t pi) {
             KeyMap &m = keymap.part(pi);
-            m.reserve(n / PartKeyMap::kParts + 64);
-            for (uint32_t r = 0; r < n; ++r) {
-                if (!live[r] || part[r] != pi) continue;
-                uint64_t klen;
-                const uint8_t *kp = raw_key(r, &klen);
-                const int64_t prev = m.upsert(kp, klen, rec_shard[r], rgchunk[r], ridx[r]);
-                if (prev >= 0 && (uint32_t)prev != rec_shard[r]) mv[pi].emplace_back(r, (uint32_t)prev);
+            const KEnt *E = kents.data() + pstart[pi];
+            const size_t ne = pstart[pi + 1] - pstart[pi];
+            uint64_t kb = 0;
+            for (size_t j = 0; j < ne; ++j) kb += E[j].klen;
+            m.reserve(ne, kb);
+            constexpr size_t kAhead = 8;
+            for (size_t j = 0; j < ne; ++j) {
+                if (j + kAhead < ne) {
+                    __builtin_prefetch(m.probe_addr(E[j + kAhead].h));
+                    __builtin_prefetch(E[j + kAhead].k);
+                }
+                const KEnt &e = E[j];
+                const int64_t prev = m.upsert_h(e.h, e.k, e.klen, e.shard, e.chunk, e.idx);
+                if (prev >= 0 && (uint32_t)prev != e.shard) mv[pi].emplace_back(e.r, (uint32_t)prev);
             }
         };
     }
@@ -3227,8 +3325,9 @@ void px_ctx::dki_commit(uint32_t gid0, const DkRec *recs, uint32_t nn, const uin
         dki.keys = nk;
         dki.keys_cap = cap;
     }
-    h2d(dki.rec + gid0, recs, (size_t)nn * sizeof(DkRec));
-    if (kbn) h2d(dki.keys + dki.keys_len, kb, kbn);
+    // (recs / kb are pinned and stay untouched until the batch's closing stream sync)
+    hcheck(hipMemcpyAsync(dki.rec + gid0, recs, (size_t)nn * sizeof(DkRec), hipMemcpyHostToDevice, stream));
+    if (kbn) hcheck(hipMemcpyAsync(dki.keys + dki.keys_len, kb, kbn, hipMemcpyHostToDevice, stream));
     dki.keys_len += kbn;
     uint32_t first = gid0, count = nn;
     if ((uint64_t)dki.nrec * 2 > dki.tab_cap) {  // a new table: every record again (newest id wins)

@@ -630,6 +630,8 @@ hipError_t seg_sort_pairs(hipStream_t s, const SortAlloc &A, uint32_t nseg, uint
     k_seg_tfill<<<(nt + 255) / 256, 256, 0, s>>>(nt, nseg, d_start, d_len, d_pre, d_tiles);
     // (a small sort -- the big groups of a single-instance round -- spreads its tiles thin:
     // 16 tiles per workgroup left ~30 workgroups, each walking 64 K elements alone)
+    // (fewer, longer histogram workgroups for one-segment sorts -- to spare the flush atomics --
+    // measured slower: a single-instance round's first sort 61 -> 195 us, r06w)
     const uint32_t tpw = std::max<uint32_t>(1, std::min<uint32_t>(kHistTiles, (nt + kHistGroups - 1) / kHistGroups));
     const uint32_t hb = (nt + tpw - 1) / tpw;
     // every pass's output pair (px_route.h: no pass writes a buffer it reads, for any pass count)
