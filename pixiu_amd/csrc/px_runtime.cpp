@@ -414,7 +414,8 @@ struct px_ctx {
     HostBuf hq_buf, hres_buf;  // pinned: decode queries up, lengths + statuses down
     HostBuf hg_buf[2];         // pinned: gather queries up (a head and a tail launch)
     HostBuf psa_pin;
-    HostBuf slot_pin;          // pinned: set_batch's slot entries on their way to the device           // pinned: px_psa.hip's count read-backs
+    HostBuf slot_pin;          // pinned: set_batch's slot entries on their way to the device
+    HostBuf dst_pin;           // pinned: set_batch's doc and comp-scratch destinations           // pinned: px_psa.hip's count read-backs
     HostBuf kp_hbuf;           // pinned: decoded key prefixes down
     DevBuf sink_buf;           // k_gst_encode's message sink for replayed docs
     PsaStats psa_stats{};      // the last set batch's suffix-array pass
@@ -1091,11 +1092,13 @@ struct px_ctx {
             for (uint32_t i = 0; i < nq; ++i) perm[i] = i;
             std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) { return q[a].chunk < q[b].chunk; });
         }
-        for (uint32_t j = 0; j < nq; ++j) {
-            const DecodeQuery &src = q[perm.empty() ? j : perm[j]];
-            qn[j] = src;
-            qn[j].nrec = src.chunk == kNone ? 0 : chunks[src.chunk].n;
-        }
+        parallel_ranges(nq, nq >= 65536 ? host_threads() : 1, [&](uint32_t lo, uint32_t hi) {
+            for (uint32_t j = lo; j < hi; ++j) {
+                const DecodeQuery &src = q[perm.empty() ? j : perm[j]];
+                qn[j] = src;
+                qn[j].nrec = src.chunk == kNone ? 0 : chunks[src.chunk].n;
+            }
+        });
         std::vector<GatherQuery> gq;
         if (timed) gq = take_gathers(qn, 0, nq, 0);
         stats.last_gather_queries = timed ? (uint32_t)gq.size() : stats.last_gather_queries;
@@ -2028,7 +2031,8 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
 
     phase.mark("arenas, doc destinations, comp scratch");
     // ---- arenas, doc destinations, comp scratch
-    std::vector<uint8_t *> dst(n, nullptr), cdst(n, nullptr);
+    // (both tables in pinned memory kept across batches, copied to the device from there)
+    auto **dst = static_cast<uint8_t **>(dst_pin.get((uint64_t)n * 16 + 64)), **cdst = dst + n;
     uint64_t scratch_bytes = 0;
     for (uint32_t r = 0; r < n; ++r)
         if (doc_len[r] != 0xffffffffu) scratch_bytes += round_up(doc_len[r], 16);
@@ -2043,7 +2047,10 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         else shard_reserve(*w.s, w.bytes, w.docs);
         uint64_t t = w.s->text_end;
         for (uint32_t r = w.r0; r < w.r1; ++r) {
-            if (doc_len[r] == 0xffffffffu) continue;
+            if (doc_len[r] == 0xffffffffu) {
+                dst[r] = cdst[r] = nullptr;
+                continue;
+            }
             dst[r] = w.s->text + t;
             t += doc_len[r];
             cdst[r] = comp_scratch + so;
@@ -2053,8 +2060,8 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     }
     auto *d_dst = (uint8_t **)heap.alloc((uint64_t)n * 8);
     auto *d_cdst = (uint8_t **)heap.alloc((uint64_t)n * 8);
-    h2d(d_dst, dst.data(), (size_t)n * 8);
-    h2d(d_cdst, cdst.data(), (size_t)n * 8);
+    hcheck(hipMemcpyAsync(d_dst, dst, (size_t)n * 8, hipMemcpyHostToDevice, stream));
+    hcheck(hipMemcpyAsync(d_cdst, cdst, (size_t)n * 8, hipMemcpyHostToDevice, stream));
     flush_shard_init();
     hcheck(launch_doc_write(stream, n, dkeys, dkoff, raw_docs ? nullptr : dvals, dvoff, d_dst));
 
@@ -2551,6 +2558,18 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         const Work &w = work[k];
         Shard &s = *w.s;
         RegAcc &a = racc[k];
+        if (!s.chunks.empty()) {  // (the live chunk's tables grown once, not by doubling)
+            Chunk &lc = chunks[s.chunks.back()];
+            const size_t want = lc.n + (w.r1 - w.r0);
+            auto grow = [want](auto &v) {  // (geometric: batches of one record stay amortised)
+                if (v.capacity() < want) v.reserve(std::max(want, v.capacity() * 2));
+            };
+            grow(lc.slots);
+            grow(lc.doc_len);
+            grow(lc.dead);
+            grow(lc.kp_off);
+            grow(lc.kp_len);
+        }
         for (uint32_t r = w.r0; r < w.r1; ++r) {
             if (doc_len[r] == 0xffffffffu) rstatus[r] = kErrInval;
             if (!placed[r]) continue;
@@ -2659,19 +2678,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             }
     }
 
-    phase.mark("span tables of the new records (full-ran");
-    // ---- span tables of the new records (full-range getitem as a gather)
-    {
-        std::vector<SpanReq> reqs;
-        reqs.reserve(n);
-        for (uint32_t r = 0; r < n; ++r)
-            if (live[r]) reqs.push_back(SpanReq{rgchunk[r], ridx[r], dst[r]});
-        const auto ts = std::chrono::steady_clock::now();
-        build_spans(reqs);
-        stats.last_span_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts).count();
-    }
-
-    phase.mark("device key index entries");
+    phase.mark("device key index ids");
     // ---- device key index: ids for this batch's live records, in record order (before the
     // CritBit inserts, whose replaces kill ids -- older ones and this batch's own)
     const bool dk = dki_enabled() && dki.valid && !raw_docs;
@@ -2690,6 +2697,7 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     DkRec *dk_new = nullptr;
     uint32_t dk_m = 0;
     std::vector<uint32_t> dk_r;  // the batch record of each entry
+    std::vector<uint64_t> dk_kbo;  // its key bytes' place
     uint8_t *dk_kb = nullptr;
     uint64_t dk_kbn = 0;
     if (dk) {
@@ -2699,67 +2707,44 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         for (uint32_t r = 0; r < n; ++r)
             if (live[r]) dk_r.push_back(r);
         const uint32_t m = (uint32_t)dk_r.size();
-        std::vector<uint64_t> kbo(m + 1);
+        std::vector<uint64_t> &kbo = dk_kbo;
+        kbo.resize(m + 1);
         pxh::parallel_prefix(m, m >= 65536 ? host_threads() : 1, kbo.data(),
                              [&](uint32_t j) -> uint64_t { return hkoff[dk_r[j] + 1] - hkoff[dk_r[j]]; });
-        for (const Work &w : work)  // (every chunk's id table sized before the threads)
-            for (uint32_t c : w.s->chunks) {
-                Chunk &ch = chunks[c];
-                if (ch.gid.size() < ch.n) ch.gid.resize(ch.n, kNone);
-            }
+        {  // (every chunk's id table sized before the threads; new tables on host threads)
+            std::vector<uint32_t> cs;
+            for (const Work &w : work)
+                for (uint32_t c : w.s->chunks)
+                    if (chunks[c].gid.size() < chunks[c].n) cs.push_back(c);
+            const std::function<void(uint32_t)> rs = [&](uint32_t i) { chunks[cs[i]].gid.resize(chunks[cs[i]].n, kNone); };
+            if (cs.size() > 4 && n >= 65536) WorkerPool::get().run((uint32_t)cs.size(), rs);
+            else for (uint32_t i = 0; i < (uint32_t)cs.size(); ++i) rs(i);
+        }
         dk_new = static_cast<DkRec *>(dk_rec_pin.get((uint64_t)m * sizeof(DkRec) + 64));
         dk_m = m;
         dk_kb = static_cast<uint8_t *>(dk_key_pin.get(kbo[m] + 64));
         dk_kbn = kbo[m];
         const uint32_t gid0 = dki.nrec;
         dki.nrec += m;
+        // ids now (the CritBit inserts below kill this batch's own replaced records by id)
         parallel_ranges(m, m >= 4096 ? host_threads() : 1, [&](uint32_t lo, uint32_t hi) {
-        std::string q;
-        for (uint32_t j = lo; j < hi; ++j) {
-            const uint32_t r = dk_r[j];
-            Chunk &ch = chunks[rgchunk[r]];
-            const uint32_t i = ridx[r];
-            ch.gid[i] = gid0 + j;
-            const uint8_t *k = hkeys.data() + hkoff[r];
-            const uint64_t kl = hkoff[r + 1] - hkoff[r];
-            DkRec d{};
-            d.key_off = dki.keys_len + kbo[j];
-            d.key_len = (uint32_t)kl;
-            if (kl) std::memcpy(dk_kb + kbo[j], k, kl);
-            if (i < ch.span.size() && ch.span[i].p) {
-                const Chunk::Span &sp = ch.span[i];
-                d.sp = sp.p;
-                d.t = sp.t;
-                d.n = sp.n;
-                d.len = sp.len;
-                if (sp.eq) {
-                    d.xsp = sp.p;
-                    d.xt = sp.t;
-                    d.xn = sp.n;
-                    d.xlen = sp.len;
-                } else {
-                    d.xsp = sp.xp;
-                    d.xt = sp.xt;
-                    d.xn = sp.xn;
-                    d.xlen = sp.xlen;
-                }
-            }
-            d.comp = ch.slots[i].comp;
-            d.doc_len = ch.doc_len[i];
-            esc_key_into(q, k, kl);
-            const bool clean = kp_matches(Leaf{rgchunk[r], i}, q);
-            d.flags = kDkLive | (clean ? kDkClean : 0u);  // (and in its trie: settled after the inserts)
-            dk_new[j] = d;
-        }
+            for (uint32_t j = lo; j < hi; ++j) chunks[rgchunk[dk_r[j]]].gid[ridx[dk_r[j]]] = gid0 + j;
         });
     }
 
-    phase.mark("CritBit inserts: every shard's own recor");
+    phase.mark("span tables + CritBit inserts (concurrent)");
+    // The CritBit inserts (host) run on a thread of their own while this one builds the span
+    // tables (GPU decode, host sizing) and fills the index entries: neither reads what the
+    // other writes (tries, dead marks and the key map there; span views and index entries
+    // here), and their host-thread pool runs take turns.
+    std::vector<uint32_t> replaced(n, 0);
+    std::exception_ptr cb_err;
+    std::thread cb_thread([&] {
+        try {
     // ---- CritBit inserts: every shard's own records in arrival order, shards on host
     // threads (their tries are independent); then a key that moved to a newer shard is
     // deleted from its older one, in record order (a shard's records all precede a newer
     // shard's, so this is the order the sequential loop would have used)
-    std::vector<uint32_t> replaced(n, 0);
     std::vector<std::pair<uint32_t, uint32_t>> moved;  // (record, older shard)
     // the key -> shard map's partitions (multi-shard stores) and the shards' tries are
     // independent: one pool run takes both (partitions first: the longer tasks)
@@ -2899,6 +2884,73 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
         cbt_delete(*shards[mv.second], crit_key(hkeys.data() + hkoff[r], hkoff[r + 1] - hkoff[r]));
         replaced[r] = 1;
     }
+
+        } catch (...) {
+            cb_err = std::current_exception();
+        }
+    });
+    struct JoinGuard {  // (a throw on this thread still joins the inserts before unwinding)
+        std::thread &t;
+        ~JoinGuard() {
+            if (t.joinable()) t.join();
+        }
+    } cb_guard{cb_thread};
+    phase.mark("span tables of the new records (full-ran");
+    // ---- span tables of the new records (full-range getitem as a gather)
+    {
+        std::vector<SpanReq> reqs;
+        reqs.reserve(n);
+        for (uint32_t r = 0; r < n; ++r)
+            if (live[r]) reqs.push_back(SpanReq{rgchunk[r], ridx[r], dst[r]});
+        const auto ts = std::chrono::steady_clock::now();
+        build_spans(reqs);
+        stats.last_span_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts).count();
+    }
+
+    if (dk) {  // the entries (span views, key bytes, clean flags) once the span tables exist
+        const uint32_t m = dk_m;
+        parallel_ranges(m, m >= 4096 ? host_threads() : 1, [&](uint32_t lo, uint32_t hi) {
+        std::string q;
+        for (uint32_t j = lo; j < hi; ++j) {
+            const uint32_t r = dk_r[j];
+            Chunk &ch = chunks[rgchunk[r]];
+            const uint32_t i = ridx[r];
+            const uint8_t *k = hkeys.data() + hkoff[r];
+            const uint64_t kl = hkoff[r + 1] - hkoff[r];
+            DkRec d{};
+            d.key_off = dki.keys_len + dk_kbo[j];
+            d.key_len = (uint32_t)kl;
+            if (kl) std::memcpy(dk_kb + dk_kbo[j], k, kl);
+            if (i < ch.span.size() && ch.span[i].p) {
+                const Chunk::Span &sp = ch.span[i];
+                d.sp = sp.p;
+                d.t = sp.t;
+                d.n = sp.n;
+                d.len = sp.len;
+                if (sp.eq) {
+                    d.xsp = sp.p;
+                    d.xt = sp.t;
+                    d.xn = sp.n;
+                    d.xlen = sp.len;
+                } else {
+                    d.xsp = sp.xp;
+                    d.xt = sp.xt;
+                    d.xn = sp.xn;
+                    d.xlen = sp.xlen;
+                }
+            }
+            d.comp = ch.slots[i].comp;
+            d.doc_len = ch.doc_len[i];
+            esc_key_into(q, k, kl);
+            const bool clean = kp_matches(Leaf{rgchunk[r], i}, q);
+            d.flags = kDkLive | (clean ? kDkClean : 0u);  // (and in its trie: settled after the inserts)
+            dk_new[j] = d;
+        }
+        });
+    }
+
+    cb_thread.join();
+    if (cb_err) std::rethrow_exception(cb_err);
 
     phase.mark("device key index");
     // a record the reference's CritBit skipped is answered by no walk: not by the index
