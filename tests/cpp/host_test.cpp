@@ -188,6 +188,19 @@ static void test_keymaps() {
         }
     }
     CHECK(km.size() == ref.size() && pm.size() == ref.size());
+    {  // set_batch's form: one-shot reserve, hash computed by the caller, prefetch address
+        pxh::KeyMap m2;
+        m2.reserve(ref.size(), 24 * ref.size());
+        for (auto &kv : ref) {
+            const auto *kb = (const uint8_t *)kv.first.data();
+            const uint64_t h = pxh::KeyMap::hash(kb, kv.first.size());
+            CHECK(m2.probe_addr(h) != nullptr);
+            CHECK(m2.upsert_h(h, kb, kv.first.size(), kv.second, 1, 2) == -1);
+            CHECK(m2.upsert_h(h, kb, kv.first.size(), kv.second + 1, 1, 2) == (int64_t)kv.second);
+        }
+        CHECK(m2.size() == ref.size());
+        for (auto &kv : ref) CHECK(m2.find((const uint8_t *)kv.first.data(), kv.first.size()) == kv.second + 1);
+    }
     for (auto &kv : ref) {
         CHECK(km.find((const uint8_t *)kv.first.data(), kv.first.size()) == kv.second);
         CHECK(pm.find((const uint8_t *)kv.first.data(), kv.first.size()) == kv.second);
@@ -268,6 +281,14 @@ static void test_parallel_ranges() {
         CHECK(once);
     }
     printf("parallel_ranges: ok\n");
+    for (uint32_t n : {0u, 1u, 65535u, 65536u, 200001u, 1000003u}) {  // parallel_prefix == the serial sum
+        std::vector<uint64_t> a(n + 1), b(n + 1, 0);
+        auto val = [](uint32_t i) -> uint64_t { return (i * 2654435761u) % 1000u; };
+        pxh::parallel_prefix(n, 8, a.data(), val);
+        for (uint32_t i = 0; i < n; ++i) b[i + 1] = b[i] + val(i);
+        CHECK(a == b);
+    }
+    printf("parallel_prefix: ok\n");
 }
 
 // seg_sort_pairs' pass routing (px_route.h): for 1..8 passes and the callers' aliasings, every
