@@ -2436,6 +2436,10 @@ __global__ void __launch_bounds__(64 * kDecWaves) k_decode_addr(const DecodeQuer
 // not the previous one + 1.  Count pass: spans (| kSpanBad for a source out
 // of the relative range, | kSpanEq when the expansion equals the doc, i.e. compat ==
 // exact).  Write pass: {rel, start} entries plus the {0, len} sentinel.
+#ifndef PX_SPAN_STEPS
+#define PX_SPAN_STEPS 8
+#endif
+constexpr uint32_t kSpanSteps = PX_SPAN_STEPS;
 PX_DEV void span_job(const SpanJob &jb) {
     const uint32_t lane = lane_id();
     const PX_GAS uint8_t *base = (const PX_GAS uint8_t *)jb.base;
@@ -2456,18 +2460,18 @@ PX_DEV void span_job(const SpanJob &jb) {
             a += uni64(jb.pq[j].out_off);
             pn = min(uni(jb.pl[j]), len - o);
         }
-        // four 64-byte steps per group: their address loads, then their doc / comp byte loads
-        // for the compat == exact test, each issued together (one wave walks a record: its
-        // dependent loads were the pass's time)
-        for (uint32_t g0 = 0; g0 < pn; g0 += 256) {
-            int32_t raw[4], vv[4];
+        // kSpanSteps 64-byte steps per group: their address loads, then their doc / comp byte
+        // loads for the compat == exact test, each issued together (one wave walks a record:
+        // its dependent loads were the pass's time; 8 steps in flight instead of 4, round 6)
+        for (uint32_t g0 = 0; g0 < pn; g0 += 64u * kSpanSteps) {
+            int32_t raw[kSpanSteps], vv[kSpanSteps];
 #pragma unroll
-            for (uint32_t u = 0; u < 4; ++u) {
+            for (uint32_t u = 0; u < kSpanSteps; ++u) {
                 const uint32_t i = g0 + 64u * u + lane;
                 raw[u] = i < pn ? a[i] : kAddrMark;
             }
 #pragma unroll
-            for (uint32_t u = 0; u < 4; ++u) {
+            for (uint32_t u = 0; u < kSpanSteps; ++u) {
                 const uint32_t i0 = g0 + 64u * u;
                 vv[u] = kAddrNone;
                 if (i0 >= pn) break;  // (wave-uniform)
@@ -2503,9 +2507,9 @@ PX_DEV void span_job(const SpanJob &jb) {
                 prev_last = __shfl(v, (int)(nl - 1));
             }
             if (eq) {
-                uint32_t bb[4], dd[4];
+                uint32_t bb[kSpanSteps], dd[kSpanSteps];
 #pragma unroll
-                for (uint32_t u = 0; u < 4; ++u) {
+                for (uint32_t u = 0; u < kSpanSteps; ++u) {
                     const uint32_t i = g0 + 64u * u + lane;
                     const bool ok = i < pn && vv[u] != kAddrNone;
                     bb[u] = ok ? base[vv[u]] : 0u;
@@ -2513,7 +2517,7 @@ PX_DEV void span_job(const SpanJob &jb) {
                 }
                 bool mis = false;
 #pragma unroll
-                for (uint32_t u = 0; u < 4; ++u) {
+                for (uint32_t u = 0; u < kSpanSteps; ++u) {
                     const uint32_t i = g0 + 64u * u + lane;
                     mis = mis || (i < pn && (vv[u] == kAddrNone || bb[u] != dd[u]));
                 }

@@ -415,7 +415,8 @@ struct px_ctx {
     HostBuf hg_buf[2];         // pinned: gather queries up (a head and a tail launch)
     HostBuf psa_pin;
     HostBuf slot_pin;          // pinned: set_batch's slot entries on their way to the device
-    HostBuf dst_pin;           // pinned: set_batch's doc and comp-scratch destinations           // pinned: px_psa.hip's count read-backs
+    HostBuf dst_pin;           // pinned: set_batch's doc and comp-scratch destinations
+    HostBuf piece_pin;         // pinned: the span build's piece queries           // pinned: px_psa.hip's count read-backs
     HostBuf kp_hbuf;           // pinned: decoded key prefixes down
     DevBuf sink_buf;           // k_gst_encode's message sink for replayed docs
     PsaStats psa_stats{};      // the last set batch's suffix-array pass
@@ -1239,29 +1240,37 @@ struct px_ctx {
         DecodeQuery *sdq = nullptr;
         uint32_t *dfirst = nullptr, *pl = nullptr;
         if (split) {
-            std::vector<DecodeQuery> sq;
+            // every record's pieces: counts, their prefix, then the queries written straight into
+            // pinned memory on host threads (a staged copy of the piece table left the GPU idle
+            // ~2 ms on config 3)
             std::vector<uint32_t> first(n + 1, 0);
             for (uint32_t k = 0; k < n; ++k) {
-                first[k] = (uint32_t)sq.size();
                 const uint32_t L = src[k].doc_len;
-                for (uint32_t a = 0, m = 0; a < L || (a == 0 && L == 0); a += kPiece, ++m) {
-                    const uint32_t b = std::min(L, a + kPiece);
-                    DecodeQuery d = qn[k];
-                    d.from = (int32_t)a;
-                    d.to = (int32_t)b;
-                    if (mode == 1) {
-                        d.out_off = qn[k].out_off + a;
-                        d.out_cap = b - a + 16;  // (exactly b - a bytes come; room past them keeps the cap from firing)
-                    } else {
-                        d.out_off = qn[k].out_off + 64ull * m;  // (k_span_pieces adds the piece's start)
-                        d.pad = L;
-                    }
-                    sq.push_back(d);
-                    if (L == 0) break;
-                }
+                first[k + 1] = first[k] + (L == 0 ? 1u : (L + kPiece - 1) / kPiece);
             }
-            first[n] = (uint32_t)sq.size();
-            const uint32_t ns = (uint32_t)sq.size();
+            auto *sq = static_cast<DecodeQuery *>(piece_pin.get((uint64_t)first[n] * sizeof(DecodeQuery) + 64));
+            parallel_ranges(n, pthr, [&](uint32_t lo, uint32_t hi) {
+                for (uint32_t k = lo; k < hi; ++k) {
+                    const uint32_t L = src[k].doc_len;
+                    DecodeQuery *o = sq + first[k];
+                    for (uint32_t a = 0, m = 0; a < L || (a == 0 && L == 0); a += kPiece, ++m) {
+                        const uint32_t b = std::min(L, a + kPiece);
+                        DecodeQuery d = qn[k];
+                        d.from = (int32_t)a;
+                        d.to = (int32_t)b;
+                        if (mode == 1) {
+                            d.out_off = qn[k].out_off + a;
+                            d.out_cap = b - a + 16;  // (exactly b - a bytes come; room past them keeps the cap from firing)
+                        } else {
+                            d.out_off = qn[k].out_off + 64ull * m;  // (k_span_pieces adds the piece's start)
+                            d.pad = L;
+                        }
+                        o[m] = d;
+                        if (L == 0) break;
+                    }
+                }
+            });
+            const uint32_t ns = first[n];
             const uint64_t o_first = round_up((uint64_t)ns * sizeof(DecodeQuery), 256);
             const uint64_t o_pl = o_first + round_up((uint64_t)(n + 1) * 4, 256);
             sub_bytes = o_pl + (uint64_t)ns * 8 + 256;
@@ -1270,7 +1279,7 @@ struct px_ctx {
             dfirst = (uint32_t *)(sub_buf + o_first);
             pl = (uint32_t *)(sub_buf + o_pl);
             uint32_t *ps = pl + ns;
-            h2d(sdq, sq.data(), (size_t)ns * sizeof(DecodeQuery));
+            hcheck(hipMemcpyAsync(sdq, sq, (size_t)ns * sizeof(DecodeQuery), hipMemcpyHostToDevice, stream));
             h2d(dfirst, first.data(), (size_t)(n + 1) * 4);
             if (mode == 0) hcheck(launch_span_pieces(stream, ns, sdq, ctab, kPiece));
             const uint32_t sw = std::min<uint32_t>(opts.decode_waves ? opts.decode_waves : 16384, ns);
