@@ -386,9 +386,12 @@ def run_config(cfg, a, rank, world, local, steps, warmup, rps, records=None, che
     r_len = torch.empty(n, dtype=torch.int32, device=dev)
     r_sts = torch.empty(n, dtype=torch.int32, device=dev)
 
+    # (the caller's device pointers, taken once: a torch data_ptr() per argument per call was
+    # part of the timed getitem)
+    ptrs = (kb.data_ptr(), ko.data_ptr(), r_off.data_ptr(), r_len.data_ptr(), r_sts.data_ptr())
+
     def get_dev(buf, mode):
-        rc, need = st.get_batch_dev(n, kb.data_ptr(), ko.data_ptr(), buf.data_ptr(), out_cap, r_off.data_ptr(),
-                                    r_len.data_ptr(), r_sts.data_ptr(), mode)
+        rc, need = st.get_batch_dev(n, ptrs[0], ptrs[1], buf.data_ptr(), out_cap, ptrs[2], ptrs[3], ptrs[4], mode)
         return rc, need
 
     def step():

@@ -164,6 +164,8 @@ class Store:
         if not h:
             raise PxError(9, "px_open (no usable HIP device?)")
         self._h = C.c_void_p(h)
+        self._need = np.zeros(1, np.uint64)  # (get_batch_dev's "needed" word, kept: one allocation less per call)
+        self._need_p = _ptr(self._need)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -289,10 +291,9 @@ class Store:
                       len_ptr: int, status_ptr: int, mode: int = COMPAT):
         """getitem with device-resident keys (CSR: bytes + n + 1 u64 offsets) and results (u64
         offsets, u32 lengths, u32 statuses, n each): px_get_batch_dev.  Returns (rc, needed)."""
-        need = np.zeros(1, np.uint64)
         rc = self._lib.px_get_batch_dev(self._h, n, keys_ptr, koff_ptr, mode, out_ptr, out_cap, off_ptr, len_ptr,
-                                        status_ptr, _ptr(need))
-        return rc, int(need[0])
+                                        status_ptr, self._need_p)
+        return rc, int(self._need[0])
 
     def get_batch_host(self, keys, out: np.ndarray, mode: int = COMPAT):
         """Expand into a caller-owned host buffer (one call, no retry); returns

@@ -386,6 +386,25 @@ struct px_ctx {
     px_opts opts{};
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_mid = nullptr;
+    hipEvent_t ev_get = nullptr;  // (a getitem batch's end: polled, not slept on)
+    // wait for the stream by polling an event: a getitem batch's ~0.8 ms of kernels ended in a
+    // blocking synchronize whose wake-up was a visible part of the call (PX_GET_SPIN=0: sleep)
+    void spin_sync() {
+        static const bool spin = [] {
+            const char *e = std::getenv("PX_GET_SPIN");
+            return !(e && e[0] == '0');
+        }();
+        if (!spin) {
+            hcheck(hipStreamSynchronize(stream));
+            return;
+        }
+        hcheck(hipEventRecord(ev_get, stream));
+        for (;;) {
+            const hipError_t q = hipEventQuery(ev_get);
+            if (q == hipSuccess) break;
+            if (q != hipErrorNotReady) hcheck(q);
+        }
+    }
     hipStream_t stream2 = nullptr;  // getitem's second decode launch (get_overlapped)
     hipEvent_t ev_join = nullptr;
     DevHeap heap;
@@ -3477,7 +3496,7 @@ int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int m
     if (dev_io) hcheck(launch_dk_results(stream, n, ctl, cap_fit, oo, dl, ds, out_off, out_len, status));
     hcheck(hipMemcpyAsync(hr, ctl, dev_io ? 32 : o_ds - o_ctl, hipMemcpyDeviceToHost, stream));
     phase.mark("wait for the device");
-    hcheck(hipStreamSynchronize(stream));
+    spin_sync();
     phase.mark("results");
     const uint8_t *res = (const uint8_t *)hr + 32;
     if (hr[3]) {  // an insert gave up: the index is not trusted again until reset
@@ -3874,6 +3893,7 @@ px_ctx *px_open(const px_opts *opts) {
         hcheck(hipEventCreate(&c->ev0));
         hcheck(hipEventCreate(&c->ev1));
         hcheck(hipEventCreate(&c->ev_mid));
+        hcheck(hipEventCreateWithFlags(&c->ev_get, hipEventDisableTiming));
         return c;
     } catch (...) {
         return nullptr;
@@ -3886,6 +3906,7 @@ void px_close(px_ctx *ctx) {
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->ev_mid) (void)hipEventDestroy(ctx->ev_mid);
+    if (ctx->ev_get) (void)hipEventDestroy(ctx->ev_get);
     for (auto &e : ctx->ring_ev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->stream2) {

@@ -213,3 +213,41 @@ def test_device_keys_and_results(store_factory):
     # too little room
     rc, need, *_ = run(keys, 4096)
     assert rc == px.PX_ESPACE and need > 4096
+
+
+def test_big_batch_repeats_across_shards(store_factory, oracle):
+    """A batch past the host-thread threshold (70,000 records, 2,000-record shards) whose keys
+    repeat inside shards and across them, then a second such batch: the key map's partitions,
+    the tries and the index entries take their parallel paths (set_batch runs the CritBit
+    inserts on a helper thread); every key answers with its newest shard's value, as the
+    per-shard oracle says"""
+    import torch
+    rng = np.random.default_rng(20261019)
+    n, rps, space = 70000, 2000, 40000
+    batches = []
+    for _ in range(2):
+        ks = [b"k%06d" % int(x) for x in rng.integers(space, size=n)]
+        vs = [bytes(rng.integers(97, 123, size=int(rng.integers(20, 100))).astype(np.uint8)) for _ in range(n)]
+        batches.append((ks, vs))
+    st = store_factory(records_per_shard=rps)
+    for ks, vs in batches:
+        r = st.set_batch(ks, vs)
+        assert int(r["status"].max()) == 0
+    want = {}
+    for ks, vs in batches:
+        for s0 in range(0, n, rps):
+            sh = oracle.new()
+            for k, v in zip(ks[s0:s0 + rps], vs[s0:s0 + rps]):
+                sh.set(k, v)
+            for k in ks[s0:s0 + rps]:
+                want[k] = sh.get(k)
+    keys = sorted(want)
+    dev = torch.device("cuda", 0)
+    out = torch.empty(16 << 20, dtype=torch.uint8, device=dev)
+    rc, off, ln, sts, _ = st.get_batch_device(keys, out.data_ptr(), out.numel(), px.COMPAT)
+    assert rc == px.PX_OK
+    host = out.cpu().numpy()
+    got = [host[int(o):int(o) + int(m)].tobytes() for o, m in zip(off, ln)]
+    assert got == [want[k] for k in keys]
+    sample = keys[::97]
+    assert st.get_batch(sample) == [want[k] for k in sample]
