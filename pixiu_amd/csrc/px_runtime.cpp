@@ -511,6 +511,7 @@ struct px_ctx {
         uint32_t *err = nullptr;  // device word: an insert gave up (cannot happen)
         std::vector<uint32_t> kills;  // ids killed (replace / delete) since the last commit
         uint32_t miss_streak = 0, skipped = 0;  // getitem batches in a row the index could not answer
+        uint32_t max_len = 0;  // the longest span-table expansion of any entry (bounds a batch's gather grid)
         std::mutex mu;
     } dki;
     static bool dki_enabled() {  // PX_DKI=0: every getitem resolves its keys on the host
@@ -2937,8 +2938,10 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
 
     if (dk) {  // the entries (span views, key bytes, clean flags) once the span tables exist
         const uint32_t m = dk_m;
+        std::atomic<uint32_t> dk_max_len{0};
         parallel_ranges(m, m >= 4096 ? host_threads() : 1, [&](uint32_t lo, uint32_t hi) {
         std::string q;
+        uint32_t lmax = 0;
         for (uint32_t j = lo; j < hi; ++j) {
             const uint32_t r = dk_r[j];
             Chunk &ch = chunks[rgchunk[r]];
@@ -2973,8 +2976,13 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
             const bool clean = kp_matches(Leaf{rgchunk[r], i}, q);
             d.flags = kDkLive | (clean ? kDkClean : 0u);  // (and in its trie: settled after the inserts)
             dk_new[j] = d;
+            lmax = std::max({lmax, (uint32_t)d.len, (uint32_t)d.xlen});
+        }
+        uint32_t cur = dk_max_len.load();
+        while (lmax > cur && !dk_max_len.compare_exchange_weak(cur, lmax)) {
         }
         });
+        dki.max_len = std::max(dki.max_len, dk_max_len.load());
     }
 
     cb_thread.join();
@@ -3450,7 +3458,12 @@ int px_ctx::dki_get(uint32_t n, const uint8_t *keys, const uint64_t *koff, int m
     // (a host buffer: device staging up to 4 GiB; a batch past it goes the host path)
     // (output offsets travel as u32 counts of 16 bytes: below 64 GiB on the device too)
     const uint64_t cap_fit = std::min<uint64_t>(out_cap, out_on_device ? (1ull << 36) - 16 : 4ull << 30);
-    const uint64_t ntask_max = std::min<uint64_t>(cap_fit / 1024 + 2, 0xffffffffull);
+    // (and by the index's longest expansion: a query's tiles are at most max(1, ceil(max_len /
+    // 32)), 64 tiles a task -- a grid sized from the caller's room alone was 4x the batch's real
+    // tasks on config 3, every spare wave dispatched only to exit)
+    const uint64_t tiles_q = std::max<uint64_t>(1, ((uint64_t)dki.max_len + kGatherTile - 1) / kGatherTile);
+    const uint64_t ntask_max =
+        std::min<uint64_t>({cap_fit / 1024 + 2, (uint64_t)n * tiles_q / 64 + 2, 0xffffffffull});
     auto *b = (uint8_t *)dk_qbuf.get(o_task + gather_task_bytes((uint32_t)ntask_max));
     auto *dkeys = dev_io ? const_cast<uint8_t *>(keys) : b;
     auto *doff = dev_io ? const_cast<uint64_t *>(koff) : (uint64_t *)(b + o_off);
