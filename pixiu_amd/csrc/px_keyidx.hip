@@ -185,54 +185,73 @@ __global__ void __launch_bounds__(256) k_dk_lookup(uint32_t nq, const uint8_t *q
         pa += s_wa[v];
         pt += s_wt[v];
     }
-    if (threadIdx.x == 0) {  // ---- look-back over the earlier workgroups
+    if (w == 0) {  // ---- look-back over the earlier workgroups, 64 of them per step (one per lane)
+        // (thread 0 alone walked back one workgroup per dependent device-scope load: the last of
+        // a 10,000-key batch's 40 workgroups waited ~39 round trips -- most of the kernel)
         const unsigned long long ta = s_wa[0] + s_wa[1] + s_wa[2] + s_wa[3], tt = s_wt[0] + s_wt[1] + s_wt[2] + s_wt[3];
         unsigned long long ea = 0, et = 0;
         if (bid == 0) {
-            __hip_atomic_store(chain, kChIncl | ta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(chain + 1, kChIncl | tt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) {
+                __hip_atomic_store(chain, kChIncl | ta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(chain + 1, kChIncl | tt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         } else {
-            __hip_atomic_store(chain + 2ull * bid, kChAgg | ta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(chain + 2ull * bid + 1, kChAgg | tt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            bool da = false, dt = false;
-            uint32_t ja = bid - 1, jt = bid - 1, spins = 0;
-            while (!(da && dt)) {
-                const unsigned long long xa =
-                    da ? 0ull : __hip_atomic_load(chain + 2ull * ja, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const unsigned long long xt =
-                    dt ? 0ull : __hip_atomic_load(chain + 2ull * jt + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) {
+                __hip_atomic_store(chain + 2ull * bid, kChAgg | ta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(chain + 2ull * bid + 1, kChAgg | tt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            // channel c (0: room, 1: tiles): its window's top workgroup, done flag, running sum
+            int64_t top[2] = {(int64_t)bid - 1, (int64_t)bid - 1};
+            bool done[2] = {false, false};
+            unsigned long long sum[2] = {0ull, 0ull};
+            uint32_t spins = 0;
+            while (!(done[0] && done[1])) {
                 bool waited = false;
-                if (!da) {
-                    if (!(xa >> 62)) {
-                        waited = true;
-                    } else {
-                        ea += xa & kChVal;
-                        if ((xa >> 62) == 2) da = true;
-                        else --ja;
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    if (done[c]) continue;  // (wave-uniform)
+                    const int64_t j = top[c] - (int64_t)lane;
+                    const bool valid = j >= 0;
+                    const unsigned long long x =
+                        valid ? __hip_atomic_load(chain + 2ull * (uint64_t)j + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+                    const uint32_t f = (uint32_t)(x >> 62);
+                    const unsigned long long pub = __ballot(valid && f != 0), inc = __ballot(valid && f == 2),
+                                             vm = __ballot(valid);
+                    // lanes [0, L]: up to the nearest inclusive prefix, or the whole window without one
+                    const uint32_t L = inc ? (uint32_t)__ffsll((long long)inc) - 1u : 63u;
+                    const unsigned long long need = (L == 63u ? ~0ull : ((2ull << L) - 1ull)) & vm;
+                    if ((pub & need) != need) {
+                        waited = true;  // (a workgroup in the range has not published yet)
+                        continue;
                     }
-                }
-                if (!dt) {
-                    if (!(xt >> 62)) {
-                        waited = true;
-                    } else {
-                        et += xt & kChVal;
-                        if ((xt >> 62) == 2) dt = true;
-                        else --jt;
+                    unsigned long long v = ((need >> lane) & 1ull) ? (x & kChVal) : 0ull;
+                    for (int o = 32; o >= 1; o >>= 1) {
+                        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o);
+                        v += (unsigned long long)lo | ((unsigned long long)hi << 32);
                     }
+                    sum[c] += v;
+                    if (inc) done[c] = true;
+                    else top[c] -= 64;  // (every valid lane published an aggregate: the next 64)
                 }
                 if (waited && ++spins > kChSpin) {  // (cannot happen; the batch then goes to the host)
-                    atomicAdd(&ctl[0], 1u << 30);
+                    if (lane == 0) atomicAdd(&ctl[0], 1u << 30);
                     break;
                 }
             }
-            __hip_atomic_store(chain + 2ull * bid, kChIncl | (ea + ta), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(chain + 2ull * bid + 1, kChIncl | (et + tt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ea = sum[0];
+            et = sum[1];
+            if (lane == 0) {
+                __hip_atomic_store(chain + 2ull * bid, kChIncl | (ea + ta), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(chain + 2ull * bid + 1, kChIncl | (et + tt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
-        s_pa = ea;
-        s_pt = et;
-        if (bid == gridDim.x - 1) {
-            ctl[1] = (uint32_t)(ea + ta);
-            ctl[2] = (uint32_t)(et + tt);
+        if (lane == 0) {
+            s_pa = ea;
+            s_pt = et;
+            if (bid == gridDim.x - 1) {
+                ctl[1] = (uint32_t)(ea + ta);
+                ctl[2] = (uint32_t)(et + tt);
+            }
         }
     }
     __syncthreads();
