@@ -2675,7 +2675,10 @@ __global__ void __launch_bounds__(256) k_gather_tasks(uint32_t nq, const GatherQ
 // (every lane of a wave that lies in one query), the span entries of that query from the
 // task's first tile on are staged in LDS by two coalesced loads per lane and each lane finds
 // its own span there, and a source load is issued only by the lanes whose span has a piece.
-constexpr uint32_t kGatherStage = 256;
+#ifndef PX_GATHER_STAGE
+#define PX_GATHER_STAGE 256
+#endif
+constexpr uint32_t kGatherStage = PX_GATHER_STAGE;
 PX_DEV void gather_task(uint32_t ti, const GatherTask *task, const GatherQuery *qs, uint32_t nq, uint8_t *out_,
                         uint32_t *out_len, uint32_t *status, uint2 *stage, uint8_t *tl) {
     const uint32_t lane = lane_id();
