@@ -2897,7 +2897,39 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     if (nthr <= 1 || n < 2048) {
         for (uint32_t t = 0; t < nk + (uint32_t)work.size(); ++t) job(t);
     } else {
-        WorkerPool::get().run(nk + (uint32_t)work.size(), job);
+        // threads of its own, not the shared pool: the span build on the calling thread takes
+        // the pool meanwhile (queued behind these tasks it waited ~6 ms for its first loop)
+        static const uint32_t own = [] {
+            const char *e = std::getenv("PX_CBT_THREADS");  // (0: the shared pool)
+            return e ? (uint32_t)std::atoi(e) : 8u;
+        }();
+        const uint32_t nt = std::min<uint32_t>(own, nk + (uint32_t)work.size());
+        if (nt >= 2) {
+            std::atomic<uint32_t> next{0};
+            std::atomic<bool> stop{false};
+            auto run = [&] {
+                for (uint32_t t; !stop.load() && (t = next.fetch_add(1)) < nk + (uint32_t)work.size();) job(t);
+            };
+            std::vector<std::thread> th;
+            th.reserve(nt - 1);
+            std::exception_ptr err;
+            std::mutex err_mu;
+            auto guarded = [&] {
+                try {
+                    run();
+                } catch (...) {
+                    std::lock_guard<std::mutex> g(err_mu);
+                    if (!err) err = std::current_exception();
+                    stop.store(true);  // (the others stop taking tasks)
+                }
+            };
+            for (uint32_t i = 1; i < nt; ++i) th.emplace_back(guarded);
+            guarded();
+            for (auto &x : th) x.join();
+            if (err) std::rethrow_exception(err);
+        } else {
+            WorkerPool::get().run(nk + (uint32_t)work.size(), job);
+        }
     }
     if (phase.on) {
         float km = 0, ks = 0, im = 0, is = 0;
