@@ -1030,13 +1030,28 @@ __global__ void __launch_bounds__(256) k_dbl_blk(const uint64_t *list, const uin
 // the key's top 16 bits and its position is the sorted value, so placing a member back
 // reads nothing scattered (otherwise the value is the gather index and the position and
 // distance come from gp / gd).
+// the shard whose range holds suffix-array index r (shards are contiguous and in order in
+// both position and rank space)
+PSA_DEV uint32_t shard_of_rank(const PsaShard *shards, uint32_t nshards, uint32_t r) {
+    uint32_t a = 0, b = nshards;  // shards[a].base <= r < shards[b].base
+    while (b - a > 1) {
+        const uint32_t c = (a + b) >> 1;
+        if (shards[c].base <= r) a = c;
+        else b = c;
+    }
+    return a;
+}
 // flat over the T gathered members: a block's 256 members span at most two groups (every
 // big group has > 4,096 members), found by one search of boff per block
 template <bool PACKED>
+// Keys are made relative to the group's shard (rank + 1 - the shard's first slot, 0 kept for a
+// complete suffix): the rank h further on lies in the same shard, so the sort needs the bit
+// length of the largest shard (23-24 bits, 3 passes of 8) instead of 32 (4 passes).
 __global__ void __launch_bounds__(256) k_big_gather(uint32_t T, uint32_t nb, const uint64_t *list, const uint32_t *boff,
                                                     const uint32_t *sa, const uint16_t *sd, const uint32_t *key,
-                                                    uint64_t *ck, uint32_t *cv, uint32_t *gp, uint16_t *gd, StepStat ss) {
-    __shared__ uint32_t sb;
+                                                    uint64_t *ck, uint32_t *cv, uint32_t *gp, uint16_t *gd, StepStat ss,
+                                                    const PsaShard *shards, uint32_t nshards) {
+    __shared__ uint32_t sb, sbase[2];
     const uint32_t k0 = blockIdx.x * blockDim.x, k = k0 + threadIdx.x;
     if (threadIdx.x == 0) {  // the group holding k0: last b with boff[b] <= k0
         uint32_t lo = 0, hi = nb;
@@ -1046,18 +1061,22 @@ __global__ void __launch_bounds__(256) k_big_gather(uint32_t T, uint32_t nb, con
             else hi = mid;
         }
         sb = lo;
+        // the shard bases of the (at most two) groups the block's members are in
+        sbase[0] = shards[shard_of_rank(shards, nshards, (uint32_t)list[lo])].base;
+        sbase[1] = lo + 1 < nb ? shards[shard_of_rank(shards, nshards, (uint32_t)list[lo + 1])].base : 0u;
     }
     __syncthreads();
     if (k >= T) return;
-    uint32_t b = sb;
-    if (b + 1 < nb && boff[b + 1] <= k) ++b;
+    uint32_t b = sb, sbi = 0;
+    if (b + 1 < nb && boff[b + 1] <= k) ++b, sbi = 1;
     const uint64_t ent = list[b];
     const uint32_t start = (uint32_t)ent, o = boff[b], i = k - o;
+    const uint32_t kr = key[start + i], rel = kr ? kr - sbase[sbi] : 0u;
     if (PACKED) {
-        ck[k] = (uint64_t)sd[start + i] << 48 | (uint64_t)b << 32 | key[start + i];
+        ck[k] = (uint64_t)sd[start + i] << 48 | (uint64_t)b << 32 | rel;
         cv[k] = sa[start + i];
     } else {
-        ck[k] = (uint64_t)b << 32 | key[start + i];
+        ck[k] = (uint64_t)b << 32 | rel;
         cv[k] = k;
         gp[k] = sa[start + i];
         gd[k] = sd[start + i];
@@ -1222,17 +1241,6 @@ PSA_DEV uint32_t tree_find(const MinTree &t, uint32_t i, uint32_t v, int dir) {
 
 // psv / nsv: for the suffix at rank r, the nearest rank to its left / right (inside its
 // shard's range) whose position is smaller; written per position
-// the shard whose range holds suffix-array index r (shards are contiguous and in order in
-// both position and rank space)
-PSA_DEV uint32_t shard_of_rank(const PsaShard *shards, uint32_t nshards, uint32_t r) {
-    uint32_t a = 0, b = nshards;  // shards[a].base <= r < shards[b].base
-    while (b - a > 1) {
-        const uint32_t c = (a + b) >> 1;
-        if (shards[c].base <= r) a = c;
-        else b = c;
-    }
-    return a;
-}
 
 // Block-level ANSV: one workgroup per kAnsvBlock ranks.  Each wave first resolves its
 // 64-rank sub-blocks by binary lifting; an element with no smaller value on a side
@@ -2318,6 +2326,13 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     // the long-group lists the window kernel filled); big groups need their count on the host
     // lists: launch the register and LDS sorters (false once every group fits a window: groups
     // only split, so a step whose input's largest group is <= kWinMax fills no list)
+    // the big groups' sort keys: ranks relative to their shard, at most the largest shard's length
+    uint32_t rel_bits = 1;
+    {
+        uint32_t maxlen = 1;
+        for (uint32_t i = 0; i < nshards; ++i) maxlen = std::max(maxlen, hshards[i].len);
+        while (rel_bits < 32 && (maxlen >> rel_bits) != 0) ++rel_bits;
+    }
     auto step = [&](bool big, bool lists = true, uint32_t *h_active = nullptr, uint32_t *h_max = nullptr) -> hipError_t {
         const uint32_t tag = (it & 1u) ? kTag : 0u;
         const StepStat ss = stats_of(it);
@@ -2365,16 +2380,16 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
                 const bool packed = nbig <= 0x10000u;
                 if (packed)
                     k_big_gather<true><<<blocks(T), tb, 0, s>>>((uint32_t)T, nbig, LL.lst[kBigClass], d_boff, sa, sd, key, ck, cv,
-                                                                gp, gd, ss);
+                                                                gp, gd, ss, shards, nshards);
                 else
                     k_big_gather<false><<<blocks(T), tb, 0, s>>>((uint32_t)T, nbig, LL.lst[kBigClass], d_boff, sa, sd, key, ck, cv,
-                                                                 gp, gd, ss);
+                                                                 gp, gd, ss, shards, nshards);
                 // every group sorted by its 32-bit keys on its own (px_sort.hip): segments = groups
                 std::vector<uint32_t> glen(nbig);
                 for (uint32_t b = 0; b < nbig; ++b) glen[b] = (uint32_t)(bl[b] >> 32);
                 auto *d_glen = S.get<uint32_t>((uint64_t)nbig * 4 + 64);
                 k_big_segs<<<(nbig + 255) / 256, 256, 0, s>>>(nbig, LL.lst[kBigClass], d_glen);
-                e = seg_sort_pairs(s, SA, nbig, seg_tile_count(glen.data(), nbig), d_boff, d_glen, 32, 8, ck, cv, nullptr,
+                e = seg_sort_pairs(s, SA, nbig, seg_tile_count(glen.data(), nbig), d_boff, d_glen, rel_bits, 8, ck, cv, nullptr,
                                    nullptr, 0, cka, cva, nullptr, nullptr, ck2, cv2, cnt + kCntSortErr);
                 S.put(d_glen);
                 if (e != hipSuccess) return e;
