@@ -2386,7 +2386,22 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     // non-OK status.  Every word was defined by k_doc_len for this batch, so a
     // violation is a kernel or transfer bug: fail loudly, never repair.
     int corrupt = 0;
-    for (uint32_t r = 0; r < n; ++r) {
+    // (the check on host threads for big batches; a range with a violation is re-run in order
+    // below so the messages and repairs come out as the serial loop made them)
+    std::atomic<bool> any_bad{false};
+    if (n >= 65536) {
+        parallel_ranges(n, host_threads(), [&](uint32_t lo, uint32_t hi) {
+            bool b = false;
+            for (uint32_t r = lo; r < hi && !b; ++r) {
+                const bool valid = doc_len[r] != 0xffffffffu;
+                const bool pl = rchunk[r] != 0xffffffffu && ridx[r] != 0xffffffffu;
+                b = pl ? (!valid || comp_len[r] == 0 || comp_len[r] > 2 * doc_len[r] + 8 || rstatus[r] > kErrSpace)
+                       : (rstatus[r] == kOk || (valid && rstatus[r] > kErrSpace));
+            }
+            if (b) any_bad.store(true);
+        });
+    }
+    for (uint32_t r = 0; r < (n < 65536 || any_bad.load() ? n : 0u); ++r) {
         const bool valid = doc_len[r] != 0xffffffffu;
         const bool placed = rchunk[r] != 0xffffffffu && ridx[r] != 0xffffffffu;
         bool bad = false;
@@ -2575,11 +2590,21 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     // registration gave them); a chunk closed by a newer one gets its total once its records
     // are in.  Then every shard's records on host threads: a shard's chunks are its own.
     std::vector<uint32_t> closing;
-    for (const Work &w : work) {
-        Shard &s = *w.s;
-        for (uint32_t r = w.r0; r < w.r1; ++r) {
-            if (!placed[r]) continue;
-            while (s.chunks.size() <= rchunk[r]) {
+    {
+        // a shard's placed records go to nondecreasing chunks: each work's last chunk (its
+        // records scanned on host threads for big batches), then the chunks opened in work order
+        std::vector<int64_t> wmax(work.size(), -1);
+        const std::function<void(uint32_t)> mx = [&](uint32_t k) {
+            int64_t m = -1;
+            for (uint32_t r = work[k].r0; r < work[k].r1; ++r)
+                if (placed[r]) m = std::max<int64_t>(m, rchunk[r]);
+            wmax[k] = m;
+        };
+        if (work.size() > 1 && n >= 65536) WorkerPool::get().run((uint32_t)work.size(), mx);
+        else for (uint32_t k = 0; k < (uint32_t)work.size(); ++k) mx(k);
+        for (size_t k = 0; k < work.size(); ++k) {
+            Shard &s = *work[k].s;
+            while (wmax[k] >= 0 && (int64_t)s.chunks.size() <= wmax[k]) {
                 if (!s.chunks.empty()) closing.push_back(s.chunks.back());
                 s.chunks.push_back(new_chunk(s.id));
             }
@@ -2688,20 +2713,24 @@ int px_ctx::set_batch(uint32_t n, const uint8_t *keys, const uint64_t *koff, con
     phase.mark("compat key prefixes (GPU decode of each ");
     // ---- compat key prefixes (GPU decode of each new record's key region)
     {
-        std::vector<KpJob> jobs;
-        std::vector<uint32_t> jrec;
-        jobs.reserve(n);
-        jrec.reserve(n);
-        for (uint32_t r = 0; r < n; ++r) {
-            if (!live[r]) continue;
-            uint64_t klen = hkoff[r + 1] - hkoff[r];
-            // first decode's room: the key, its 251,0 and a few escapes (a prefix that does
-            // not fit is decoded again with the whole doc's room; 1 M keys copied 2 klen + 66
-            // bytes each down for ~klen + 2 used)
-            jobs.push_back(KpJob{rgchunk[r], ridx[r], doc_len[r],
-                                 (uint32_t)std::min<uint64_t>(doc_len[r] + 64, klen + 2 + 30)});
-            jrec.push_back(r);
-        }
+        // the live records' jobs in record order (a prefix of the live flags places them, on host
+        // threads for big batches)
+        std::vector<uint64_t> lp(n + 1);
+        const uint32_t th = n >= 65536 ? host_threads() : 1;
+        pxh::parallel_prefix(n, th, lp.data(), [&](uint32_t r) -> uint64_t { return live[r] ? 1u : 0u; });
+        std::vector<KpJob> jobs(lp[n]);
+        std::vector<uint32_t> jrec(lp[n]);
+        parallel_ranges(n, th, [&](uint32_t lo, uint32_t hi) {
+            for (uint32_t r = lo; r < hi; ++r) {
+                if (!live[r]) continue;
+                const uint64_t klen = hkoff[r + 1] - hkoff[r];
+                // first decode's room: the key, its 251,0 and a few escapes (a prefix that does
+                // not fit is decoded again with the whole doc's room; 1 M keys copied 2 klen + 66
+                // bytes each down for ~klen + 2 used)
+                jobs[lp[r]] = KpJob{rgchunk[r], ridx[r], doc_len[r], (uint32_t)std::min<uint64_t>(doc_len[r] + 64, klen + 2 + 30)};
+                jrec[lp[r]] = r;
+            }
+        });
         std::vector<uint32_t> kst;
         decode_key_prefixes(jobs, kst);
         for (size_t i = 0; i < jobs.size(); ++i)
