@@ -377,18 +377,16 @@ PSA_DEV void push_long(const LongLists &L, bool valid, uint64_t ent) {
 // zeroed by the caller; a word is flag << 62 | (head + 1), the flag 1 for the workgroup's own
 // last head (0: none in it), 2 for the last head at or before its end.
 constexpr unsigned long long kG0Agg = 1ull << 62, kG0Incl = 2ull << 62, kG0Val = (1ull << 62) - 1ull;
-PSA_DEV bool head_at(const uint64_t *skeys, uint32_t N, uint32_t r, uint32_t syms) {
+PSA_DEV bool head_at(const uint64_t *skeys, uint32_t N, uint32_t r) {
     if (r == 0 || r >= N) return true;
-    const uint64_t km = key_mask(syms), k = skeys[r] & km;
-    return k != (skeys[r - 1] & km) || key_done(k, syms);
+    const uint64_t k = skeys[r] & kKeyMask;
+    return k != (skeys[r - 1] & kKeyMask) || (k & 511u) == 0;
 }
 constexpr uint32_t kG0Rows = 16, kG0Slots = kG0Rows * 256;  // slots per workgroup: rows of 256
 __global__ void __launch_bounds__(256) k_psa_groups0(uint32_t N, const uint32_t *sa, const uint64_t *skeys,
                                                      unsigned long long *chain, uint32_t *err, uint32_t *rank, uint16_t *sd,
-                                                     uint8_t *act, uint32_t *gsz, StepStat ss, uint32_t syms) {
+                                                     uint8_t *act, uint32_t *gsz, StepStat ss) {
     __shared__ uint32_t s_bid, s_w[2][4], s_pre;
-    const uint64_t km = key_mask(syms);
-    const uint32_t dlsh = key_dl_shift(syms);
     const uint32_t nb = gridDim.x;
     if (threadIdx.x == 0) s_bid = atomicAdd((uint32_t *)(chain + nb), 1u);  // (tickets: look-back never waits on a later one)
     __syncthreads();
@@ -409,13 +407,13 @@ __global__ void __launch_bounds__(256) k_psa_groups0(uint32_t N, const uint32_t 
 #pragma unroll
     for (uint32_t i = 0; i < kG0Rows; ++i) {
         const uint32_t r = base + i * 256u + threadIdx.x;
-        const uint64_t k = kc[i] & km;
+        const uint64_t k = kc[i] & kKeyMask;
         // (every lane shuffles: a lane left out of a shuffle hands its neighbour nothing)
         const uint64_t sl = shfl64(kc[i], (lane + 63u) & 63u), sr = shfl64(kc[i], (lane + 1u) & 63u);
-        const uint64_t kl = (lane == 0 ? ke[i] : sl) & km;
-        const uint64_t kr = (lane == 63 ? ke[i] : sr) & km;
-        const bool f = r < N && (r == 0 || k != kl || key_done(k, syms));
-        if (r < N && (r + 1 >= N || kr != k || key_done(kr, syms))) hnm |= 1u << i;  // r + 1 starts the next group (or the end)
+        const uint64_t kl = (lane == 0 ? ke[i] : sl) & kKeyMask;
+        const uint64_t kr = (lane == 63 ? ke[i] : sr) & kKeyMask;
+        const bool f = r < N && (r == 0 || k != kl || (k & 511u) == 0);
+        if (r < N && (r + 1 >= N || kr != k || (kr & 511u) == 0)) hnm |= 1u << i;  // r + 1 starts the next group (or the end)
         uint32_t v = f ? r + 1u : 0u;
         for (uint32_t o = 1; o < 64; o <<= 1) {
             const uint32_t y = (uint32_t)__shfl_up((int)v, o);
@@ -432,7 +430,7 @@ __global__ void __launch_bounds__(256) k_psa_groups0(uint32_t N, const uint32_t 
         // a workgroup holding a head knows its inclusive value at once
         __hip_atomic_store(chain + bid, (agg || bid == 0 ? kG0Incl : kG0Agg) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         uint32_t pre = 0, spins = 0;
-        if (bid > 0 && !head_at(skeys, N, base, syms)) {  // (its first slot's head lies before it)
+        if (bid > 0 && !head_at(skeys, N, base)) {  // (its first slot's head lies before it)
             for (uint32_t j = bid - 1;;) {
                 const unsigned long long x = __hip_atomic_load(chain + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (!(x >> 62)) {
@@ -462,7 +460,7 @@ __global__ void __launch_bounds__(256) k_psa_groups0(uint32_t N, const uint32_t 
         rank[pp[i]] = hd;
         const uint32_t a = (hd != r || !hn) ? 1u : 0u;  // in a group of >= 2
         a_all += a;
-        sd[r] = a ? (uint16_t)((kc[i] >> dlsh) & 15u) : (uint16_t)0;
+        sd[r] = a ? (uint16_t)((kc[i] >> kDlShift) & 15u) : (uint16_t)0;
         act[r] = (uint8_t)a;
         if (!(hd == r && !hn)) gsz[r] = 0;  // (not the start of a group of >= 2)
         if (hn && hd != r) {                // the last element of a group of >= 2
@@ -2239,11 +2237,9 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
     // shards are contiguous in position space and their suffix-array ranges are the same
     // ranges, so each shard sorts on its own and no key carries the shard)
     // (PX_PSA_SYMS = 2..6 for tests and measurements: fewer symbols give odd pass counts,
-    // which px_route.h routes; more do not fit below the reach bits, kDlShift -- except 7 as
-    // raw bytes and a length, px_sort.h kRawSyms: 59 key bits, 7 passes)
+    // which px_route.h routes; more do not fit below the reach bits, kDlShift)
     uint32_t syms = 6;
-    if (const char *ev_syms = std::getenv("PX_PSA_SYMS")) syms = (uint32_t)std::min(7, std::max(2, std::atoi(ev_syms)));
-    const uint32_t key_bits = syms == kRawSyms ? kKeyBitsRaw : 9 * syms;
+    if (const char *ev_syms = std::getenv("PX_PSA_SYMS")) syms = (uint32_t)std::min(6, std::max(2, std::atoi(ev_syms)));
     {
         const uint32_t slices = std::max<uint32_t>(1, std::min<uint32_t>(64, 16384 / ndocs));
         const uint64_t nw = (uint64_t)ndocs * slices;
@@ -2259,7 +2255,7 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         k_psa_segs<<<(nshards + 255) / 256, 256, 0, s>>>(nshards, shards, segs, segs + nshards);
         auto *va = S.get<uint32_t>(n64 * 4), *vb = S.get<uint32_t>(n64 * 4);
         // passes: text -> keys -> keys2 -> keys -> keys2 -> keys -> (keys2, sa)
-        PSA_CHECK(seg_sort_pairs(s, SA, nshards, seg_tile_count(slen.data(), nshards), segs, segs + nshards, key_bits, 9,
+        PSA_CHECK(seg_sort_pairs(s, SA, nshards, seg_tile_count(slen.data(), nshards), segs, segs + nshards, 9 * syms, 9,
                                  nullptr, nullptr, G, dist, syms, keys, va, keys2, vb, keys2, sa, cnt + kCntSortErr));
         S.put(segs);
         S.put(va);
@@ -2280,7 +2276,7 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
         auto *chain = (unsigned long long *)keys;  // (the pass buffers are spent: the look-back chain and its ticket)
         const uint32_t g0 = (uint32_t)((n64 + kG0Slots - 1) / kG0Slots);
         PSA_CHECK(hipMemsetAsync(chain, 0, ((uint64_t)g0 + 1) * 8, s));
-        k_psa_groups0<<<g0, 256, 0, s>>>(N, sa, keys2, chain, cnt + kCntSortErr, rank, sd, act, gsz, region(0), syms);
+        k_psa_groups0<<<g0, 256, 0, s>>>(N, sa, keys2, chain, cnt + kCntSortErr, rank, sd, act, gsz, region(0));
     }
     k_stat_sum<<<1, 64, 0, s>>>(region(0).sh, cnt + kCntSorted + kMaxSteps, cnt + kCntActive, cnt + kCntMax);
     S.put(keys);

@@ -26,21 +26,6 @@ struct SegTile {
 // their low kKeyBits.
 constexpr uint32_t kDlShift = 58, kKeyBits = 54;
 constexpr uint64_t kKeyMask = (1ull << kKeyBits) - 1ull;
-// The 7-symbol first key (syms == kRawSyms, opt-in PX_PSA_SYMS=7): the 7 raw bytes (zero past
-// the doc end) above a 3-bit length min(left, 7), 59 bits, the reach above them.  It orders
-// like 7 symbols of 9 bits (a shorter string's zero padding ties, its length then sorts it
-// first); a suffix is complete (its whole string in the key) iff its length field is < 7.
-// Its 7 passes of 9 bits would reach the reach bits: every sort masks its last digit to its
-// key bits (the reach, the most significant digit bits, would otherwise order first).
-constexpr uint32_t kRawSyms = 7, kDlShiftRaw = 59, kKeyBitsRaw = 59;
-__host__ __device__ inline uint32_t key_dl_shift(uint32_t syms) { return syms == kRawSyms ? kDlShiftRaw : kDlShift; }
-__host__ __device__ inline uint64_t key_mask(uint32_t syms) {
-    return syms == kRawSyms ? (1ull << kKeyBitsRaw) - 1ull : kKeyMask;
-}
-// the key holds its suffix's whole string (shorter than `syms` symbols)
-__host__ __device__ inline bool key_done(uint64_t k, uint32_t syms) {
-    return syms == kRawSyms ? (k & 7u) != 7u : (k & 511u) == 0;
-}
 
 // device scratch borrowed from the caller (px_psa.hip's Scratch / the runtime heap)
 struct SortAlloc {

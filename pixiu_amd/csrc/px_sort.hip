@@ -55,20 +55,12 @@ typedef PX_GAS uint32_t gu32;
 // the first suffix sort's key of text position p (k_psa_key0's layout without the shard):
 // 8 text bytes by two aligned 8-byte loads and a funnel shift (G is 8-byte aligned and
 // padded), then `syms` symbols of 9 bits; the doubling reach above them (px_sort.h kDlShift)
-// (syms == kRawSyms: px_sort.h's 7 raw bytes and length)
-SD uint64_t raw_key(uint64_t x, uint32_t left) {
-    uint64_t k = __builtin_bswap64(x) >> 8;  // bytes 0..6, byte 0 highest
-    if (left < 7u) k &= ~((1ull << (8u * (7u - left))) - 1ull);
-    const uint32_t dl = min(15u, 32u - (uint32_t)__clz(left > 7u ? (left - 1u) / 7u : 0u));
-    return (k << 3 | min(left, 7u)) | (uint64_t)dl << kDlShiftRaw;
-}
 SD uint64_t text_key(const uint8_t *G, const uint16_t *dist, uint32_t p, uint32_t syms) {
     gcu64 *G8 = (gcu64 *)G;
     const uint32_t w = p >> 3, sh = (p & 7u) * 8u;
     uint64_t x = G8[w];
     if (sh) x = (x >> sh) | (G8[w + 1] << (64u - sh));
     const uint32_t left = ((gcu16 *)dist)[p];
-    if (syms == kRawSyms) return raw_key(x, left);
     uint64_t k = 0;
     for (uint32_t s = 0; s < syms; ++s) k = k << 9 | (s < left ? ((x >> (8 * s)) & 0xffu) + 1u : 0u);
     // steps k < 15 with (syms << k) < left: 2^k <= (left - 1) / syms, i.e. that quotient's bit length
@@ -85,7 +77,6 @@ SD uint64_t text_key_lds(const uint64_t *tw, uint32_t w0, const uint16_t *dist, 
     uint64_t x = tw[w];
     if (sh) x = (x >> sh) | (tw[w + 1] << (64u - sh));
     const uint32_t left = ((gcu16 *)dist)[p];
-    if (syms == kRawSyms) return raw_key(x, left);
     uint64_t k = 0;
     for (uint32_t s = 0; s < syms; ++s) k = k << 9 | (s < left ? ((x >> (8 * s)) & 0xffu) + 1u : 0u);
     const uint32_t q = left > syms ? (left - 1u) / syms : 0u;
@@ -133,20 +124,13 @@ SD uint32_t block_excl_scan(uint32_t v, uint32_t *red, uint32_t *tot) {
     return before + x - v;
 }
 
-// the digit at `shift` of a sort by key bits [0, bits): the last pass's digit is narrower
-// (the 7-symbol first key keeps its doubling reach above bit 58, px_sort.h kRawSyms)
-template <int RB>
-SD uint32_t digit_mask(uint32_t bits, uint32_t shift) {
-    return bits - shift >= (uint32_t)RB ? (1u << RB) - 1u : (1u << (bits - shift)) - 1u;
-}
-
 // ---------------------------------------------------------------- histogram
 // per segment and pass, the digit counts of its elements (one workgroup per `tpw` <= kHistTiles
 // tiles; LDS counts flushed to the segment's global counts when the segment changes)
 template <int RB, bool TEXT>
 __global__ void __launch_bounds__(kThreads) k_seg_hist(const SegTile *tiles, uint32_t ntiles, uint32_t tpw, const uint64_t *kin,
                                                        const uint8_t *G, const uint16_t *dist, uint32_t syms,
-                                                       uint32_t passes, uint32_t *ghist, uint32_t bits) {
+                                                       uint32_t passes, uint32_t *ghist) {
     constexpr uint32_t BINS = 1u << RB;
     __shared__ uint32_t h[kMaxPasses * BINS];
     const uint32_t t0 = blockIdx.x * tpw, t1 = min(ntiles, t0 + tpw);
@@ -174,7 +158,7 @@ __global__ void __launch_bounds__(kThreads) k_seg_hist(const SegTile *tiles, uin
             if (ok) k = TEXT ? text_key(G, dist, T.start + j, syms) : ((gcu64 *)kin)[T.start + j];
             const uint64_t valid = __ballot(ok);
             for (uint32_t p = 0; p < passes; ++p) {
-                const uint32_t d = (uint32_t)(k >> (RB * p)) & digit_mask<RB>(bits, RB * p);
+                const uint32_t d = (uint32_t)(k >> (RB * p)) & (BINS - 1u);
                 const uint64_t m = match_digit<RB>(d, valid);
                 if (ok && (m & lanes_below()) == 0) atomicAdd(&h[p * BINS + d], (uint32_t)__popcll(m));
             }
@@ -317,7 +301,7 @@ __global__ void __launch_bounds__(kThreads, PX_SORT_WPE) k_seg_pass(const SegTil
                                                        const uint32_t *vin_, uint64_t *kout_, uint32_t *vout_,
                                                        uint32_t pass, uint32_t passes, const uint32_t *base,
                                                        uint32_t *status, const uint8_t *G, const uint16_t *dist,
-                                                       uint32_t syms, uint32_t *err, uint32_t *status_next, uint32_t bits) {
+                                                       uint32_t syms, uint32_t *err, uint32_t *status_next) {
     constexpr uint32_t BINS = 1u << RB, BPT = BINS / kThreads;
     // (the tile number and the scan's partials live in s_dst's first words, which are written only
     // after both are spent)
@@ -332,7 +316,7 @@ __global__ void __launch_bounds__(kThreads, PX_SORT_WPE) k_seg_pass(const SegTil
     gcu32 *vin = (gcu32 *)vin_;
     gu64 *kout = (gu64 *)kout_;
     gu32 *vout = (gu32 *)vout_;
-    const uint32_t lane = lane_id(), w = threadIdx.x >> 6, shift = RB * pass, dmask = digit_mask<RB>(bits, shift);
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6, shift = RB * pass;
     if (threadIdx.x == 0) s_tile = atomicAdd(tile_ctr, 1u);  // tiles start in order: look-back never waits on a later one
     for (uint32_t i = threadIdx.x; i < kWaves * BINS; i += kThreads) (&wh[0][0])[i] = 0;
     __syncthreads();
@@ -372,7 +356,7 @@ __global__ void __launch_bounds__(kThreads, PX_SORT_WPE) k_seg_pass(const SegTil
 #pragma unroll
     for (uint32_t it = 0; it < kItems; ++it) {
         const bool ok = j0 + it * 64 < T.count;
-        const uint32_t d = (uint32_t)(k[it] >> shift) & dmask;
+        const uint32_t d = (uint32_t)(k[it] >> shift) & (BINS - 1u);
         const uint64_t m = match_digit<RB>(d, __ballot(ok));
         uint32_t prev = 0;
         if (ok) prev = wh[w][d];
@@ -456,7 +440,7 @@ __global__ void __launch_bounds__(kThreads, PX_SORT_WPE) k_seg_pass(const SegTil
     uint16_t at[kItems];
 #pragma unroll
     for (uint32_t it = 0; it < kItems; ++it) {
-        const uint32_t d = (uint32_t)(k[it] >> shift) & dmask;
+        const uint32_t d = (uint32_t)(k[it] >> shift) & (BINS - 1u);
         at[it] = (uint16_t)(s_excl[d] + wh[w][d] + r[it]);
         if (j0 + it * 64 < T.count) {
             stage[at[it]] = k[it];
@@ -661,12 +645,12 @@ hipError_t seg_sort_pairs(hipStream_t s, const SortAlloc &A, uint32_t nseg, uint
     }
 #define PX_SORT_RB(RB_)                                                                                            \
     do {                                                                                                           \
-        if (text && RB_ == 9 && passes == syms && syms != kRawSyms)                                                \
+        if (text && RB_ == 9 && passes == syms)                                                                    \
             k_seg_hist_text<<<hb, kThreads, 0, s>>>(d_tiles, nt, tpw, G, dist, syms, d_hist);                           \
         else if (text)                                                                                             \
-            k_seg_hist<RB_, true><<<hb, kThreads, 0, s>>>(d_tiles, nt, tpw, nullptr, G, dist, syms, passes, d_hist, bits);\
+            k_seg_hist<RB_, true><<<hb, kThreads, 0, s>>>(d_tiles, nt, tpw, nullptr, G, dist, syms, passes, d_hist);    \
         else                                                                                                       \
-            k_seg_hist<RB_, false><<<hb, kThreads, 0, s>>>(d_tiles, nt, tpw, k0, nullptr, nullptr, 0, passes, d_hist, bits);\
+            k_seg_hist<RB_, false><<<hb, kThreads, 0, s>>>(d_tiles, nt, tpw, k0, nullptr, nullptr, 0, passes, d_hist);  \
         k_seg_base<RB_><<<nseg * passes, kThreads, 0, s>>>(d_hist, d_start, passes, d_base);                      \
         const uint64_t *ki = k0;                                                                                   \
         const uint32_t *vi = v0;                                                                                   \
@@ -681,10 +665,10 @@ hipError_t seg_sort_pairs(hipStream_t s, const SortAlloc &A, uint32_t nseg, uint
             }                                                                                                      \
             if (text && p == 0)                                                                                    \
                 k_seg_pass<RB_, true><<<nt, kThreads, 0, s>>>(d_tiles, d_ctr + p, nullptr, nullptr, ko, vo, p,     \
-                                                              passes, d_base, st, G, dist, syms, err, sn, bits);   \
+                                                              passes, d_base, st, G, dist, syms, err, sn);         \
             else                                                                                                   \
                 k_seg_pass<RB_, false><<<nt, kThreads, 0, s>>>(d_tiles, d_ctr + p, ki, vi, ko, vo, p, passes,      \
-                                                               d_base, st, nullptr, nullptr, 0, err, sn, bits);    \
+                                                               d_base, st, nullptr, nullptr, 0, err, sn);          \
             ki = ko;                                                                                               \
             vi = vo;                                                                                               \
             e = hipGetLastError();                                                                                 \

@@ -164,12 +164,12 @@ def test_segmented_sort_equals_radix(cfg, n, rps, store_factory):
     assert out[0] == out[1]
 
 
-@pytest.mark.parametrize("syms", [5, 3, 4, 7])
+@pytest.mark.parametrize("syms", [5, 3, 4])
 @pytest.mark.parametrize("cfg,n,rps", [(3, 64, 32), (5, 400, 200), (4, 20000, 0)])
 def test_odd_pass_first_sort(syms, cfg, n, rps, store_factory, monkeypatch):
     """The first suffix sort with 5 / 3 passes (odd: its last pass used to read and write the
     same key buffer, px_route.h) and 4: the same bytes and placement as the default 6-symbol
-    sort; 7 is the raw-byte + length key (px_sort.h kRawSyms, 7 passes).  (5, 400, 200) is config 5 across MemPool rotations, the shape of round 5's second
+    sort.  (5, 400, 200) is config 5 across MemPool rotations, the shape of round 5's second
     fault; (4, 20000, 0) the 251-heavy single instance."""
     from pixiu_amd import synth
     cp = synth.make(cfg, n)
