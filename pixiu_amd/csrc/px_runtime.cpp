@@ -1311,7 +1311,14 @@ struct px_ctx {
             if (mode == 0) hcheck(launch_span_pieces(stream, ns, sdq, ctab, kPiece));
             const uint32_t sw = std::min<uint32_t>(opts.decode_waves ? opts.decode_waves : 16384, ns);
             auto *sframes = (Frame *)scratch_frames.get((uint64_t)sw * depth * sizeof(Frame));
-            hcheck(launch_decode_addr(stream, sdq, ns, ctab, addr, pl, ps, sframes, depth, sw | (xcd ? 0x80000000u : 0u)));
+            // (the pieces in launch order: the XCD remap measured 0.65 ms slower here -- config 3's
+            // decode + count 13.6 against 12.9 ms over 6 and 4 batches, CHANGELOG round 6; the
+            // pieces' tail, not L2 locality, bounds this decode.  PX_SPAN_XCD=1 restores it)
+            static const bool span_xcd = [] {
+                const char *e = std::getenv("PX_SPAN_XCD");
+                return e && e[0] == '1';
+            }();
+            hcheck(launch_decode_addr(stream, sdq, ns, ctab, addr, pl, ps, sframes, depth, sw | (span_xcd ? 0x80000000u : 0u)));
             hcheck(launch_span_agg(stream, n, dfirst, pl, ps, dq, dl, ds));
         } else {
             hcheck(launch_decode_addr(stream, dq, n, ctab, addr, dl, ds, frames, depth, waves | (xcd ? 0x80000000u : 0u)));
