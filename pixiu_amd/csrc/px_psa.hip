@@ -2193,6 +2193,7 @@ bool env_on(const char *name) {
     const char *v = std::getenv(name);
     return v && *v == '1';
 }
+constexpr uint32_t kPinUnset = 0xffffffffu;  // a late step's pinned count not yet written
 constexpr uint32_t kMaxSteps = 20;  // h doubles from >= 5 past 65,535 (the longest doc) in 15
 // persistent grids of the doubling kernels (grid-stride over windows, and over lists whose
 // sizes only the device knows)
@@ -2441,6 +2442,11 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
             if (it >= kMaxSteps) return hipErrorUnknown;
             // (k_stat_sum writes step k's counts into pin[256 + k] / pin[288 + k] itself)
             static const bool pin_copy = env_on("PX_PIN_COPY");  // (A/B: the counts copied back)
+            // (a sentinel first: a count the kernel's store has not yet made visible reads as the
+            // sentinel, never as a stale value, and is then fetched from the device -- a stale
+            // nonzero count had the host enqueue empty steps up to kMaxSteps, 90-260 ms, r06fin2)
+            pin[256 + it] = kPinUnset;
+            pin[288 + it] = kPinUnset;
             PSA_CHECK(step(false, known_max > kWinMax, pin_copy ? nullptr : pin + 256 + it, pin_copy ? nullptr : pin + 288 + it));
             const uint32_t k = it - 1;
             if (pin_copy) {
@@ -2450,8 +2456,14 @@ hipError_t psa_run(hipStream_t s, const PsaAlloc &A, uint32_t ndocs, const PsaDo
             PSA_CHECK(hipEventRecord(sev.e[k], s));
             if (k >= it0 + 1) {
                 PSA_CHECK(hipEventSynchronize(sev.e[k - 1]));
-                done = pin[256 + k - 1] == 0;
-                known_max = pin[288 + k - 1];
+                uint32_t got[2] = {__atomic_load_n(pin + 256 + k - 1, __ATOMIC_ACQUIRE),
+                                   __atomic_load_n(pin + 288 + k - 1, __ATOMIC_ACQUIRE)};
+                if (got[0] == kPinUnset || got[1] == kPinUnset) {  // (not visible yet: the device's own words)
+                    PSA_CHECK(hipMemcpy(&got[0], cnt + kCntActive + 1 + (k - 1), 4, hipMemcpyDeviceToHost));
+                    PSA_CHECK(hipMemcpy(&got[1], cnt + kCntMax + 1 + (k - 1), 4, hipMemcpyDeviceToHost));
+                }
+                done = got[0] == 0;
+                known_max = got[1];
             }
         }
     }
